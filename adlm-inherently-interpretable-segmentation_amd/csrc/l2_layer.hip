@@ -1,0 +1,621 @@
+// l2_layer.hip — the PPNet prototype layer on gfx950: fused forward and a two-kernel
+// backward, all on f32-input MFMA (v_mfma_f32_32x32x2_f32, an exact f32 fma chain).
+//
+// Reference: model.py:203-221 (_l2_convolution), 231-237 (distance_2_similarity),
+// 259-283 (forward_from_conv_features, patch_classification branch), and the autograd
+// graph of those ops for the backward.
+//
+// Index space: pixels are flattened over the batch, g = b*HW + n, and cut into 32-pixel
+// tiles; prototypes are padded to Pp = ceil(P/32)*32 (zero rows), classes to 32.
+//
+//   l2_fwd_kernel      "layout A" tiles S[p][n] (prototype on the register rows, pixel on
+//                      the lane) -> D stored NCHW with 128-B row segments; the activation
+//                      tile is already the B operand of the last-layer MFMA (rows = p).
+//   l2_bwd_x_kernel    layout A again: recompute S, g_act = W^T g_logits, g_s, and
+//                      g_x = P^T (-2 g_s) accumulated over p-tiles (sums over rows: no
+//                      lane movement), + 2 x sum_p g_s.
+//   l2_bwd_pw_kernel   "layout B" tiles S[n][p] (pixel on the rows): g_P^T and g_W sum over
+//                      pixels = over rows, so the g_s / act tiles feed the MFMA A/B operands
+//                      directly. One workgroup per (p-tile, pixel split); per-workgroup
+//                      partial slabs, reduced by l2_bwd_reduce_kernel in a fixed order
+//                      (bitwise reproducible, no atomics).
+#include "protoseg_device.h"
+#include "protoseg_host.h"
+
+namespace protoseg {
+
+namespace {
+
+constexpr int kFwdWaves = 8;   // 512-thread workgroups share one LDS prototype image
+constexpr int kPwWaves = 4;
+constexpr int kLdx = 33;       // padded row of the per-wave X tile in bwd_pw
+constexpr int kLdt = 33;       // padded row of a prototype tile [C][33]
+
+// Stage prototypes tile-major as Pt[pt][c][33] (a 32-prototype tile per [C][33] block) and
+// p2[p] = sum_c p^2 (model.py:210-211). Every read is conflict-free: lanes over p (distance
+// A operand, consecutive words) and lanes over c (g_x A operand, stride 33); and every
+// per-register offset is a compile-time immediate on one lane base.
+template <int NC>
+__device__ void stage_prototypes(float* Pt, float* p2s, const float* __restrict__ protos, int P, int Pp) {
+  constexpr int C = NC * 32;
+  for (int idx = threadIdx.x; idx < Pp * C; idx += blockDim.x) {
+    const int p = idx / C;
+    const int c = idx - p * C;
+    Pt[((p >> 5) * C + c) * kLdt + (p & 31)] = (p < P) ? protos[static_cast<size_t>(p) * C + c] : 0.f;
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < Pp; p += blockDim.x) {
+#pragma clang fp contract(off)
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const float v = Pt[((p >> 5) * C + c) * kLdt + (p & 31)];
+      s += v * v;
+    }
+    p2s[p] = s;
+  }
+}
+
+// Same p2 as stage_prototypes, for one prototype row read from global memory.
+template <int NC>
+__device__ float proto_norm2(const float* __restrict__ protos, int p, bool valid) {
+#pragma clang fp contract(off)
+  constexpr int C = NC * 32;
+  float s = 0.f;
+  if (valid) {
+    for (int c = 0; c < C; ++c) {
+      const float v = protos[static_cast<size_t>(p) * C + c];
+      s += v * v;
+    }
+  }
+  return s;
+}
+
+// Loads the 32-pixel tile of x for this lane in layout-A order: xv[ct][r] = x[c][pixel j]
+// with c = 32ct + acc_row(r, h). Returns the full ||x||^2 of the lane's pixel (both
+// half-waves hold the same value).
+template <typename TX, int NC>
+__device__ __forceinline__ float load_x_tile(const TX* __restrict__ xb, int HW, bool valid, float (&xv)[NC][16]) {
+  const int h = (threadIdx.x & 63) >> 5;
+  const TX* xh = xb + static_cast<size_t>(4 * h) * HW;
+  float x2 = 0.f;
+#pragma unroll
+  for (int ct = 0; ct < NC; ++ct) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      // channel c = 32ct + acc_row(r, h); unconditional load (invalid lanes read pixel 0
+      // of image 0), then select: a conditional load makes hipcc branch and drain vmcnt
+      const float v = XIO<TX>::load(xh, static_cast<size_t>(ct * 32 + row_of(r)) * HW);
+      xv[ct][r] = valid ? v : 0.f;
+      x2 = fmaf(xv[ct][r], xv[ct][r], x2);
+    }
+  }
+  x2 += __shfl_xor(x2, 32);
+  return x2;
+}
+
+template <typename TX, int NC>
+__global__ __launch_bounds__(kFwdWaves * 64) void l2_fwd_kernel(
+    const TX* __restrict__ x, int HW, int npix, const float* __restrict__ protos, int P, int Pp,
+    const float* __restrict__ w_last, int K, float eps, int act_kind, float* __restrict__ dist,
+    float* __restrict__ act_out, float* __restrict__ logits) {
+  constexpr int C = NC * 32;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* Pt = smem;                      // [Pp/32][C][33]
+  float* Wl = Pt + (Pp / 32) * C * kLdt;  // [Pp][32]: W[k][p] at p*32 + k
+  float* p2s = Wl + Pp * 32;     // [Pp]
+  const bool do_logits = logits != nullptr;
+  if (do_logits) {
+    for (int idx = threadIdx.x; idx < Pp * 32; idx += blockDim.x) {
+      const int p = idx >> 5, k = idx & 31;
+      Wl[idx] = (p < P && k < K) ? w_last[static_cast<size_t>(k) * P + p] : 0.f;
+    }
+  }
+  stage_prototypes<NC>(Pt, p2s, protos, P, Pp);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
+  const int ntiles = (npix + 31) / 32;
+  const int npt = Pp / 32;
+  for (int t = blockIdx.x * kFwdWaves + wave; t < ntiles; t += gridDim.x * kFwdWaves) {
+    const int g = t * 32 + j;
+    const bool valid = g < npix;
+    const int b = valid ? g / HW : 0;
+    const int n = valid ? g - b * HW : 0;
+    float xv[NC][16];
+    const float x2 = load_x_tile<TX, NC>(x + static_cast<size_t>(b) * C * HW + n, HW, valid, xv);
+
+    f32x16 lacc = zero16();
+#pragma unroll 1
+    for (int pt = 0; pt < npt; ++pt) {
+      // row p = pt*32 + 4h + row_of(r) of D[b] (clamped to a valid row for padded lanes)
+      float* dpt = dist ? dist + (static_cast<size_t>(b) * P + pt * 32 + 4 * h) * HW + n : nullptr;
+      f32x16 acc = zero16();
+      const float* Pa = Pt + pt * C * kLdt + j;
+#pragma unroll
+      for (int ct = 0; ct < NC; ++ct)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc = mfma32(Pa[(ct * 32 + acc_row(r, h)) * kLdt], xv[ct][r], acc);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int p = pt * 32 + acc_row(r, h);
+        const float d = l2_distance(x2, p2s[p], acc[r]);
+        const bool st = valid && p < P;
+        if (dpt && st) dpt[static_cast<size_t>(row_of(r)) * HW] = d;
+        const float a = activation(d, eps, act_kind);
+        if (act_out && st) act_out[static_cast<size_t>(g) * P + p] = a;
+        acc[r] = a;
+      }
+      if (do_logits) {
+        const float* Wa = Wl + pt * 32 * 32 + j;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) lacc = mfma32(Wa[acc_row(r, h) * 32], acc[r], lacc);
+      }
+    }
+    if (do_logits && valid) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int k = acc_row(r, h);
+        if (k < K) logits[static_cast<size_t>(g) * K + k] = lacc[r];
+      }
+    }
+  }
+}
+
+template <typename TX, int NC>
+__global__ __launch_bounds__(kFwdWaves * 64) void l2_bwd_x_kernel(
+    const TX* __restrict__ x, int HW, int npix, const float* __restrict__ protos, int P, int Pp,
+    const float* __restrict__ w_last, int K, float eps, int act_kind, const float* __restrict__ g_logits,
+    const float* __restrict__ g_dist, TX* __restrict__ g_x) {
+  constexpr int C = NC * 32;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* Pt = smem;                      // [Pp/32][C][33]
+  float* Wt = Pt + (Pp / 32) * C * kLdt;  // [Pp/32][32][32]: W[k][p] at (p>>5)*1024 + k*32 + (p&31)
+  float* p2s = Wt + Pp * 32;     // [Pp]
+  if (g_logits) {
+    for (int idx = threadIdx.x; idx < Pp * 32; idx += blockDim.x) {
+      const int pt = idx >> 10, k = (idx >> 5) & 31, p = pt * 32 + (idx & 31);
+      Wt[idx] = (p < P && k < K) ? w_last[static_cast<size_t>(k) * P + p] : 0.f;
+    }
+  }
+  stage_prototypes<NC>(Pt, p2s, protos, P, Pp);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
+  const int ntiles = (npix + 31) / 32;
+  const int npt = Pp / 32;
+  const int KS = (K + 1) / 2;
+  for (int t = blockIdx.x * kFwdWaves + wave; t < ntiles; t += gridDim.x * kFwdWaves) {
+    const int g = t * 32 + j;
+    const bool valid = g < npix;
+    const int b = valid ? g / HW : 0;
+    const int n = valid ? g - b * HW : 0;
+    float xv[NC][16];
+    const float x2 = load_x_tile<TX, NC>(x + static_cast<size_t>(b) * C * HW + n, HW, valid, xv);
+    // B operand of g_act^T = W^T g_logits^T: lane (h, j) holds g_logits[pixel j][k = 2s+h].
+    float gl[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int k = 2 * s + h;
+      const bool ok = valid && k < K;
+      const float v = g_logits ? g_logits[ok ? static_cast<size_t>(g) * K + k : 0] : 0.f;
+      gl[s] = ok ? v : 0.f;
+    }
+
+    f32x16 gx[NC];
+#pragma unroll
+    for (int ct = 0; ct < NC; ++ct) gx[ct] = zero16();
+    float gsum = 0.f;
+#pragma unroll 1
+    for (int pt = 0; pt < npt; ++pt) {
+      f32x16 acc = zero16();
+      const float* Pa = Pt + pt * C * kLdt + j;
+#pragma unroll
+      for (int ct = 0; ct < NC; ++ct)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc = mfma32(Pa[(ct * 32 + acc_row(r, h)) * kLdt], xv[ct][r], acc);
+      const float* gdpt = g_dist ? g_dist + (static_cast<size_t>(b) * P + pt * 32 + 4 * h) * HW + n : nullptr;
+      f32x16 gacc = zero16();
+      if (g_logits) {
+        const float* Wa = Wt + pt * 1024 + j;
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+          if (s < KS) gacc = mfma32(Wa[(2 * s + h) * 32], gl[s], gacc);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int p = pt * 32 + acc_row(r, h);
+        const float d = l2_distance(x2, p2s[p], acc[r]);
+        float gd = g_logits ? gacc[r] * activation_grad(d, eps, act_kind) : 0.f;
+        if (gdpt) {
+          const bool ok = valid && p < P;
+          const float v = gdpt[ok ? static_cast<size_t>(row_of(r)) * HW : 0];
+          gd += ok ? v : 0.f;
+        }
+        const float gs = (d > 0.f && p < P) ? gd : 0.f;  // relu backward: grad * (out > 0)
+        gsum += gs;
+        acc[r] = -2.f * gs;                               // d(-2*xp)/dxp folded into the operand
+      }
+#pragma unroll
+      for (int ct = 0; ct < NC; ++ct) {
+        const float* Pc = Pt + (pt * C + ct * 32 + j) * kLdt;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) gx[ct] = mfma32(Pc[acc_row(r, h)], acc[r], gx[ct]);
+      }
+    }
+    gsum += __shfl_xor(gsum, 32);
+    if (valid) {
+      TX* gxh = g_x + (static_cast<size_t>(b) * C + 4 * h) * HW + n;
+#pragma unroll
+      for (int ct = 0; ct < NC; ++ct)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          // channel c = 32ct + acc_row(r, h). conv(x^2, ones) backward then pow backward:
+          // gsum * (2x); plus the xp branch accumulated in gx.
+          XIO<TX>::store(gxh, static_cast<size_t>(ct * 32 + row_of(r)) * HW, gx[ct][r] + gsum * (2.f * xv[ct][r]));
+        }
+    }
+  }
+}
+
+template <typename TX, int NC>
+__global__ __launch_bounds__(kPwWaves * 64) void l2_bwd_pw_kernel(
+    const TX* __restrict__ x, int HW, int npix, const float* __restrict__ protos, int P, int Pp,
+    const float* __restrict__ w_last, int K, float eps, int act_kind, const float* __restrict__ g_logits,
+    const float* __restrict__ g_dist, float* __restrict__ slab_gp, float* __restrict__ slab_gw,
+    float* __restrict__ slab_gs) {
+  constexpr int C = NC * 32;
+  // LDS: Pl[C][32] prototype tile (B operand of S), Wl[32][32] class tile (B operand of
+  // g_act), then one Xl[C][33] pixel tile per wave (A operand of S, B operand of g_P).
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* Pl = smem;
+  float* Wl = Pl + C * 32;
+  float* Xall = Wl + 32 * 32;
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
+  float* Xl = Xall + wave * C * kLdx;
+  const int pt = blockIdx.x;
+  const int p = pt * 32 + j;  // this lane's prototype column
+  const bool pvalid = p < P;
+
+  for (int idx = threadIdx.x; idx < C * 32; idx += blockDim.x) {
+    const int c = idx >> 5, pp = pt * 32 + (idx & 31);
+    Pl[idx] = pp < P ? protos[static_cast<size_t>(pp) * C + c] : 0.f;
+  }
+  for (int idx = threadIdx.x; idx < 32 * 32; idx += blockDim.x) {
+    const int k = idx >> 5, pp = pt * 32 + (idx & 31);
+    Wl[idx] = (g_logits && k < K && pp < P) ? w_last[static_cast<size_t>(k) * P + pp] : 0.f;
+  }
+  const float p2 = proto_norm2<NC>(protos, p, pvalid);
+  const int KS = (K + 1) / 2;
+  __syncthreads();
+
+  f32x16 gp[NC];
+#pragma unroll
+  for (int ct = 0; ct < NC; ++ct) gp[ct] = zero16();
+  f32x16 gw = zero16();
+  float gsum = 0.f;
+
+  const int ntiles = (npix + 31) / 32;
+  for (int t = blockIdx.y * kPwWaves + wave; t < ntiles; t += gridDim.y * kPwWaves) {
+    const int g0 = t * 32;
+    const int g = g0 + j;  // pixel staged by this lane
+    const bool valid = g < npix;
+    const int b = valid ? g / HW : 0;
+    const int n = valid ? g - b * HW : 0;
+
+    wave_lds_fence();  // the previous tile's reads of Xl are complete
+    float x2;
+    {
+      float xv[NC][16];
+      x2 = load_x_tile<TX, NC>(x + static_cast<size_t>(b) * C * HW + n, HW, valid, xv);
+#pragma unroll
+      for (int ct = 0; ct < NC; ++ct)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) Xl[(ct * 32 + acc_row(r, h)) * kLdx + j] = xv[ct][r];
+    }
+    float gl[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int k = 2 * s + h;
+      const bool ok = valid && k < K;
+      const float v = g_logits ? g_logits[ok ? static_cast<size_t>(g) * K + k : 0] : 0.f;
+      gl[s] = ok ? v : 0.f;
+    }
+    wave_lds_fence();  // Xl writes of every lane are visible
+
+    // S[n][p]: A = x (lane i = pixel, k = channel pair), B = P (lane j = prototype).
+    f32x16 acc = zero16();
+    {
+      const float* Xa = Xl + 4 * h * kLdx + j;
+      const float* Pb = Pl + 4 * h * 32 + j;
+#pragma unroll
+      for (int ct = 0; ct < NC; ++ct)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          acc = mfma32(Xa[(ct * 32 + row_of(r)) * kLdx], Pb[(ct * 32 + row_of(r)) * 32], acc);
+    }
+    f32x16 gacc = zero16();
+    if (g_logits) {
+      const float* Wb = Wl + h * 32 + j;
+#pragma unroll
+      for (int s = 0; s < 16; ++s)
+        if (s < KS) gacc = mfma32(gl[s], Wb[2 * s * 32], gacc);
+    }
+
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int nr = acc_row(r, h);
+      const bool rvalid = g0 + nr < npix;
+      const float x2n = __shfl(x2, nr);
+      const float d = l2_distance(x2n, p2, acc[r]);
+      const float a = activation(d, eps, act_kind);
+      float gd = g_logits ? gacc[r] * activation_grad(d, eps, act_kind) : 0.f;
+      if (g_dist) {  // row nr's (image, pixel) comes from the lane that staged it
+        const bool ok = rvalid && pvalid;
+        const int br = __shfl(b, nr), nn = __shfl(n, nr);
+        const float v = g_dist[ok ? (static_cast<unsigned>(br) * P + p) * static_cast<unsigned>(HW) + nn : 0u];
+        gd += ok ? v : 0.f;
+      }
+      const float gs = (d > 0.f && pvalid && rvalid) ? gd : 0.f;
+      gsum += gs;
+      acc[r] = -2.f * gs;
+      gacc[r] = rvalid ? a : 0.f;
+    }
+
+    // g_P^T tile: A = -2 g_s (lane = prototype, k = pixel rows), B = x (lane = channel).
+#pragma unroll
+    for (int ct = 0; ct < NC; ++ct) {
+      const float* Xc = Xl + (ct * 32 + j) * kLdx + 4 * h;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gp[ct] = mfma32(acc[r], Xc[row_of(r)], gp[ct]);
+    }
+    // g_W tile: A = g_logits^T (lane = class), B = act (lane = prototype).
+    if (g_logits) {
+      const int gh = g0 + 4 * h;
+      const float* glh = g_logits + static_cast<unsigned>(gh) * K + j;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const bool ok = gh + row_of(r) < npix && j < K;
+        const float v = glh[ok ? row_of(r) * K : 0];
+        gw = mfma32(ok ? v : 0.f, gacc[r], gw);
+      }
+    }
+  }
+
+  // Workgroup reduction of the per-wave partials through LDS, fixed wave order.
+  __syncthreads();
+  float* R = Xall + wave * C * kLdx;  // >= 32*C + 32 floats per wave
+#pragma unroll
+  for (int ct = 0; ct < NC; ++ct)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) R[acc_row(r, h) * C + ct * 32 + j] = gp[ct][r];
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 32 * C; idx += blockDim.x) {
+    float s = 0.f;
+    for (int w = 0; w < kPwWaves; ++w) s += Xall[w * C * kLdx + idx];
+    const int pr = idx / C, c = idx - pr * C;
+    slab_gp[(static_cast<size_t>(blockIdx.y) * Pp + pt * 32 + pr) * C + c] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) R[acc_row(r, h) * 32 + j] = gw[r];
+  gsum += __shfl_xor(gsum, 32);
+  if (h == 0) R[1024 + j] = gsum;
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 32 * 32 + 32; idx += blockDim.x) {
+    float s = 0.f;
+    for (int w = 0; w < kPwWaves; ++w) s += Xall[w * C * kLdx + idx];
+    if (idx < 1024) {
+      const int k = idx >> 5, pc = idx & 31;
+      slab_gw[(static_cast<size_t>(blockIdx.y) * 32 + k) * Pp + pt * 32 + pc] = s;
+    } else {
+      slab_gs[static_cast<size_t>(blockIdx.y) * Pp + pt * 32 + (idx - 1024)] = s;
+    }
+  }
+}
+
+__global__ void l2_bwd_reduce_kernel(const float* __restrict__ slab_gp, const float* __restrict__ slab_gw,
+                                     const float* __restrict__ slab_gs, int S, int P, int Pp, int C, int K,
+                                     const float* __restrict__ protos, float* __restrict__ g_protos,
+                                     float* __restrict__ g_w) {
+  const long long e = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (g_protos && e < static_cast<long long>(P) * C) {
+    const int p = static_cast<int>(e / C), c = static_cast<int>(e - static_cast<long long>(p) * C);
+    float s = 0.f, gs = 0.f;
+    for (int si = 0; si < S; ++si) {
+      s += slab_gp[(static_cast<size_t>(si) * Pp + p) * C + c];
+      gs += slab_gs[static_cast<size_t>(si) * Pp + p];
+    }
+    // conv weight grad of xp (-2 g_s folded) + pow backward of p2: gs * (2p)
+    g_protos[e] = s + gs * (2.f * protos[e]);
+  }
+  if (g_w && e < static_cast<long long>(K) * P) {
+    const int k = static_cast<int>(e / P), p = static_cast<int>(e - static_cast<long long>(k) * P);
+    float s = 0.f;
+    for (int si = 0; si < S; ++si) s += slab_gw[(static_cast<size_t>(si) * 32 + k) * Pp + p];
+    g_w[e] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Host side.
+
+struct Geometry {
+  int C, P, Pp, K, HW;
+  int npix, ntiles;
+};
+
+int padded_protos(int P) { return static_cast<int>(ceil_div(P, 32) * 32); }
+
+size_t layer_lds_bytes(int C, int Pp) {
+  return (static_cast<size_t>(Pp / 32) * C * kLdt + static_cast<size_t>(Pp) * 32 + Pp) * sizeof(float);
+}
+
+int nc_of(int C) { return C == 32 ? 1 : C == 64 ? 2 : C == 128 ? 4 : 0; }
+
+int validate(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P, int K,
+             int act_kind, Geometry* geo) {
+  if (!x || !protos) return fail(PROTOSEG_ERR_INVALID, "x and protos must be non-null");
+  if (B <= 0 || H <= 0 || W <= 0 || P <= 0 || K < 0)
+    return fail(PROTOSEG_ERR_INVALID, "bad shape B=%d H=%d W=%d P=%d K=%d", B, H, W, P, K);
+  if (x_dtype != PROTOSEG_F32 && x_dtype != PROTOSEG_BF16)
+    return fail(PROTOSEG_ERR_UNSUPPORTED, "x_dtype %d (f32 or bf16 only)", x_dtype);
+  if (act_kind != PROTOSEG_ACT_LOG && act_kind != PROTOSEG_ACT_LINEAR)
+    return fail(PROTOSEG_ERR_UNSUPPORTED, "act_kind %d", act_kind);
+  if (!protoseg_l2_supported(C, P, K))
+    return fail(PROTOSEG_ERR_UNSUPPORTED, "C=%d P=%d K=%d outside the kernel family", C, P, K);
+  geo->C = C;
+  geo->P = P;
+  geo->Pp = padded_protos(P);
+  geo->K = K;
+  geo->HW = H * W;
+  const long long npix = static_cast<long long>(B) * H * W;
+  const long long big = npix * (C > P ? C : P);
+  if (big >= (1LL << 31) - 64)
+    return fail(PROTOSEG_ERR_UNSUPPORTED, "B*H*W*max(C,P)=%lld >= 2^31 elements: split the batch", big);
+  geo->npix = static_cast<int>(npix);
+  geo->ntiles = static_cast<int>(ceil_div(npix, 32));
+  return PROTOSEG_OK;
+}
+
+// Grid for the pixel-major kernels: every resident workgroup slot once, no more than the tiles.
+int layer_grid(const Geometry& geo) {
+  const size_t lds = layer_lds_bytes(geo.C, geo.Pp);
+  const int per_cu = static_cast<int>(kMaxLds / lds) > 0 ? static_cast<int>(kMaxLds / lds) : 1;
+  const long long want = ceil_div(geo.ntiles, kFwdWaves);
+  const long long cap = 256LL * (per_cu < 2 ? per_cu : 2);
+  return static_cast<int>(want < cap ? want : cap);
+}
+
+// Pixel splits of the bwd_pw grid: ~512 workgroups in all.
+int pw_splits(long long ntiles, int Pp) {
+  const long long npt = Pp / 32;
+  long long s = 512 / npt;
+  if (s < 1) s = 1;
+  const long long need = ceil_div(ntiles, kPwWaves);
+  return static_cast<int>(s < need ? s : need);
+}
+
+template <typename TX, int NC>
+int launch_fwd(const Geometry& geo, const void* x, const float* protos, const float* w_last, float eps,
+               int act_kind, float* dist, float* act, float* logits, hipStream_t stream) {
+  auto kernel = l2_fwd_kernel<TX, NC>;
+  if (int st = ensure_lds<l2_fwd_kernel<TX, NC>>()) return st;
+  const size_t lds = layer_lds_bytes(geo.C, geo.Pp);
+  hipLaunchKernelGGL(kernel, dim3(layer_grid(geo)), dim3(kFwdWaves * 64), lds, stream,
+                     static_cast<const TX*>(x), geo.HW, geo.npix, protos, geo.P, geo.Pp, w_last, geo.K, eps,
+                     act_kind, dist, act, logits);
+  return check_launch("l2_fwd_kernel");
+}
+
+template <typename TX, int NC>
+int launch_bwd(const Geometry& geo, const void* x, const float* protos, const float* w_last, float eps,
+               int act_kind, const float* g_logits, const float* g_dist, void* g_x, float* g_protos, float* g_w,
+               float* ws, hipStream_t stream) {
+  if (g_x) {
+    auto kernel = l2_bwd_x_kernel<TX, NC>;
+    if (int st = ensure_lds<l2_bwd_x_kernel<TX, NC>>()) return st;
+    hipLaunchKernelGGL(kernel, dim3(layer_grid(geo)), dim3(kFwdWaves * 64), layer_lds_bytes(geo.C, geo.Pp),
+                       stream, static_cast<const TX*>(x), geo.HW, geo.npix, protos, geo.P, geo.Pp, w_last, geo.K,
+                       eps, act_kind, g_logits, g_dist, static_cast<TX*>(g_x));
+    if (int st = check_launch("l2_bwd_x_kernel")) return st;
+  }
+  if (g_protos || g_w) {
+    const int S = pw_splits(geo.ntiles, geo.Pp);
+    float* slab_gp = ws;
+    float* slab_gw = slab_gp + static_cast<size_t>(S) * geo.Pp * geo.C;
+    float* slab_gs = slab_gw + static_cast<size_t>(S) * 32 * geo.Pp;
+    auto kernel = l2_bwd_pw_kernel<TX, NC>;
+    const size_t lds = (static_cast<size_t>(geo.C) * 32 + 32 * 32 + static_cast<size_t>(kPwWaves) * geo.C * kLdx) *
+                       sizeof(float);
+    if (int st = ensure_lds<l2_bwd_pw_kernel<TX, NC>>()) return st;
+    hipLaunchKernelGGL(kernel, dim3(geo.Pp / 32, S), dim3(kPwWaves * 64), lds, stream,
+                       static_cast<const TX*>(x), geo.HW, geo.npix, protos, geo.P, geo.Pp, w_last, geo.K, eps,
+                       act_kind, g_logits, g_dist, slab_gp, slab_gw, slab_gs);
+    if (int st = check_launch("l2_bwd_pw_kernel")) return st;
+    const long long n = static_cast<long long>(geo.P) * (geo.C > geo.K ? geo.C : geo.K);
+    hipLaunchKernelGGL(l2_bwd_reduce_kernel, dim3(static_cast<unsigned>(ceil_div(n, 256))), dim3(256), 0, stream,
+                       slab_gp, slab_gw, slab_gs, S, geo.P, geo.Pp, geo.C, geo.K, protos, g_protos,
+                       g_logits ? g_w : nullptr);
+    if (int st = check_launch("l2_bwd_reduce_kernel")) return st;
+  }
+  return PROTOSEG_OK;
+}
+
+template <typename Fn>
+int dispatch(int x_dtype, int C, Fn&& fn) {
+  const int nc = nc_of(C);
+  if (x_dtype == PROTOSEG_F32) {
+    if (nc == 1) return fn(static_cast<float*>(nullptr), std::integral_constant<int, 1>());
+    if (nc == 2) return fn(static_cast<float*>(nullptr), std::integral_constant<int, 2>());
+    if (nc == 4) return fn(static_cast<float*>(nullptr), std::integral_constant<int, 4>());
+  } else {
+    if (nc == 1) return fn(static_cast<uint16_t*>(nullptr), std::integral_constant<int, 1>());
+    if (nc == 2) return fn(static_cast<uint16_t*>(nullptr), std::integral_constant<int, 2>());
+    if (nc == 4) return fn(static_cast<uint16_t*>(nullptr), std::integral_constant<int, 4>());
+  }
+  return fail(PROTOSEG_ERR_UNSUPPORTED, "C=%d", C);
+}
+
+}  // namespace
+
+}  // namespace protoseg
+
+using namespace protoseg;
+
+extern "C" int protoseg_l2_supported(int C, int P, int K) {
+  if (nc_of(C) == 0 || P <= 0 || K < 0 || K > 32) return 0;
+  return layer_lds_bytes(C, padded_protos(P)) <= kMaxLds ? 1 : 0;
+}
+
+extern "C" int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P,
+                               const float* w_last, int K, float eps, int act_kind, float* dist_out,
+                               float* act_out, float* logits_out, protoseg_stream_t stream) {
+  Geometry geo;
+  if (int st = validate(x, x_dtype, B, C, H, W, protos, P, K, act_kind, &geo)) return st;
+  if (logits_out && (!w_last || K <= 0)) return fail(PROTOSEG_ERR_INVALID, "logits_out needs w_last and K > 0");
+  if (!dist_out && !act_out && !logits_out) return PROTOSEG_OK;
+  return dispatch(x_dtype, C, [&](auto tx, auto nc) {
+    using TX = std::remove_pointer_t<decltype(tx)>;
+    return launch_fwd<TX, decltype(nc)::value>(geo, x, protos, w_last, eps, act_kind, dist_out, act_out,
+                                               logits_out, reinterpret_cast<hipStream_t>(stream));
+  });
+}
+
+extern "C" size_t protoseg_l2_bwd_workspace_size(int B, int C, int H, int W, int P, int K) {
+  (void)K;
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || P <= 0) return 0;
+  const int Pp = padded_protos(P);
+  const long long ntiles = ceil_div(static_cast<long long>(B) * H * W, 32);
+  const size_t S = static_cast<size_t>(pw_splits(ntiles, Pp));
+  const size_t floats = S * Pp * C + S * 32 * Pp + S * Pp;
+  return ((floats * sizeof(float) + 255) / 256) * 256;
+}
+
+extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P,
+                               const float* w_last, int K, float eps, int act_kind, const float* g_logits,
+                               const float* g_dist, void* g_x, float* g_protos, float* g_w, void* workspace,
+                               size_t workspace_bytes, protoseg_stream_t stream) {
+  Geometry geo;
+  if (int st = validate(x, x_dtype, B, C, H, W, protos, P, K, act_kind, &geo)) return st;
+  if (g_logits && (!w_last || K <= 0)) return fail(PROTOSEG_ERR_INVALID, "g_logits needs w_last and K > 0");
+  if (g_w && !g_logits) return fail(PROTOSEG_ERR_INVALID, "g_w needs g_logits");
+  if (g_protos || g_w) {
+    const size_t need = protoseg_l2_bwd_workspace_size(B, C, H, W, P, K);
+    if (!workspace || workspace_bytes < need)
+      return fail(PROTOSEG_ERR_INVALID, "workspace %zu B < %zu B", workspace_bytes, need);
+  }
+  if (!g_logits && !g_dist) {  // no upstream gradient: every output is zero
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const size_t esz = x_dtype == PROTOSEG_F32 ? 4 : 2;
+    if (g_x && hipMemsetAsync(g_x, 0, geo.npix * C * esz, s) != hipSuccess) return check_launch("memset g_x");
+    if (g_protos && hipMemsetAsync(g_protos, 0, static_cast<size_t>(P) * C * 4, s) != hipSuccess)
+      return check_launch("memset g_protos");
+    return PROTOSEG_OK;
+  }
+  return dispatch(x_dtype, C, [&](auto tx, auto nc) {
+    using TX = std::remove_pointer_t<decltype(tx)>;
+    return launch_bwd<TX, decltype(nc)::value>(geo, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_x,
+                                               g_protos, g_w, static_cast<float*>(workspace),
+                                               reinterpret_cast<hipStream_t>(stream));
+  });
+}

@@ -1,0 +1,36 @@
+// protoseg_host.h — host-side helpers for the C ABI launchers (status, errors, LDS opt-in).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <mutex>
+#include <type_traits>
+
+#include "protoseg_hip.h"
+
+namespace protoseg {
+
+// Records a formatted message in the thread-local error slot and returns `code`.
+int fail(int code, const char* fmt, ...);
+
+// Maps a pending launch error to PROTOSEG_ERR_HIP (with text) or returns PROTOSEG_OK.
+int check_launch(const char* what);
+
+// gfx950 has 160 KiB of LDS per CU; a kernel opts in once to dynamic LDS above 64 KiB.
+constexpr size_t kMaxLds = 160 * 1024;
+
+// One flag per kernel (the template parameter is the kernel itself).
+template <auto kernel>
+int ensure_lds() {
+  static std::once_flag once;
+  static hipError_t status = hipSuccess;
+  std::call_once(once, [] {
+    status = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 static_cast<int>(kMaxLds));
+  });
+  if (status != hipSuccess) return fail(PROTOSEG_ERR_HIP, "hipFuncSetAttribute: %s", hipGetErrorString(status));
+  return PROTOSEG_OK;
+}
+
+inline long long ceil_div(long long a, long long b) { return (a + b - 1) / b; }
+
+}  // namespace protoseg

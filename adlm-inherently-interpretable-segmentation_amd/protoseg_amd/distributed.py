@@ -1,0 +1,131 @@
+"""Data-parallel plumbing: one process per GPU, torch.distributed over RCCL ("nccl" on ROCm).
+
+Two exchange steps exist on the hot path:
+  * training: gradients are summed over ranks once per optimizer step (on the iter_size
+    accumulation boundary of module.py:235-243). ``GradientBuckets`` flattens the
+    parameters into a few large contiguous buckets (xGMI rings are per-link bound, so few
+    big collectives beat many small ones) and all-reduces each bucket asynchronously;
+  * push: images are independent, so each rank scans a contiguous shard and one MIN
+    all-reduce over packed 64-bit keys (distance bits << 32 | image index) reproduces the
+    serial scan's "strictly smaller, earlier image wins" order exactly (push.py:101, 265);
+    the owner of each winning key then contributes the feature vector / patch index.
+The reference itself has no collectives (every config sets Trainer.gpus = 1).
+"""
+from __future__ import annotations
+
+import os
+from typing import Iterable, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+INT32_MAX = 2 ** 31 - 1
+
+
+def world_info(group=None) -> Tuple[int, int]:
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(group), dist.get_world_size(group)
+    return 0, 1
+
+
+def shard_bounds(n: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous [lo, hi) shard of n items; shard sizes differ by at most one."""
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def init_from_env(backend: Optional[str] = None) -> Tuple[int, int, int]:
+    """Initialises the default process group from torchrun's env (RANK/WORLD_SIZE/...).
+    Returns (rank, local_rank, world_size); a no-op single process without those vars."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend=backend)
+    return rank, local_rank, world
+
+
+def reduce_push_state(state, group=None) -> None:
+    """Merges per-rank push minima into the global one, identically on every rank."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return
+    bits = state.dist.contiguous().view(torch.int32).to(torch.int64)  # d >= 0 (relu) or +inf
+    img = torch.where(state.img >= 0, state.img, torch.full_like(state.img, INT32_MAX))
+    key = (bits << 32) | img
+    gkey = key.clone()
+    dist.all_reduce(gkey, op=dist.ReduceOp.MIN, group=group)
+    mine = (key == gkey) & (state.img >= 0)
+    fmap = torch.where(mine[:, None], state.fmap, torch.zeros_like(state.fmap))
+    patch = torch.where(mine, state.patch.to(torch.int64) + 1, torch.zeros_like(img))
+    dist.all_reduce(fmap, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(patch, op=dist.ReduceOp.SUM, group=group)
+    gimg = gkey & 0xFFFFFFFF
+    state.dist.copy_((gkey >> 32).to(torch.int32).view(torch.float32))
+    state.img.copy_(torch.where(gimg == INT32_MAX, torch.full_like(gimg, -1), gimg))
+    state.patch.copy_((patch - 1).to(torch.int32))
+    state.fmap.copy_(fmap)
+    gathered: List[dict] = [None] * dist.get_world_size(group)  # type: ignore[list-item]
+    dist.all_gather_object(gathered, state.geometry, group=group)
+    for g in gathered:
+        state.geometry.update(g)
+
+
+class GradientBuckets:
+    """Sums .grad of ``params`` over ranks with a few large asynchronous all-reduces.
+
+    Buckets are filled in reverse registration order (the order backward produces grads),
+    each up to ``bucket_mb`` MiB; ``allreduce()`` launches them all and ``wait()`` averages.
+    Used for the prototype-layer gradients in bench.py and for full models in train.py.
+    """
+
+    def __init__(self, params: Iterable[torch.nn.Parameter], bucket_mb: float = 64.0, group=None,
+                 average: bool = True):
+        self.params = [p for p in params if p.requires_grad]
+        self.group = group
+        self.average = average
+        limit = int(bucket_mb * 2 ** 20)
+        self.buckets: List[List[torch.nn.Parameter]] = []
+        cur, size = [], 0
+        for p in reversed(self.params):
+            nbytes = p.numel() * p.element_size()
+            if cur and size + nbytes > limit:
+                self.buckets.append(cur)
+                cur, size = [], 0
+            cur.append(p)
+            size += nbytes
+        if cur:
+            self.buckets.append(cur)
+        self._pending = []
+
+    def allreduce(self) -> None:
+        rank, world = world_info(self.group)
+        if world == 1:
+            return
+        self._pending = []
+        for bucket in self.buckets:
+            grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in bucket]
+            flat = torch.cat([g.reshape(-1) for g in grads])
+            work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            self._pending.append((bucket, flat, work))
+
+    def wait(self) -> None:
+        _, world = world_info(self.group)
+        for bucket, flat, work in self._pending:
+            work.wait()
+            if self.average:
+                flat.div_(world)
+            off = 0
+            for p in bucket:
+                n = p.numel()
+                g = flat[off:off + n].view_as(p)
+                if p.grad is None:
+                    p.grad = g.clone()
+                else:
+                    p.grad.copy_(g)
+                off += n
+        self._pending = []

@@ -1,0 +1,152 @@
+"""torch.library custom ops over the C ABI: the prototype layer forward and its backward.
+
+``prototype_layer(x, protos, w_last, ...)`` is the autograd-aware entry used by ``PPNet``:
+one fused HIP kernel produces distances (NCHW), logits (NHWC) and optionally activations;
+the backward recomputes distances from ``x`` and calls the two backward kernels.
+
+Reference: model.py:203-221 (_l2_convolution), 231-237 (distance_2_similarity),
+259-283 (forward_from_conv_features, patch_classification branch); the backward is the
+autograd graph of those ops (the reference has no custom backward).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from . import _lib
+
+ACT_KINDS = {"log": _lib.ACT_LOG, "linear": _lib.ACT_LINEAR}
+
+
+def _x_dtype(x: Tensor) -> int:
+    if x.dtype == torch.float32:
+        return _lib.F32
+    if x.dtype == torch.bfloat16:
+        return _lib.BF16
+    raise _lib.ProtosegError(f"feature map dtype {x.dtype} unsupported (float32 or bfloat16)")
+
+
+def supported(C: int, P: int, K: int) -> bool:
+    return bool(_lib.load().protoseg_l2_supported(C, P, K))
+
+
+@torch.library.custom_op("protoseg::l2_forward", mutates_args=(), device_types="cuda")
+def l2_forward(x: Tensor, protos: Tensor, w_last: Tensor, eps: float, act_kind: int, with_dist: bool,
+               with_logits: bool, with_act: bool) -> Tuple[Tensor, Tensor, Tensor]:
+    """Fused prototype-layer forward. Returns (dist [B,P,H,W], logits [B,H,W,K], act [B*H*W,P]);
+    outputs not requested are empty tensors."""
+    dev = _lib.require_device(x, protos, w_last)
+    x = x.contiguous()
+    protos = protos.contiguous()
+    w_last = w_last.contiguous()
+    B, C, H, W = x.shape
+    P, K = protos.shape[0], w_last.shape[0]
+    f32 = dict(device=dev, dtype=torch.float32)
+    dist = torch.empty((B, P, H, W) if with_dist else (0,), **f32)
+    logits = torch.empty((B, H, W, K) if with_logits else (0,), **f32)
+    act = torch.empty((B * H * W, P) if with_act else (0,), **f32)
+    with torch.cuda.device(dev):
+        _lib.call("protoseg_l2_fwd", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P,
+                  _lib.ptr(w_last), K, float(eps), int(act_kind), _lib.ptr(dist), _lib.ptr(act),
+                  _lib.ptr(logits), _lib.stream_of(dev))
+    return dist, logits, act
+
+
+@l2_forward.register_fake
+def _(x, protos, w_last, eps, act_kind, with_dist, with_logits, with_act):
+    B, C, H, W = x.shape
+    P, K = protos.shape[0], w_last.shape[0]
+    e = lambda *s: x.new_empty(s, dtype=torch.float32)  # noqa: E731
+    return (e(B, P, H, W) if with_dist else e(0), e(B, H, W, K) if with_logits else e(0),
+            e(B * H * W, P) if with_act else e(0))
+
+
+@torch.library.custom_op("protoseg::l2_backward", mutates_args=(), device_types="cuda")
+def l2_backward(x: Tensor, protos: Tensor, w_last: Tensor, g_logits: Optional[Tensor], g_dist: Optional[Tensor],
+                eps: float, act_kind: int, need_x: bool, need_protos: bool,
+                need_w: bool) -> Tuple[Tensor, Tensor, Tensor]:
+    """Backward of l2_forward with respect to (x, protos, w_last); unrequested grads are empty."""
+    dev = _lib.require_device(x, protos, w_last, g_logits, g_dist)
+    x = x.contiguous()
+    protos = protos.contiguous()
+    w_last = w_last.contiguous()
+    g_logits = g_logits.contiguous().float() if g_logits is not None else None
+    g_dist = g_dist.contiguous().float() if g_dist is not None else None
+    B, C, H, W = x.shape
+    P, K = protos.shape[0], w_last.shape[0]
+    need_w = need_w and g_logits is not None
+    g_x = torch.empty_like(x) if need_x else x.new_empty(0)
+    g_p = torch.empty((P, C), device=dev, dtype=torch.float32) if need_protos else x.new_empty(0, dtype=torch.float32)
+    g_w = torch.empty((K, P), device=dev, dtype=torch.float32) if need_w else x.new_empty(0, dtype=torch.float32)
+    if need_w is False and g_logits is None and need_protos is False and need_x is False:
+        return g_x, g_p, g_w
+    lib = _lib.load()
+    ws_bytes = lib.protoseg_l2_bwd_workspace_size(B, C, H, W, P, K) if (need_protos or need_w) else 0
+    ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8) if ws_bytes else None
+    with torch.cuda.device(dev):
+        _lib.call("protoseg_l2_bwd", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P, _lib.ptr(w_last), K,
+                  float(eps), int(act_kind), _lib.ptr(g_logits), _lib.ptr(g_dist), _lib.ptr(g_x), _lib.ptr(g_p),
+                  _lib.ptr(g_w), _lib.ptr(ws), ws_bytes, _lib.stream_of(dev))
+    return g_x, g_p, g_w
+
+
+@l2_backward.register_fake
+def _(x, protos, w_last, g_logits, g_dist, eps, act_kind, need_x, need_protos, need_w):
+    B, C, H, W = x.shape
+    P, K = protos.shape[0], w_last.shape[0]
+    need_w = need_w and g_logits is not None
+    return (torch.empty_like(x) if need_x else x.new_empty(0),
+            x.new_empty((P, C), dtype=torch.float32) if need_protos else x.new_empty(0, dtype=torch.float32),
+            x.new_empty((K, P), dtype=torch.float32) if need_w else x.new_empty(0, dtype=torch.float32))
+
+
+def _setup_context(ctx, inputs, output):
+    x, protos, w_last, eps, act_kind, with_dist, with_logits, with_act = inputs
+    ctx.save_for_backward(x, protos, w_last)
+    ctx.eps = eps
+    ctx.act_kind = act_kind
+    ctx.set_materialize_grads(False)  # unused outputs give None, not a zero-filled [B,P,H,W]
+
+
+def _backward(ctx, g_dist, g_logits, g_act):
+    if g_act is not None:
+        raise NotImplementedError("gradient through return_activations=True outputs is not implemented")
+    x, protos, w_last = ctx.saved_tensors
+    need_x, need_p, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+    if g_dist is None and g_logits is None:
+        return None, None, None, None, None, None, None, None
+    g_x, g_p, g_w = l2_backward(x, protos, w_last, g_logits, g_dist, ctx.eps, ctx.act_kind, need_x, need_p,
+                                need_w and g_logits is not None)
+    return (g_x if need_x else None, g_p if need_p else None, g_w if (need_w and g_w.numel()) else None,
+            None, None, None, None, None)
+
+
+torch.library.register_autograd("protoseg::l2_forward", _backward, setup_context=_setup_context)
+
+
+def prototype_layer(x: Tensor, prototype_vectors: Tensor, last_layer_weight: Tensor, eps: float = 1e-4,
+                    activation: str = "log", with_dist: bool = True, with_logits: bool = True,
+                    with_act: bool = False) -> Tuple[Tensor, Tensor, Tensor]:
+    """Distances, logits and activations of the PPNet prototype layer (1x1 prototypes).
+
+    x: [B, C, H, W] add-on-layer output (float32 or bfloat16); prototype_vectors: [P, C, 1, 1]
+    or [P, C]; last_layer_weight: [K, P]. Returns (distances [B,P,H,W], logits [B,H,W,K],
+    activations [B*H*W, P]) with unrequested outputs empty.
+    """
+    if activation not in ACT_KINDS:
+        raise _lib.ProtosegError(f"activation {activation!r} has no HIP kernel ('log' or 'linear')")
+    protos = prototype_vectors.reshape(prototype_vectors.shape[0], -1)
+    if protos.shape[1] != x.shape[1]:
+        raise _lib.ProtosegError(f"prototype depth {protos.shape[1]} != feature channels {x.shape[1]}")
+    if tuple(prototype_vectors.shape[2:]) not in ((), (1, 1)):
+        raise _lib.ProtosegError(f"only 1x1 prototypes are supported, got {tuple(prototype_vectors.shape)}")
+    return torch.ops.protoseg.l2_forward(x, protos, last_layer_weight, float(eps), ACT_KINDS[activation],
+                                         with_dist, with_logits, with_act)
+
+
+def l2_distances(x: Tensor, prototype_vectors: Tensor, eps: float = 1e-4) -> Tensor:
+    """model.py:203-221 _l2_convolution: squared L2 distance map [B, P, H, W]."""
+    w_dummy = x.new_zeros((1, prototype_vectors.shape[0]), dtype=torch.float32)
+    return prototype_layer(x, prototype_vectors, w_dummy, eps, "log", True, False, False)[0]

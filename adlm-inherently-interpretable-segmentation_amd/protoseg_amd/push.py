@@ -1,0 +1,271 @@
+"""Prototype push (nearest-patch projection) on the HIP kernels.
+
+Mirrors reference segmentation/push.py:24-158 (``push_prototypes``) and the argmin core of
+162-280 (``update_prototypes_on_image``). The reference copies every image's distance map to
+the host and runs a 2M-iteration Python loop per image plus a per-prototype gather and
+np.argmin; here the label->patch mask, the fused distance + masked argmin and the strict-'<'
+merge all run on the device, and the host only touches P-sized results at the end.
+
+Semantics kept from the reference:
+  * patch of pixel (i, j) = (int(i / (H / h)), int(j / (W / w))) in float64 (push.py:201-223);
+  * class c > 0 marks class index c-1 (push.py:222-223); prototypes of a class absent from
+    the image are skipped (push.py:255-256);
+  * a prototype moves only on a strictly smaller distance; images are visited in
+    ``dataset.img_ids`` order, so an earlier image wins a tie (push.py:101, 265);
+  * receptive-field boxes push.py:288-307, dedup push.py:147-155, prune model.py:311-336.
+Ties between patches of ONE image resolve to the lowest patch index; the reference's order
+there is the iteration order of a Python set (push.py:214, 230). See DESIGN.md.
+
+Out of scope (host-side visualisation, needs cv2/matplotlib): the PNG outputs and the
+high-activation bound boxes of push.py:309-481 (``proto_bound_boxes`` stay -1).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+import numpy as np
+import torch
+from torch import Tensor
+
+from . import _lib
+
+# segmentation/constants.py:6-7 (ImageNet statistics used by to_normalized_tensor)
+CITYSCAPES_MEAN = (0.485, 0.456, 0.406)
+CITYSCAPES_STD = (0.229, 0.224, 0.225)
+
+
+def _label_dtype(t: Tensor) -> int:
+    return {torch.int64: _lib.I64, torch.int32: _lib.I32, torch.uint8: _lib.U8}.get(t.dtype, -1)
+
+
+def patch_class_mask(labels: Tensor, h: int, w: int, lut: Optional[Tensor] = None) -> Tensor:
+    """labels [n, H, W] (int64 / int32 / uint8, device) -> int32 [n, h*w] holding the uint32
+    class bitmask of each patch (bit k <=> a pixel of class k+1). ``lut`` [L] int32 maps raw
+    label ids first (CITYSCAPES_19_EVAL_CATEGORIES / PASCAL_ID_MAPPING as a table)."""
+    dev = _lib.require_device(labels, lut)
+    if labels.dim() == 2:
+        labels = labels.unsqueeze(0)
+    labels = labels.contiguous()
+    dt = _label_dtype(labels)
+    if dt < 0:
+        raise _lib.ProtosegError(f"label dtype {labels.dtype} unsupported (int64, int32, uint8)")
+    n, H, W = labels.shape
+    mask = torch.empty((n, h * w), device=dev, dtype=torch.int32)
+    lut_c = lut.to(torch.int32).contiguous() if lut is not None else None
+    with torch.cuda.device(dev):
+        _lib.call("protoseg_patch_class_mask", _lib.ptr(labels), dt, n, H, W, h, w, _lib.ptr(lut_c),
+                  0 if lut_c is None else lut_c.numel(), _lib.ptr(mask), _lib.stream_of(dev))
+    return mask
+
+
+def push_argmin(x: Tensor, protos: Tensor, proto_class: Tensor, mask: Tensor) -> Tensor:
+    """Per image and prototype, the masked minimum key (float_bits(d) << 32 | patch) as int64
+    storage of uint64 [n, P]; -1 (all ones) when the image has no patch of the class."""
+    dev = _lib.require_device(x, protos, proto_class, mask)
+    x = x.float().contiguous()
+    protos = protos.reshape(protos.shape[0], -1).float().contiguous()
+    n, C, h, w = x.shape
+    P = protos.shape[0]
+    keys = torch.empty((n, P), device=dev, dtype=torch.int64)
+    with torch.cuda.device(dev):
+        _lib.call("protoseg_push_argmin", _lib.ptr(x), n, C, h, w, _lib.ptr(protos), P,
+                  _lib.ptr(proto_class.to(torch.int32).contiguous()), _lib.ptr(mask.contiguous()), _lib.ptr(keys),
+                  _lib.stream_of(dev))
+    return keys
+
+
+def decode_keys(keys: Tensor):
+    """int64-stored uint64 keys -> (dist float32, patch int64, found bool)."""
+    k = keys.to(torch.int64)
+    found = k != -1
+    hi = ((k >> 32) & 0xFFFFFFFF).to(torch.int32)
+    dist = hi.view(torch.float32) if hi.is_contiguous() else hi.contiguous().view(torch.float32)
+    return dist, (k & 0xFFFFFFFF), found
+
+
+@dataclass
+class PushState:
+    """Running global minimum (push.py:55-61): distance, image index, patch index, feature vector."""
+    dist: Tensor
+    img: Tensor
+    patch: Tensor
+    fmap: Tensor
+    # per image index: (H_img, W_img, h, w) needed for the receptive-field boxes
+    geometry: Dict[int, tuple] = field(default_factory=dict)
+
+    @classmethod
+    def create(cls, P: int, C: int, device) -> "PushState":
+        return cls(dist=torch.full((P,), math.inf, device=device, dtype=torch.float32),
+                   img=torch.full((P,), -1, device=device, dtype=torch.int64),
+                   patch=torch.full((P,), -1, device=device, dtype=torch.int32),
+                   fmap=torch.zeros((P, C), device=device, dtype=torch.float32))
+
+
+def push_update(state: PushState, x: Tensor, labels: Tensor, protos: Tensor, proto_class: Tensor, first_img: int,
+                lut: Optional[Tensor] = None) -> None:
+    """One batch of images (dataset indices first_img ..): mask -> argmin -> strict-'<' merge."""
+    x = x.float().contiguous()
+    n, C, h, w = x.shape
+    if labels.dim() == 2:
+        labels = labels.unsqueeze(0)
+    mask = patch_class_mask(labels, h, w, lut)
+    keys = push_argmin(x, protos, proto_class, mask)
+    dev = x.device
+    P = keys.shape[1]
+    with torch.cuda.device(dev):
+        _lib.call("protoseg_push_merge", _lib.ptr(keys), n, int(first_img), _lib.ptr(x), C, h * w, P,
+                  _lib.ptr(state.dist), _lib.ptr(state.img), _lib.ptr(state.patch), _lib.ptr(state.fmap),
+                  _lib.stream_of(dev))
+    H, W = labels.shape[-2:]
+    for i in range(n):
+        state.geometry[first_img + i] = (int(H), int(W), int(h), int(w))
+
+
+def prototype_classes(ppnet) -> Tensor:
+    """push.py:251: target_class = argmax(prototype_class_identity[j])."""
+    return torch.argmax(ppnet.prototype_class_identity, dim=1).to(torch.int32)
+
+
+def rf_boxes(state: PushState, proto_class: np.ndarray, with_class: bool = True) -> np.ndarray:
+    """push.py:288-307: [img, h_start, h_end, w_start, w_end(, class)] in float64 arithmetic."""
+    img = state.img.cpu().numpy()
+    patch = state.patch.cpu().numpy()
+    P = img.shape[0]
+    boxes = np.full((P, 6 if with_class else 5), -1, dtype=np.int64)
+    for j in range(P):
+        if img[j] < 0:
+            continue
+        H, W, h, w = state.geometry[int(img[j])]
+        patch_height, patch_width = H / h, W / w
+        patch_i, patch_j = divmod(int(patch[j]), w)
+        boxes[j, 0] = img[j]
+        boxes[j, 1] = int(patch_i * patch_height)
+        boxes[j, 2] = int(patch_i * patch_height + patch_height) + 1
+        boxes[j, 3] = int(patch_j * patch_width)
+        boxes[j, 4] = int(patch_j * patch_width + patch_width) + 1
+        if with_class:
+            boxes[j, 5] = proto_class[j]
+    return boxes
+
+
+def lut_from_convert_targets(convert_targets) -> Optional[np.ndarray]:
+    """Turns the reference's ``np.vectorize(MAPPING.get)`` (dataset.py:63-69) into a table."""
+    fn = getattr(convert_targets, "pyfunc", convert_targets)
+    mapping = getattr(fn, "__self__", None)
+    if not isinstance(mapping, dict) or not mapping:
+        return None
+    keys = [k for k in mapping if isinstance(k, (int, np.integer))]
+    if len(keys) != len(mapping) or min(keys) < 0:
+        return None
+    lut = np.full(max(keys) + 1, -1, dtype=np.int32)
+    for k, v in mapping.items():
+        lut[k] = v
+    return lut
+
+
+def to_normalized_tensor(img, mean=CITYSCAPES_MEAN, std=CITYSCAPES_STD) -> Tensor:
+    """find_nearest.py:21-24: ToTensor (uint8 HWC -> float CHW / 255) then Normalize."""
+    arr = np.asarray(img, dtype=np.uint8)
+    t = torch.from_numpy(arr.copy()).permute(2, 0, 1).float().div(255.0)
+    m = torch.tensor(mean, dtype=torch.float32).view(-1, 1, 1)
+    s = torch.tensor(std, dtype=torch.float32).view(-1, 1, 1)
+    return (t - m) / s
+
+
+def dedup_and_prune(ppnet, fmap: np.ndarray, root_dir: Optional[str], log: Callable = print) -> List[int]:
+    """push.py:143-155: write prototypes, np.unique(axis=0) dedup, prune, unique_prototypes.json."""
+    shape = tuple(ppnet.prototype_shape)
+    update = np.reshape(fmap.astype(np.float64), shape)
+    ppnet.prototype_vectors.data.copy_(torch.tensor(update, dtype=torch.float32).to(ppnet.prototype_vectors.device))
+    _, unique_index = np.unique(update, axis=0, return_index=True)
+    unique_set = set(int(i) for i in unique_index)
+    duplicate_idx = [i for i in range(ppnet.num_prototypes) if i not in unique_set]
+    log(f"Removing {len(duplicate_idx)} duplicate prototypes.")
+    ppnet.prune_prototypes(duplicate_idx)
+    if root_dir is not None:
+        os.makedirs(root_dir, exist_ok=True)
+        with open(os.path.join(root_dir, "unique_prototypes.json"), "w") as fp:
+            json.dump([int(i) for i in sorted(unique_index)], fp)
+    return duplicate_idx
+
+
+def push_prototypes(dataset, prototype_network_parallel, prototype_layer_stride=1,
+                    root_dir_for_saving_prototypes=None, epoch_number=None, prototype_img_filename_prefix=None,
+                    prototype_self_act_filename_prefix=None, proto_bound_boxes_filename_prefix=None,
+                    save_prototype_class_identity=True, log=print, pascal=False,
+                    prototype_activation_function_in_numpy=None, images_per_batch: int = 1,
+                    process_group=None):
+    """Drop-in for segmentation/push.py:24-158 (same arguments and side effects, minus the
+    visualisation PNGs). With torch.distributed initialised (or ``process_group`` given) and
+    world size > 1, every rank scans a contiguous shard of ``dataset.img_ids`` and the shards
+    are merged exactly (distributed.reduce_push_state): the result equals the serial scan."""
+    from PIL import Image
+
+    from .distributed import reduce_push_state, shard_bounds, world_info
+
+    ppnet = prototype_network_parallel.module if hasattr(prototype_network_parallel, "module") \
+        else prototype_network_parallel
+    ppnet.eval()
+    log("\tpush")
+    start = time.time()
+    device = ppnet.prototype_vectors.device
+    P, C = ppnet.num_prototypes, ppnet.prototype_shape[1]
+    proto_class_t = prototype_classes(ppnet).to(device)
+    proto_class = proto_class_t.cpu().numpy()
+    state = PushState.create(P, C, device)
+
+    proto_epoch_dir = None
+    if root_dir_for_saving_prototypes is not None:
+        proto_epoch_dir = (os.path.join(root_dir_for_saving_prototypes, f"epoch-{epoch_number}")
+                           if epoch_number is not None else root_dir_for_saving_prototypes)
+        os.makedirs(proto_epoch_dir, exist_ok=True)
+    if prototype_img_filename_prefix is not None or prototype_self_act_filename_prefix is not None:
+        log("\tprototype visualisation PNGs are not produced by this build (host-side, out of scope)")
+
+    convert = getattr(dataset, "convert_targets", None)
+    lut_np = lut_from_convert_targets(convert) if convert is not None else None
+    lut = torch.from_numpy(lut_np).to(device) if lut_np is not None else None
+    mean = getattr(dataset, "mean", CITYSCAPES_MEAN)
+    std = getattr(dataset, "std", CITYSCAPES_STD)
+    rank, world = world_info(process_group)
+    lo, hi = shard_bounds(len(dataset.img_ids), rank, world)
+
+    log("Updating prototypes...")
+    with torch.no_grad():
+        for push_iter in range(lo, hi):
+            img_id = dataset.img_ids[push_iter]
+            with open(dataset.get_img_path(img_id), "rb") as f:
+                img = Image.open(f).convert("RGB")
+            margin = dataset.image_margin_size
+            img = img.crop((margin, margin, img.width - margin, img.height - margin))
+            gt_ann = np.load(os.path.join(dataset.annotations_dir, img_id + ".npy"))
+            if convert is not None and lut is None:
+                gt_ann = convert(gt_ann)
+            labels = torch.as_tensor(np.ascontiguousarray(gt_ann)).to(device)
+            if labels.dtype not in (torch.int64, torch.int32, torch.uint8):
+                labels = labels.to(torch.int64)
+            img_tensor = to_normalized_tensor(img, mean, std).unsqueeze(0).to(device)
+            conv_features = ppnet.conv_features(img_tensor)
+            push_update(state, conv_features, labels, ppnet.prototype_vectors, proto_class_t, push_iter, lut)
+
+    if world > 1:
+        reduce_push_state(state, process_group)
+
+    with_class = bool(save_prototype_class_identity)
+    proto_rf_boxes = rf_boxes(state, proto_class, with_class)
+    proto_bound_boxes = np.full_like(proto_rf_boxes, -1)
+    if proto_epoch_dir is not None and proto_bound_boxes_filename_prefix is not None:
+        np.save(os.path.join(proto_epoch_dir, f"{proto_bound_boxes_filename_prefix}-receptive_field{epoch_number}.npy"),
+                proto_rf_boxes)
+        np.save(os.path.join(proto_epoch_dir, f"{proto_bound_boxes_filename_prefix}{epoch_number}.npy"),
+                proto_bound_boxes)
+
+    log("\tExecuting push ...")
+    dedup_and_prune(ppnet, state.fmap.cpu().numpy(), root_dir_for_saving_prototypes, log)
+    log(f"\tpush time: \t{time.time() - start}")
+    return state

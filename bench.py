@@ -1,0 +1,355 @@
+#!/usr/bin/env python3
+"""bench.py — ProtoSeg hot path on MI355X: prototype-layer training step + prototype push.
+
+Workload (BASELINE.json configs[1], cityscapes_no_kld_imnet): 513x513 crops -> 65x65 feature
+maps, C=64, P=190 (19 classes x 10), K=19. One "step" = the prototype layer's forward
+(distances + logits, one fused kernel) and backward (g_x, g_prototypes, g_last_layer) over a
+batch of B images per GPU, plus the data-parallel gradient all-reduce (RCCL) when N>1.
+Synthetic data (seed 20220227): X = sigmoid(N(0, 2^2)), prototypes U[0,1),
+last layer from the class identity; inputs resident in HBM before timing starts.
+
+Also measured (second BASELINE metric, "push argmin ms/img"): the push of full-resolution
+images (1024x2048 labels, 129x257 maps, P=190) through mask -> fused argmin -> merge.
+
+Prints ONE JSON line (rank 0). Run: python bench.py [--gpus N --steps K --warmup W], or under
+torch.distributed.run for N>1 (one process per GPU, RCCL).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "adlm-inherently-interpretable-segmentation_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from protoseg_amd import _lib  # noqa: E402
+from protoseg_amd.distributed import init_from_env  # noqa: E402
+
+PEAK_HBM_GBPS = 8000.0       # MI355X_MICROARCH.md chip table (spec)
+PEAK_F32_MFMA_TFLOPS = 157.3  # dense f32-input MFMA (v_mfma_f32_32x32x2_f32), MI355X_MICROARCH.md
+SEED = 20220227
+
+
+def baseline_metric() -> str:
+    try:
+        with open(os.path.join(ROOT, "BASELINE.json")) as f:
+            return json.load(f)["metric"]
+    except (OSError, KeyError, ValueError):
+        return "training img/s (513x513, 19 prototypes/class) at 1/2/4/8 MI355X; push argmin ms/img"
+
+
+class LayerStep:
+    """Preallocated buffers + direct C-ABI launches (no per-step allocation)."""
+
+    def __init__(self, B, C, h, w, P, K, x_dtype, device, seed):
+        gen = torch.Generator(device="cpu").manual_seed(seed)
+        self.B, self.C, self.h, self.w, self.P, self.K = B, C, h, w, P, K
+        x = torch.sigmoid(2.0 * torch.randn(B, C, h, w, generator=gen))
+        self.x = x.to(device=device, dtype=x_dtype).contiguous()
+        self.protos = torch.rand(P, C, generator=gen).to(device)
+        ident = torch.zeros(P, K)
+        per = P // K
+        for i in range(K):
+            ident[i * per:(i + 1) * per, i] = 1
+        self.w_last = (ident.t() * 1.5 - 0.5).contiguous().to(device)  # 1 own class, -0.5 else
+        self.g_logits = (torch.randn(B, h, w, K, generator=gen) / (B * h * w)).to(device)
+        f32 = dict(device=device, dtype=torch.float32)
+        self.dist = torch.empty(B, P, h, w, **f32)
+        self.logits = torch.empty(B, h, w, K, **f32)
+        self.g_x = torch.empty_like(self.x)
+        self.g_p = torch.empty(P, C, **f32)
+        self.g_w = torch.empty(K, P, **f32)
+        lib = _lib.load()
+        self.ws_bytes = lib.protoseg_l2_bwd_workspace_size(B, C, h, w, P, K)
+        self.ws = torch.empty(self.ws_bytes, device=device, dtype=torch.uint8)
+        self.xdt = _lib.F32 if x_dtype == torch.float32 else _lib.BF16
+        self.device = device
+        self.grad_flat = torch.empty(P * C + K * P, **f32)
+
+    def _stream(self):
+        return _lib.stream_of(self.device)
+
+    def fwd(self):
+        _lib.call("protoseg_l2_fwd", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w, _lib.ptr(self.protos),
+                  self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, _lib.ptr(self.dist), ctypes.c_void_p(None),
+                  _lib.ptr(self.logits), self._stream())
+
+    def bwd_x(self):
+        _lib.call("protoseg_l2_bwd", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w, _lib.ptr(self.protos),
+                  self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, _lib.ptr(self.g_logits),
+                  ctypes.c_void_p(None), _lib.ptr(self.g_x), ctypes.c_void_p(None), ctypes.c_void_p(None),
+                  ctypes.c_void_p(None), 0, self._stream())
+
+    def bwd_pw(self):
+        _lib.call("protoseg_l2_bwd", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w, _lib.ptr(self.protos),
+                  self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, _lib.ptr(self.g_logits),
+                  ctypes.c_void_p(None), ctypes.c_void_p(None), _lib.ptr(self.g_p), _lib.ptr(self.g_w),
+                  _lib.ptr(self.ws), self.ws_bytes, self._stream())
+
+    def allreduce(self, world):
+        if world > 1:
+            self.grad_flat[: self.P * self.C].copy_(self.g_p.view(-1))
+            self.grad_flat[self.P * self.C:].copy_(self.g_w.view(-1))
+            dist.all_reduce(self.grad_flat)
+
+    # algorithmic work per launch (unpadded P, K)
+    def work(self):
+        n = self.B * self.h * self.w
+        xb = self.x.element_size()
+        mm = 2.0 * n * self.P * self.C
+        last = 2.0 * n * self.P * self.K
+        return {
+            "l2_fwd_kernel": (mm + last + 2.0 * n * self.C, n * self.C * xb + n * self.P * 4 + n * self.K * 4),
+            "l2_bwd_x_kernel": (2 * mm + last, n * self.C * xb + n * self.K * 4 + n * self.C * xb),
+            "l2_bwd_pw_kernel": (2 * mm + 2 * last, n * self.C * xb + n * self.K * 4),
+        }
+
+
+def roofline_entry(flops, nbytes, seconds):
+    t_mfma = flops / (PEAK_F32_MFMA_TFLOPS * 1e12)
+    t_hbm = nbytes / (PEAK_HBM_GBPS * 1e9)
+    if t_mfma >= t_hbm:
+        ach = flops / seconds / 1e12
+        return {"bound": "mfma", "achieved": round(ach, 3), "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / PEAK_F32_MFMA_TFLOPS, 4)}
+    ach = nbytes / seconds / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+            "frac": round(ach / PEAK_HBM_GBPS, 4)}
+
+
+def pmc_traffic(kernel: str, config_key: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary, if one
+    was collected for this exact configuration (profiles/pmc_traffic.json), else None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            data = json.load(f)
+        return data[config_key][kernel]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def time_layer(step: LayerStep, steps: int, warmup: int, world: int):
+    for _ in range(warmup):
+        step.fwd()
+        step.bwd_x()
+        step.bwd_pw()
+        step.allreduce(world)
+    torch.cuda.synchronize()
+    names = ["l2_fwd_kernel", "l2_bwd_x_kernel", "l2_bwd_pw_kernel"]
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        e = ev[s]
+        e[0].record()
+        step.fwd()
+        e[1].record()
+        step.bwd_x()
+        e[2].record()
+        step.bwd_pw()
+        e[3].record()
+        step.allreduce(world)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    per_kernel = {n: [] for n in names}
+    for e in ev:
+        for i, n in enumerate(names):
+            per_kernel[n].append(e[i].elapsed_time(e[i + 1]) * 1e-3)
+    return elapsed, {n: float(np.mean(v)) for n, v in per_kernel.items()}
+
+
+def cpu_layer_baseline(C, h, w, P, K, budget_s):
+    """Oracle (op-for-op torch-CPU restatement of model.py) fwd+bwd per image, host threads."""
+    from oracle import protoseg_oracle as po
+    threads = max(1, min(16, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    x, protos, w_last = po.synthetic_inputs(1, C, h, w, P, K, SEED)
+    g = torch.randn(1, h, w, K)
+    po.forward_backward(x, protos, w_last, g, None)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        po.forward_backward(x, protos, w_last, g, None)
+        n += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 3), "unit": "img/s", "cores": threads, "kind": "port",
+            "sample": f"{n} images of the oracle fwd+bwd (torch-CPU restatement of model.py:203-283 + autograd), "
+                      f"1x{C}x{h}x{w}, P={P}, K={K}, {dt:.1f} s"}
+
+
+def make_push_inputs(n_img, C, H, W, h, w, P, K, device, seed):
+    gen = torch.Generator().manual_seed(seed)
+    x = torch.sigmoid(2.0 * torch.randn(n_img, C, h, w, generator=gen)).to(device)
+    protos = torch.rand(P, C, generator=gen).to(device)
+    rng = np.random.default_rng(seed)
+    blocks = rng.integers(0, K + 1, size=(n_img, H // 16, W // 16)).astype(np.uint8)
+    labels = torch.from_numpy(np.repeat(np.repeat(blocks, 16, 1), 16, 2)).to(device)
+    pc = (torch.arange(P) // (P // K)).to(torch.int32).to(device)
+    return x, protos, labels, pc
+
+
+def time_push(n_img, steps, warmup, device, C=64, H=1024, W=2048, h=129, w=257, P=190, K=19):
+    from protoseg_amd import push as dpush
+    x, protos, labels, pc = make_push_inputs(n_img, C, H, W, h, w, P, K, device, SEED)
+    state = dpush.PushState.create(P, C, device)
+    keys = torch.empty((n_img, P), device=device, dtype=torch.int64)
+    mask = torch.empty((n_img, h * w), device=device, dtype=torch.int32)
+    stream = _lib.stream_of(device)
+
+    def run(ev=None):
+        _lib.call("protoseg_patch_class_mask", _lib.ptr(labels), _lib.U8, n_img, H, W, h, w, ctypes.c_void_p(None), 0,
+                  _lib.ptr(mask), stream)
+        if ev is not None:
+            ev[0].record()
+        _lib.call("protoseg_push_argmin", _lib.ptr(x), n_img, C, h, w, _lib.ptr(protos), P, _lib.ptr(pc),
+                  _lib.ptr(mask), _lib.ptr(keys), stream)
+        if ev is not None:
+            ev[1].record()
+        _lib.call("protoseg_push_merge", _lib.ptr(keys), n_img, 0, _lib.ptr(x), C, h * w, P, _lib.ptr(state.dist),
+                  _lib.ptr(state.img), _lib.ptr(state.patch), _lib.ptr(state.fmap), stream)
+
+    for _ in range(warmup):
+        run()
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps)]
+    t0 = time.perf_counter()
+    for s in range(steps):
+        run(evs[s])
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    argmin_s = float(np.mean([e[0].elapsed_time(e[1]) for e in evs])) * 1e-3
+    flops = 2.0 * n_img * h * w * P * C
+    nbytes = n_img * (C * h * w * 4 + H * W * 1)
+    return {"ms_per_img": round(elapsed / (steps * n_img) * 1e3, 4), "images_per_call": n_img,
+            "workload": f"push mask+argmin+merge, labels {H}x{W} u8, map {C}x{h}x{w} f32, P={P}, K={K}",
+            "argmin_kernel_ms_per_img": round(argmin_s / n_img * 1e3, 4),
+            "roofline": roofline_entry(flops, nbytes, argmin_s) | {"kernel": "push_argmin_kernel"}}
+
+
+def cpu_push_baseline(budget_s, C=64, H=1024, W=2048, h=129, w=257, P=190, K=19):
+    """Oracle restatement of push.py:184-281 (Python loops, single thread) on one image."""
+    from oracle import protoseg_oracle as po
+    from oracle import push_oracle as pu
+    x, protos, labels, pc = make_push_inputs(1, C, H, W, h, w, P, K, "cpu", SEED)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        d = po.l2_convolution(x, protos[:, :, None, None], torch.ones(P, C, 1, 1))[0]
+        st = pu.PushOracleState(P, C)
+        pu.update_prototypes_on_image_core(st, x[0].numpy(), d.permute(1, 2, 0).numpy(), labels[0].numpy(),
+                                           pc.numpy(), K, 0)
+        n += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"ms_per_img": round(dt / n * 1e3, 1), "cores": 1, "kind": "port",
+            "sample": f"{n} image(s): oracle push.py:184-281 loops (per-pixel patch sets + per-prototype argmin), "
+                      f"{H}x{W} labels, {C}x{h}x{w} map, P={P}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
+    ap.add_argument("--protos", type=int, default=190)
+    ap.add_argument("--classes", type=int, default=19)
+    ap.add_argument("--channels", type=int, default=64)
+    ap.add_argument("--fmap", type=int, default=65, help="feature-map side (513 crop -> 65)")
+    ap.add_argument("--x-dtype", choices=["f32", "bf16"], default="f32")
+    ap.add_argument("--push-images", type=int, default=8)
+    ap.add_argument("--push-steps", type=int, default=5)
+    ap.add_argument("--no-push", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    rank, local_rank, world = init_from_env()
+    if world != args.gpus and rank == 0:
+        print(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}", file=sys.stderr)
+    device = torch.device(f"cuda:{local_rank}")
+    torch.cuda.set_device(device)
+    x_dtype = torch.float32 if args.x_dtype == "f32" else torch.bfloat16
+
+    step = LayerStep(args.batch, args.channels, args.fmap, args.fmap, args.protos, args.classes, x_dtype, device,
+                     SEED + rank)
+    elapsed, per_kernel = time_layer(step, args.steps, args.warmup, world)
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    images = args.batch * world * args.steps
+    value = images / elapsed
+
+    push = None
+    if not args.no_push:
+        push = time_push(args.push_images, args.push_steps, 1, device)
+
+    if rank == 0:
+        work = step.work()
+        dominant = max(per_kernel, key=per_kernel.get)
+        flops, nbytes = work[dominant]
+        roof = roofline_entry(flops, nbytes, per_kernel[dominant])
+        config_key = f"B{args.batch}_C{args.channels}_{args.fmap}x{args.fmap}_P{args.protos}_K{args.classes}_{args.x_dtype}"
+        roof["traffic"] = pmc_traffic(dominant, config_key)
+        roof["kernel"] = dominant
+        kernels = {}
+        for n, s in per_kernel.items():
+            f, b = work[n]
+            kernels[n] = {"ms": round(s * 1e3, 4), "tflops": round(f / s / 1e12, 2), "gbps": round(b / s / 1e9, 1)}
+        out = {
+            "metric": baseline_metric(),
+            "value": round(value, 1),
+            "unit": "img/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32" if args.x_dtype == "f32" else "bf16-in/f32",
+            "data": "synthetic (seeded; SURVEY.md §8d shapes), inputs resident in HBM",
+            "config": {"workload": "cityscapes_no_kld_imnet prototype layer fwd+bwd (+RCCL grad all-reduce "
+                                   "when N>1), 513x513 crop -> 65x65 map",
+                       "global_batch": args.batch * world, "per_gpu_batch": args.batch,
+                       "channels": args.channels, "prototypes": args.protos, "classes": args.classes,
+                       "parallelism": f"dp{world}"},
+            "roofline": roof,
+            "kernels": kernels,
+        }
+        if push is not None:
+            out["push"] = push
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_layer_baseline(args.channels, args.fmap, args.fmap, args.protos, args.classes,
+                                                     args.cpu_seconds)
+            if push is not None:
+                out["push"]["cpu_baseline"] = cpu_push_baseline(args.cpu_seconds)
+                out["push"]["speedup_vs_cpu"] = round(out["push"]["cpu_baseline"]["ms_per_img"] /
+                                                      push["ms_per_img"], 1)
+            out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
+        print(json.dumps(out))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,150 @@
+/*
+ * protoseg_hip.h — C ABI of libprotoseg_hip.so, the MI355X (gfx950) hot path of ProtoSeg.
+ *
+ * The reference (tijaz17skane/ADLM-Inherently-Interpretable-Segmentation) has no native code:
+ * every entry point below replaces a sequence of stock PyTorch ops or host Python loops.
+ * The reference interface each one replaces is cited next to it (paths relative to the
+ * reference root).
+ *
+ * Conventions (all entry points):
+ *  - device pointers, plain integer shapes, a stream; no torch types;
+ *  - tensors are dense, row-major, in the layouts stated per argument;
+ *  - outputs are caller-allocated; the only temporary memory is the caller-owned workspace
+ *    sized by the matching *_workspace_size() call; no hidden hipMalloc / sync, so every
+ *    call can be captured into a hipGraph;
+ *  - return PROTOSEG_OK (0) or a protoseg_status code; protoseg_last_error() gives text;
+ *  - reentrant: the only global state is a once-initialised per-kernel LDS attribute table.
+ */
+#ifndef PROTOSEG_HIP_H_
+#define PROTOSEG_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Same object as hipStream_t (struct ihipStream_t*); NULL = the legacy default stream. */
+typedef struct ihipStream_t* protoseg_stream_t;
+
+enum protoseg_status {
+  PROTOSEG_OK = 0,
+  PROTOSEG_ERR_INVALID = 1,      /* bad pointer / shape combination                      */
+  PROTOSEG_ERR_UNSUPPORTED = 2,  /* valid request outside the compiled kernel family      */
+  PROTOSEG_ERR_HIP = 3           /* a HIP runtime call or kernel launch failed            */
+};
+
+enum protoseg_dtype {
+  PROTOSEG_F32 = 0,   /* float                                     */
+  PROTOSEG_BF16 = 1,  /* bfloat16 bits in uint16_t                  */
+  PROTOSEG_I64 = 2,   /* int64 labels (reference convert_targets)   */
+  PROTOSEG_I32 = 3,
+  PROTOSEG_U8 = 4
+};
+
+/* model.py:231-237 distance_2_similarity: 'log' -> log((d+1)/(d+eps)); 'linear' -> -d */
+enum protoseg_act { PROTOSEG_ACT_LOG = 0, PROTOSEG_ACT_LINEAR = 1 };
+
+int protoseg_version(void);                 /* MAJOR*10000 + MINOR*100 + PATCH */
+const char* protoseg_last_error(void);      /* thread-local text of the last failure */
+
+/*
+ * Prototype layer forward. Replaces model.py:203-221 (_l2_convolution), 231-237
+ * (distance_2_similarity) and 259-283 (forward_from_conv_features, patch-classification
+ * branch: permute -> activation -> last_layer -> reshape), i.e. 2 conv2d + 9 elementwise
+ * passes + 1 Linear, by one fused kernel.
+ *
+ *   x       [B, C, H, W]  x_dtype (PROTOSEG_F32 | PROTOSEG_BF16), the add-on-layer output
+ *   protos  [P, C]        f32 (prototype_vectors, 1x1 kernels flattened)
+ *   w_last  [K, P]        f32 (last_layer.weight, no bias); may be NULL iff logits_out is NULL
+ *   dist_out   [B, P, H, W]   f32 or NULL   distances (model.py:219, NCHW)
+ *   act_out    [B*H*W, P]     f32 or NULL   prototype activations (model.py:273)
+ *   logits_out [B, H, W, K]   f32 or NULL   logits NHWC (model.py:278)
+ * Supported: C in {32, 64, 128}; P <= 384 (C=64) — see protoseg_l2_supported(); K <= 32.
+ */
+int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, int W,
+                    const float* protos, int P, const float* w_last, int K,
+                    float eps, int act_kind,
+                    float* dist_out, float* act_out, float* logits_out,
+                    protoseg_stream_t stream);
+
+/*
+ * Prototype layer backward: the autograd graph of model.py:203-221, 231-237, 266-278
+ * (the reference has no custom backward). Distances are recomputed from x, never re-read.
+ *
+ *   g_logits [B, H, W, K] f32 or NULL   upstream grad of logits
+ *   g_dist   [B, P, H, W] f32 or NULL   upstream grad of distances (KLD loss, module.py:167-208)
+ *   g_x      [B, C, H, W] x_dtype or NULL
+ *   g_protos [P, C] f32 or NULL   (overwritten, not accumulated)
+ *   g_w      [K, P] f32 or NULL   (overwritten; requires g_logits)
+ *   workspace: protoseg_l2_bwd_workspace_size(...) bytes, 256-B aligned.
+ */
+size_t protoseg_l2_bwd_workspace_size(int B, int C, int H, int W, int P, int K);
+int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, int W,
+                    const float* protos, int P, const float* w_last, int K,
+                    float eps, int act_kind,
+                    const float* g_logits, const float* g_dist,
+                    void* g_x, float* g_protos, float* g_w,
+                    void* workspace, size_t workspace_bytes,
+                    protoseg_stream_t stream);
+
+/* 1 if (C, P, K) is inside the compiled kernel family, else 0. */
+int protoseg_l2_supported(int C, int P, int K);
+
+/*
+ * Push, step 1: label map -> per-patch class bitmask. Replaces segmentation/push.py:184-186
+ * (convert_targets via np.vectorize) and 214-223 (the per-pixel Python loop building
+ * class_to_patch_index_dict). Pixel (i, j) of class c > 0 marks patch
+ * (int(i / (H_img / h)), int(j / (W_img / w))) for class c-1, divisions in float64.
+ *
+ *   label  [n_img, H_img, W_img] label_dtype (PROTOSEG_I64 | PROTOSEG_I32 | PROTOSEG_U8)
+ *   lut    [lut_size] int32 or NULL: label = lut[raw] (CITYSCAPES_19_EVAL_CATEGORIES etc.);
+ *          raw values outside [0, lut_size) are ignored
+ *   mask   [n_img, h, w] uint32: bit k set <=> a pixel of class k+1 falls in the patch
+ * Classes above 32 are ignored (the reference would raise KeyError for class > num_classes).
+ */
+int protoseg_patch_class_mask(const void* label, int label_dtype, int n_img, int H_img, int W_img,
+                              int h, int w, const int32_t* lut, int lut_size,
+                              uint32_t* mask, protoseg_stream_t stream);
+
+/*
+ * Push, step 2: for every image and prototype, the masked argmin of the distance over the
+ * patches of the prototype's class. Replaces segmentation/push.py:193 + 209-263 (distances
+ * for the whole image, D2H copy, per-prototype gather of class patches and np.argmin).
+ * Distances are computed in-kernel with the same arithmetic as protoseg_l2_fwd.
+ *
+ *   x           [n_img, C, h, w] f32
+ *   proto_class [P] int32: argmax(prototype_class_identity[p]) (push.py:251); <0 = never pushed
+ *   mask        [n_img, h*w] uint32 from protoseg_patch_class_mask
+ *   img_keys    [n_img, P] uint64 out: (float_bits(d_min) << 32) | patch_index, or
+ *               UINT64_MAX when the image holds no patch of the prototype's class.
+ * Ties inside one image resolve to the lowest patch index (the reference's order is the
+ * iteration order of a Python set, push.py:214-230).
+ */
+int protoseg_push_argmin(const float* x, int n_img, int C, int h, int w,
+                         const float* protos, int P, const int32_t* proto_class,
+                         const uint32_t* mask, uint64_t* img_keys, protoseg_stream_t stream);
+
+/*
+ * Push, step 3: fold a batch of per-image keys into the running global minimum in image
+ * order with a strict '<' (push.py:101, 265-281: earlier images win ties), and gather the
+ * winning feature vector (push.py:276-280).
+ *
+ *   img_keys      [n_img, P] from protoseg_push_argmin on the same x
+ *   first_img     dataset index of image 0 of this batch
+ *   global_dist   [P] f32 in/out (init +inf)
+ *   global_img    [P] int64 in/out (init -1)
+ *   global_patch  [P] int32 in/out (init -1)
+ *   global_fmap   [P, C] f32 in/out
+ */
+int protoseg_push_merge(const uint64_t* img_keys, int n_img, int64_t first_img,
+                        const float* x, int C, int hw, int P,
+                        float* global_dist, int64_t* global_img, int32_t* global_patch,
+                        float* global_fmap, protoseg_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PROTOSEG_HIP_H_ */

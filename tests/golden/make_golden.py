@@ -1,0 +1,86 @@
+"""Generates the committed golden vectors from the oracle (CPU restatement of the reference).
+
+The reference repository ships no tests or fixtures for this path and its Python cannot be
+run here, so these vectors freeze the oracle's outputs on seeded inputs;
+tests/test_oracle.py re-derives them bit for bit and the GPU tests compare the HIP kernels
+against them. Run:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import protoseg_oracle as po  # noqa: E402
+from oracle import push_oracle as pu  # noqa: E402
+
+SEED = 20220227
+
+
+def l2_case(B, C, h, w, P, K, seed):
+    x, protos, w_last = po.synthetic_inputs(B, C, h, w, P, K, seed)
+    gen = torch.Generator().manual_seed(seed + 1)
+    # a trained-looking last layer: identity init plus noise
+    w_last = w_last + 0.1 * torch.randn(w_last.shape, generator=gen)
+    g_logits = torch.randn(B, h, w, K, generator=gen)
+    g_dist = 0.01 * torch.randn(B, P, h, w, generator=gen)
+    logits, dist, gx, gp, gw = po.forward_backward(x, protos, w_last, g_logits, None)
+    _, _, gx_d, gp_d, _ = po.forward_backward(x, protos, w_last, g_logits, g_dist)
+    _, act = po.forward_from_conv_features(x, protos[:, :, None, None], w_last, return_activations=True)
+    return dict(x=x.numpy(), protos=protos.numpy(), w_last=w_last.numpy(), g_logits=g_logits.numpy(),
+                g_dist=g_dist.numpy(), logits=logits.numpy(), dist=dist.numpy(), act=act.detach().numpy(),
+                g_x=gx.numpy(), g_protos=gp.numpy(), g_w=gw.numpy(), g_x_with_gdist=gx_d.numpy(),
+                g_protos_with_gdist=gp_d.numpy())
+
+
+def push_case(n_img, C, H, W, h, w, P, K, seed):
+    rng = np.random.default_rng(seed)
+    gen = torch.Generator().manual_seed(seed)
+    x = torch.sigmoid(2.0 * torch.randn(n_img, C, h, w, generator=gen))
+    protos = torch.rand(P, C, generator=gen)
+    identity = po.class_identity(P, K)
+    proto_class = torch.argmax(identity, dim=1).numpy().astype(np.int32)
+    # raw Cityscapes ids 0..28 in blocks, so classes cover contiguous regions
+    raw = rng.integers(0, 29, size=(n_img, H // 4, W // 4))
+    raw = np.repeat(np.repeat(raw, 4, axis=1), 4, axis=2)[:, :H, :W].astype(np.int64)
+    labels = np.stack([pu.convert_targets(r) for r in raw]).astype(np.int64)
+    state = pu.PushOracleState(P, C)
+    dists, masks = [], []
+    for i in range(n_img):
+        d = po.l2_convolution(x[i:i + 1], protos[:, :, None, None], torch.ones(P, C, 1, 1))[0]
+        proto_dist_ = d.permute(1, 2, 0).numpy()
+        sets = pu.class_to_patch_index_dict(labels[i], h, w, K)
+        masks.append(pu.bitmask_from_dict(sets, h, w))
+        pu.update_prototypes_on_image_core(state, x[i].numpy(), proto_dist_, labels[i], proto_class, K, i, sets)
+        dists.append(d.numpy())
+    unique_index, duplicate_idx = pu.dedup(state.global_min_fmap_patches.reshape(P, C, 1, 1))
+    return dict(x=x.numpy(), protos=protos.numpy(), proto_class=proto_class, raw_labels=raw, labels=labels,
+                dist=np.stack(dists), mask=np.stack(masks), global_min_proto_dist=state.global_min_proto_dist,
+                global_min_fmap_patches=state.global_min_fmap_patches.reshape(P, C), winner_patch=state.winner_patch,
+                proto_rf_boxes=state.proto_rf_boxes, unique_index=np.asarray(unique_index),
+                duplicate_idx=np.asarray(duplicate_idx, dtype=np.int64))
+
+
+CASES = {
+    "l2_small": lambda: l2_case(2, 64, 17, 17, 38, 19, SEED),
+    "l2_ragged": lambda: l2_case(3, 32, 7, 11, 21, 3, SEED + 7),
+    "push_small": lambda: push_case(3, 64, 64, 128, 8, 16, 38, 19, SEED),
+}
+
+
+def main():
+    for name, fn in CASES.items():
+        arrays = fn()
+        path = os.path.join(HERE, f"{name}.npz")
+        np.savez_compressed(path, **arrays)
+        print(f"wrote {path} ({os.path.getsize(path)} B)")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,64 @@
+"""CPU: the C-ABI library loads and exports every symbol include/protoseg_hip.h declares;
+the pure-host entry points (no GPU call) behave as documented."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from protoseg_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "protoseg_hip.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(protoseg_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    names = declared_symbols()
+    assert len(names) >= 9
+    for name in names:
+        assert hasattr(lib, name), name
+    assert set(names) == set(_lib.SIGNATURES), "ctypes signatures out of sync with the header"
+
+
+def test_version_and_supported_shapes():
+    lib = _lib.load()
+    assert lib.protoseg_version() == 10000
+    assert lib.protoseg_l2_supported(64, 190, 19) == 1
+    assert lib.protoseg_l2_supported(64, 361, 19) == 1
+    assert lib.protoseg_l2_supported(32, 38, 3) == 1
+    assert lib.protoseg_l2_supported(128, 64, 32) == 1
+    assert lib.protoseg_l2_supported(48, 190, 19) == 0    # C outside the kernel family
+    assert lib.protoseg_l2_supported(64, 190, 33) == 0    # more than 32 classes
+    assert lib.protoseg_l2_supported(64, 1000, 19) == 0   # prototypes exceed LDS
+
+
+def test_workspace_size_is_host_only_and_aligned():
+    lib = _lib.load()
+    n = lib.protoseg_l2_bwd_workspace_size(32, 64, 65, 65, 190, 19)
+    assert n > 0 and n % 256 == 0
+    assert lib.protoseg_l2_bwd_workspace_size(0, 64, 65, 65, 190, 19) == 0
+
+
+def test_argument_validation_returns_status_without_gpu():
+    lib = _lib.load()
+    null = ctypes.c_void_p(None)
+    st = lib.protoseg_l2_fwd(null, 0, 1, 64, 2, 2, null, 19, null, 19, 1e-4, 0, null, null, null, null)
+    assert st == _lib.ERR_INVALID
+    assert b"non-null" in lib.protoseg_last_error()
+    dummy = ctypes.c_void_p(16)  # never dereferenced: validation fails first
+    st = lib.protoseg_l2_fwd(dummy, 7, 1, 64, 2, 2, dummy, 19, dummy, 19, 1e-4, 0, null, null, null, null)
+    assert st == _lib.ERR_UNSUPPORTED
+    st = lib.protoseg_l2_fwd(dummy, 0, 1, 48, 2, 2, dummy, 19, dummy, 19, 1e-4, 0, null, null, null, null)
+    assert st == _lib.ERR_UNSUPPORTED
+    st = lib.protoseg_patch_class_mask(null, 2, 1, 4, 4, 2, 2, null, 0, null, null)
+    assert st == _lib.ERR_INVALID
+    st = lib.protoseg_push_argmin(dummy, 1, 48, 2, 2, dummy, 3, dummy, dummy, dummy, null)
+    assert st == _lib.ERR_UNSUPPORTED
+    with pytest.raises(_lib.ProtosegError, match="status 1"):
+        _lib.call("protoseg_push_merge", null, 1, 0, null, 64, 4, 3, null, null, null, null, null)

@@ -1,0 +1,102 @@
+"""CPU, world_size 2 over gloo: the sharded-push reduction equals the serial scan, and the
+bucketed gradient all-reduce averages exactly."""
+import math
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from protoseg_amd.distributed import GradientBuckets, reduce_push_state, shard_bounds
+from protoseg_amd.push import PushState
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _serial_truth(per_image):
+    """Strict '<' in image order over (dist, patch, fmap) per image and prototype."""
+    n_img, P = len(per_image), per_image[0][0].shape[0]
+    best = [math.inf] * P
+    img = [-1] * P
+    patch = [-1] * P
+    fmap = [None] * P
+    for i in range(n_img):
+        d, q, f = per_image[i]
+        for j in range(P):
+            if float(d[j]) < best[j]:
+                best[j], img[j], patch[j], fmap[j] = float(d[j]), i, int(q[j]), f[j]
+    return best, img, patch, fmap
+
+
+def _make_images(n_img, P, C):
+    gen = torch.Generator().manual_seed(7)
+    out = []
+    for i in range(n_img):
+        d = torch.randint(0, 6, (P,), generator=gen).float() / 4  # many exact ties across images
+        d[torch.rand(P, generator=gen) < 0.2] = math.inf            # class absent in this image
+        q = torch.randint(0, 500, (P,), generator=gen, dtype=torch.int32)
+        f = torch.rand(P, C, generator=gen)
+        out.append((d, q, f))
+    return out
+
+
+def _worker(rank, world, port, n_img, P, C, result_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        images = _make_images(n_img, P, C)
+        lo, hi = shard_bounds(n_img, rank, world)
+        st = PushState.create(P, C, "cpu")
+        for i in range(lo, hi):  # host emulation of the device merge for this rank's shard
+            d, q, f = images[i]
+            better = d < st.dist
+            st.dist = torch.where(better, d, st.dist)
+            st.img = torch.where(better, torch.full_like(st.img, i), st.img)
+            st.patch = torch.where(better, q, st.patch)
+            st.fmap = torch.where(better[:, None], f, st.fmap)
+            st.geometry[i] = (8, 8, 2, 2)
+        reduce_push_state(st)
+        # gradient buckets: rank-dependent grads, tiny buckets to force several collectives
+        params = [torch.nn.Parameter(torch.zeros(n)) for n in (5, 300, 17)]
+        for k, p in enumerate(params):
+            p.grad = torch.full_like(p, float(rank + 1) * (k + 1))
+        gb = GradientBuckets(params, bucket_mb=1e-3)
+        gb.allreduce()
+        gb.wait()
+        grads = [p.grad.clone() for p in params]
+        result_q.put((rank, st.dist, st.img, st.patch, st.fmap, len(st.geometry), grads, len(gb.buckets)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_img", [5, 8])
+def test_sharded_push_reduction_equals_serial_scan(n_img):
+    world, P, C = 2, 23, 6
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_img, P, C, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    best, img, patch, fmap = _serial_truth(_make_images(n_img, P, C))
+    for rank, d, im, pa, fm, ngeo, grads, nbuckets in results:
+        assert ngeo == n_img
+        for j in range(P):
+            if img[j] < 0:
+                assert im[j].item() == -1 and math.isinf(d[j].item())
+                continue
+            assert (d[j].item(), im[j].item(), pa[j].item()) == (best[j], img[j], patch[j])
+            assert torch.equal(fm[j], fmap[j])
+        assert nbuckets == 3
+        for k, g in enumerate(grads):
+            assert torch.allclose(g, torch.full_like(g, 1.5 * (k + 1)))  # mean of rank+1 over 2 ranks

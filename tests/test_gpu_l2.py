@@ -1,0 +1,188 @@
+"""Parity of the HIP prototype layer (forward + backward) with the oracle, through the C ABI.
+
+Tolerances (north_star: "fp32 distances within 1e-4 rel"): distances are compared as
+|d - d_ref| <= 1e-4 * max(|d_ref|, 1) + 2e-6 * (||x||^2 + ||p||^2); the second term is the
+cancellation bound of the expanded form relu(||x||^2 - 2x.p + ||p||^2) that both the reference
+and the kernel evaluate in f32 (it matters only where d << ||x||^2). Activations, logits and
+gradients: rtol 1e-4 of the tensor's own scale.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import protoseg_oracle as po
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    from protoseg_amd import ops
+    return ops
+
+
+def _norm_bound(x, protos):
+    x2 = (x.double() ** 2).sum(1, keepdim=True)  # [B,1,h,w]
+    p2 = (protos.double() ** 2).sum(1).view(1, -1, 1, 1)
+    return x2 + p2
+
+
+def assert_dist_close(d, d_ref, x, protos):
+    d, d_ref = d.double().cpu(), d_ref.double().cpu()
+    bound = 1e-4 * torch.clamp(d_ref.abs(), min=1.0) + 2e-6 * _norm_bound(x.cpu(), protos.cpu())
+    err = (d - d_ref).abs()
+    assert bool((err <= bound).all()), f"max err {err.max().item():.3e}, worst ratio {(err / bound).max().item():.3f}"
+
+
+def assert_scaled_close(a, ref, rtol=1e-4, name=""):
+    a, ref = a.double().cpu(), ref.double().cpu()
+    scale = ref.abs().max().item() + 1e-30
+    err = (a - ref).abs().max().item()
+    assert err <= rtol * scale, f"{name}: max err {err:.3e} > {rtol:g} * scale {scale:.3e}"
+
+
+def run_layer(x, protos, w_last, activation="log", with_act=False, device="cuda:0"):
+    ops = _ops()
+    return ops.prototype_layer(x.to(device), protos.to(device), w_last.to(device), 1e-4, activation,
+                               True, True, with_act)
+
+
+@pytest.mark.parametrize("name", ["l2_small", "l2_ragged"])
+def test_forward_matches_golden(device, name):
+    g = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    x, protos, w_last = (torch.from_numpy(g[k]) for k in ("x", "protos", "w_last"))
+    dist, logits, act = run_layer(x, protos, w_last, with_act=True, device=device)
+    torch.cuda.synchronize()
+    assert_dist_close(dist, torch.from_numpy(g["dist"]), x, protos)
+    assert_scaled_close(logits, torch.from_numpy(g["logits"]), 1e-4, "logits")
+    assert_scaled_close(act, torch.from_numpy(g["act"]), 1e-4, "act")
+
+
+@pytest.mark.parametrize("name", ["l2_small", "l2_ragged"])
+def test_backward_matches_golden(device, name):
+    ops = _ops()
+    g = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    x, protos, w_last, g_logits, g_dist = (torch.from_numpy(g[k]).to(device) for k in
+                                           ("x", "protos", "w_last", "g_logits", "g_dist"))
+    gx, gp, gw = ops.l2_backward(x, protos, w_last, g_logits, None, 1e-4, 0, True, True, True)
+    torch.cuda.synchronize()
+    assert_scaled_close(gx, torch.from_numpy(g["g_x"]), 1e-4, "g_x")
+    assert_scaled_close(gp, torch.from_numpy(g["g_protos"]), 1e-4, "g_protos")
+    assert_scaled_close(gw, torch.from_numpy(g["g_w"]), 1e-4, "g_w")
+    gx2, gp2, _ = ops.l2_backward(x, protos, w_last, g_logits, g_dist, 1e-4, 0, True, True, False)
+    assert_scaled_close(gx2, torch.from_numpy(g["g_x_with_gdist"]), 1e-4, "g_x(+g_dist)")
+    assert_scaled_close(gp2, torch.from_numpy(g["g_protos_with_gdist"]), 1e-4, "g_protos(+g_dist)")
+
+
+@pytest.mark.parametrize("B,C,h,w,P,K", [
+    (1, 64, 1, 1, 19, 19),        # a single pixel
+    (2, 64, 5, 3, 32, 19),        # P exactly one tile
+    (1, 64, 33, 1, 33, 5),        # P one over a tile, pixel tail of 1
+    (2, 32, 9, 9, 10, 2),         # C = 32
+    (1, 128, 6, 7, 64, 32),       # C = 128, K = 32 (max)
+    (2, 64, 65, 65, 190, 19),     # cityscapes crop, 10 prototypes/class
+    (1, 64, 65, 65, 361, 19),     # 19 prototypes/class
+])
+@pytest.mark.parametrize("activation", ["log", "linear"])
+def test_forward_backward_vs_oracle(device, B, C, h, w, P, K, activation):
+    x, protos, w_last = po.synthetic_inputs(B, C, h, w, P, K, seed=B * 1000 + C + h + P)
+    gen = torch.Generator().manual_seed(5)
+    w_last = w_last + 0.05 * torch.randn(w_last.shape, generator=gen)
+    g_logits = torch.randn(B, h, w, K, generator=gen)
+    dist, logits, _ = run_layer(x, protos, w_last, activation, device=device)
+    ref_logits, ref_dist, ref_gx, ref_gp, ref_gw = po.forward_backward(x, protos, w_last, g_logits, None, activation)
+    assert_dist_close(dist, ref_dist, x, protos)
+    assert_scaled_close(logits, ref_logits, 1e-4, "logits")
+    ops = _ops()
+    gx, gp, gw = ops.l2_backward(x.to(device), protos.to(device), w_last.to(device), g_logits.to(device), None,
+                                 1e-4, ops.ACT_KINDS[activation], True, True, True)
+    assert_scaled_close(gx, ref_gx, 1e-4, "g_x")
+    assert_scaled_close(gp, ref_gp, 1e-4, "g_protos")
+    assert_scaled_close(gw, ref_gw, 1e-4, "g_w")
+
+
+def test_bf16_features(device):
+    """bf16 feature maps are read exactly (bf16 -> f32 is exact) and computed in f32."""
+    x, protos, w_last = po.synthetic_inputs(2, 64, 17, 19, 57, 19, seed=3)
+    xb = x.to(torch.bfloat16)
+    dist, logits, _ = run_layer(xb, protos, w_last, device=device)
+    ref_logits, ref_dist = po.forward_from_conv_features(xb.float(), protos[:, :, None, None], w_last)
+    assert_dist_close(dist, ref_dist, xb.float(), protos)
+    assert_scaled_close(logits, ref_logits, 1e-4, "logits")
+    ops = _ops()
+    g_logits = torch.randn(2, 17, 19, 19)
+    gx, gp, _ = ops.l2_backward(xb.to(device), protos.to(device), w_last.to(device), g_logits.to(device), None,
+                                1e-4, 0, True, True, False)
+    assert gx.dtype == torch.bfloat16
+    _, _, ref_gx, ref_gp, _ = po.forward_backward(xb.float(), protos, w_last, g_logits, None)
+    assert_scaled_close(gx.float(), ref_gx, 1e-2, "g_x(bf16 out)")
+    assert_scaled_close(gp, ref_gp, 1e-4, "g_protos")
+
+
+def test_known_answer_zero_distance(device):
+    """x equal to a prototype at a pixel -> d = 0 (relu clamps) -> act = log(1/1e-4) = 9.2103."""
+    x, protos, w_last = po.synthetic_inputs(1, 64, 4, 4, 19, 19, seed=11)
+    x[0, :, 2, 3] = protos[7]
+    dist, logits, act = run_layer(x, protos, w_last, with_act=True, device=device)
+    d = dist[0, 7, 2, 3].item()
+    assert d <= 2e-6 * 2 * (protos[7] ** 2).sum().item()
+    a = act.view(1, 4, 4, 19)[0, 2, 3, 7].item()
+    assert abs(a - float(np.log((d + 1) / (d + 1e-4)))) < 1e-4
+    if d == 0.0:
+        assert abs(a - 9.210340371976184) < 1e-5
+
+
+def test_distances_match_float64_bruteforce(device):
+    """Size-independent property at the full 65x65 crop: d == ||x - p||^2 within the f32 bound."""
+    x, protos, w_last = po.synthetic_inputs(4, 64, 65, 65, 190, 19, seed=17)
+    dist, _, _ = run_layer(x, protos, w_last, device=device)
+    xd = x.double().permute(0, 2, 3, 1).reshape(-1, 64)
+    exact = torch.cdist(xd, protos.double()) ** 2
+    exact = exact.reshape(4, 65, 65, 190).permute(0, 3, 1, 2)
+    assert_dist_close(dist, exact, x, protos)
+
+
+def test_deterministic(device):
+    """No atomics on the float path: two runs are bitwise identical."""
+    ops = _ops()
+    x, protos, w_last = po.synthetic_inputs(3, 64, 40, 41, 190, 19, seed=23)
+    x, protos, w_last = x.to(device), protos.to(device), w_last.to(device)
+    g = torch.randn(3, 40, 41, 19, device=device)
+    r1 = ops.l2_backward(x, protos, w_last, g, None, 1e-4, 0, True, True, True)
+    r2 = ops.l2_backward(x, protos, w_last, g, None, 1e-4, 0, True, True, True)
+    for a, b in zip(r1, r2):
+        assert torch.equal(a, b)
+
+
+def test_ppnet_autograd_matches_oracle(device):
+    """PPNet.forward_from_conv_features + autograd through the custom op == oracle autograd."""
+    from protoseg_amd.model import PPNet
+    from protoseg_amd.deeplab import deeplabv2_resnet101_features
+    feats = deeplabv2_resnet101_features(n_blocks=(1, 1, 1, 1), scales=[])
+    net = PPNet(feats, 513, (38, 64, 1, 1), None, 19, add_on_layers_type="deeplab_simple",
+                patch_classification=True).to(device)
+    x, _, _ = po.synthetic_inputs(2, 64, 9, 9, 38, 19, seed=29)
+    xd = x.to(device).requires_grad_(True)
+    logits, dist = net.forward_from_conv_features(xd)
+    loss = logits.square().sum() + 0.1 * dist.sum()
+    loss.backward()
+    ref_logits, ref_dist = po.forward_from_conv_features(x, net.prototype_vectors.detach().cpu(),
+                                                         net.last_layer.weight.detach().cpu())
+    g_logits = 2 * ref_logits
+    _, _, ref_gx, ref_gp, ref_gw = po.forward_backward(x, net.prototype_vectors.detach().cpu(),
+                                                       net.last_layer.weight.detach().cpu(), g_logits,
+                                                       torch.full_like(ref_dist, 0.1))
+    assert_scaled_close(logits.detach(), ref_logits, 1e-4, "logits")
+    assert_scaled_close(xd.grad, ref_gx, 1e-4, "g_x")
+    assert_scaled_close(net.prototype_vectors.grad.reshape(38, 64), ref_gp, 1e-4, "g_protos")
+    assert_scaled_close(net.last_layer.weight.grad, ref_gw, 1e-4, "g_w")
+
+
+def test_cpu_tensors_fail_loudly():
+    from protoseg_amd import ops
+    x, protos, w_last = po.synthetic_inputs(1, 64, 2, 2, 19, 19)
+    with pytest.raises((RuntimeError, NotImplementedError)):
+        ops.prototype_layer(x, protos, w_last)

@@ -1,0 +1,170 @@
+"""Parity of the HIP push kernels with the push oracle (segmentation/push.py restated).
+
+Bar: bit-exact for the integer work (patch class masks, winning patch / image indices, rf
+boxes, dedup). Winning distances and feature vectors are compared exactly where the oracle's
+minimum is separated from the runner-up by more than the f32 rounding bound of the distance;
+inside that bound either candidate is a correct answer of the same computation and the test
+checks that the kernel's pick is one of them.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import protoseg_oracle as po
+from oracle import push_oracle as pu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+pytestmark = pytest.mark.gpu
+
+
+def _push():
+    from protoseg_amd import push
+    return push
+
+
+def _lut():
+    lut = np.full(29, -1, dtype=np.int32)
+    for k, v in pu.CITYSCAPES_19_EVAL_CATEGORIES.items():
+        lut[k] = v
+    return torch.from_numpy(lut)
+
+
+@pytest.mark.parametrize("dtype", [torch.int64, torch.int32, torch.uint8])
+def test_patch_mask_matches_golden(device, dtype):
+    push = _push()
+    g = np.load(os.path.join(GOLDEN, "push_small.npz"))
+    labels = torch.from_numpy(g["labels"]).to(dtype).to(device)
+    mask = push.patch_class_mask(labels, 8, 16)
+    assert np.array_equal(mask.cpu().numpy().view(np.uint32), g["mask"])
+    raw = torch.from_numpy(g["raw_labels"]).to(dtype).to(device)
+    mask_lut = push.patch_class_mask(raw, 8, 16, _lut().to(device))
+    assert np.array_equal(mask_lut.cpu().numpy().view(np.uint32), g["mask"])
+
+
+@pytest.mark.parametrize("H,W,h,w", [(1024, 2048, 129, 257), (513, 513, 65, 65), (100, 37, 13, 5), (7, 9, 7, 9)])
+def test_patch_mask_vs_oracle_geometry(device, H, W, h, w):
+    """Non-integer patch sizes (1024/129 = 7.94): the float64 pixel->patch division must match."""
+    push = _push()
+    rng = np.random.default_rng(H + W)
+    labels = rng.integers(0, 20, size=(2, H, W)).astype(np.int64)
+    labels[:, : H // 3] = 0  # a void band
+    mask = push.patch_class_mask(torch.from_numpy(labels).to(device), h, w).cpu().numpy().view(np.uint32)
+    for i in range(2):
+        assert np.array_equal(mask[i], pu.class_patch_bitmask_fast(labels[i], h, w))
+    if H * W <= 100 * 37:
+        sets = pu.class_to_patch_index_dict(labels[0], h, w, 19)
+        assert np.array_equal(mask[0], pu.bitmask_from_dict(sets, h, w))
+
+
+def test_push_matches_golden_serial_scan(device):
+    """3 images scanned in order: winners, distances, feature vectors and rf boxes."""
+    push = _push()
+    g = np.load(os.path.join(GOLDEN, "push_small.npz"))
+    x = torch.from_numpy(g["x"]).to(device)
+    protos = torch.from_numpy(g["protos"]).to(device)
+    pc = torch.from_numpy(g["proto_class"]).to(device)
+    labels = torch.from_numpy(g["labels"]).to(device)
+    P, C = protos.shape
+    state = push.PushState.create(P, C, device)
+    for i in range(x.shape[0]):  # one image per call, as push_prototypes does
+        push.push_update(state, x[i:i + 1], labels[i], protos, pc, i)
+    _check_against_oracle(state, g, push)
+    # the same scan as one batched call
+    state_b = push.PushState.create(P, C, device)
+    push.push_update(state_b, x, labels, protos, pc, 0)
+    for a, b in ((state.dist, state_b.dist), (state.img, state_b.img), (state.patch, state_b.patch),
+                 (state.fmap, state_b.fmap)):
+        assert torch.equal(a, b)
+
+
+def _check_against_oracle(state, g, push):
+    ref_d = g["global_min_proto_dist"]
+    dist = state.dist.cpu().numpy().astype(np.float64)
+    img = state.img.cpu().numpy()
+    patch = state.patch.cpu().numpy()
+    boxes = push.rf_boxes(state, g["proto_class"])
+    ref_boxes = g["proto_rf_boxes"]
+    n_img, _, h, w = g["x"].shape
+    for j in range(ref_d.shape[0]):
+        if np.isinf(ref_d[j]):
+            assert img[j] == -1 and np.isinf(dist[j])
+            continue
+        # the reference's own candidates for prototype j and their runner-up gap
+        cand = []
+        for i in range(n_img):
+            member = (g["mask"][i] >> g["proto_class"][j]) & 1
+            d = g["dist"][i, j].reshape(-1)
+            cand += [(d[q], i, q) for q in np.nonzero(member)[0]]
+        cand.sort()
+        bound = 1e-5 * (1.0 + abs(cand[0][0])) + 4e-6 * 64
+        if len(cand) == 1 or cand[1][0] - cand[0][0] > bound:
+            assert (img[j], patch[j]) == (ref_boxes[j, 0], g["winner_patch"][j]), f"prototype {j}"
+            assert np.array_equal(boxes[j], ref_boxes[j])
+            assert np.array_equal(state.fmap[j].cpu().numpy(), g["global_min_fmap_patches"][j].astype(np.float32))
+        else:
+            near = {(i, q) for d, i, q in cand if d - cand[0][0] <= bound}
+            assert (img[j], patch[j]) in near
+        assert abs(dist[j] - ref_d[j]) <= bound
+
+
+def test_push_multi_image_vs_oracle_loop(device):
+    """Random 2-image scan against the literal Python loop of push.py (small images)."""
+    push = _push()
+    n_img, C, H, W, h, w, P, K = 2, 64, 40, 72, 10, 18, 57, 19
+    gen = torch.Generator().manual_seed(31)
+    x = torch.sigmoid(2 * torch.randn(n_img, C, h, w, generator=gen))
+    protos = torch.rand(P, C, generator=gen)
+    pc = torch.argmax(po.class_identity(P, K), dim=1).numpy().astype(np.int32)
+    labels = np.random.default_rng(3).integers(0, K + 1, size=(n_img, H, W)).astype(np.int64)
+    ost = pu.PushOracleState(P, C)
+    dists, masks = [], []
+    for i in range(n_img):
+        d = po.l2_convolution(x[i:i + 1], protos[:, :, None, None], torch.ones(P, C, 1, 1))[0]
+        sets = pu.class_to_patch_index_dict(labels[i], h, w, K)
+        pu.update_prototypes_on_image_core(ost, x[i].numpy(), d.permute(1, 2, 0).numpy(), labels[i], pc, K, i, sets)
+        dists.append(d.numpy())
+        masks.append(pu.bitmask_from_dict(sets, h, w))
+    g = dict(x=x.numpy(), proto_class=pc, dist=np.stack(dists), mask=np.stack(masks),
+             global_min_proto_dist=ost.global_min_proto_dist,
+             global_min_fmap_patches=ost.global_min_fmap_patches.reshape(P, C), winner_patch=ost.winner_patch,
+             proto_rf_boxes=ost.proto_rf_boxes)
+    state = push.PushState.create(P, C, device)
+    push.push_update(state, x.to(device), torch.from_numpy(labels).to(device), protos.to(device),
+                     torch.from_numpy(pc).to(device), 0)
+    _check_against_oracle(state, g, push)
+
+
+def test_push_full_resolution_properties(device):
+    """1024x2048 labels, 129x257 map, 190 prototypes: each key is the masked minimum of the
+    oracle's distances (float64 brute force), and lies in the prototype's class mask."""
+    push = _push()
+    C, H, W, h, w, P, K = 64, 1024, 2048, 129, 257, 190, 19
+    gen = torch.Generator().manual_seed(37)
+    x = torch.sigmoid(2 * torch.randn(1, C, h, w, generator=gen))
+    protos = torch.rand(P, C, generator=gen)
+    pc = torch.argmax(po.class_identity(P, K), dim=1).to(torch.int32)
+    rng = np.random.default_rng(41)
+    labels = np.repeat(np.repeat(rng.integers(0, K + 1, size=(H // 16, W // 16)), 16, 0), 16, 1).astype(np.uint8)
+    mask = push.patch_class_mask(torch.from_numpy(labels).to(device), h, w)
+    keys = push.push_argmin(x.to(device), protos.to(device), pc.to(device), mask)
+    d, patch, found = push.decode_keys(keys[0].cpu())
+    m = mask.cpu().numpy().view(np.uint32)[0]
+    assert np.array_equal(m, pu.class_patch_bitmask_fast(labels, h, w))
+    xd = x[0].double().reshape(C, -1).t()
+    exact = (torch.cdist(xd, protos.double()) ** 2).numpy()  # [h*w, P]
+    norm = (xd ** 2).sum(1).numpy()[:, None] + (protos.double() ** 2).sum(1).numpy()[None, :]
+    for j in range(P):
+        member = ((m >> int(pc[j])) & 1).astype(bool)
+        if not member.any():
+            assert not bool(found[j])
+            continue
+        q = int(patch[j])
+        assert member[q]
+        cand = exact[member, j]
+        best = cand.min()
+        tol = 2e-6 * norm[member, j].max() + 1e-5 * (1 + best)
+        assert exact[q, j] <= best + 2 * tol
+        assert abs(float(d[j]) - exact[q, j]) <= tol

@@ -1,0 +1,91 @@
+"""CPU: pin the oracle before trusting it — golden vectors, analytic known answers, and the
+vectorised push helpers against the literal reference loops."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import protoseg_oracle as po
+from oracle import push_oracle as pu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("name", ["l2_small", "l2_ragged"])
+def test_oracle_reproduces_l2_golden(name):
+    g = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    x, protos, w_last, g_logits = (torch.from_numpy(g[k]) for k in ("x", "protos", "w_last", "g_logits"))
+    logits, dist, gx, gp, gw = po.forward_backward(x, protos, w_last, g_logits, None)
+    # torch-CPU kernels may reorder sums across hosts: equal to f32 rounding, not bitwise
+    for got, key in ((logits, "logits"), (dist, "dist"), (gx, "g_x"), (gp, "g_protos"), (gw, "g_w")):
+        ref = torch.from_numpy(g[key])
+        assert torch.allclose(got, ref, rtol=1e-5, atol=1e-5 * ref.abs().max().item()), key
+
+
+def test_distance_is_squared_l2():
+    """Analytic: relu(x2 - 2xp + p2) == ||x - p||^2 within the f32 cancellation bound."""
+    x, protos, _ = po.synthetic_inputs(2, 64, 9, 7, 23, 1, seed=1)
+    d = po.l2_convolution(x, protos[:, :, None, None], torch.ones(23, 64, 1, 1))
+    xd = x.double().permute(0, 2, 3, 1).reshape(-1, 64)
+    exact = (torch.cdist(xd, protos.double()) ** 2).reshape(2, 9, 7, 23).permute(0, 3, 1, 2)
+    assert torch.allclose(d.double(), exact, atol=2e-6 * 128, rtol=1e-5)
+
+
+def test_known_answers():
+    """x = prototype -> d = 0 -> log(1/eps) = 9.2103; identity last layer reproduces the
+    set_last_layer_incorrect_connection(-0.5) logits."""
+    x, protos, _ = po.synthetic_inputs(1, 64, 2, 2, 4, 2, seed=2)
+    x[0, :, 1, 1] = protos[2]
+    d = po.l2_convolution(x, protos[:, :, None, None], torch.ones(4, 64, 1, 1))
+    assert d[0, 2, 1, 1].item() <= 1e-5
+    assert abs(po.distance_2_similarity(torch.zeros(1)).item() - np.log(1 / 1e-4)) < 1e-5
+    identity = po.class_identity(4, 2)
+    w = po.last_layer_init(identity)
+    assert torch.equal(w, torch.tensor([[1.0, 1.0, -0.5, -0.5], [-0.5, -0.5, 1.0, 1.0]]))
+    act = torch.tensor([[1.0, 2.0, 3.0, 4.0]])
+    assert torch.allclose(torch.nn.functional.linear(act, w), torch.tensor([[-0.5, 5.5]]))
+
+
+def test_push_oracle_reproduces_golden():
+    g = np.load(os.path.join(GOLDEN, "push_small.npz"))
+    x, protos, labels = g["x"], g["protos"], g["labels"]
+    n_img, C, h, w = x.shape
+    P = protos.shape[0]
+    state = pu.PushOracleState(P, C)
+    for i in range(n_img):
+        d = po.l2_convolution(torch.from_numpy(x[i:i + 1]), torch.from_numpy(protos)[:, :, None, None],
+                              torch.ones(P, C, 1, 1))[0]
+        assert np.allclose(d.numpy(), g["dist"][i], rtol=1e-6, atol=1e-5)
+        sets = pu.class_to_patch_index_dict(labels[i], h, w, 19)
+        assert np.array_equal(pu.bitmask_from_dict(sets, h, w), g["mask"][i])
+        pu.update_prototypes_on_image_core(state, x[i], g["dist"][i].transpose(1, 2, 0), labels[i],
+                                           g["proto_class"], 19, i, sets)
+    assert np.array_equal(state.global_min_proto_dist, g["global_min_proto_dist"])
+    assert np.array_equal(state.proto_rf_boxes, g["proto_rf_boxes"])
+    assert np.array_equal(state.winner_patch, g["winner_patch"])
+    uniq, dup = pu.dedup(state.global_min_fmap_patches)
+    assert np.array_equal(uniq, g["unique_index"])
+
+
+@pytest.mark.parametrize("H,W,h,w", [(64, 128, 8, 16), (100, 37, 13, 5), (250, 513, 33, 65)])
+def test_fast_bitmask_equals_reference_loop(H, W, h, w):
+    """Non-integer patch sizes (250/33, 513/65) exercise the float64 pixel->patch division."""
+    rng = np.random.default_rng(H)
+    y = rng.integers(0, 20, size=(H, W))
+    sets = pu.class_to_patch_index_dict(y, h, w, 19)
+    assert np.array_equal(pu.bitmask_from_dict(sets, h, w), pu.class_patch_bitmask_fast(y, h, w))
+
+
+def test_masked_argmin_fast_matches_loop():
+    rng = np.random.default_rng(5)
+    h, w, P, K = 6, 9, 12, 4
+    D = rng.random((h, w, P)).astype(np.float32)
+    y = rng.integers(0, K + 1, size=(30, 45))
+    pc = [p % K for p in range(P)]
+    sets = pu.class_to_patch_index_dict(y, h, w, K)
+    best, idx, _ = pu.masked_argmin_fast(D, pu.bitmask_from_dict(sets, h, w), pc)
+    st = pu.PushOracleState(P, 1)
+    pu.update_prototypes_on_image_core(st, np.zeros((1, h, w), np.float32), D, y, pc, K, 0, sets)
+    assert np.array_equal(st.winner_patch, idx)
+    assert np.array_equal(st.global_min_proto_dist.astype(np.float32), best)
