@@ -1,0 +1,118 @@
+// bf16_split.h — exact-ish f32 products on bf16 MFMA (v_mfma_f32_32x32x16_bf16) by operand
+// splitting, plus the XOR-swizzled LDS image helpers shared by the bf16 kernels.
+//
+// A float v is split into T bf16 terms v = t0 + t1 (+ t2) + e with |e| <= 2^-8T |v| (each
+// subtraction below is exact in f32). A product a*b is then the sum of the T(T+1)/2 largest
+// cross terms, accumulated in f32 by the MFMA:
+//   T = 2: a0b1 + a1b0 + a0b0              (3 MFMAs; |rel err| ~ 3*2^-16 per product)
+//   T = 3: a1b1 + a2b0 + a0b2 + a1b0 + a0b1 + a0b0   (6 MFMAs; f32-class accuracy)
+// (smallest terms first). At 16x the f32-MFMA rate this is 5.3x / 2.7x cheaper than
+// v_mfma_f32_32x32x2_f32 for the same products.
+//
+// MFMA 32x32x16 bf16 lane maps (cdna_hip_programming.md §3): lane l, h = l>>5:
+//   A: A[i = l&31][k = 8h + jj], jj = 0..7 (one 16-B fragment per lane)
+//   B: B[k = 8h + jj][j = l&31]
+//   C/D: same as every 32x32 shape: col = l&31, row = acc_row(r, h)
+// An accumulator used as the next B operand (or A operand, transposed product) supplies,
+// for k-step s (s = 0, 1 over the tile's 32 rows), registers 8s..8s+7: element jj of half h
+// is row 16s + 8(jj>>2) + 4h + (jj&3) — perm_row(). The other operand must follow it.
+#pragma once
+#include "protoseg_device.h"
+
+namespace protoseg {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16;
+
+__device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// v -> T bf16 terms, most significant first.
+template <int T>
+__device__ __forceinline__ void split_terms(float v, bf16 (&t)[T]) {
+  float rest = v;
+#pragma unroll
+  for (int i = 0; i < T; ++i) {
+    t[i] = static_cast<bf16>(rest);
+    rest = rest - static_cast<float>(t[i]);
+  }
+}
+
+// 8 floats -> T packed fragments.
+template <int T>
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8 (&out)[T]) {
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) {
+    bf16 t[T];
+    split_terms<T>(v[jj], t);
+#pragma unroll
+    for (int i = 0; i < T; ++i) out[i][jj] = t[i];
+  }
+}
+
+template <int T>
+__device__ __forceinline__ f32x16 mma_split(const bf16x8 (&a)[T], const bf16x8 (&b)[T], f32x16 acc) {
+  if constexpr (T == 1) {
+    acc = mfma_bf16(a[0], b[0], acc);
+  } else if constexpr (T == 2) {
+    acc = mfma_bf16(a[0], b[1], acc);
+    acc = mfma_bf16(a[1], b[0], acc);
+    acc = mfma_bf16(a[0], b[0], acc);
+  } else {
+    acc = mfma_bf16(a[1], b[1], acc);
+    acc = mfma_bf16(a[2], b[0], acc);
+    acc = mfma_bf16(a[0], b[2], acc);
+    acc = mfma_bf16(a[1], b[0], acc);
+    acc = mfma_bf16(a[0], b[1], acc);
+    acc = mfma_bf16(a[0], b[0], acc);
+  }
+  return acc;
+}
+
+// Row of element jj (half h, k-step s) when a 32x32 accumulator is used as an operand.
+__device__ __forceinline__ constexpr int perm_row(int s, int h, int jj) {
+  return 16 * s + 8 * (jj >> 2) + 4 * h + (jj & 3);
+}
+// Storage position e (0..31) of a permuted 32-element row -> logical index.
+__device__ __forceinline__ constexpr int perm_of(int e) { return perm_row(e >> 4, (e >> 3) & 1, e & 7); }
+
+// Accumulator registers 8s..8s+7 split into T operand fragments.
+template <int T>
+__device__ __forceinline__ void acc_operand(const f32x16& acc, int s, bf16x8 (&out)[T]) {
+  float v[8];
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) v[jj] = acc[8 * s + jj];
+  split8<T>(v, out);
+}
+
+// XOR swizzle of the 16-B chunk index for an LDS image whose rows hold CPR chunks, making
+// ds_read_b128 of 16 different rows at the same logical chunk conflict-free (the four
+// 16-lane groups of ds_read_b128, MI355X_MICROARCH.md §LDS).
+template <int CPR>
+__device__ __forceinline__ constexpr int swz(int row) {
+  static_assert(CPR == 4 || CPR == 8 || CPR == 16, "row length");
+  if constexpr (CPR == 4) return (row >> 2) & 3;
+  if constexpr (CPR == 8) return (row >> 1) & 7;
+  return row & 15;
+}
+
+// Element offset (in bf16 units) of chunk `chunk` of `row` in an image with CPR chunks per row.
+template <int CPR>
+__device__ __forceinline__ int img_off(int row, int chunk) {
+  return row * (CPR * 8) + ((chunk ^ swz<CPR>(row)) << 3);
+}
+
+template <int T>
+__device__ __forceinline__ void load_frag(const bf16* img, int plane_elems, int off, bf16x8 (&out)[T]) {
+#pragma unroll
+  for (int t = 0; t < T; ++t) out[t] = *reinterpret_cast<const bf16x8*>(img + t * plane_elems + off);
+}
+
+template <int T>
+__device__ __forceinline__ void store_frag(bf16* img, int plane_elems, int off, const bf16x8 (&in)[T]) {
+#pragma unroll
+  for (int t = 0; t < T; ++t) *reinterpret_cast<bf16x8*>(img + t * plane_elems + off) = in[t];
+}
+
+}  // namespace protoseg

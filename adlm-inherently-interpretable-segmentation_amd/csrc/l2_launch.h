@@ -1,0 +1,31 @@
+// l2_launch.h — internal interface between the C ABI (l2_layer.hip) and the two kernel
+// families of the prototype layer: exact f32-MFMA (l2_layer.hip) and bf16 split-MFMA
+// (l2_bf16.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+namespace protoseg {
+
+struct Geometry {
+  int C, P, Pp, K, HW;
+  int npix, ntiles;  // B*H*W pixels, 32-pixel tiles
+};
+
+// bf16 split family (C = 64). `terms` = 2 (3 products) or 3 (6 products).
+bool bf16_fwd_fits(const Geometry& g, int terms);
+bool bf16_bwd_x_fits(const Geometry& g, int terms);
+bool bf16_bwd_pw_fits(const Geometry& g, int terms);
+size_t bf16_bwd_pw_workspace(const Geometry& g);
+
+int launch_fwd_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const float* protos,
+                    const float* w_last, float eps, int act_kind, float* dist, float* act, float* logits,
+                    hipStream_t stream);
+int launch_bwd_x_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const float* protos,
+                      const float* w_last, float eps, int act_kind, const float* g_logits, const float* g_dist,
+                      void* g_x, hipStream_t stream);
+int launch_bwd_pw_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const float* protos,
+                       const float* w_last, float eps, int act_kind, const float* g_logits, const float* g_dist,
+                       float* g_protos, float* g_w, float* ws, hipStream_t stream);
+
+}  // namespace protoseg

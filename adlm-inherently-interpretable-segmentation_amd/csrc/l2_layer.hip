@@ -20,6 +20,7 @@
 //                      partial slabs, reduced by l2_bwd_reduce_kernel in a fixed order
 //                      (bitwise reproducible, no atomics).
 #include "protoseg_device.h"
+#include "l2_launch.h"
 #include "protoseg_host.h"
 
 namespace protoseg {
@@ -439,11 +440,6 @@ __global__ void l2_bwd_reduce_kernel(const float* __restrict__ slab_gp, const fl
 // ---------------------------------------------------------------------------------------
 // Host side.
 
-struct Geometry {
-  int C, P, Pp, K, HW;
-  int npix, ntiles;
-};
-
 int padded_protos(int P) { return static_cast<int>(ceil_div(P, 32) * 32); }
 
 size_t layer_lds_bytes(int C, int Pp) {
@@ -453,7 +449,7 @@ size_t layer_lds_bytes(int C, int Pp) {
 int nc_of(int C) { return C == 32 ? 1 : C == 64 ? 2 : C == 128 ? 4 : 0; }
 
 int validate(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P, int K,
-             int act_kind, Geometry* geo) {
+             int act_kind, int precision, Geometry* geo) {
   if (!x || !protos) return fail(PROTOSEG_ERR_INVALID, "x and protos must be non-null");
   if (B <= 0 || H <= 0 || W <= 0 || P <= 0 || K < 0)
     return fail(PROTOSEG_ERR_INVALID, "bad shape B=%d H=%d W=%d P=%d K=%d", B, H, W, P, K);
@@ -461,6 +457,8 @@ int validate(const void* x, int x_dtype, int B, int C, int H, int W, const float
     return fail(PROTOSEG_ERR_UNSUPPORTED, "x_dtype %d (f32 or bf16 only)", x_dtype);
   if (act_kind != PROTOSEG_ACT_LOG && act_kind != PROTOSEG_ACT_LINEAR)
     return fail(PROTOSEG_ERR_UNSUPPORTED, "act_kind %d", act_kind);
+  if (precision < PROTOSEG_PREC_BF16X3 || precision > PROTOSEG_PREC_F32)
+    return fail(PROTOSEG_ERR_UNSUPPORTED, "precision %d", precision);
   if (!protoseg_l2_supported(C, P, K))
     return fail(PROTOSEG_ERR_UNSUPPORTED, "C=%d P=%d K=%d outside the kernel family", C, P, K);
   geo->C = C;
@@ -498,47 +496,49 @@ int pw_splits(long long ntiles, int Pp) {
 template <typename TX, int NC>
 int launch_fwd(const Geometry& geo, const void* x, const float* protos, const float* w_last, float eps,
                int act_kind, float* dist, float* act, float* logits, hipStream_t stream) {
-  auto kernel = l2_fwd_kernel<TX, NC>;
   if (int st = ensure_lds<l2_fwd_kernel<TX, NC>>()) return st;
   const size_t lds = layer_lds_bytes(geo.C, geo.Pp);
-  hipLaunchKernelGGL(kernel, dim3(layer_grid(geo)), dim3(kFwdWaves * 64), lds, stream,
+  hipLaunchKernelGGL((l2_fwd_kernel<TX, NC>), dim3(layer_grid(geo)), dim3(kFwdWaves * 64), lds, stream,
                      static_cast<const TX*>(x), geo.HW, geo.npix, protos, geo.P, geo.Pp, w_last, geo.K, eps,
                      act_kind, dist, act, logits);
   return check_launch("l2_fwd_kernel");
 }
 
 template <typename TX, int NC>
-int launch_bwd(const Geometry& geo, const void* x, const float* protos, const float* w_last, float eps,
-               int act_kind, const float* g_logits, const float* g_dist, void* g_x, float* g_protos, float* g_w,
-               float* ws, hipStream_t stream) {
-  if (g_x) {
-    auto kernel = l2_bwd_x_kernel<TX, NC>;
-    if (int st = ensure_lds<l2_bwd_x_kernel<TX, NC>>()) return st;
-    hipLaunchKernelGGL(kernel, dim3(layer_grid(geo)), dim3(kFwdWaves * 64), layer_lds_bytes(geo.C, geo.Pp),
-                       stream, static_cast<const TX*>(x), geo.HW, geo.npix, protos, geo.P, geo.Pp, w_last, geo.K,
-                       eps, act_kind, g_logits, g_dist, static_cast<TX*>(g_x));
-    if (int st = check_launch("l2_bwd_x_kernel")) return st;
-  }
-  if (g_protos || g_w) {
-    const int S = pw_splits(geo.ntiles, geo.Pp);
-    float* slab_gp = ws;
-    float* slab_gw = slab_gp + static_cast<size_t>(S) * geo.Pp * geo.C;
-    float* slab_gs = slab_gw + static_cast<size_t>(S) * 32 * geo.Pp;
-    auto kernel = l2_bwd_pw_kernel<TX, NC>;
-    const size_t lds = (static_cast<size_t>(geo.C) * 32 + 32 * 32 + static_cast<size_t>(kPwWaves) * geo.C * kLdx) *
-                       sizeof(float);
-    if (int st = ensure_lds<l2_bwd_pw_kernel<TX, NC>>()) return st;
-    hipLaunchKernelGGL(kernel, dim3(geo.Pp / 32, S), dim3(kPwWaves * 64), lds, stream,
-                       static_cast<const TX*>(x), geo.HW, geo.npix, protos, geo.P, geo.Pp, w_last, geo.K, eps,
-                       act_kind, g_logits, g_dist, slab_gp, slab_gw, slab_gs);
-    if (int st = check_launch("l2_bwd_pw_kernel")) return st;
-    const long long n = static_cast<long long>(geo.P) * (geo.C > geo.K ? geo.C : geo.K);
-    hipLaunchKernelGGL(l2_bwd_reduce_kernel, dim3(static_cast<unsigned>(ceil_div(n, 256))), dim3(256), 0, stream,
-                       slab_gp, slab_gw, slab_gs, S, geo.P, geo.Pp, geo.C, geo.K, protos, g_protos,
-                       g_logits ? g_w : nullptr);
-    if (int st = check_launch("l2_bwd_reduce_kernel")) return st;
-  }
-  return PROTOSEG_OK;
+int launch_bwd_x(const Geometry& geo, const void* x, const float* protos, const float* w_last, float eps,
+                 int act_kind, const float* g_logits, const float* g_dist, void* g_x, hipStream_t stream) {
+  if (int st = ensure_lds<l2_bwd_x_kernel<TX, NC>>()) return st;
+  hipLaunchKernelGGL((l2_bwd_x_kernel<TX, NC>), dim3(layer_grid(geo)), dim3(kFwdWaves * 64),
+                     layer_lds_bytes(geo.C, geo.Pp), stream, static_cast<const TX*>(x), geo.HW, geo.npix, protos,
+                     geo.P, geo.Pp, w_last, geo.K, eps, act_kind, g_logits, g_dist, static_cast<TX*>(g_x));
+  return check_launch("l2_bwd_x_kernel");
+}
+
+size_t f32_pw_workspace(const Geometry& geo) {
+  const size_t S = static_cast<size_t>(pw_splits(geo.ntiles, geo.Pp));
+  return (S * geo.Pp * geo.C + S * 32 * geo.Pp + S * geo.Pp) * sizeof(float);
+}
+
+template <typename TX, int NC>
+int launch_bwd_pw(const Geometry& geo, const void* x, const float* protos, const float* w_last, float eps,
+                  int act_kind, const float* g_logits, const float* g_dist, float* g_protos, float* g_w, float* ws,
+                  hipStream_t stream) {
+  const int S = pw_splits(geo.ntiles, geo.Pp);
+  float* slab_gp = ws;
+  float* slab_gw = slab_gp + static_cast<size_t>(S) * geo.Pp * geo.C;
+  float* slab_gs = slab_gw + static_cast<size_t>(S) * 32 * geo.Pp;
+  const size_t lds = (static_cast<size_t>(geo.C) * 32 + 32 * 32 + static_cast<size_t>(kPwWaves) * geo.C * kLdx) *
+                     sizeof(float);
+  if (int st = ensure_lds<l2_bwd_pw_kernel<TX, NC>>()) return st;
+  hipLaunchKernelGGL((l2_bwd_pw_kernel<TX, NC>), dim3(geo.Pp / 32, S), dim3(kPwWaves * 64), lds, stream,
+                     static_cast<const TX*>(x), geo.HW, geo.npix, protos, geo.P, geo.Pp, w_last, geo.K, eps, act_kind,
+                     g_logits, g_dist, slab_gp, slab_gw, slab_gs);
+  if (int st = check_launch("l2_bwd_pw_kernel")) return st;
+  const long long n = static_cast<long long>(geo.P) * (geo.C > geo.K ? geo.C : geo.K);
+  hipLaunchKernelGGL(l2_bwd_reduce_kernel, dim3(static_cast<unsigned>(ceil_div(n, 256))), dim3(256), 0, stream,
+                     slab_gp, slab_gw, slab_gs, S, geo.P, geo.Pp, geo.C, geo.K, protos, g_protos,
+                     g_logits ? g_w : nullptr);
+  return check_launch("l2_bwd_reduce_kernel");
 }
 
 template <typename Fn>
@@ -556,6 +556,23 @@ int dispatch(int x_dtype, int C, Fn&& fn) {
   return fail(PROTOSEG_ERR_UNSUPPORTED, "C=%d", C);
 }
 
+// Split terms of the bf16 family for a precision request; 0 = use the f32-MFMA family.
+int terms_of(int precision) {
+  return precision == PROTOSEG_PREC_BF16X3 ? 2 : precision == PROTOSEG_PREC_BF16X6 ? 3 : 0;
+}
+
+Geometry geometry_of(int B, int C, int H, int W, int P, int K) {
+  Geometry g;
+  g.C = C;
+  g.P = P;
+  g.Pp = padded_protos(P);
+  g.K = K;
+  g.HW = H * W;
+  g.npix = B * H * W;
+  g.ntiles = static_cast<int>(ceil_div(g.npix, 32));
+  return g;
+}
+
 }  // namespace
 
 }  // namespace protoseg
@@ -568,35 +585,40 @@ extern "C" int protoseg_l2_supported(int C, int P, int K) {
 }
 
 extern "C" int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P,
-                               const float* w_last, int K, float eps, int act_kind, float* dist_out,
+                               const float* w_last, int K, float eps, int act_kind, int precision, float* dist_out,
                                float* act_out, float* logits_out, protoseg_stream_t stream) {
   Geometry geo;
-  if (int st = validate(x, x_dtype, B, C, H, W, protos, P, K, act_kind, &geo)) return st;
+  if (int st = validate(x, x_dtype, B, C, H, W, protos, P, K, act_kind, precision, &geo)) return st;
   if (logits_out && (!w_last || K <= 0)) return fail(PROTOSEG_ERR_INVALID, "logits_out needs w_last and K > 0");
   if (!dist_out && !act_out && !logits_out) return PROTOSEG_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int terms = terms_of(precision);
+  if (terms && bf16_fwd_fits(geo, terms))
+    return launch_fwd_bf16(geo, x_dtype == PROTOSEG_BF16, terms, x, protos, w_last, eps, act_kind, dist_out, act_out,
+                           logits_out, s);
   return dispatch(x_dtype, C, [&](auto tx, auto nc) {
     using TX = std::remove_pointer_t<decltype(tx)>;
     return launch_fwd<TX, decltype(nc)::value>(geo, x, protos, w_last, eps, act_kind, dist_out, act_out,
-                                               logits_out, reinterpret_cast<hipStream_t>(stream));
+                                               logits_out, s);
   });
 }
 
 extern "C" size_t protoseg_l2_bwd_workspace_size(int B, int C, int H, int W, int P, int K) {
-  (void)K;
   if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || P <= 0) return 0;
-  const int Pp = padded_protos(P);
-  const long long ntiles = ceil_div(static_cast<long long>(B) * H * W, 32);
-  const size_t S = static_cast<size_t>(pw_splits(ntiles, Pp));
-  const size_t floats = S * Pp * C + S * 32 * Pp + S * Pp;
-  return ((floats * sizeof(float) + 255) / 256) * 256;
+  if (static_cast<long long>(B) * H * W >= (1LL << 31)) return 0;
+  const Geometry g = geometry_of(B, C, H, W, P, K);
+  size_t need = f32_pw_workspace(g);
+  const size_t b16 = bf16_bwd_pw_workspace(g);
+  if (C == 64 && b16 > need) need = b16;
+  return ((need + 255) / 256) * 256;
 }
 
 extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P,
-                               const float* w_last, int K, float eps, int act_kind, const float* g_logits,
-                               const float* g_dist, void* g_x, float* g_protos, float* g_w, void* workspace,
-                               size_t workspace_bytes, protoseg_stream_t stream) {
+                               const float* w_last, int K, float eps, int act_kind, int precision,
+                               const float* g_logits, const float* g_dist, void* g_x, float* g_protos, float* g_w,
+                               void* workspace, size_t workspace_bytes, protoseg_stream_t stream) {
   Geometry geo;
-  if (int st = validate(x, x_dtype, B, C, H, W, protos, P, K, act_kind, &geo)) return st;
+  if (int st = validate(x, x_dtype, B, C, H, W, protos, P, K, act_kind, precision, &geo)) return st;
   if (g_logits && (!w_last || K <= 0)) return fail(PROTOSEG_ERR_INVALID, "g_logits needs w_last and K > 0");
   if (g_w && !g_logits) return fail(PROTOSEG_ERR_INVALID, "g_w needs g_logits");
   if (g_protos || g_w) {
@@ -604,18 +626,38 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
     if (!workspace || workspace_bytes < need)
       return fail(PROTOSEG_ERR_INVALID, "workspace %zu B < %zu B", workspace_bytes, need);
   }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (!g_logits && !g_dist) {  // no upstream gradient: every output is zero
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const size_t esz = x_dtype == PROTOSEG_F32 ? 4 : 2;
-    if (g_x && hipMemsetAsync(g_x, 0, geo.npix * C * esz, s) != hipSuccess) return check_launch("memset g_x");
+    if (g_x && hipMemsetAsync(g_x, 0, static_cast<size_t>(geo.npix) * C * esz, s) != hipSuccess)
+      return check_launch("memset g_x");
     if (g_protos && hipMemsetAsync(g_protos, 0, static_cast<size_t>(P) * C * 4, s) != hipSuccess)
       return check_launch("memset g_protos");
     return PROTOSEG_OK;
   }
-  return dispatch(x_dtype, C, [&](auto tx, auto nc) {
-    using TX = std::remove_pointer_t<decltype(tx)>;
-    return launch_bwd<TX, decltype(nc)::value>(geo, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_x,
-                                               g_protos, g_w, static_cast<float*>(workspace),
-                                               reinterpret_cast<hipStream_t>(stream));
-  });
+  const int terms = terms_of(precision);
+  const bool xb = x_dtype == PROTOSEG_BF16;
+  float* ws = static_cast<float*>(workspace);
+  if (g_x) {
+    int st;
+    if (terms && bf16_bwd_x_fits(geo, terms))
+      st = launch_bwd_x_bf16(geo, xb, terms, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_x, s);
+    else
+      st = dispatch(x_dtype, C, [&](auto tx, auto nc) {
+        using TX = std::remove_pointer_t<decltype(tx)>;
+        return launch_bwd_x<TX, decltype(nc)::value>(geo, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_x, s);
+      });
+    if (st) return st;
+  }
+  if (g_protos || g_w) {
+    if (terms && bf16_bwd_pw_fits(geo, terms))
+      return launch_bwd_pw_bf16(geo, xb, terms, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_protos, g_w, ws,
+                                s);
+    return dispatch(x_dtype, C, [&](auto tx, auto nc) {
+      using TX = std::remove_pointer_t<decltype(tx)>;
+      return launch_bwd_pw<TX, decltype(nc)::value>(geo, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_protos,
+                                                    g_w, ws, s);
+    });
+  }
+  return PROTOSEG_OK;
 }

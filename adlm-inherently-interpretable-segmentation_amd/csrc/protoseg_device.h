@@ -83,6 +83,13 @@ __device__ __forceinline__ void wave_lds_fence() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
+// Bitwise OR of a 32-bit value over the 64 lanes of the wave (result in every lane).
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) v |= __shfl_xor(v, m);
+  return v;
+}
+
 __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m) {
   const uint32_t lo = __shfl_xor(static_cast<uint32_t>(v), m);
   const uint32_t hi = __shfl_xor(static_cast<uint32_t>(v >> 32), m);

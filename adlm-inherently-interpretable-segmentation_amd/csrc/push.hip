@@ -85,6 +85,8 @@ __global__ __launch_bounds__(kArgminWaves * 64) void push_argmin_kernel(
   }
   const int cls = pvalid ? proto_class[p] : -1;
   const bool active = cls >= 0 && cls < 32;
+  // classes of this wave's 32 prototypes: a tile without any of them is skipped
+  const uint32_t wave_classes = wave_or(active ? (1u << cls) : 0u);
   const float* xi = x + static_cast<size_t>(img) * C * HW;
   const uint32_t* mi = mask + static_cast<size_t>(img) * HW;
 
@@ -107,7 +109,7 @@ __global__ __launch_bounds__(kArgminWaves * 64) void push_argmin_kernel(
     const uint32_t mk0 = mi[valid ? n : 0];
     const uint32_t mk = valid ? mk0 : 0u;
     // skip tiles holding no patch of any class of this wave's prototypes
-    if (!__any(active && ((mk >> (cls & 31)) & 1u))) continue;
+    if ((wave_or(mk) & wave_classes) == 0u) continue;
 
     f32x16 acc = zero16();
 #pragma unroll

@@ -26,6 +26,9 @@ OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_HIP = 0, 1, 2, 3
 F32, BF16, I64, I32, U8 = 0, 1, 2, 3, 4
 # enum protoseg_act
 ACT_LOG, ACT_LINEAR = 0, 1
+# enum protoseg_precision
+PREC_BF16X3, PREC_BF16X6, PREC_F32 = 0, 1, 2
+PRECISIONS = {"bf16x3": PREC_BF16X3, "bf16x6": PREC_BF16X6, "f32": PREC_F32}
 
 _vp, _i, _f, _sz, _i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_int64
 
@@ -34,10 +37,10 @@ SIGNATURES = {
     "protoseg_version": (_i, []),
     "protoseg_last_error": (ctypes.c_char_p, []),
     "protoseg_l2_supported": (_i, [_i, _i, _i]),
-    "protoseg_l2_fwd": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _vp, _vp, _vp, _vp]),
+    "protoseg_l2_fwd": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _i, _vp, _vp, _vp, _vp]),
     "protoseg_l2_bwd_workspace_size": (_sz, [_i, _i, _i, _i, _i, _i]),
-    "protoseg_l2_bwd": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _vp, _vp, _vp, _vp, _vp, _vp, _sz,
-                             _vp]),
+    "protoseg_l2_bwd": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp,
+                             _sz, _vp]),
     "protoseg_patch_class_mask": (_i, [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp]),
     "protoseg_push_argmin": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp]),
     "protoseg_push_merge": (_i, [_vp, _i, _i64, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]),

@@ -38,6 +38,7 @@ class PPNet(nn.Module):
         super().__init__()
         self.img_size = img_size
         self.epsilon = 1e-4
+        self.precision = None  # None: ops.DEFAULT_PRECISION ("bf16x3"); or "bf16x6" / "f32"
         self.bottleneck_stride = bottleneck_stride
         self.patch_classification = patch_classification
         self.prototype_vectors = nn.Parameter(torch.rand(prototype_shape), requires_grad=True)  # model.py:54
@@ -131,7 +132,7 @@ class PPNet(nn.Module):
 
     def _l2_convolution(self, x):
         """model.py:203-221 on the HIP kernel: relu(||x||^2 - 2 x.p + ||p||^2), [B, P, H, W]."""
-        return ops.l2_distances(x, self.prototype_vectors, self.epsilon)
+        return ops.l2_distances(x, self.prototype_vectors, self.epsilon, getattr(self, "precision", None))
 
     def prototype_distances(self, x):
         return self._l2_convolution(self.conv_features(x))
@@ -173,7 +174,8 @@ class PPNet(nn.Module):
                 return (logits, acts) if return_activations else (logits, distances)
             distances, logits, acts = ops.prototype_layer(
                 conv_features, self.prototype_vectors, self.last_layer.weight, self.epsilon, act_name,
-                with_dist=not return_activations, with_logits=True, with_act=return_activations)
+                with_dist=not return_activations, with_logits=True, with_act=return_activations,
+                precision=getattr(self, "precision", None))
             return (logits, acts) if return_activations else (logits, distances)
 
         # ProtoPNet global min pooling (model.py:284-299); distances from the kernel

@@ -10,6 +10,7 @@ autograd graph of those ops (the reference has no custom backward).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -18,6 +19,17 @@ from torch import Tensor
 from . import _lib
 
 ACT_KINDS = {"log": _lib.ACT_LOG, "linear": _lib.ACT_LINEAR}
+PRECISIONS = _lib.PRECISIONS
+# bf16x3: bf16 MFMA on 2-term split operands (|rel err| ~1e-5 on distances, the default);
+# bf16x6: 3-term split (f32-class); f32: v_mfma_f32_32x32x2_f32 (exact f32 fma chain).
+DEFAULT_PRECISION = os.environ.get("PROTOSEG_PRECISION", "bf16x3")
+
+
+def precision_code(precision: Optional[str]) -> int:
+    name = DEFAULT_PRECISION if precision is None else precision
+    if name not in PRECISIONS:
+        raise _lib.ProtosegError(f"precision {name!r} unknown (one of {sorted(PRECISIONS)})")
+    return PRECISIONS[name]
 
 
 def _x_dtype(x: Tensor) -> int:
@@ -33,8 +45,8 @@ def supported(C: int, P: int, K: int) -> bool:
 
 
 @torch.library.custom_op("protoseg::l2_forward", mutates_args=(), device_types="cuda")
-def l2_forward(x: Tensor, protos: Tensor, w_last: Tensor, eps: float, act_kind: int, with_dist: bool,
-               with_logits: bool, with_act: bool) -> Tuple[Tensor, Tensor, Tensor]:
+def l2_forward(x: Tensor, protos: Tensor, w_last: Tensor, eps: float, act_kind: int, precision: int,
+               with_dist: bool, with_logits: bool, with_act: bool) -> Tuple[Tensor, Tensor, Tensor]:
     """Fused prototype-layer forward. Returns (dist [B,P,H,W], logits [B,H,W,K], act [B*H*W,P]);
     outputs not requested are empty tensors."""
     dev = _lib.require_device(x, protos, w_last)
@@ -49,13 +61,13 @@ def l2_forward(x: Tensor, protos: Tensor, w_last: Tensor, eps: float, act_kind: 
     act = torch.empty((B * H * W, P) if with_act else (0,), **f32)
     with torch.cuda.device(dev):
         _lib.call("protoseg_l2_fwd", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P,
-                  _lib.ptr(w_last), K, float(eps), int(act_kind), _lib.ptr(dist), _lib.ptr(act),
+                  _lib.ptr(w_last), K, float(eps), int(act_kind), int(precision), _lib.ptr(dist), _lib.ptr(act),
                   _lib.ptr(logits), _lib.stream_of(dev))
     return dist, logits, act
 
 
 @l2_forward.register_fake
-def _(x, protos, w_last, eps, act_kind, with_dist, with_logits, with_act):
+def _(x, protos, w_last, eps, act_kind, precision, with_dist, with_logits, with_act):
     B, C, H, W = x.shape
     P, K = protos.shape[0], w_last.shape[0]
     e = lambda *s: x.new_empty(s, dtype=torch.float32)  # noqa: E731
@@ -65,7 +77,7 @@ def _(x, protos, w_last, eps, act_kind, with_dist, with_logits, with_act):
 
 @torch.library.custom_op("protoseg::l2_backward", mutates_args=(), device_types="cuda")
 def l2_backward(x: Tensor, protos: Tensor, w_last: Tensor, g_logits: Optional[Tensor], g_dist: Optional[Tensor],
-                eps: float, act_kind: int, need_x: bool, need_protos: bool,
+                eps: float, act_kind: int, precision: int, need_x: bool, need_protos: bool,
                 need_w: bool) -> Tuple[Tensor, Tensor, Tensor]:
     """Backward of l2_forward with respect to (x, protos, w_last); unrequested grads are empty."""
     dev = _lib.require_device(x, protos, w_last, g_logits, g_dist)
@@ -87,13 +99,14 @@ def l2_backward(x: Tensor, protos: Tensor, w_last: Tensor, g_logits: Optional[Te
     ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8) if ws_bytes else None
     with torch.cuda.device(dev):
         _lib.call("protoseg_l2_bwd", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P, _lib.ptr(w_last), K,
-                  float(eps), int(act_kind), _lib.ptr(g_logits), _lib.ptr(g_dist), _lib.ptr(g_x), _lib.ptr(g_p),
+                  float(eps), int(act_kind), int(precision), _lib.ptr(g_logits), _lib.ptr(g_dist), _lib.ptr(g_x),
+                  _lib.ptr(g_p),
                   _lib.ptr(g_w), _lib.ptr(ws), ws_bytes, _lib.stream_of(dev))
     return g_x, g_p, g_w
 
 
 @l2_backward.register_fake
-def _(x, protos, w_last, g_logits, g_dist, eps, act_kind, need_x, need_protos, need_w):
+def _(x, protos, w_last, g_logits, g_dist, eps, act_kind, precision, need_x, need_protos, need_w):
     B, C, H, W = x.shape
     P, K = protos.shape[0], w_last.shape[0]
     need_w = need_w and g_logits is not None
@@ -103,10 +116,11 @@ def _(x, protos, w_last, g_logits, g_dist, eps, act_kind, need_x, need_protos, n
 
 
 def _setup_context(ctx, inputs, output):
-    x, protos, w_last, eps, act_kind, with_dist, with_logits, with_act = inputs
+    x, protos, w_last, eps, act_kind, precision, with_dist, with_logits, with_act = inputs
     ctx.save_for_backward(x, protos, w_last)
     ctx.eps = eps
     ctx.act_kind = act_kind
+    ctx.precision = precision
     ctx.set_materialize_grads(False)  # unused outputs give None, not a zero-filled [B,P,H,W]
 
 
@@ -116,11 +130,11 @@ def _backward(ctx, g_dist, g_logits, g_act):
     x, protos, w_last = ctx.saved_tensors
     need_x, need_p, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
     if g_dist is None and g_logits is None:
-        return None, None, None, None, None, None, None, None
-    g_x, g_p, g_w = l2_backward(x, protos, w_last, g_logits, g_dist, ctx.eps, ctx.act_kind, need_x, need_p,
-                                need_w and g_logits is not None)
+        return None, None, None, None, None, None, None, None, None
+    g_x, g_p, g_w = l2_backward(x, protos, w_last, g_logits, g_dist, ctx.eps, ctx.act_kind, ctx.precision, need_x,
+                                need_p, need_w and g_logits is not None)
     return (g_x if need_x else None, g_p if need_p else None, g_w if (need_w and g_w.numel()) else None,
-            None, None, None, None, None)
+            None, None, None, None, None, None)
 
 
 torch.library.register_autograd("protoseg::l2_forward", _backward, setup_context=_setup_context)
@@ -128,7 +142,7 @@ torch.library.register_autograd("protoseg::l2_forward", _backward, setup_context
 
 def prototype_layer(x: Tensor, prototype_vectors: Tensor, last_layer_weight: Tensor, eps: float = 1e-4,
                     activation: str = "log", with_dist: bool = True, with_logits: bool = True,
-                    with_act: bool = False) -> Tuple[Tensor, Tensor, Tensor]:
+                    with_act: bool = False, precision: Optional[str] = None) -> Tuple[Tensor, Tensor, Tensor]:
     """Distances, logits and activations of the PPNet prototype layer (1x1 prototypes).
 
     x: [B, C, H, W] add-on-layer output (float32 or bfloat16); prototype_vectors: [P, C, 1, 1]
@@ -143,10 +157,10 @@ def prototype_layer(x: Tensor, prototype_vectors: Tensor, last_layer_weight: Ten
     if tuple(prototype_vectors.shape[2:]) not in ((), (1, 1)):
         raise _lib.ProtosegError(f"only 1x1 prototypes are supported, got {tuple(prototype_vectors.shape)}")
     return torch.ops.protoseg.l2_forward(x, protos, last_layer_weight, float(eps), ACT_KINDS[activation],
-                                         with_dist, with_logits, with_act)
+                                         precision_code(precision), with_dist, with_logits, with_act)
 
 
-def l2_distances(x: Tensor, prototype_vectors: Tensor, eps: float = 1e-4) -> Tensor:
+def l2_distances(x: Tensor, prototype_vectors: Tensor, eps: float = 1e-4, precision: Optional[str] = None) -> Tensor:
     """model.py:203-221 _l2_convolution: squared L2 distance map [B, P, H, W]."""
     w_dummy = x.new_zeros((1, prototype_vectors.shape[0]), dtype=torch.float32)
-    return prototype_layer(x, prototype_vectors, w_dummy, eps, "log", True, False, False)[0]
+    return prototype_layer(x, prototype_vectors, w_dummy, eps, "log", True, False, False, precision)[0]

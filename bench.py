@@ -39,6 +39,11 @@ from protoseg_amd.distributed import init_from_env  # noqa: E402
 
 PEAK_HBM_GBPS = 8000.0       # MI355X_MICROARCH.md chip table (spec)
 PEAK_F32_MFMA_TFLOPS = 157.3  # dense f32-input MFMA (v_mfma_f32_32x32x2_f32), MI355X_MICROARCH.md
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # dense bf16 MFMA (spec, no sparsity), MI355X_MICROARCH.md
+# Peak rate of f32-product FLOPs per precision mode: the bf16 split modes execute 3 or 6
+# bf16 MFMA products per algorithmic f32 product (bf16_split.h).
+PRODUCT_PEAK_TFLOPS = {"bf16x3": PEAK_BF16_MFMA_TFLOPS / 3, "bf16x6": PEAK_BF16_MFMA_TFLOPS / 6,
+                       "f32": PEAK_F32_MFMA_TFLOPS}
 SEED = 20220227
 
 
@@ -53,7 +58,7 @@ def baseline_metric() -> str:
 class LayerStep:
     """Preallocated buffers + direct C-ABI launches (no per-step allocation)."""
 
-    def __init__(self, B, C, h, w, P, K, x_dtype, device, seed):
+    def __init__(self, B, C, h, w, P, K, x_dtype, device, seed, precision="bf16x3"):
         gen = torch.Generator(device="cpu").manual_seed(seed)
         self.B, self.C, self.h, self.w, self.P, self.K = B, C, h, w, P, K
         x = torch.sigmoid(2.0 * torch.randn(B, C, h, w, generator=gen))
@@ -77,24 +82,25 @@ class LayerStep:
         self.xdt = _lib.F32 if x_dtype == torch.float32 else _lib.BF16
         self.device = device
         self.grad_flat = torch.empty(P * C + K * P, **f32)
+        self.prec = _lib.PRECISIONS[precision]
 
     def _stream(self):
         return _lib.stream_of(self.device)
 
     def fwd(self):
         _lib.call("protoseg_l2_fwd", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w, _lib.ptr(self.protos),
-                  self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, _lib.ptr(self.dist), ctypes.c_void_p(None),
+                  self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec, _lib.ptr(self.dist), ctypes.c_void_p(None),
                   _lib.ptr(self.logits), self._stream())
 
     def bwd_x(self):
         _lib.call("protoseg_l2_bwd", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w, _lib.ptr(self.protos),
-                  self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, _lib.ptr(self.g_logits),
+                  self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec, _lib.ptr(self.g_logits),
                   ctypes.c_void_p(None), _lib.ptr(self.g_x), ctypes.c_void_p(None), ctypes.c_void_p(None),
                   ctypes.c_void_p(None), 0, self._stream())
 
     def bwd_pw(self):
         _lib.call("protoseg_l2_bwd", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w, _lib.ptr(self.protos),
-                  self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, _lib.ptr(self.g_logits),
+                  self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec, _lib.ptr(self.g_logits),
                   ctypes.c_void_p(None), ctypes.c_void_p(None), _lib.ptr(self.g_p), _lib.ptr(self.g_w),
                   _lib.ptr(self.ws), self.ws_bytes, self._stream())
 
@@ -104,26 +110,34 @@ class LayerStep:
             self.grad_flat[self.P * self.C:].copy_(self.g_w.view(-1))
             dist.all_reduce(self.grad_flat)
 
+    def kernel_names(self):
+        """rocprof names of the kernels behind the fwd / bwd_x / bwd_pw calls (bwd_pw's call
+        also runs the slab-reduce kernel, timed inside its segment)."""
+        sfx = "" if self.prec == _lib.PREC_F32 or self.C != 64 else "_bf16"
+        return [f"l2_fwd{sfx}_kernel", f"l2_bwd_x{sfx}_kernel", f"l2_bwd_pw{sfx}_kernel"]
+
     # algorithmic work per launch (unpadded P, K; SURVEY.md §8d)
     def work(self):
         n = self.B * self.h * self.w
         xb = self.x.element_size()
         mm = 2.0 * n * self.P * self.C
         last = 2.0 * n * self.P * self.K
+        f, x, pw = self.kernel_names()
         return {
-            "l2_fwd_kernel": (mm + last + 2.0 * n * self.C, n * self.C * xb + n * self.P * 4 + n * self.K * 4),
-            "l2_bwd_x_kernel": (2 * mm + last, n * self.C * xb + n * self.K * 4 + n * self.C * xb),
-            "l2_bwd_pw_kernel": (2 * mm + 2 * last, n * self.C * xb + n * self.K * 4),
+            f: (mm + last + 2.0 * n * self.C, n * self.C * xb + n * self.P * 4 + n * self.K * 4),
+            x: (2 * mm + last, n * self.C * xb + n * self.K * 4 + n * self.C * xb),
+            pw: (2 * mm + 2 * last, n * self.C * xb + n * self.K * 4),
         }
 
 
-def roofline_entry(flops, nbytes, seconds):
-    t_mfma = flops / (PEAK_F32_MFMA_TFLOPS * 1e12)
+def roofline_entry(flops, nbytes, seconds, precision="f32"):
+    peak = PRODUCT_PEAK_TFLOPS[precision]
+    t_mfma = flops / (peak * 1e12)
     t_hbm = nbytes / (PEAK_HBM_GBPS * 1e9)
     if t_mfma >= t_hbm:
         ach = flops / seconds / 1e12
-        return {"bound": "mfma", "achieved": round(ach, 3), "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(ach / PEAK_F32_MFMA_TFLOPS, 4)}
+        return {"bound": "mfma", "achieved": round(ach, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
+                "frac": round(ach / peak, 4)}
     ach = nbytes / seconds / 1e9
     return {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
             "frac": round(ach / PEAK_HBM_GBPS, 4)}
@@ -147,7 +161,7 @@ def time_layer(step: LayerStep, steps: int, warmup: int, world: int):
         step.bwd_pw()
         step.allreduce(world)
     torch.cuda.synchronize()
-    names = ["l2_fwd_kernel", "l2_bwd_x_kernel", "l2_bwd_pw_kernel"]
+    names = step.kernel_names()
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
     if world > 1:
         dist.barrier()
@@ -240,7 +254,7 @@ def time_push(n_img, steps, warmup, device, C=64, H=1024, W=2048, h=129, w=257, 
     return {"ms_per_img": round(elapsed / (steps * n_img) * 1e3, 4), "images_per_call": n_img,
             "workload": f"push mask+argmin+merge, labels {H}x{W} u8, map {C}x{h}x{w} f32, P={P}, K={K}",
             "argmin_kernel_ms_per_img": round(argmin_s / n_img * 1e3, 4),
-            "roofline": roofline_entry(flops, nbytes, argmin_s) | {"kernel": "push_argmin_kernel"}}
+            "roofline": roofline_entry(flops, nbytes, argmin_s, "f32") | {"kernel": "push_argmin_kernel"}}
 
 
 def cpu_push_baseline(budget_s, C=64, H=1024, W=2048, h=129, w=257, P=190, K=19):
@@ -274,6 +288,8 @@ def main():
     ap.add_argument("--channels", type=int, default=64)
     ap.add_argument("--fmap", type=int, default=65, help="feature-map side (513 crop -> 65)")
     ap.add_argument("--x-dtype", choices=["f32", "bf16"], default="f32")
+    ap.add_argument("--precision", choices=["bf16x3", "bf16x6", "f32"], default="bf16x3",
+                    help="product arithmetic of the prototype layer (bf16_split.h)")
     ap.add_argument("--push-images", type=int, default=8)
     ap.add_argument("--push-steps", type=int, default=5)
     ap.add_argument("--no-push", action="store_true")
@@ -289,7 +305,7 @@ def main():
     x_dtype = torch.float32 if args.x_dtype == "f32" else torch.bfloat16
 
     step = LayerStep(args.batch, args.channels, args.fmap, args.fmap, args.protos, args.classes, x_dtype, device,
-                     SEED + rank)
+                     SEED + rank, args.precision)
     elapsed, per_kernel = time_layer(step, args.steps, args.warmup, world)
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
@@ -306,8 +322,9 @@ def main():
         work = step.work()
         dominant = max(per_kernel, key=per_kernel.get)
         flops, nbytes = work[dominant]
-        roof = roofline_entry(flops, nbytes, per_kernel[dominant])
-        config_key = f"B{args.batch}_C{args.channels}_{args.fmap}x{args.fmap}_P{args.protos}_K{args.classes}_{args.x_dtype}"
+        roof = roofline_entry(flops, nbytes, per_kernel[dominant], args.precision)
+        config_key = (f"B{args.batch}_C{args.channels}_{args.fmap}x{args.fmap}_P{args.protos}_K{args.classes}"
+                      f"_{args.x_dtype}_{args.precision}")
         roof["traffic"] = pmc_traffic(dominant, config_key)
         roof["kernel"] = dominant
         kernels = {}
@@ -325,7 +342,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32" if args.x_dtype == "f32" else "bf16-in/f32",
+            "dtype": f"{args.x_dtype} in; {args.precision} products, f32 accumulate",
             "data": "synthetic (seeded; SURVEY.md §8d shapes), inputs resident in HBM",
             "config": {"workload": "cityscapes_no_kld_imnet prototype layer fwd+bwd (+RCCL grad all-reduce "
                                    "when N>1), 513x513 crop -> 65x65 map",

@@ -46,6 +46,13 @@ enum protoseg_dtype {
 /* model.py:231-237 distance_2_similarity: 'log' -> log((d+1)/(d+eps)); 'linear' -> -d */
 enum protoseg_act { PROTOSEG_ACT_LOG = 0, PROTOSEG_ACT_LINEAR = 1 };
 
+/* Arithmetic of the x.p / W.act / gradient products (always f32 accumulation):
+ *  BF16X3  operands split in 2 bf16 terms, 3 bf16 MFMAs per product (|rel err| ~ 1e-5 on d)
+ *  BF16X6  operands split in 3 bf16 terms, 6 bf16 MFMAs per product (f32-class)
+ *  F32     v_mfma_f32_32x32x2_f32: an exact f32 fma chain
+ * A request the bf16 family cannot serve (C != 64, LDS) runs on the F32 family. */
+enum protoseg_precision { PROTOSEG_PREC_BF16X3 = 0, PROTOSEG_PREC_BF16X6 = 1, PROTOSEG_PREC_F32 = 2 };
+
 int protoseg_version(void);                 /* MAJOR*10000 + MINOR*100 + PATCH */
 const char* protoseg_last_error(void);      /* thread-local text of the last failure */
 
@@ -62,10 +69,11 @@ const char* protoseg_last_error(void);      /* thread-local text of the last fai
  *   act_out    [B*H*W, P]     f32 or NULL   prototype activations (model.py:273)
  *   logits_out [B, H, W, K]   f32 or NULL   logits NHWC (model.py:278)
  * Supported: C in {32, 64, 128}; P <= 384 (C=64) — see protoseg_l2_supported(); K <= 32.
+ * The bf16 family serves C = 64 (P <= 384 forward / pw-backward, P <= 224 x-backward).
  */
 int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, int W,
                     const float* protos, int P, const float* w_last, int K,
-                    float eps, int act_kind,
+                    float eps, int act_kind, int precision,
                     float* dist_out, float* act_out, float* logits_out,
                     protoseg_stream_t stream);
 
@@ -83,7 +91,7 @@ int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, int W,
 size_t protoseg_l2_bwd_workspace_size(int B, int C, int H, int W, int P, int K);
 int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, int W,
                     const float* protos, int P, const float* w_last, int K,
-                    float eps, int act_kind,
+                    float eps, int act_kind, int precision,
                     const float* g_logits, const float* g_dist,
                     void* g_x, float* g_protos, float* g_w,
                     void* workspace, size_t workspace_bytes,

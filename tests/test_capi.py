@@ -48,14 +48,16 @@ def test_workspace_size_is_host_only_and_aligned():
 def test_argument_validation_returns_status_without_gpu():
     lib = _lib.load()
     null = ctypes.c_void_p(None)
-    st = lib.protoseg_l2_fwd(null, 0, 1, 64, 2, 2, null, 19, null, 19, 1e-4, 0, null, null, null, null)
+    st = lib.protoseg_l2_fwd(null, 0, 1, 64, 2, 2, null, 19, null, 19, 1e-4, 0, 0, null, null, null, null)
     assert st == _lib.ERR_INVALID
     assert b"non-null" in lib.protoseg_last_error()
     dummy = ctypes.c_void_p(16)  # never dereferenced: validation fails first
-    st = lib.protoseg_l2_fwd(dummy, 7, 1, 64, 2, 2, dummy, 19, dummy, 19, 1e-4, 0, null, null, null, null)
+    st = lib.protoseg_l2_fwd(dummy, 7, 1, 64, 2, 2, dummy, 19, dummy, 19, 1e-4, 0, 0, null, null, null, null)
     assert st == _lib.ERR_UNSUPPORTED
-    st = lib.protoseg_l2_fwd(dummy, 0, 1, 48, 2, 2, dummy, 19, dummy, 19, 1e-4, 0, null, null, null, null)
+    st = lib.protoseg_l2_fwd(dummy, 0, 1, 48, 2, 2, dummy, 19, dummy, 19, 1e-4, 0, 0, null, null, null, null)
     assert st == _lib.ERR_UNSUPPORTED
+    st = lib.protoseg_l2_fwd(dummy, 0, 1, 64, 2, 2, dummy, 19, dummy, 19, 1e-4, 0, 9, null, null, null, null)
+    assert st == _lib.ERR_UNSUPPORTED and b"precision" in lib.protoseg_last_error()
     st = lib.protoseg_patch_class_mask(null, 2, 1, 4, 4, 2, 2, null, 0, null, null)
     assert st == _lib.ERR_INVALID
     st = lib.protoseg_push_argmin(dummy, 1, 48, 2, 2, dummy, 3, dummy, dummy, dummy, null)

@@ -44,35 +44,44 @@ def assert_scaled_close(a, ref, rtol=1e-4, name=""):
     assert err <= rtol * scale, f"{name}: max err {err:.3e} > {rtol:g} * scale {scale:.3e}"
 
 
-def run_layer(x, protos, w_last, activation="log", with_act=False, device="cuda:0"):
+PRECISIONS = ["bf16x3", "bf16x6", "f32"]
+
+
+def prec(name):
+    return _ops().PRECISIONS[name]
+
+
+def run_layer(x, protos, w_last, activation="log", with_act=False, device="cuda:0", precision="bf16x3"):
     ops = _ops()
     return ops.prototype_layer(x.to(device), protos.to(device), w_last.to(device), 1e-4, activation,
-                               True, True, with_act)
+                               True, True, with_act, precision)
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("name", ["l2_small", "l2_ragged"])
-def test_forward_matches_golden(device, name):
+def test_forward_matches_golden(device, name, precision):
     g = np.load(os.path.join(GOLDEN, f"{name}.npz"))
     x, protos, w_last = (torch.from_numpy(g[k]) for k in ("x", "protos", "w_last"))
-    dist, logits, act = run_layer(x, protos, w_last, with_act=True, device=device)
+    dist, logits, act = run_layer(x, protos, w_last, with_act=True, device=device, precision=precision)
     torch.cuda.synchronize()
     assert_dist_close(dist, torch.from_numpy(g["dist"]), x, protos)
     assert_scaled_close(logits, torch.from_numpy(g["logits"]), 1e-4, "logits")
     assert_scaled_close(act, torch.from_numpy(g["act"]), 1e-4, "act")
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("name", ["l2_small", "l2_ragged"])
-def test_backward_matches_golden(device, name):
+def test_backward_matches_golden(device, name, precision):
     ops = _ops()
     g = np.load(os.path.join(GOLDEN, f"{name}.npz"))
     x, protos, w_last, g_logits, g_dist = (torch.from_numpy(g[k]).to(device) for k in
                                            ("x", "protos", "w_last", "g_logits", "g_dist"))
-    gx, gp, gw = ops.l2_backward(x, protos, w_last, g_logits, None, 1e-4, 0, True, True, True)
+    gx, gp, gw = ops.l2_backward(x, protos, w_last, g_logits, None, 1e-4, 0, prec(precision), True, True, True)
     torch.cuda.synchronize()
     assert_scaled_close(gx, torch.from_numpy(g["g_x"]), 1e-4, "g_x")
     assert_scaled_close(gp, torch.from_numpy(g["g_protos"]), 1e-4, "g_protos")
     assert_scaled_close(gw, torch.from_numpy(g["g_w"]), 1e-4, "g_w")
-    gx2, gp2, _ = ops.l2_backward(x, protos, w_last, g_logits, g_dist, 1e-4, 0, True, True, False)
+    gx2, gp2, _ = ops.l2_backward(x, protos, w_last, g_logits, g_dist, 1e-4, 0, prec(precision), True, True, False)
     assert_scaled_close(gx2, torch.from_numpy(g["g_x_with_gdist"]), 1e-4, "g_x(+g_dist)")
     assert_scaled_close(gp2, torch.from_numpy(g["g_protos_with_gdist"]), 1e-4, "g_protos(+g_dist)")
 
@@ -87,46 +96,49 @@ def test_backward_matches_golden(device, name):
     (1, 64, 65, 65, 361, 19),     # 19 prototypes/class
 ])
 @pytest.mark.parametrize("activation", ["log", "linear"])
-def test_forward_backward_vs_oracle(device, B, C, h, w, P, K, activation):
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_forward_backward_vs_oracle(device, B, C, h, w, P, K, activation, precision):
     x, protos, w_last = po.synthetic_inputs(B, C, h, w, P, K, seed=B * 1000 + C + h + P)
     gen = torch.Generator().manual_seed(5)
     w_last = w_last + 0.05 * torch.randn(w_last.shape, generator=gen)
     g_logits = torch.randn(B, h, w, K, generator=gen)
-    dist, logits, _ = run_layer(x, protos, w_last, activation, device=device)
+    dist, logits, _ = run_layer(x, protos, w_last, activation, device=device, precision=precision)
     ref_logits, ref_dist, ref_gx, ref_gp, ref_gw = po.forward_backward(x, protos, w_last, g_logits, None, activation)
     assert_dist_close(dist, ref_dist, x, protos)
     assert_scaled_close(logits, ref_logits, 1e-4, "logits")
     ops = _ops()
     gx, gp, gw = ops.l2_backward(x.to(device), protos.to(device), w_last.to(device), g_logits.to(device), None,
-                                 1e-4, ops.ACT_KINDS[activation], True, True, True)
+                                 1e-4, ops.ACT_KINDS[activation], prec(precision), True, True, True)
     assert_scaled_close(gx, ref_gx, 1e-4, "g_x")
     assert_scaled_close(gp, ref_gp, 1e-4, "g_protos")
     assert_scaled_close(gw, ref_gw, 1e-4, "g_w")
 
 
-def test_bf16_features(device):
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_bf16_features(device, precision):
     """bf16 feature maps are read exactly (bf16 -> f32 is exact) and computed in f32."""
     x, protos, w_last = po.synthetic_inputs(2, 64, 17, 19, 57, 19, seed=3)
     xb = x.to(torch.bfloat16)
-    dist, logits, _ = run_layer(xb, protos, w_last, device=device)
+    dist, logits, _ = run_layer(xb, protos, w_last, device=device, precision=precision)
     ref_logits, ref_dist = po.forward_from_conv_features(xb.float(), protos[:, :, None, None], w_last)
     assert_dist_close(dist, ref_dist, xb.float(), protos)
     assert_scaled_close(logits, ref_logits, 1e-4, "logits")
     ops = _ops()
     g_logits = torch.randn(2, 17, 19, 19)
     gx, gp, _ = ops.l2_backward(xb.to(device), protos.to(device), w_last.to(device), g_logits.to(device), None,
-                                1e-4, 0, True, True, False)
+                                1e-4, 0, prec(precision), True, True, False)
     assert gx.dtype == torch.bfloat16
     _, _, ref_gx, ref_gp, _ = po.forward_backward(xb.float(), protos, w_last, g_logits, None)
     assert_scaled_close(gx.float(), ref_gx, 1e-2, "g_x(bf16 out)")
     assert_scaled_close(gp, ref_gp, 1e-4, "g_protos")
 
 
-def test_known_answer_zero_distance(device):
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_known_answer_zero_distance(device, precision):
     """x equal to a prototype at a pixel -> d = 0 (relu clamps) -> act = log(1/1e-4) = 9.2103."""
     x, protos, w_last = po.synthetic_inputs(1, 64, 4, 4, 19, 19, seed=11)
     x[0, :, 2, 3] = protos[7]
-    dist, logits, act = run_layer(x, protos, w_last, with_act=True, device=device)
+    dist, logits, act = run_layer(x, protos, w_last, with_act=True, device=device, precision=precision)
     d = dist[0, 7, 2, 3].item()
     assert d <= 2e-6 * 2 * (protos[7] ** 2).sum().item()
     a = act.view(1, 4, 4, 19)[0, 2, 3, 7].item()
@@ -135,24 +147,26 @@ def test_known_answer_zero_distance(device):
         assert abs(a - 9.210340371976184) < 1e-5
 
 
-def test_distances_match_float64_bruteforce(device):
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_distances_match_float64_bruteforce(device, precision):
     """Size-independent property at the full 65x65 crop: d == ||x - p||^2 within the f32 bound."""
     x, protos, w_last = po.synthetic_inputs(4, 64, 65, 65, 190, 19, seed=17)
-    dist, _, _ = run_layer(x, protos, w_last, device=device)
+    dist, _, _ = run_layer(x, protos, w_last, device=device, precision=precision)
     xd = x.double().permute(0, 2, 3, 1).reshape(-1, 64)
     exact = torch.cdist(xd, protos.double()) ** 2
     exact = exact.reshape(4, 65, 65, 190).permute(0, 3, 1, 2)
     assert_dist_close(dist, exact, x, protos)
 
 
-def test_deterministic(device):
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_deterministic(device, precision):
     """No atomics on the float path: two runs are bitwise identical."""
     ops = _ops()
     x, protos, w_last = po.synthetic_inputs(3, 64, 40, 41, 190, 19, seed=23)
     x, protos, w_last = x.to(device), protos.to(device), w_last.to(device)
     g = torch.randn(3, 40, 41, 19, device=device)
-    r1 = ops.l2_backward(x, protos, w_last, g, None, 1e-4, 0, True, True, True)
-    r2 = ops.l2_backward(x, protos, w_last, g, None, 1e-4, 0, True, True, True)
+    r1 = ops.l2_backward(x, protos, w_last, g, None, 1e-4, 0, prec(precision), True, True, True)
+    r2 = ops.l2_backward(x, protos, w_last, g, None, 1e-4, 0, prec(precision), True, True, True)
     for a, b in zip(r1, r2):
         assert torch.equal(a, b)
 
