@@ -116,3 +116,68 @@ __device__ __forceinline__ void store_frag(bf16* img, int plane_elems, int off, 
 }
 
 }  // namespace protoseg
+
+namespace protoseg {
+
+// ---- buffer-resource memory ops: out-of-range offsets are dropped (stores) or read 0 (loads),
+// which replaces per-element exec-mask branches. Descriptors are built from kernel arguments
+// (wave-uniform), and every tensor is < 2^31 bytes (checked on the host), so a lane offset of
+// kOOB plus any uniform offset stays out of range without wrapping.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr unsigned kOOB = 0x80000000u;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), static_cast<short>(0), static_cast<int>(bytes),
+                                           0x00020000);
+}
+
+template <typename TX> struct BufIO;
+template <> struct BufIO<float> {
+  static __device__ __forceinline__ float load(rsrc_t r, unsigned voff, unsigned soff) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+  }
+  static __device__ __forceinline__ void store(rsrc_t r, float v, unsigned voff, unsigned soff) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, 0);
+  }
+};
+template <> struct BufIO<uint16_t> {
+  static __device__ __forceinline__ float load(rsrc_t r, unsigned voff, unsigned soff) {
+    return __uint_as_float(static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0)) << 16);
+  }
+  static __device__ __forceinline__ void store(rsrc_t r, float v, unsigned voff, unsigned soff) {
+    const uint16_t b = __builtin_bit_cast(uint16_t, static_cast<bf16>(v));  // RNE, NaN kept
+    __builtin_amdgcn_raw_buffer_store_b16(b, r, voff, soff, 0);
+  }
+};
+
+// Fast activation for the bf16 family: v_rcp_f32 + v_log_f32 (log2) instead of the IEEE
+// division and the denormal-safe logf sequence. The ratio (d+1)/(d+eps) lies in (1, 1e4],
+// where v_log_f32 is accurate to ~1 ulp.
+template <int ACT>
+__device__ __forceinline__ float act_fast(float d, float eps) {
+  if constexpr (ACT == 0) {
+    const float r = (d + 1.f) * __builtin_amdgcn_rcpf(d + eps);
+    return __builtin_amdgcn_logf(r) * 0.6931471805599453f;
+  } else {
+    return -d;
+  }
+}
+// d act / d d ; log: (eps - 1) / ((d + 1)(d + eps))
+template <int ACT>
+__device__ __forceinline__ float act_grad_fast(float d, float eps) {
+  if constexpr (ACT == 0) {
+    return (eps - 1.f) * __builtin_amdgcn_rcpf((d + 1.f) * (d + eps));
+  } else {
+    return -1.f;
+  }
+}
+
+// Channel of k-step q, element jj, half h in the shared channel order of the bf16 family:
+// chan_of(q, h, jj) = 32*(q>>1) + perm_row(q&1, h, jj). With it the x fragments a lane loads
+// for the distance GEMM hold exactly the channels of its g_x accumulator registers
+// (gx[ct] register 8s+jj <-> q = 2ct+s), so no lane movement is needed in the backward.
+__device__ __forceinline__ constexpr int chan_of(int q, int h, int jj) { return 32 * (q >> 1) + perm_row(q & 1, h, jj); }
+// The lane-independent part (h = 0).
+__device__ __forceinline__ constexpr int chan_base(int q, int jj) { return chan_of(q, 0, jj); }
+
+}  // namespace protoseg

@@ -1,19 +1,24 @@
 // l2_bf16.hip — the prototype layer on bf16 MFMA with split operands (bf16_split.h), C = 64.
 //
 // Same math and outputs as the f32-MFMA family in l2_layer.hip (reference model.py:203-237,
-// 259-283 and their autograd), at 5.3x (T=2) / 2.7x (T=3) fewer matrix-core cycles, which
-// moves the forward from MFMA-bound to HBM-bound (the D write dominates its bytes).
+// 259-283 and their autograd), at 5.3x (T=2) / 2.7x (T=3) fewer matrix-core cycles.
 //
 //   l2_fwd_bf16_kernel     layout A (rows p, cols n): distances -> NCHW stores, activation in
 //                          registers, logits = W . act with the accumulator as B operand.
+//                          Each wave prefetches its next pixel tile during the current one.
 //   l2_bwd_x_bf16_kernel   layout A: recompute S, g_act = W^T g_logits^T, g_s, and
 //                          g_x^T = P^T (-2 g_s) with the accumulator as B operand.
 //   l2_bwd_pw_bf16_kernel  layout B (rows n, cols p): one workgroup = S streams x npt waves,
 //                          wave (stream, w) owns prototype tile w; each 32-pixel tile is read
-//                          from HBM once, staged in LDS as bf16 images, and shared by the
-//                          npt waves; g_P^T and g_W accumulate in registers (the accumulator
-//                          is their A / B operand), one partial slab per workgroup.
+//                          from HBM once (prefetched into registers one tile ahead), staged in
+//                          LDS as bf16 images and shared by the npt waves; g_P^T and g_W
+//                          accumulate in registers (the accumulator is their A / B operand),
+//                          one partial slab per workgroup.
 //   l2_bwd_reduce_bf16_kernel  deterministic parallel sum of the slabs (+ 2p * sum g_s).
+//
+// Memory ops go through buffer resources (out-of-range lanes read 0 / drop their store), the
+// activation is a template parameter, and every kernel uses the channel order chan_of() for
+// the distance GEMM, so all three compute bit-identical distances for the same inputs.
 #include "bf16_split.h"
 #include "l2_launch.h"
 #include "protoseg_host.h"
@@ -27,21 +32,19 @@ constexpr int kNQ = kC / 16;   // channel k-steps of 16
 constexpr int kWavesA = 8;     // layout-A kernels: 8 waves, one 32-pixel tile each at a time
 constexpr int kLdf = 33;       // padded fp32 staging rows
 
-template <typename TX>
-__device__ __forceinline__ float ldx(const TX* p, size_t i) { return XIO<TX>::load(p, i); }
-
-// P image [T][Pp][64]: row p natural channel chunks (CPR 8) — A operand of S (layout A).
+// P image [T][Pp][64]: row p, chunk 2q+h = channels chan_of(q, h, 0..7) (CPR 8).
+// Operand of S in every kernel: A in layout A (lane = p), B in layout B (lane = p).
 template <int T>
 __device__ void stage_p_rows(bf16* img, const float* __restrict__ protos, int P, int Pp) {
   const int plane = Pp * kC;
   for (int idx = threadIdx.x; idx < Pp * 8; idx += blockDim.x) {
-    const int p = idx >> 3, q8 = idx & 7;
+    const int p = idx >> 3, e8 = idx & 7, q = e8 >> 1, h = e8 & 1;
     float v[8];
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) v[jj] = p < P ? protos[static_cast<size_t>(p) * kC + q8 * 8 + jj] : 0.f;
+    for (int jj = 0; jj < 8; ++jj) v[jj] = p < P ? protos[static_cast<size_t>(p) * kC + chan_of(q, h, jj)] : 0.f;
     bf16x8 f[T];
     split8<T>(v, f);
-    store_frag<T>(img, plane, img_off<8>(p, q8), f);
+    store_frag<T>(img, plane, img_off<8>(p, e8), f);
   }
 }
 
@@ -82,7 +85,8 @@ __device__ void stage_w_perm(bf16* img, const float* __restrict__ w, int K, int 
   }
 }
 
-// W^T image [T][Pp][32 k] natural classes (CPR 4) — A operand of g_act^T = W^T g_logits^T.
+// W^T image [T][Pp][32 k] natural classes (CPR 4) — operand of g_act: A in layout A
+// (lane = p), B in layout B (lane = p).
 template <int T>
 __device__ void stage_wt_rows(bf16* img, const float* __restrict__ w, int K, int P, int Pp) {
   const int plane = Pp * 32;
@@ -100,8 +104,7 @@ __device__ void stage_wt_rows(bf16* img, const float* __restrict__ w, int K, int
   }
 }
 
-// ||p||^2 exactly as the f32 family (sequential, no contraction) so that every kernel
-// computes bit-identical distances for the same inputs.
+// ||p||^2 exactly as the f32 family (sequential, no contraction).
 __device__ float proto_norm2_64(const float* __restrict__ protos, int p, bool valid) {
 #pragma clang fp contract(off)
   float s = 0.f;
@@ -114,34 +117,47 @@ __device__ float proto_norm2_64(const float* __restrict__ protos, int p, bool va
   return s;
 }
 
-// Layout-A x tile of this lane: xb[q] = x[16q + 8h + 0..7][pixel j] split in T terms;
-// returns ||x||^2 (f32 fma chain over the lane's half of the channels, then the two halves).
-template <typename TX, int T>
-__device__ __forceinline__ float load_x_frags(const TX* __restrict__ x, int b, int n, int HW, bool valid,
-                                              bf16x8 (&xb)[kNQ][T]) {
-  const int h = (threadIdx.x & 63) >> 5;
-  const TX* xh = x + (static_cast<size_t>(b) * kC + 8 * h) * HW + n;
+// Byte offset of this lane's pixel at channel 4h of image b (layout A lane = pixel j), or kOOB.
+template <typename TX>
+__device__ __forceinline__ unsigned x_lane_off(int t, int ntiles, int npix, int HW) {
+  const int j = threadIdx.x & 31, h = (threadIdx.x & 63) >> 5;
+  const int g = t * 32 + j;
+  if (t >= ntiles || g >= npix) return kOOB;
+  const int b = g / HW, n = g - b * HW;
+  return static_cast<unsigned>(((b * kC + 4 * h) * HW + n) * static_cast<int>(sizeof(TX)));
+}
+
+// Raw layout-A x of one tile: raw[q*8 + jj] = x[chan_of(q, h, jj)][pixel j] (0 when out of range).
+template <typename TX>
+__device__ __forceinline__ void load_x_raw(rsrc_t rx, unsigned off, unsigned cs, float (&raw)[kNQ * 8]) {
+#pragma unroll
+  for (int q = 0; q < kNQ; ++q)
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) raw[q * 8 + jj] = BufIO<TX>::load(rx, off, chan_base(q, jj) * cs);
+}
+
+// Split fragments + ||x||^2 (fma chain over the lane's half of the channels, then both halves).
+template <int T>
+__device__ __forceinline__ float x_frags(const float (&raw)[kNQ * 8], bf16x8 (&xb)[kNQ][T]) {
   float x2 = 0.f;
 #pragma unroll
   for (int q = 0; q < kNQ; ++q) {
     float v[8];
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
-      const float t = ldx(xh, static_cast<size_t>(16 * q + jj) * HW);
-      v[jj] = valid ? t : 0.f;
+      v[jj] = raw[q * 8 + jj];
       x2 = fmaf(v[jj], v[jj], x2);
     }
     split8<T>(v, xb[q]);
   }
-  x2 += __shfl_xor(x2, 32);
-  return x2;
+  return x2 + __shfl_xor(x2, 32);
 }
 
-template <typename TX, int T>
+template <typename TX, int T, int ACT>
 __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
-    const TX* __restrict__ x, int HW, int npix, const float* __restrict__ protos, int P, int Pp,
-    const float* __restrict__ w_last, int K, float eps, int act_kind, float* __restrict__ dist,
-    float* __restrict__ act_out, float* __restrict__ logits) {
+    const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const float* __restrict__ protos, int P, int Pp,
+    const float* __restrict__ w_last, int K, float eps, float* __restrict__ dist, unsigned d_bytes,
+    float* __restrict__ act_out, unsigned a_bytes, float* __restrict__ logits, unsigned l_bytes) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   bf16* Pimg = reinterpret_cast<bf16*>(smem_raw);                // [T][Pp][64]
   bf16* Wimg = Pimg + T * Pp * kC;                               // [T][Pp][32]
@@ -152,16 +168,27 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
   for (int p = threadIdx.x; p < Pp; p += blockDim.x) p2s[p] = proto_norm2_64(protos, p, p < P);
   __syncthreads();
 
+  const rsrc_t rx = make_rsrc(x, x_bytes), rd = make_rsrc(dist, d_bytes);
+  const rsrc_t ra = make_rsrc(act_out, a_bytes), rl = make_rsrc(logits, l_bytes);
+  const unsigned cs = static_cast<unsigned>(HW) * sizeof(TX);
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
   const int ntiles = (npix + 31) / 32;
   const int npt = Pp / 32;
-  for (int t = blockIdx.x * kWavesA + wave; t < ntiles; t += gridDim.x * kWavesA) {
+  const int stride = gridDim.x * kWavesA;
+  int t = blockIdx.x * kWavesA + wave;
+  float raw[kNQ * 8];
+  load_x_raw<TX>(rx, x_lane_off<TX>(t, ntiles, npix, HW), cs, raw);
+  for (; t < ntiles; t += stride) {
+    bf16x8 xb[kNQ][T];
+    const float x2 = x_frags<T>(raw, xb);
+    load_x_raw<TX>(rx, x_lane_off<TX>(t + stride, ntiles, npix, HW), cs, raw);  // prefetch next tile
+
     const int g = t * 32 + j;
     const bool valid = g < npix;
     const int b = valid ? g / HW : 0;
     const int n = valid ? g - b * HW : 0;
-    bf16x8 xb[kNQ][T];
-    const float x2 = load_x_frags<TX, T>(x, b, n, HW, valid, xb);
+    const unsigned dbase = valid ? static_cast<unsigned>(((b * P + 4 * h) * HW + n) * 4) : kOOB;
+    const unsigned abase = valid ? static_cast<unsigned>((g * P + 4 * h) * 4) : kOOB;
 
     f32x16 lacc = zero16();
 #pragma unroll 1
@@ -173,15 +200,15 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
         load_frag<T>(Pimg, Pp * kC, img_off<8>(pt * 32 + j, 2 * q + h), pa);
         acc = mma_split<T>(pa, xb[q], acc);
       }
-      float* dpt = dist ? dist + (static_cast<size_t>(b) * P + pt * 32 + 4 * h) * HW + n : nullptr;
+      const int prem = P - pt * 32 - 4 * h;  // rows of this tile (and half) below P
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int p = pt * 32 + acc_row(r, h);
         const float d = l2_distance(x2, p2s[p], acc[r]);
-        const bool st = valid && p < P;
-        if (dpt && st) dpt[static_cast<size_t>(row_of(r)) * HW] = d;
-        const float a = activation(d, eps, act_kind);
-        if (act_out && st) act_out[static_cast<size_t>(g) * P + p] = a;
+        const bool pin = row_of(r) < prem;
+        if (dist) BufIO<float>::store(rd, d, pin ? dbase : kOOB, static_cast<unsigned>((pt * 32 + row_of(r)) * HW * 4));
+        const float a = act_fast<ACT>(d, eps);
+        if (act_out) BufIO<float>::store(ra, a, pin ? abase : kOOB, static_cast<unsigned>((pt * 32 + row_of(r)) * 4));
         acc[r] = a;
       }
       if (do_logits) {
@@ -194,21 +221,21 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
         }
       }
     }
-    if (do_logits && valid) {
+    if (do_logits) {
+      const unsigned lbase = valid ? static_cast<unsigned>((g * K + 4 * h) * 4) : kOOB;
+      const int krem = K - 4 * h;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int k = acc_row(r, h);
-        if (k < K) logits[static_cast<size_t>(g) * K + k] = lacc[r];
-      }
+      for (int r = 0; r < 16; ++r)
+        BufIO<float>::store(rl, lacc[r], row_of(r) < krem ? lbase : kOOB, static_cast<unsigned>(row_of(r) * 4));
     }
   }
 }
 
-template <typename TX, int T>
+template <typename TX, int T, int ACT>
 __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
-    const TX* __restrict__ x, int HW, int npix, const float* __restrict__ protos, int P, int Pp,
-    const float* __restrict__ w_last, int K, float eps, int act_kind, const float* __restrict__ g_logits,
-    const float* __restrict__ g_dist, TX* __restrict__ g_x) {
+    const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const float* __restrict__ protos, int P, int Pp,
+    const float* __restrict__ w_last, int K, float eps, const float* __restrict__ g_logits, unsigned gl_bytes,
+    const float* __restrict__ g_dist, unsigned gd_bytes, TX* __restrict__ g_x) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   bf16* Pimg = reinterpret_cast<bf16*>(smem_raw);                 // [T][Pp][64]
   bf16* PTimg = Pimg + T * Pp * kC;                               // [T][npt*64][32]
@@ -220,31 +247,39 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
   for (int p = threadIdx.x; p < Pp; p += blockDim.x) p2s[p] = proto_norm2_64(protos, p, p < P);
   __syncthreads();
 
+  const rsrc_t rx = make_rsrc(x, x_bytes), rg = make_rsrc(g_logits, gl_bytes);
+  const rsrc_t rgd = make_rsrc(g_dist, gd_bytes), rgx = make_rsrc(g_x, x_bytes);
+  const unsigned cs = static_cast<unsigned>(HW) * sizeof(TX);
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
   const int ntiles = (npix + 31) / 32;
   const int npt = Pp / 32;
   const int KS = (K + 15) / 16;  // class k-steps of 16
   for (int t = blockIdx.x * kWavesA + wave; t < ntiles; t += gridDim.x * kWavesA) {
+    const unsigned xoff = x_lane_off<TX>(t, ntiles, npix, HW);
+    float raw[kNQ * 8];
+    load_x_raw<TX>(rx, xoff, cs, raw);
     const int g = t * 32 + j;
     const bool valid = g < npix;
     const int b = valid ? g / HW : 0;
     const int n = valid ? g - b * HW : 0;
-    bf16x8 xb[kNQ][T];
-    const float x2 = load_x_frags<TX, T>(x, b, n, HW, valid, xb);
     // B operand of g_act^T: lane (h, j) holds g_logits[pixel j][16s + 8h + jj]
     bf16x8 glb[2][T];
+    {
+      const unsigned gbase = valid ? static_cast<unsigned>((g * K + 8 * h) * 4) : kOOB;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      float v[8];
+      for (int s = 0; s < 2; ++s) {
+        float v[8];
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        const int k = 16 * s + 8 * h + jj;
-        const bool ok = g_logits && valid && k < K;
-        const float t0 = g_logits ? g_logits[ok ? static_cast<size_t>(g) * K + k : 0] : 0.f;
-        v[jj] = ok ? t0 : 0.f;
+        for (int jj = 0; jj < 8; ++jj) {
+          const float t0 = BufIO<float>::load(rg, gbase, static_cast<unsigned>((16 * s + jj) * 4));
+          v[jj] = (16 * s + 8 * h + jj < K) ? t0 : 0.f;
+        }
+        split8<T>(v, glb[s]);
       }
-      split8<T>(v, glb[s]);
     }
+    bf16x8 xb[kNQ][T];
+    const float x2 = x_frags<T>(raw, xb);
+    const unsigned gdbase = valid ? static_cast<unsigned>(((b * P + 4 * h) * HW + n) * 4) : kOOB;
 
     f32x16 gx[2] = {zero16(), zero16()};
     float gsum = 0.f;
@@ -268,18 +303,16 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
           }
         }
       }
-      const float* gdpt = g_dist ? g_dist + (static_cast<size_t>(b) * P + pt * 32 + 4 * h) * HW + n : nullptr;
+      const int prem = P - pt * 32 - 4 * h;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int p = pt * 32 + acc_row(r, h);
         const float d = l2_distance(x2, p2s[p], acc[r]);
-        float gd = g_logits ? gacc[r] * activation_grad(d, eps, act_kind) : 0.f;
-        if (gdpt) {
-          const bool ok = valid && p < P;
-          const float v = gdpt[ok ? static_cast<size_t>(row_of(r)) * HW : 0];
-          gd += ok ? v : 0.f;
-        }
-        const float gs = (d > 0.f && p < P) ? gd : 0.f;
+        const bool pin = row_of(r) < prem;
+        float gd = g_logits ? gacc[r] * act_grad_fast<ACT>(d, eps) : 0.f;
+        if (g_dist)
+          gd += BufIO<float>::load(rgd, pin ? gdbase : kOOB, static_cast<unsigned>((pt * 32 + row_of(r)) * HW * 4));
+        const float gs = (d > 0.f && pin) ? gd : 0.f;  // relu backward: grad * (out > 0)
         gsum += gs;
         acc[r] = -2.f * gs;
       }
@@ -296,73 +329,85 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
       }
     }
     gsum += __shfl_xor(gsum, 32);
-    if (valid) {
-      const TX* xh = x + (static_cast<size_t>(b) * kC + 4 * h) * HW + n;
-      TX* gxh = g_x + (static_cast<size_t>(b) * kC + 4 * h) * HW + n;
+    // gx[ct] register 8s+jj is channel chan_of(2ct+s, h, jj) — the channel of raw[(2ct+s)*8+jj].
+    // conv(x^2, ones) backward then pow backward: gsum * (2x); plus the xp branch in gx.
 #pragma unroll
-      for (int ct = 0; ct < 2; ++ct)
+    for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const size_t off = static_cast<size_t>(ct * 32 + row_of(r)) * HW;
-          XIO<TX>::store(gxh, off, gx[ct][r] + gsum * (2.f * ldx(xh, off)));
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const int q = 2 * ct + s;
+          BufIO<TX>::store(rgx, gx[ct][8 * s + jj] + gsum * (2.f * raw[q * 8 + jj]), xoff, chan_base(q, jj) * cs);
         }
-    }
   }
 }
 
-// ---- bwd_pw: per-stream LDS staging area ------------------------------------------------
+// ---- bwd_pw ----------------------------------------------------------------------------------
 template <int T>
 struct PwStage {
   static constexpr int kXf = kC * kLdf;        // fp32 [64][33]
   static constexpr int kGf = 32 * kLdf;        // fp32 [32][33]
-  static constexpr int kXA = T * 32 * kC;      // bf16 [T][32 n][64 c]   CPR 8
+  static constexpr int kXA = T * 32 * kC;      // bf16 [T][32 n][64 c]   CPR 8, chan_of order
   static constexpr int kXB = T * kC * 32;      // bf16 [T][64 c][32 n~]  CPR 4, permuted n
   static constexpr int kGA = T * 32 * 32;      // bf16 [T][32 n][32 k]   CPR 4
   static constexpr int kGT = T * 32 * 32;      // bf16 [T][32 k][32 n~]  CPR 4, permuted n
-  // byte layout: Xf | Gf | x2[32] | rowb[32] | rown[32] | XA | XB | GA | GT
-  static constexpr int kBytes = (kXf + kGf + 32) * 4 + 2 * 32 * 4 + (kXA + kXB + kGA + kGT) * 2;
+  // byte layout: Xf | Gf | x2[32] | rowoff[32] | XA | XB | GA | GT
+  static constexpr int kBytes = (kXf + kGf + 32) * 4 + 32 * 4 + (kXA + kXB + kGA + kGT) * 2;
 };
 
 template <int T>
-__device__ __forceinline__ void pw_carve(unsigned char* base, float*& Xf, float*& Gf, float*& x2s, int*& rowb,
-                                         int*& rown, bf16*& XA, bf16*& XB, bf16*& GA, bf16*& GT) {
+__device__ __forceinline__ void pw_carve(unsigned char* base, float*& Xf, float*& Gf, float*& x2s,
+                                         unsigned*& rowoff, bf16*& XA, bf16*& XB, bf16*& GA, bf16*& GT) {
   using S = PwStage<T>;
   Xf = reinterpret_cast<float*>(base);
   Gf = Xf + S::kXf;
   x2s = Gf + S::kGf;
-  rowb = reinterpret_cast<int*>(x2s + 32);
-  rown = rowb + 32;
-  XA = reinterpret_cast<bf16*>(rown + 32);
+  rowoff = reinterpret_cast<unsigned*>(x2s + 32);
+  XA = reinterpret_cast<bf16*>(rowoff + 32);
   XB = XA + S::kXA;
   GA = XB + S::kXB;
   GT = GA + S::kGA;
 }
 
-template <typename TX, int T>
-__global__ __launch_bounds__(768) void l2_bwd_pw_bf16_kernel(
-    const TX* __restrict__ x, int HW, int npix, const float* __restrict__ protos, int P, int Pp,
-    const float* __restrict__ w_last, int K, float eps, int act_kind, const float* __restrict__ g_logits,
-    const float* __restrict__ g_dist, int streams, float* __restrict__ slab) {
+// Staging: the npt*64 threads of a stream load that stream's next tile into registers one tile
+// ahead — x[c][pixel] (2048 elements) and g_logits[pixel][class] (1024). Thread ts covers
+// pixel ts&31 (x) / class ts&31 (g_logits) and rows (ts>>5) + i*2npt, so the per-i part of
+// every address is wave-uniform. NPTC is a lower bound on npt that sizes the register arrays.
+template <int NPTC>
+struct PwLoads {
+  static constexpr int kNX = (kC * 32 + NPTC * 64 - 1) / (NPTC * 64);
+  static constexpr int kNG = (32 * 32 + NPTC * 64 - 1) / (NPTC * 64);
+};
+
+// Launch bound per class: npt 1 -> 2 streams x 1 wave; 2..3 -> <= 6 waves; 4..5 -> <= 10; 6..12 -> <= 12.
+template <int NPTC>
+constexpr int pw_max_threads() { return NPTC == 1 ? 128 : NPTC == 2 ? 384 : NPTC == 4 ? 640 : 768; }
+
+template <typename TX, int T, int ACT, int NPTC>
+__global__ __launch_bounds__(pw_max_threads<NPTC>()) void l2_bwd_pw_bf16_kernel(
+    const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const float* __restrict__ protos, int P, int Pp,
+    const float* __restrict__ w_last, int K, float eps, const float* __restrict__ g_logits, unsigned gl_bytes,
+    const float* __restrict__ g_dist, unsigned gd_bytes, int streams, float* __restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  constexpr int kNX = PwLoads<NPTC>::kNX, kNG = PwLoads<NPTC>::kNG;
   const int npt = Pp / 32;
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
-  const int stream = wave / npt;                 // which pixel stream this wave works on
+  const int stream = wave / npt;                 // which pixel stream this wave computes on
   const int w = wave - stream * npt;             // prototype tile owned by this wave
-  const int nt_stream = npt * 64;                // threads per stream
-  const int tid_s = threadIdx.x - stream * nt_stream;
-  // LDS: [P image | W^T image | stream staging areas]. P rows (B operand of S) and W^T rows
-  // (B operand of g_act) are read per tile from LDS rather than held in registers.
-  bf16* Pimg = reinterpret_cast<bf16*>(smem_raw);      // [T][Pp][64]  CPR 8
+
+  // LDS: [P image | W^T image | stream staging areas]
+  bf16* Pimg = reinterpret_cast<bf16*>(smem_raw);      // [T][Pp][64]  CPR 8 (chan_of order)
   bf16* WTimg = Pimg + T * Pp * kC;                    // [T][Pp][32]  CPR 4
   unsigned char* stage_root = reinterpret_cast<unsigned char*>(WTimg + T * Pp * 32);
   stage_p_rows<T>(Pimg, protos, P, Pp);
   stage_wt_rows<T>(WTimg, w_last, g_logits ? K : 0, P, Pp);
-  unsigned char* stage_base = stage_root + static_cast<size_t>(stream) * PwStage<T>::kBytes;
   float *Xf, *Gf, *x2s;
-  int *rowb, *rown;
+  unsigned* rowoff;
   bf16 *XA, *XB, *GA, *GT;
-  pw_carve<T>(stage_base, Xf, Gf, x2s, rowb, rown, XA, XB, GA, GT);
+  pw_carve<T>(stage_root + static_cast<size_t>(stream) * PwStage<T>::kBytes, Xf, Gf, x2s, rowoff, XA, XB, GA, GT);
 
+  const rsrc_t rx = make_rsrc(x, x_bytes), rg = make_rsrc(g_logits, gl_bytes), rgd = make_rsrc(g_dist, gd_bytes);
   const int p = w * 32 + j;  // this lane's prototype column
   const bool pvalid = p < P;
   const float p2 = proto_norm2_64(protos, p, pvalid);
@@ -374,43 +419,61 @@ __global__ __launch_bounds__(768) void l2_bwd_pw_bf16_kernel(
 
   const int ntiles = (npix + 31) / 32;
   const int total_streams = gridDim.x * streams;
-  const int my_stream = blockIdx.x * streams + stream;
   const int iters = (ntiles + total_streams - 1) / total_streams;  // uniform across the workgroup
-  for (int it = 0; it < iters; ++it) {
-    const int t = my_stream + it * total_streams;
-    const bool tile_ok = t < ntiles;
-    // ---- stage: global -> fp32 LDS (coalesced along pixels) ----
-    __syncthreads();  // previous tile's operand reads are done
-    for (int idx = tid_s; idx < kC * 32; idx += nt_stream) {
-      const int c = idx >> 5, nn = idx & 31;
-      const int g = t * 32 + nn;
-      const bool ok = tile_ok && g < npix;
-      const int b = ok ? g / HW : 0;
-      const int n = ok ? g - b * HW : 0;
-      const float v = ldx(x, (static_cast<size_t>(b) * kC + c) * HW + n);
-      Xf[c * kLdf + nn] = ok ? v : 0.f;
-      if (c == 0) {
-        rowb[nn] = ok ? b : -1;
-        rown[nn] = n;
-      }
+  const int tid_s = threadIdx.x - stream * npt * 64;
+  const int nt_stream = npt * 64;
+  const int rstep = 2 * npt;            // rows advanced per load index i
+  const int r0 = tid_s >> 5, col = tid_s & 31;
+  const unsigned xs_step = static_cast<unsigned>(rstep * HW) * sizeof(TX);
+  const unsigned gs_step = static_cast<unsigned>(rstep * K) * 4u;
+
+  float xr[kNX], gr[kNG];
+  auto stage_load = [&](int it) {
+    const int t = blockIdx.x * streams + stream + it * total_streams;
+    const int g = t * 32 + col;
+    unsigned xo = kOOB;
+    if (t < ntiles && g < npix) {
+      const int b = g / HW;
+      xo = static_cast<unsigned>(((b * kC + r0) * HW + (g - b * HW)) * static_cast<int>(sizeof(TX)));
     }
-    for (int idx = tid_s; idx < 32 * 32; idx += nt_stream) {
-      const int nn = idx >> 5, k = idx & 31;
-      const int g = t * 32 + nn;
-      const bool ok = g_logits && tile_ok && g < npix && k < K;
-      const float v = g_logits ? g_logits[ok ? static_cast<size_t>(g) * K + k : 0] : 0.f;
-      Gf[nn * kLdf + k] = ok ? v : 0.f;
+    const int lim = t < ntiles ? min(32, npix - t * 32) : 0;  // valid pixel rows of g_logits
+    const unsigned go = (t < ntiles && col < K) ? static_cast<unsigned>(((t * 32 + r0) * K + col) * 4) : kOOB;
+#pragma unroll
+    for (int i = 0; i < kNX; ++i)
+      xr[i] = BufIO<TX>::load(rx, (r0 + i * rstep < kC) ? xo : kOOB, i * xs_step);
+#pragma unroll
+    for (int i = 0; i < kNG; ++i)
+      gr[i] = BufIO<float>::load(rg, (r0 + i * rstep < lim) ? go : kOOB, i * gs_step);
+  };
+
+  stage_load(0);
+  for (int it = 0; it < iters; ++it) {
+    const int t = blockIdx.x * streams + stream + it * total_streams;
+    __syncthreads();  // previous tile's operand reads are done
+    // ---- prefetched registers -> fp32 LDS staging ----
+#pragma unroll
+    for (int i = 0; i < kNX; ++i)
+      if (r0 + i * rstep < kC) Xf[(r0 + i * rstep) * kLdf + col] = xr[i];
+#pragma unroll
+    for (int i = 0; i < kNG; ++i)
+      if (r0 + i * rstep < 32) Gf[(r0 + i * rstep) * kLdf + col] = gr[i];
+    stage_load(it + 1);  // prefetch the next tile while this one is converted and computed
+    if (tid_s < 32) {    // per-row g_dist offset (b, n) of this tile
+      const int g = t * 32 + tid_s;
+      const bool ok = t < ntiles && g < npix;
+      const int b = ok ? g / HW : 0;
+      rowoff[tid_s] = ok ? static_cast<unsigned>((b * P * HW + (g - b * HW)) * 4) : kOOB;
     }
     __syncthreads();
     // ---- convert to split bf16 operand images ----
-    for (int idx = tid_s; idx < 32 * 8; idx += nt_stream) {  // XA: row n, chunk q8
-      const int nn = idx >> 3, q8 = idx & 7;
+    for (int idx = tid_s; idx < 32 * 8; idx += nt_stream) {  // XA: row n, chunk e8 = (q, h)
+      const int nn = idx >> 3, e8 = idx & 7, q = e8 >> 1, hh = e8 & 1;
       float v[8];
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) v[jj] = Xf[(q8 * 8 + jj) * kLdf + nn];
+      for (int jj = 0; jj < 8; ++jj) v[jj] = Xf[chan_of(q, hh, jj) * kLdf + nn];
       bf16x8 f[T];
       split8<T>(v, f);
-      store_frag<T>(XA, 32 * kC, img_off<8>(nn, q8), f);
+      store_frag<T>(XA, 32 * kC, img_off<8>(nn, e8), f);
     }
     for (int idx = tid_s; idx < kC * 4; idx += nt_stream) {  // XB: row c, permuted pixels
       const int c = idx >> 2, e8 = idx & 3;
@@ -435,14 +498,14 @@ __global__ __launch_bounds__(768) void l2_bwd_pw_bf16_kernel(
       store_frag<T>(GA, 32 * 32, img_off<4>(r, e8), f);
       store_frag<T>(GT, 32 * 32, img_off<4>(r, e8), ft);
     }
-    if (tid_s < 32) {  // ||x||^2 per pixel, the same chain as load_x_frags
+    if (tid_s < 32) {  // ||x||^2 per pixel: the chain of x_frags (half 0, half 1, then the sum)
       const int nn = tid_s;
       float s0 = 0.f, s1 = 0.f;
 #pragma unroll
       for (int q = 0; q < kNQ; ++q)
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) {
-          const float a = Xf[(16 * q + jj) * kLdf + nn], c = Xf[(16 * q + 8 + jj) * kLdf + nn];
+          const float a = Xf[chan_of(q, 0, jj) * kLdf + nn], c = Xf[chan_of(q, 1, jj) * kLdf + nn];
           s0 = fmaf(a, a, s0);
           s1 = fmaf(c, c, s1);
         }
@@ -471,19 +534,16 @@ __global__ __launch_bounds__(768) void l2_bwd_pw_bf16_kernel(
         }
       }
     }
+    const unsigned pcol = static_cast<unsigned>(p * HW * 4);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int nr = acc_row(r, h);
-      const int br = rowb[nr];
-      const bool rvalid = br >= 0;
+      const unsigned ro = rowoff[nr];
+      const bool rvalid = ro != kOOB;
       const float d = l2_distance(x2s[nr], p2, acc[r]);
-      const float a = activation(d, eps, act_kind);
-      float gd = g_logits ? gacc[r] * activation_grad(d, eps, act_kind) : 0.f;
-      if (g_dist) {
-        const bool ok = rvalid && pvalid;
-        const float v = g_dist[ok ? (static_cast<size_t>(br) * P + p) * HW + rown[nr] : 0];
-        gd += ok ? v : 0.f;
-      }
+      const float a = act_fast<ACT>(d, eps);
+      float gd = g_logits ? gacc[r] * act_grad_fast<ACT>(d, eps) : 0.f;
+      if (g_dist) gd += BufIO<float>::load(rgd, (rvalid && pvalid) ? ro + pcol : kOOB, 0);
       const float gs = (d > 0.f && pvalid && rvalid) ? gd : 0.f;
       gsum += gs;
       acc[r] = -2.f * gs;
@@ -533,25 +593,29 @@ __global__ __launch_bounds__(768) void l2_bwd_pw_bf16_kernel(
       for (int r = 0; r < 16; ++r) {
         const int pr = acc_row(r, h);
         float v = gp[ct][r];
-        for (int s2 = 1; s2 < streams; ++s2) v += red[static_cast<size_t>((s2 - 1) * npt + w) * kPerWave + pr * kC + ct * 32 + j];
+        for (int s2 = 1; s2 < streams; ++s2)
+          v += red[static_cast<size_t>((s2 - 1) * npt + w) * kPerWave + pr * kC + ct * 32 + j];
         my_slab[static_cast<size_t>(w * 32 + pr) * kC + ct * 32 + j] = v;
       }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int k = acc_row(r, h);
       float v = gw[r];
-      for (int s2 = 1; s2 < streams; ++s2) v += red[static_cast<size_t>((s2 - 1) * npt + w) * kPerWave + 32 * kC + k * 32 + j];
+      for (int s2 = 1; s2 < streams; ++s2)
+        v += red[static_cast<size_t>((s2 - 1) * npt + w) * kPerWave + 32 * kC + k * 32 + j];
       my_slab[static_cast<size_t>(Pp) * kC + static_cast<size_t>(k) * Pp + w * 32 + j] = v;
     }
     if (h == 0) {
       float v = gsum;
-      for (int s2 = 1; s2 < streams; ++s2) v += red[static_cast<size_t>((s2 - 1) * npt + w) * kPerWave + 32 * kC + 1024 + j];
+      for (int s2 = 1; s2 < streams; ++s2)
+        v += red[static_cast<size_t>((s2 - 1) * npt + w) * kPerWave + 32 * kC + 1024 + j];
       my_slab[static_cast<size_t>(Pp) * kC + 32 * Pp + w * 32 + j] = v;
     }
   }
 }
 
-// Slab sum: 64 elements x 4 slab groups per workgroup, groups combined in fixed order.
+// Slab sum: 64 elements x 4 slab groups per workgroup, groups combined in fixed order; each
+// thread keeps 8 independent loads in flight.
 __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __restrict__ slab, int S, int P,
                                                                   int Pp, int K, const float* __restrict__ protos,
                                                                   float* __restrict__ g_protos,
@@ -561,19 +625,35 @@ __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __
   const int E = Pp * kC + 32 * Pp + Pp;
   const int e = blockIdx.x * 64 + (threadIdx.x & 63);
   const int grp = threadIdx.x >> 6;
+  const bool active = e < Pp * kC + 32 * Pp;
   const bool is_gp = e < Pp * kC;
   const int p_of_e = is_gp ? e / kC : 0;
+  const int gs_e = Pp * kC + 32 * Pp + p_of_e;
   float s = 0.f, gs = 0.f;
-  if (e < Pp * kC + 32 * Pp) {
-    for (int si = grp; si < S; si += 4) {
+  if (active) {
+    int si = grp;
+    for (; si + 28 < S; si += 32) {  // 8 slabs per step for this group
+      float v[8], u[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        v[k] = slab[static_cast<size_t>(si + 4 * k) * E + e];
+        u[k] = is_gp ? slab[static_cast<size_t>(si + 4 * k) * E + gs_e] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s += v[k];
+        gs += u[k];
+      }
+    }
+    for (; si < S; si += 4) {
       s += slab[static_cast<size_t>(si) * E + e];
-      if (is_gp) gs += slab[static_cast<size_t>(si) * E + Pp * kC + 32 * Pp + p_of_e];
+      if (is_gp) gs += slab[static_cast<size_t>(si) * E + gs_e];
     }
   }
   part[grp][threadIdx.x & 63] = s;
   gpart[grp][threadIdx.x & 63] = gs;
   __syncthreads();
-  if (grp != 0 || e >= Pp * kC + 32 * Pp) return;
+  if (grp != 0 || !active) return;
   const int l = threadIdx.x;
   const float tot = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
   if (is_gp) {
@@ -589,6 +669,7 @@ __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __
   }
 }
 
+// ---- host side ---------------------------------------------------------------------------------
 size_t fwd_lds(const Geometry& g, int terms) { return static_cast<size_t>(g.Pp) * (terms * (kC + 32) * 2 + 4); }
 size_t bwd_x_lds(const Geometry& g, int terms) {
   return static_cast<size_t>(g.Pp) * (terms * (2 * kC + 32) * 2 + 4);
@@ -607,45 +688,55 @@ int pw_grid(const Geometry& g) {
   const int need = static_cast<int>(ceil_div(g.ntiles, streams));
   return need < 256 ? need : 256;
 }
+// npt class sizing the staging registers: the largest of {1, 2, 4, 6} not above npt.
+int pw_nptc(const Geometry& g) {
+  const int npt = g.Pp / 32;
+  return npt >= 6 ? 6 : npt >= 4 ? 4 : npt >= 2 ? 2 : 1;
+}
 
-template <typename TX, int T>
-int fwd_t(const Geometry& g, const void* x, const float* protos, const float* w_last, float eps, int act_kind,
+struct Bytes {
+  unsigned x, d, a, l, gl, gd;
+};
+
+template <typename TX, int T, int ACT>
+int fwd_t(const Geometry& g, const Bytes& nb, const void* x, const float* protos, const float* w_last, float eps,
           float* dist, float* act, float* logits, hipStream_t stream) {
-  if (int st = ensure_lds<l2_fwd_bf16_kernel<TX, T>>()) return st;
+  if (int st = ensure_lds<l2_fwd_bf16_kernel<TX, T, ACT>>()) return st;
   const size_t lds = fwd_lds(g, T);
   const int per_cu = static_cast<int>(kMaxLds / lds);
   const int cap = 256 * (per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu));
   const int want = static_cast<int>(ceil_div(g.ntiles, kWavesA));
-  hipLaunchKernelGGL((l2_fwd_bf16_kernel<TX, T>), dim3(want < cap ? want : cap), dim3(kWavesA * 64), lds, stream,
-                     static_cast<const TX*>(x), g.HW, g.npix, protos, g.P, g.Pp, w_last, g.K, eps, act_kind, dist,
-                     act, logits);
+  hipLaunchKernelGGL((l2_fwd_bf16_kernel<TX, T, ACT>), dim3(want < cap ? want : cap), dim3(kWavesA * 64), lds,
+                     stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, protos, g.P, g.Pp, w_last, g.K, eps, dist,
+                     nb.d, act, nb.a, logits, nb.l);
   return check_launch("l2_fwd_bf16_kernel");
 }
 
-template <typename TX, int T>
-int bwd_x_t(const Geometry& g, const void* x, const float* protos, const float* w_last, float eps, int act_kind,
+template <typename TX, int T, int ACT>
+int bwd_x_t(const Geometry& g, const Bytes& nb, const void* x, const float* protos, const float* w_last, float eps,
             const float* g_logits, const float* g_dist, void* g_x, hipStream_t stream) {
-  if (int st = ensure_lds<l2_bwd_x_bf16_kernel<TX, T>>()) return st;
+  if (int st = ensure_lds<l2_bwd_x_bf16_kernel<TX, T, ACT>>()) return st;
   const size_t lds = bwd_x_lds(g, T);
   const int per_cu = static_cast<int>(kMaxLds / lds);
   const int cap = 256 * (per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu));
   const int want = static_cast<int>(ceil_div(g.ntiles, kWavesA));
-  hipLaunchKernelGGL((l2_bwd_x_bf16_kernel<TX, T>), dim3(want < cap ? want : cap), dim3(kWavesA * 64), lds, stream,
-                     static_cast<const TX*>(x), g.HW, g.npix, protos, g.P, g.Pp, w_last, g.K, eps, act_kind, g_logits,
-                     g_dist, static_cast<TX*>(g_x));
+  hipLaunchKernelGGL((l2_bwd_x_bf16_kernel<TX, T, ACT>), dim3(want < cap ? want : cap), dim3(kWavesA * 64), lds,
+                     stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, protos, g.P, g.Pp, w_last, g.K, eps,
+                     g_logits, nb.gl, g_dist, nb.gd, static_cast<TX*>(g_x));
   return check_launch("l2_bwd_x_bf16_kernel");
 }
 
-template <typename TX, int T>
-int bwd_pw_t(const Geometry& g, const void* x, const float* protos, const float* w_last, float eps, int act_kind,
-             const float* g_logits, const float* g_dist, float* g_protos, float* g_w, float* ws, hipStream_t stream) {
-  if (int st = ensure_lds<l2_bwd_pw_bf16_kernel<TX, T>>()) return st;
+template <typename TX, int T, int ACT, int NPTC>
+int bwd_pw_nptc(const Geometry& g, const Bytes& nb, const void* x, const float* protos, const float* w_last, float eps,
+               const float* g_logits, const float* g_dist, float* g_protos, float* g_w, float* ws,
+               hipStream_t stream) {
+  if (int st = ensure_lds<l2_bwd_pw_bf16_kernel<TX, T, ACT, NPTC>>()) return st;
   const int streams = pw_streams(g);
   const int grid = pw_grid(g);
   const int threads = streams * (g.Pp / 32) * 64;
-  hipLaunchKernelGGL((l2_bwd_pw_bf16_kernel<TX, T>), dim3(grid), dim3(threads), pw_lds(g, T), stream,
-                     static_cast<const TX*>(x), g.HW, g.npix, protos, g.P, g.Pp, w_last, g.K, eps, act_kind, g_logits,
-                     g_dist, streams, ws);
+  hipLaunchKernelGGL((l2_bwd_pw_bf16_kernel<TX, T, ACT, NPTC>), dim3(grid), dim3(threads), pw_lds(g, T), stream,
+                     static_cast<const TX*>(x), nb.x, g.HW, g.npix, protos, g.P, g.Pp, w_last, g.K, eps, g_logits,
+                     nb.gl, g_dist, nb.gd, streams, ws);
   if (int st = check_launch("l2_bwd_pw_bf16_kernel")) return st;
   const int elems = g.Pp * kC + 32 * g.Pp;
   hipLaunchKernelGGL(l2_bwd_reduce_bf16_kernel, dim3(static_cast<unsigned>(ceil_div(elems, 64))), dim3(256), 0,
@@ -653,22 +744,66 @@ int bwd_pw_t(const Geometry& g, const void* x, const float* protos, const float*
   return check_launch("l2_bwd_reduce_bf16_kernel");
 }
 
-template <typename Fn>
-int by_type(bool x_bf16, int terms, Fn&& fn) {
-  if (terms == 2) {
-    return x_bf16 ? fn(static_cast<uint16_t*>(nullptr), std::integral_constant<int, 2>())
-                  : fn(static_cast<float*>(nullptr), std::integral_constant<int, 2>());
+template <typename TX, int T, int ACT>
+int bwd_pw_t(const Geometry& g, const Bytes& nb, const void* x, const float* protos, const float* w_last, float eps,
+             const float* g_logits, const float* g_dist, float* g_protos, float* g_w, float* ws, hipStream_t stream) {
+  switch (pw_nptc(g)) {
+    case 6:
+      return bwd_pw_nptc<TX, T, ACT, 6>(g, nb, x, protos, w_last, eps, g_logits, g_dist, g_protos, g_w, ws, stream);
+    case 4:
+      return bwd_pw_nptc<TX, T, ACT, 4>(g, nb, x, protos, w_last, eps, g_logits, g_dist, g_protos, g_w, ws, stream);
+    case 2:
+      return bwd_pw_nptc<TX, T, ACT, 2>(g, nb, x, protos, w_last, eps, g_logits, g_dist, g_protos, g_w, ws, stream);
+    default:
+      return bwd_pw_nptc<TX, T, ACT, 1>(g, nb, x, protos, w_last, eps, g_logits, g_dist, g_protos, g_w, ws, stream);
   }
-  return x_bf16 ? fn(static_cast<uint16_t*>(nullptr), std::integral_constant<int, 3>())
-                : fn(static_cast<float*>(nullptr), std::integral_constant<int, 3>());
+}
+
+template <typename Fn>
+int by_type(bool x_bf16, int terms, int act_kind, Fn&& fn) {
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  using A0 = std::integral_constant<int, 0>;
+  using A1 = std::integral_constant<int, 1>;
+  float* f = nullptr;
+  uint16_t* b = nullptr;
+  if (act_kind == 0) {
+    if (terms == 2) return x_bf16 ? fn(b, I2(), A0()) : fn(f, I2(), A0());
+    return x_bf16 ? fn(b, I3(), A0()) : fn(f, I3(), A0());
+  }
+  if (terms == 2) return x_bf16 ? fn(b, I2(), A1()) : fn(f, I2(), A1());
+  return x_bf16 ? fn(b, I3(), A1()) : fn(f, I3(), A1());
+}
+
+Bytes bytes_of(const Geometry& g, bool x_bf16) {
+  Bytes nb;
+  const unsigned long long npix = static_cast<unsigned long long>(g.npix);
+  nb.x = static_cast<unsigned>(npix * kC * (x_bf16 ? 2 : 4));
+  nb.d = static_cast<unsigned>(npix * g.P * 4);
+  nb.a = nb.d;
+  nb.l = static_cast<unsigned>(npix * g.K * 4);
+  nb.gl = nb.l;
+  nb.gd = nb.d;
+  return nb;
 }
 
 }  // namespace
 
-bool bf16_fwd_fits(const Geometry& g, int terms) { return g.C == kC && fwd_lds(g, terms) <= kMaxLds; }
-bool bf16_bwd_x_fits(const Geometry& g, int terms) { return g.C == kC && bwd_x_lds(g, terms) <= kMaxLds; }
+// Every buffer these kernels address must stay below 2^31 bytes (kOOB arithmetic).
+bool bf16_sizes_ok(const Geometry& g) {
+  const unsigned long long npix = static_cast<unsigned long long>(g.npix);
+  const unsigned long long big = npix * 4ull * static_cast<unsigned long long>(g.P > kC ? g.P : kC);
+  return big < (1ull << 31);
+}
+
+bool bf16_fwd_fits(const Geometry& g, int terms) {
+  return g.C == kC && fwd_lds(g, terms) <= kMaxLds && bf16_sizes_ok(g);
+}
+bool bf16_bwd_x_fits(const Geometry& g, int terms) {
+  return g.C == kC && bwd_x_lds(g, terms) <= kMaxLds && bf16_sizes_ok(g);
+}
 bool bf16_bwd_pw_fits(const Geometry& g, int terms) {
-  return g.C == kC && g.Pp <= 384 && pw_lds(g, terms) <= kMaxLds;
+  return g.C == kC && g.Pp <= 384 && pw_lds(g, terms) <= kMaxLds && bf16_sizes_ok(g);
 }
 size_t bf16_bwd_pw_workspace(const Geometry& g) {
   return static_cast<size_t>(pw_grid(g)) * (static_cast<size_t>(g.Pp) * kC + 32 * g.Pp + g.Pp) * sizeof(float);
@@ -677,28 +812,33 @@ size_t bf16_bwd_pw_workspace(const Geometry& g) {
 int launch_fwd_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const float* protos,
                     const float* w_last, float eps, int act_kind, float* dist, float* act, float* logits,
                     hipStream_t stream) {
-  return by_type(x_bf16, terms, [&](auto tx, auto tt) {
+  const Bytes nb = bytes_of(g, x_bf16);
+  return by_type(x_bf16, terms, act_kind, [&](auto tx, auto tt, auto aa) {
     using TX = std::remove_pointer_t<decltype(tx)>;
-    return fwd_t<TX, decltype(tt)::value>(g, x, protos, w_last, eps, act_kind, dist, act, logits, stream);
+    return fwd_t<TX, decltype(tt)::value, decltype(aa)::value>(g, nb, x, protos, w_last, eps, dist, act, logits,
+                                                               stream);
   });
 }
 
 int launch_bwd_x_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const float* protos,
                       const float* w_last, float eps, int act_kind, const float* g_logits, const float* g_dist,
                       void* g_x, hipStream_t stream) {
-  return by_type(x_bf16, terms, [&](auto tx, auto tt) {
+  const Bytes nb = bytes_of(g, x_bf16);
+  return by_type(x_bf16, terms, act_kind, [&](auto tx, auto tt, auto aa) {
     using TX = std::remove_pointer_t<decltype(tx)>;
-    return bwd_x_t<TX, decltype(tt)::value>(g, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_x, stream);
+    return bwd_x_t<TX, decltype(tt)::value, decltype(aa)::value>(g, nb, x, protos, w_last, eps, g_logits, g_dist, g_x,
+                                                                 stream);
   });
 }
 
 int launch_bwd_pw_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const float* protos,
                        const float* w_last, float eps, int act_kind, const float* g_logits, const float* g_dist,
                        float* g_protos, float* g_w, float* ws, hipStream_t stream) {
-  return by_type(x_bf16, terms, [&](auto tx, auto tt) {
+  const Bytes nb = bytes_of(g, x_bf16);
+  return by_type(x_bf16, terms, act_kind, [&](auto tx, auto tt, auto aa) {
     using TX = std::remove_pointer_t<decltype(tx)>;
-    return bwd_pw_t<TX, decltype(tt)::value>(g, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_protos, g_w, ws,
-                                             stream);
+    return bwd_pw_t<TX, decltype(tt)::value, decltype(aa)::value>(g, nb, x, protos, w_last, eps, g_logits, g_dist,
+                                                                  g_protos, g_w, ws, stream);
   });
 }
 

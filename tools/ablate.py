@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--protos", type=int, default=190)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--precision", default="bf16x3")
+    ap.add_argument("--only", default="", help="comma-separated variant names (default: all)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     B, C, h, w, P, K = args.batch, 64, 65, 65, args.protos, 19
@@ -57,6 +58,8 @@ def main():
         "bwd_pw": lambda: _lib.call("protoseg_l2_bwd", P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 0, prec,
                                     P_(gl), null, null, P_(gp), P_(gw), P_(ws), ws_b, s()),
     }
+    if args.only:
+        variants = {k: v for k, v in variants.items() if k in args.only.split(",")}
     for fn in variants.values():
         fn()
     torch.cuda.synchronize()
