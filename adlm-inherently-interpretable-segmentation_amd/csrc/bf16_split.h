@@ -181,3 +181,33 @@ __device__ __forceinline__ constexpr int chan_of(int q, int h, int jj) { return 
 __device__ __forceinline__ constexpr int chan_base(int q, int jj) { return chan_of(q, 0, jj); }
 
 }  // namespace protoseg
+
+// ---- optional per-wave phase timestamps (debug builds: make stamps) --------------------------
+// STAMP(slot) records s_memtime for (workgroup, wave, slot) into g_stamps; the host reads them
+// with protoseg_debug_stamps(). Compiled out unless PROTOSEG_STAMPS is defined.
+#ifdef PROTOSEG_STAMPS
+namespace protoseg {
+constexpr int kStampSlots = 8;
+constexpr int kStampCap = 1 << 17;
+__device__ extern unsigned long long g_stamps[kStampCap];
+}  // namespace protoseg
+#define STAMP(slot)                                                                                   \
+  do {                                                                                                \
+    const unsigned _w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);                          \
+    if ((threadIdx.x & 63) == 0 && _w * ::protoseg::kStampSlots + (slot) < ::protoseg::kStampCap)      \
+      ::protoseg::g_stamps[_w * ::protoseg::kStampSlots + (slot)] = __builtin_amdgcn_s_memtime();     \
+  } while (0)
+#define STAMP_RT(slot)                                                                                \
+  do {                                                                                                \
+    const unsigned _w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);                          \
+    if ((threadIdx.x & 63) == 0 && _w * ::protoseg::kStampSlots + (slot) < ::protoseg::kStampCap)      \
+      ::protoseg::g_stamps[_w * ::protoseg::kStampSlots + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define STAMP_RT(slot) \
+  do {                 \
+  } while (0)
+#define STAMP(slot) \
+  do {              \
+  } while (0)
+#endif

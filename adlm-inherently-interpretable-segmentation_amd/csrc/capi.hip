@@ -29,3 +29,4 @@ int check_launch(const char* what) {
 extern "C" int protoseg_version(void) { return 1 * 10000 + 0 * 100 + 0; }
 
 extern "C" const char* protoseg_last_error(void) { return protoseg::g_last_error; }
+

@@ -35,9 +35,9 @@ constexpr int kLdf = 33;       // padded fp32 staging rows
 // P image [T][Pp][64]: row p, chunk 2q+h = channels chan_of(q, h, 0..7) (CPR 8).
 // Operand of S in every kernel: A in layout A (lane = p), B in layout B (lane = p).
 template <int T>
-__device__ void stage_p_rows(bf16* img, const float* __restrict__ protos, int P, int Pp) {
+__device__ void stage_p_rows(bf16* img, const float* __restrict__ protos, int P, int Pp, int tid, int nth) {
   const int plane = Pp * kC;
-  for (int idx = threadIdx.x; idx < Pp * 8; idx += blockDim.x) {
+  for (int idx = tid; idx < Pp * 8; idx += nth) {
     const int p = idx >> 3, e8 = idx & 7, q = e8 >> 1, h = e8 & 1;
     float v[8];
 #pragma unroll
@@ -50,9 +50,9 @@ __device__ void stage_p_rows(bf16* img, const float* __restrict__ protos, int P,
 
 // P^T image [T][npt][64 c][32 p-permuted] (CPR 4) — A operand of g_x^T = P^T g_s.
 template <int T>
-__device__ void stage_pt_perm(bf16* img, const float* __restrict__ protos, int P, int Pp) {
+__device__ void stage_pt_perm(bf16* img, const float* __restrict__ protos, int P, int Pp, int tid, int nth) {
   const int plane = Pp * kC;
-  for (int idx = threadIdx.x; idx < (Pp / 32) * kC * 4; idx += blockDim.x) {
+  for (int idx = tid; idx < (Pp / 32) * kC * 4; idx += nth) {
     const int pt = idx / (kC * 4), c = (idx >> 2) & (kC - 1), e8 = idx & 3;
     float v[8];
 #pragma unroll
@@ -68,9 +68,9 @@ __device__ void stage_pt_perm(bf16* img, const float* __restrict__ protos, int P
 
 // W image [T][npt][32 k][32 p-permuted] (CPR 4) — A operand of logits = W . act.
 template <int T>
-__device__ void stage_w_perm(bf16* img, const float* __restrict__ w, int K, int P, int Pp) {
+__device__ void stage_w_perm(bf16* img, const float* __restrict__ w, int K, int P, int Pp, int tid, int nth) {
   const int plane = Pp * 32;
-  for (int idx = threadIdx.x; idx < Pp * 4; idx += blockDim.x) {
+  for (int idx = tid; idx < Pp * 4; idx += nth) {
     const int row = idx >> 2, e8 = idx & 3;  // row = pt*32 + k
     const int pt = row >> 5, k = row & 31;
     float v[8];
@@ -88,9 +88,9 @@ __device__ void stage_w_perm(bf16* img, const float* __restrict__ w, int K, int 
 // W^T image [T][Pp][32 k] natural classes (CPR 4) — operand of g_act: A in layout A
 // (lane = p), B in layout B (lane = p).
 template <int T>
-__device__ void stage_wt_rows(bf16* img, const float* __restrict__ w, int K, int P, int Pp) {
+__device__ void stage_wt_rows(bf16* img, const float* __restrict__ w, int K, int P, int Pp, int tid, int nth) {
   const int plane = Pp * 32;
-  for (int idx = threadIdx.x; idx < Pp * 4; idx += blockDim.x) {
+  for (int idx = tid; idx < Pp * 4; idx += nth) {
     const int p = idx >> 2, e8 = idx & 3;
     float v[8];
 #pragma unroll
@@ -101,6 +101,19 @@ __device__ void stage_wt_rows(bf16* img, const float* __restrict__ w, int K, int
     bf16x8 f[T];
     split8<T>(v, f);
     store_frag<T>(img, plane, img_off<4>(p, e8), f);
+  }
+}
+
+// v[r] = rows[acc_row(r, h) - 4h] for a 16-B aligned LDS row block (4 x ds_read_b128): the
+// per-row scalars of one accumulator tile, read once instead of per element.
+__device__ __forceinline__ void load_rows16(const float* rows, float (&v)[16]) {
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    const float4 q = *reinterpret_cast<const float4*>(rows + 8 * g4);
+    v[4 * g4] = q.x;
+    v[4 * g4 + 1] = q.y;
+    v[4 * g4 + 2] = q.z;
+    v[4 * g4 + 3] = q.w;
   }
 }
 
@@ -115,6 +128,63 @@ __device__ float proto_norm2_64(const float* __restrict__ protos, int p, bool va
     }
   }
   return s;
+}
+
+// Operand images of the prototypes and the last layer, built once per call by
+// l2_prep_bf16_kernel into a global block laid out exactly as the kernels' LDS regions, so each
+// workgroup fills its LDS with 16-B LDS-DMA copies (one round trip) instead of re-deriving them.
+//   [P image T*Pp*128 B | W^T image T*Pp*64 | ||p||^2 (Pp floats, padded to 1 KiB) |
+//    P^T image T*Pp*128 | W image T*Pp*64]      (every region a multiple of 1 KiB)
+struct ImgOffsets {
+  int p, wt, p2, pt, w, total;
+};
+__host__ __device__ inline ImgOffsets img_offsets(int Pp, int T) {
+  ImgOffsets o;
+  o.p = 0;
+  o.wt = T * Pp * 128;
+  o.p2 = o.wt + T * Pp * 64;
+  o.pt = o.p2 + ((Pp * 4 + 1023) & ~1023);
+  o.w = o.pt + T * Pp * 128;
+  o.total = o.w + T * Pp * 64;
+  return o;
+}
+
+// blockIdx.y selects the image, so the five loops (each a few load round trips) run concurrently.
+template <int T>
+__global__ __launch_bounds__(256) void l2_prep_bf16_kernel(const float* __restrict__ protos, int P, int Pp,
+                                                           const float* __restrict__ w_last, int K,
+                                                           unsigned char* __restrict__ block) {
+  const ImgOffsets o = img_offsets(Pp, T);
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+  switch (blockIdx.y) {
+    case 0:
+      stage_p_rows<T>(reinterpret_cast<bf16*>(block + o.p), protos, P, Pp, tid, nth);
+      break;
+    case 1:
+      stage_wt_rows<T>(reinterpret_cast<bf16*>(block + o.wt), w_last, w_last ? K : 0, P, Pp, tid, nth);
+      break;
+    case 2:
+      stage_pt_perm<T>(reinterpret_cast<bf16*>(block + o.pt), protos, P, Pp, tid, nth);
+      break;
+    case 3:
+      stage_w_perm<T>(reinterpret_cast<bf16*>(block + o.w), w_last, w_last ? K : 0, P, Pp, tid, nth);
+      break;
+    default: {
+      float* p2 = reinterpret_cast<float*>(block + o.p2);
+      for (int p = tid; p < (o.pt - o.p2) / 4; p += nth) p2[p] = proto_norm2_64(protos, p, p < P);
+    }
+  }
+}
+
+// Workgroup-wide copy of `bytes` (a multiple of 1 KiB) from global to LDS by 16-B LDS-DMA
+// (global_load_lds_dwordx4: one wave-instruction moves 1 KiB, lane-linear). The caller's
+// __syncthreads() waits for it.
+__device__ __forceinline__ void lds_copy(void* lds, const unsigned char* src, int bytes) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int off = wave * 1024; off < bytes; off += nw * 1024)
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)(src + off + lane * 16),
+        (__attribute__((address_space(3))) void*)(static_cast<unsigned char*>(lds) + off), 16, 0, 0);
 }
 
 // Byte offset of this lane's pixel at channel 4h of image b (layout A lane = pixel j), or kOOB.
@@ -153,20 +223,24 @@ __device__ __forceinline__ float x_frags(const float (&raw)[kNQ * 8], bf16x8 (&x
   return x2 + __shfl_xor(x2, 32);
 }
 
-template <typename TX, int T, int ACT>
+template <typename TX, int T, int ACT, bool ACTS>
 __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
-    const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const float* __restrict__ protos, int P, int Pp,
-    const float* __restrict__ w_last, int K, float eps, float* __restrict__ dist, unsigned d_bytes,
+    const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const unsigned char* __restrict__ img, int P, int Pp,
+    int K, float eps, float* __restrict__ dist, unsigned d_bytes,
     float* __restrict__ act_out, unsigned a_bytes, float* __restrict__ logits, unsigned l_bytes) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  STAMP(0);
+  STAMP_RT(7);
+  const ImgOffsets io = img_offsets(Pp, T);
   bf16* Pimg = reinterpret_cast<bf16*>(smem_raw);                // [T][Pp][64]
   bf16* Wimg = Pimg + T * Pp * kC;                               // [T][Pp][32]
   float* p2s = reinterpret_cast<float*>(Wimg + T * Pp * 32);     // [Pp]
   const bool do_logits = logits != nullptr;
-  stage_p_rows<T>(Pimg, protos, P, Pp);
-  if (do_logits) stage_w_perm<T>(Wimg, w_last, K, P, Pp);
-  for (int p = threadIdx.x; p < Pp; p += blockDim.x) p2s[p] = proto_norm2_64(protos, p, p < P);
+  lds_copy(Pimg, img + io.p, io.wt - io.p);
+  lds_copy(Wimg, img + io.w, io.total - io.w);
+  lds_copy(p2s, img + io.p2, io.pt - io.p2);
   __syncthreads();
+  STAMP(1);
 
   const rsrc_t rx = make_rsrc(x, x_bytes), rd = make_rsrc(dist, d_bytes);
   const rsrc_t ra = make_rsrc(act_out, a_bytes), rl = make_rsrc(logits, l_bytes);
@@ -181,6 +255,8 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
   for (; t < ntiles; t += stride) {
     bf16x8 xb[kNQ][T];
     const float x2 = x_frags<T>(raw, xb);
+    const bool first = t == static_cast<int>(blockIdx.x) * kWavesA + wave;
+    if (first) STAMP(2);
     load_x_raw<TX>(rx, x_lane_off<TX>(t + stride, ntiles, npix, HW), cs, raw);  // prefetch next tile
 
     const int g = t * 32 + j;
@@ -201,16 +277,25 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
         acc = mma_split<T>(pa, xb[q], acc);
       }
       const int prem = P - pt * 32 - 4 * h;  // rows of this tile (and half) below P
+      float p2r[16];
+      load_rows16(p2s + pt * 32 + 4 * h, p2r);
+      // Distances / activations: no branches per element (a null output has a zero-size
+      // buffer resource, so its stores are dropped); full prototype tiles skip the row test.
+      auto epilogue = [&](auto full) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int p = pt * 32 + acc_row(r, h);
-        const float d = l2_distance(x2, p2s[p], acc[r]);
-        const bool pin = row_of(r) < prem;
-        if (dist) BufIO<float>::store(rd, d, pin ? dbase : kOOB, static_cast<unsigned>((pt * 32 + row_of(r)) * HW * 4));
-        const float a = act_fast<ACT>(d, eps);
-        if (act_out) BufIO<float>::store(ra, a, pin ? abase : kOOB, static_cast<unsigned>((pt * 32 + row_of(r)) * 4));
-        acc[r] = a;
-      }
+        for (int r = 0; r < 16; ++r) {
+          const float d = l2_distance(x2, p2r[r], acc[r]);
+          const bool pin = decltype(full)::value || row_of(r) < prem;
+          BufIO<float>::store(rd, d, pin ? dbase : kOOB, static_cast<unsigned>((pt * 32 + row_of(r)) * HW * 4));
+          const float a = act_fast<ACT>(d, eps);
+          if constexpr (ACTS) BufIO<float>::store(ra, a, pin ? abase : kOOB, static_cast<unsigned>((pt * 32 + row_of(r)) * 4));
+          acc[r] = a;
+        }
+      };
+      if ((pt + 1) * 32 <= P)
+        epilogue(std::true_type());
+      else
+        epilogue(std::false_type());
       if (do_logits) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
@@ -220,7 +305,9 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
           lacc = mma_split<T>(wa, ab, lacc);
         }
       }
+      if (pt == 0 && first) STAMP(3);
     }
+    if (first) STAMP(4);
     if (do_logits) {
       const unsigned lbase = valid ? static_cast<unsigned>((g * K + 4 * h) * 4) : kOOB;
       const int krem = K - 4 * h;
@@ -228,23 +315,26 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
       for (int r = 0; r < 16; ++r)
         BufIO<float>::store(rl, lacc[r], row_of(r) < krem ? lbase : kOOB, static_cast<unsigned>(row_of(r) * 4));
     }
+    if (first) STAMP(5);
   }
+  STAMP(6);
 }
 
-template <typename TX, int T, int ACT>
+template <typename TX, int T, int ACT, bool GD>
 __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
-    const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const float* __restrict__ protos, int P, int Pp,
-    const float* __restrict__ w_last, int K, float eps, const float* __restrict__ g_logits, unsigned gl_bytes,
+    const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const unsigned char* __restrict__ img, int P, int Pp,
+    int K, float eps, const float* __restrict__ g_logits, unsigned gl_bytes,
     const float* __restrict__ g_dist, unsigned gd_bytes, TX* __restrict__ g_x) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const ImgOffsets io = img_offsets(Pp, T);
   bf16* Pimg = reinterpret_cast<bf16*>(smem_raw);                 // [T][Pp][64]
   bf16* PTimg = Pimg + T * Pp * kC;                               // [T][npt*64][32]
   bf16* WTimg = PTimg + T * Pp * kC;                              // [T][Pp][32]
   float* p2s = reinterpret_cast<float*>(WTimg + T * Pp * 32);     // [Pp]
-  stage_p_rows<T>(Pimg, protos, P, Pp);
-  stage_pt_perm<T>(PTimg, protos, P, Pp);
-  if (g_logits) stage_wt_rows<T>(WTimg, w_last, K, P, Pp);
-  for (int p = threadIdx.x; p < Pp; p += blockDim.x) p2s[p] = proto_norm2_64(protos, p, p < P);
+  lds_copy(Pimg, img + io.p, io.wt - io.p);
+  lds_copy(PTimg, img + io.pt, io.w - io.pt);
+  lds_copy(WTimg, img + io.wt, io.p2 - io.wt);
+  lds_copy(p2s, img + io.p2, io.pt - io.p2);
   __syncthreads();
 
   const rsrc_t rx = make_rsrc(x, x_bytes), rg = make_rsrc(g_logits, gl_bytes);
@@ -285,6 +375,14 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
     float gsum = 0.f;
 #pragma unroll 1
     for (int pt = 0; pt < npt; ++pt) {
+      float gdv[16];  // upstream distance gradient of this tile, loaded before the MFMAs
+      if constexpr (GD) {
+        const int prem_gd = P - pt * 32 - 4 * h;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          gdv[r] = BufIO<float>::load(rgd, row_of(r) < prem_gd ? gdbase : kOOB,
+                                      static_cast<unsigned>((pt * 32 + row_of(r)) * HW * 4));
+      }
       f32x16 acc = zero16();
 #pragma unroll
       for (int q = 0; q < kNQ; ++q) {
@@ -304,18 +402,24 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
         }
       }
       const int prem = P - pt * 32 - 4 * h;
+      float p2r[16];
+      load_rows16(p2s + pt * 32 + 4 * h, p2r);
+      auto epilogue = [&](auto full) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int p = pt * 32 + acc_row(r, h);
-        const float d = l2_distance(x2, p2s[p], acc[r]);
-        const bool pin = row_of(r) < prem;
-        float gd = g_logits ? gacc[r] * act_grad_fast<ACT>(d, eps) : 0.f;
-        if (g_dist)
-          gd += BufIO<float>::load(rgd, pin ? gdbase : kOOB, static_cast<unsigned>((pt * 32 + row_of(r)) * HW * 4));
-        const float gs = (d > 0.f && pin) ? gd : 0.f;  // relu backward: grad * (out > 0)
-        gsum += gs;
-        acc[r] = -2.f * gs;
-      }
+        for (int r = 0; r < 16; ++r) {
+          const float d = l2_distance(x2, p2r[r], acc[r]);
+          const bool pin = decltype(full)::value || row_of(r) < prem;
+          float gd = gacc[r] * act_grad_fast<ACT>(d, eps);  // gacc is 0 without g_logits
+          if constexpr (GD) gd += gdv[r];
+          const float gs = (d > 0.f && pin) ? gd : 0.f;  // relu backward: grad * (out > 0)
+          gsum += gs;
+          acc[r] = -2.f * gs;
+        }
+      };
+      if ((pt + 1) * 32 <= P)
+        epilogue(std::true_type());
+      else
+        epilogue(std::false_type());
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         bf16x8 gsb[T];
@@ -384,10 +488,10 @@ struct PwLoads {
 template <int NPTC>
 constexpr int pw_max_threads() { return NPTC == 1 ? 128 : NPTC == 2 ? 384 : NPTC == 4 ? 640 : 768; }
 
-template <typename TX, int T, int ACT, int NPTC>
+template <typename TX, int T, int ACT, int NPTC, bool GD>
 __global__ __launch_bounds__(pw_max_threads<NPTC>()) void l2_bwd_pw_bf16_kernel(
-    const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const float* __restrict__ protos, int P, int Pp,
-    const float* __restrict__ w_last, int K, float eps, const float* __restrict__ g_logits, unsigned gl_bytes,
+    const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const unsigned char* __restrict__ img, int P, int Pp,
+    int K, float eps, const float* __restrict__ g_logits, unsigned gl_bytes,
     const float* __restrict__ g_dist, unsigned gd_bytes, int streams, float* __restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   constexpr int kNX = PwLoads<NPTC>::kNX, kNG = PwLoads<NPTC>::kNG;
@@ -397,11 +501,11 @@ __global__ __launch_bounds__(pw_max_threads<NPTC>()) void l2_bwd_pw_bf16_kernel(
   const int w = wave - stream * npt;             // prototype tile owned by this wave
 
   // LDS: [P image | W^T image | stream staging areas]
+  const ImgOffsets io = img_offsets(Pp, T);
   bf16* Pimg = reinterpret_cast<bf16*>(smem_raw);      // [T][Pp][64]  CPR 8 (chan_of order)
   bf16* WTimg = Pimg + T * Pp * kC;                    // [T][Pp][32]  CPR 4
   unsigned char* stage_root = reinterpret_cast<unsigned char*>(WTimg + T * Pp * 32);
-  stage_p_rows<T>(Pimg, protos, P, Pp);
-  stage_wt_rows<T>(WTimg, w_last, g_logits ? K : 0, P, Pp);
+  lds_copy(Pimg, img + io.p, io.p2 - io.p);  // P and W^T images are adjacent in the block
   float *Xf, *Gf, *x2s;
   unsigned* rowoff;
   bf16 *XA, *XB, *GA, *GT;
@@ -410,7 +514,7 @@ __global__ __launch_bounds__(pw_max_threads<NPTC>()) void l2_bwd_pw_bf16_kernel(
   const rsrc_t rx = make_rsrc(x, x_bytes), rg = make_rsrc(g_logits, gl_bytes), rgd = make_rsrc(g_dist, gd_bytes);
   const int p = w * 32 + j;  // this lane's prototype column
   const bool pvalid = p < P;
-  const float p2 = proto_norm2_64(protos, p, pvalid);
+  const float p2 = reinterpret_cast<const float*>(img + io.p2)[p];
   const int KS = (K + 15) / 16;
 
   f32x16 gp[2] = {zero16(), zero16()};
@@ -514,6 +618,20 @@ __global__ __launch_bounds__(pw_max_threads<NPTC>()) void l2_bwd_pw_bf16_kernel(
     __syncthreads();
 
     // ---- compute: this wave's prototype tile against the staged pixel tile ----
+    // Rows past npix hold x = 0 and g_logits = 0 (out-of-range loads), so they contribute exact
+    // zeros to g_P and g_W; columns p >= P have zero W^T rows, so g_s = 0 there.
+    float x2r[16], gdv[16];
+    load_rows16(x2s + 4 * h, x2r);
+    if constexpr (GD) {
+      float rof[16];
+      load_rows16(reinterpret_cast<const float*>(rowoff) + 4 * h, rof);
+      const unsigned pcol = static_cast<unsigned>(p * HW * 4);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const unsigned ro = __float_as_uint(rof[r]);
+        gdv[r] = BufIO<float>::load(rgd, (ro != kOOB && pvalid) ? ro + pcol : kOOB, 0);
+      }
+    }
     f32x16 acc = zero16();
 #pragma unroll
     for (int q = 0; q < kNQ; ++q) {
@@ -534,20 +652,15 @@ __global__ __launch_bounds__(pw_max_threads<NPTC>()) void l2_bwd_pw_bf16_kernel(
         }
       }
     }
-    const unsigned pcol = static_cast<unsigned>(p * HW * 4);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int nr = acc_row(r, h);
-      const unsigned ro = rowoff[nr];
-      const bool rvalid = ro != kOOB;
-      const float d = l2_distance(x2s[nr], p2, acc[r]);
-      const float a = act_fast<ACT>(d, eps);
-      float gd = g_logits ? gacc[r] * act_grad_fast<ACT>(d, eps) : 0.f;
-      if (g_dist) gd += BufIO<float>::load(rgd, (rvalid && pvalid) ? ro + pcol : kOOB, 0);
-      const float gs = (d > 0.f && pvalid && rvalid) ? gd : 0.f;
+      const float d = l2_distance(x2r[r], p2, acc[r]);
+      float gd = gacc[r] * act_grad_fast<ACT>(d, eps);
+      if constexpr (GD) gd += gdv[r];
+      const float gs = d > 0.f ? gd : 0.f;
       gsum += gs;
       acc[r] = -2.f * gs;
-      gacc[r] = rvalid ? a : 0.f;
+      gacc[r] = act_fast<ACT>(d, eps);
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -670,9 +783,10 @@ __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __
 }
 
 // ---- host side ---------------------------------------------------------------------------------
-size_t fwd_lds(const Geometry& g, int terms) { return static_cast<size_t>(g.Pp) * (terms * (kC + 32) * 2 + 4); }
+size_t p2_pad(const Geometry& g) { return (static_cast<size_t>(g.Pp) * 4 + 1023) & ~static_cast<size_t>(1023); }
+size_t fwd_lds(const Geometry& g, int terms) { return static_cast<size_t>(g.Pp) * terms * (kC + 32) * 2 + p2_pad(g); }
 size_t bwd_x_lds(const Geometry& g, int terms) {
-  return static_cast<size_t>(g.Pp) * (terms * (2 * kC + 32) * 2 + 4);
+  return static_cast<size_t>(g.Pp) * terms * (2 * kC + 32) * 2 + p2_pad(g);
 }
 // Pixel streams per workgroup: 2 when 2*npt waves fit the 768-thread launch bound.
 int pw_streams(const Geometry& g) { return (g.Pp / 32) * 2 <= 12 ? 2 : 1; }
@@ -698,45 +812,45 @@ struct Bytes {
   unsigned x, d, a, l, gl, gd;
 };
 
-template <typename TX, int T, int ACT>
-int fwd_t(const Geometry& g, const Bytes& nb, const void* x, const float* protos, const float* w_last, float eps,
-          float* dist, float* act, float* logits, hipStream_t stream) {
-  if (int st = ensure_lds<l2_fwd_bf16_kernel<TX, T, ACT>>()) return st;
+template <typename TX, int T, int ACT, bool ACTS>
+int fwd_t(const Geometry& g, const Bytes& nb, const void* x, const unsigned char* img, float eps, float* dist,
+          float* act, float* logits, hipStream_t stream) {
+  if (int st = ensure_lds<l2_fwd_bf16_kernel<TX, T, ACT, ACTS>>()) return st;
   const size_t lds = fwd_lds(g, T);
-  const int per_cu = static_cast<int>(kMaxLds / lds);
-  const int cap = 256 * (per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu));
+  // Persistent: one generation of resident workgroups; waves stride over the tiles and
+  // prefetch their next tile.
+  const int cap = resident_blocks<l2_fwd_bf16_kernel<TX, T, ACT, ACTS>>(kWavesA * 64, lds);
   const int want = static_cast<int>(ceil_div(g.ntiles, kWavesA));
-  hipLaunchKernelGGL((l2_fwd_bf16_kernel<TX, T, ACT>), dim3(want < cap ? want : cap), dim3(kWavesA * 64), lds,
-                     stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, protos, g.P, g.Pp, w_last, g.K, eps, dist,
-                     nb.d, act, nb.a, logits, nb.l);
+  hipLaunchKernelGGL((l2_fwd_bf16_kernel<TX, T, ACT, ACTS>), dim3(want < cap ? want : cap), dim3(kWavesA * 64), lds,
+                     stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, img, g.P, g.Pp, g.K, eps, dist, nb.d, act,
+                     nb.a, logits, nb.l);
   return check_launch("l2_fwd_bf16_kernel");
 }
 
-template <typename TX, int T, int ACT>
-int bwd_x_t(const Geometry& g, const Bytes& nb, const void* x, const float* protos, const float* w_last, float eps,
+template <typename TX, int T, int ACT, bool GD>
+int bwd_x_t(const Geometry& g, const Bytes& nb, const void* x, const unsigned char* img, float eps,
             const float* g_logits, const float* g_dist, void* g_x, hipStream_t stream) {
-  if (int st = ensure_lds<l2_bwd_x_bf16_kernel<TX, T, ACT>>()) return st;
+  if (int st = ensure_lds<l2_bwd_x_bf16_kernel<TX, T, ACT, GD>>()) return st;
   const size_t lds = bwd_x_lds(g, T);
-  const int per_cu = static_cast<int>(kMaxLds / lds);
-  const int cap = 256 * (per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu));
+  const int cap = resident_blocks<l2_bwd_x_bf16_kernel<TX, T, ACT, GD>>(kWavesA * 64, lds);
   const int want = static_cast<int>(ceil_div(g.ntiles, kWavesA));
-  hipLaunchKernelGGL((l2_bwd_x_bf16_kernel<TX, T, ACT>), dim3(want < cap ? want : cap), dim3(kWavesA * 64), lds,
-                     stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, protos, g.P, g.Pp, w_last, g.K, eps,
-                     g_logits, nb.gl, g_dist, nb.gd, static_cast<TX*>(g_x));
+  hipLaunchKernelGGL((l2_bwd_x_bf16_kernel<TX, T, ACT, GD>), dim3(want < cap ? want : cap), dim3(kWavesA * 64), lds,
+                     stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, img, g.P, g.Pp, g.K, eps, g_logits, nb.gl,
+                     g_dist, nb.gd, static_cast<TX*>(g_x));
   return check_launch("l2_bwd_x_bf16_kernel");
 }
 
-template <typename TX, int T, int ACT, int NPTC>
-int bwd_pw_nptc(const Geometry& g, const Bytes& nb, const void* x, const float* protos, const float* w_last, float eps,
-               const float* g_logits, const float* g_dist, float* g_protos, float* g_w, float* ws,
-               hipStream_t stream) {
-  if (int st = ensure_lds<l2_bwd_pw_bf16_kernel<TX, T, ACT, NPTC>>()) return st;
+template <typename TX, int T, int ACT, int NPTC, bool GD>
+int bwd_pw_nptc(const Geometry& g, const Bytes& nb, const void* x, const float* protos, const unsigned char* img,
+                float eps, const float* g_logits, const float* g_dist, float* g_protos, float* g_w, float* ws,
+                hipStream_t stream) {
+  if (int st = ensure_lds<l2_bwd_pw_bf16_kernel<TX, T, ACT, NPTC, GD>>()) return st;
   const int streams = pw_streams(g);
   const int grid = pw_grid(g);
   const int threads = streams * (g.Pp / 32) * 64;
-  hipLaunchKernelGGL((l2_bwd_pw_bf16_kernel<TX, T, ACT, NPTC>), dim3(grid), dim3(threads), pw_lds(g, T), stream,
-                     static_cast<const TX*>(x), nb.x, g.HW, g.npix, protos, g.P, g.Pp, w_last, g.K, eps, g_logits,
-                     nb.gl, g_dist, nb.gd, streams, ws);
+  hipLaunchKernelGGL((l2_bwd_pw_bf16_kernel<TX, T, ACT, NPTC, GD>), dim3(grid), dim3(threads), pw_lds(g, T), stream,
+                     static_cast<const TX*>(x), nb.x, g.HW, g.npix, img, g.P, g.Pp, g.K, eps, g_logits, nb.gl, g_dist,
+                     nb.gd, streams, ws);
   if (int st = check_launch("l2_bwd_pw_bf16_kernel")) return st;
   const int elems = g.Pp * kC + 32 * g.Pp;
   hipLaunchKernelGGL(l2_bwd_reduce_bf16_kernel, dim3(static_cast<unsigned>(ceil_div(elems, 64))), dim3(256), 0,
@@ -744,18 +858,19 @@ int bwd_pw_nptc(const Geometry& g, const Bytes& nb, const void* x, const float* 
   return check_launch("l2_bwd_reduce_bf16_kernel");
 }
 
-template <typename TX, int T, int ACT>
-int bwd_pw_t(const Geometry& g, const Bytes& nb, const void* x, const float* protos, const float* w_last, float eps,
-             const float* g_logits, const float* g_dist, float* g_protos, float* g_w, float* ws, hipStream_t stream) {
+template <typename TX, int T, int ACT, bool GD>
+int bwd_pw_t(const Geometry& g, const Bytes& nb, const void* x, const float* protos, const unsigned char* img,
+             float eps, const float* g_logits, const float* g_dist, float* g_protos, float* g_w, float* ws,
+             hipStream_t stream) {
   switch (pw_nptc(g)) {
     case 6:
-      return bwd_pw_nptc<TX, T, ACT, 6>(g, nb, x, protos, w_last, eps, g_logits, g_dist, g_protos, g_w, ws, stream);
+      return bwd_pw_nptc<TX, T, ACT, 6, GD>(g, nb, x, protos, img, eps, g_logits, g_dist, g_protos, g_w, ws, stream);
     case 4:
-      return bwd_pw_nptc<TX, T, ACT, 4>(g, nb, x, protos, w_last, eps, g_logits, g_dist, g_protos, g_w, ws, stream);
+      return bwd_pw_nptc<TX, T, ACT, 4, GD>(g, nb, x, protos, img, eps, g_logits, g_dist, g_protos, g_w, ws, stream);
     case 2:
-      return bwd_pw_nptc<TX, T, ACT, 2>(g, nb, x, protos, w_last, eps, g_logits, g_dist, g_protos, g_w, ws, stream);
+      return bwd_pw_nptc<TX, T, ACT, 2, GD>(g, nb, x, protos, img, eps, g_logits, g_dist, g_protos, g_w, ws, stream);
     default:
-      return bwd_pw_nptc<TX, T, ACT, 1>(g, nb, x, protos, w_last, eps, g_logits, g_dist, g_protos, g_w, ws, stream);
+      return bwd_pw_nptc<TX, T, ACT, 1, GD>(g, nb, x, protos, img, eps, g_logits, g_dist, g_protos, g_w, ws, stream);
   }
 }
 
@@ -775,15 +890,19 @@ int by_type(bool x_bf16, int terms, int act_kind, Fn&& fn) {
   return x_bf16 ? fn(b, I3(), A1()) : fn(f, I3(), A1());
 }
 
-Bytes bytes_of(const Geometry& g, bool x_bf16) {
+// Buffer-resource sizes; a null tensor gets 0 bytes, so every access through it is dropped
+// (stores) or reads 0 (loads) without a branch in the kernel.
+Bytes bytes_of(const Geometry& g, bool x_bf16, const void* dist, const void* act, const void* logits,
+               const void* g_logits, const void* g_dist) {
   Bytes nb;
   const unsigned long long npix = static_cast<unsigned long long>(g.npix);
+  const unsigned d = static_cast<unsigned>(npix * g.P * 4), l = static_cast<unsigned>(npix * g.K * 4);
   nb.x = static_cast<unsigned>(npix * kC * (x_bf16 ? 2 : 4));
-  nb.d = static_cast<unsigned>(npix * g.P * 4);
-  nb.a = nb.d;
-  nb.l = static_cast<unsigned>(npix * g.K * 4);
-  nb.gl = nb.l;
-  nb.gd = nb.d;
+  nb.d = dist ? d : 0u;
+  nb.a = act ? d : 0u;
+  nb.l = logits ? l : 0u;
+  nb.gl = g_logits ? l : 0u;
+  nb.gd = g_dist ? d : 0u;
   return nb;
 }
 
@@ -809,37 +928,73 @@ size_t bf16_bwd_pw_workspace(const Geometry& g) {
   return static_cast<size_t>(pw_grid(g)) * (static_cast<size_t>(g.Pp) * kC + 32 * g.Pp + g.Pp) * sizeof(float);
 }
 
-int launch_fwd_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const float* protos,
-                    const float* w_last, float eps, int act_kind, float* dist, float* act, float* logits,
-                    hipStream_t stream) {
-  const Bytes nb = bytes_of(g, x_bf16);
+size_t bf16_image_bytes(const Geometry& g, int terms) {
+  return static_cast<size_t>(img_offsets(g.Pp, terms).total);
+}
+
+int launch_prep_bf16(const Geometry& g, int terms, const float* protos, const float* w_last, void* img,
+                     hipStream_t stream) {
+  const int items = g.Pp * 8;  // the largest image loop (P rows x 8 chunks)
+  const dim3 grid(static_cast<unsigned>(ceil_div(items, 256)), 5);
+  unsigned char* blk = static_cast<unsigned char*>(img);
+  if (terms == 2)
+    hipLaunchKernelGGL(l2_prep_bf16_kernel<2>, grid, dim3(256), 0, stream, protos, g.P, g.Pp, w_last, g.K, blk);
+  else
+    hipLaunchKernelGGL(l2_prep_bf16_kernel<3>, grid, dim3(256), 0, stream, protos, g.P, g.Pp, w_last, g.K, blk);
+  return check_launch("l2_prep_bf16_kernel");
+}
+
+int launch_fwd_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const void* img, float eps, int act_kind,
+                    float* dist, float* act, float* logits, hipStream_t stream) {
+  const Bytes nb = bytes_of(g, x_bf16, dist, act, logits, nullptr, nullptr);
+  const unsigned char* blk = static_cast<const unsigned char*>(img);
   return by_type(x_bf16, terms, act_kind, [&](auto tx, auto tt, auto aa) {
     using TX = std::remove_pointer_t<decltype(tx)>;
-    return fwd_t<TX, decltype(tt)::value, decltype(aa)::value>(g, nb, x, protos, w_last, eps, dist, act, logits,
-                                                               stream);
+    constexpr int kT = decltype(tt)::value, kA = decltype(aa)::value;
+    if (act) return fwd_t<TX, kT, kA, true>(g, nb, x, blk, eps, dist, act, logits, stream);
+    return fwd_t<TX, kT, kA, false>(g, nb, x, blk, eps, dist, act, logits, stream);
   });
 }
 
-int launch_bwd_x_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const float* protos,
-                      const float* w_last, float eps, int act_kind, const float* g_logits, const float* g_dist,
-                      void* g_x, hipStream_t stream) {
-  const Bytes nb = bytes_of(g, x_bf16);
+int launch_bwd_x_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const void* img, float eps,
+                      int act_kind, const float* g_logits, const float* g_dist, void* g_x, hipStream_t stream) {
+  const Bytes nb = bytes_of(g, x_bf16, nullptr, nullptr, nullptr, g_logits, g_dist);
+  const unsigned char* blk = static_cast<const unsigned char*>(img);
   return by_type(x_bf16, terms, act_kind, [&](auto tx, auto tt, auto aa) {
     using TX = std::remove_pointer_t<decltype(tx)>;
-    return bwd_x_t<TX, decltype(tt)::value, decltype(aa)::value>(g, nb, x, protos, w_last, eps, g_logits, g_dist, g_x,
-                                                                 stream);
+    constexpr int kT = decltype(tt)::value, kA = decltype(aa)::value;
+    if (g_dist) return bwd_x_t<TX, kT, kA, true>(g, nb, x, blk, eps, g_logits, g_dist, g_x, stream);
+    return bwd_x_t<TX, kT, kA, false>(g, nb, x, blk, eps, g_logits, g_dist, g_x, stream);
   });
 }
 
-int launch_bwd_pw_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const float* protos,
-                       const float* w_last, float eps, int act_kind, const float* g_logits, const float* g_dist,
-                       float* g_protos, float* g_w, float* ws, hipStream_t stream) {
-  const Bytes nb = bytes_of(g, x_bf16);
+int launch_bwd_pw_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const float* protos, const void* img,
+                       float eps, int act_kind, const float* g_logits, const float* g_dist, float* g_protos,
+                       float* g_w, float* ws, hipStream_t stream) {
+  const Bytes nb = bytes_of(g, x_bf16, nullptr, nullptr, nullptr, g_logits, g_dist);
+  const unsigned char* blk = static_cast<const unsigned char*>(img);
   return by_type(x_bf16, terms, act_kind, [&](auto tx, auto tt, auto aa) {
     using TX = std::remove_pointer_t<decltype(tx)>;
-    return bwd_pw_t<TX, decltype(tt)::value, decltype(aa)::value>(g, nb, x, protos, w_last, eps, g_logits, g_dist,
-                                                                  g_protos, g_w, ws, stream);
+    constexpr int kT = decltype(tt)::value, kA = decltype(aa)::value;
+    if (g_dist) return bwd_pw_t<TX, kT, kA, true>(g, nb, x, protos, blk, eps, g_logits, g_dist, g_protos, g_w, ws, stream);
+    return bwd_pw_t<TX, kT, kA, false>(g, nb, x, protos, blk, eps, g_logits, g_dist, g_protos, g_w, ws, stream);
   });
 }
 
 }  // namespace protoseg
+
+#ifdef PROTOSEG_STAMPS
+namespace protoseg {
+__device__ unsigned long long g_stamps[kStampCap];
+}
+// Debug builds only: copy (and clear) the per-wave phase stamps of the last launches.
+extern "C" int protoseg_debug_stamps(void* dst, size_t bytes) {
+  using protoseg::g_stamps;
+  const size_t n = bytes < sizeof(g_stamps) ? bytes : sizeof(g_stamps);
+  if (hipDeviceSynchronize() != hipSuccess) return 3;
+  if (dst && hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps), n, 0, hipMemcpyDeviceToHost) != hipSuccess) return 3;
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamps)) != hipSuccess) return 3;
+  return hipMemset(p, 0, sizeof(g_stamps)) == hipSuccess ? 0 : 3;
+}
+#endif

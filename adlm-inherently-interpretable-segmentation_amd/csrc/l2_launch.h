@@ -18,14 +18,18 @@ bool bf16_bwd_x_fits(const Geometry& g, int terms);
 bool bf16_bwd_pw_fits(const Geometry& g, int terms);
 size_t bf16_bwd_pw_workspace(const Geometry& g);
 
-int launch_fwd_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const float* protos,
-                    const float* w_last, float eps, int act_kind, float* dist, float* act, float* logits,
-                    hipStream_t stream);
-int launch_bwd_x_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const float* protos,
-                      const float* w_last, float eps, int act_kind, const float* g_logits, const float* g_dist,
-                      void* g_x, hipStream_t stream);
-int launch_bwd_pw_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const float* protos,
-                       const float* w_last, float eps, int act_kind, const float* g_logits, const float* g_dist,
-                       float* g_protos, float* g_w, float* ws, hipStream_t stream);
+// Operand-image block (split P, P^T, W, W^T images and ||p||^2 in the kernels' LDS layout),
+// built once per call by launch_prep_bf16 and shared by the kernels of that call.
+size_t bf16_image_bytes(const Geometry& g, int terms);
+int launch_prep_bf16(const Geometry& g, int terms, const float* protos, const float* w_last, void* img,
+                     hipStream_t stream);
+
+int launch_fwd_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const void* img, float eps, int act_kind,
+                    float* dist, float* act, float* logits, hipStream_t stream);
+int launch_bwd_x_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const void* img, float eps,
+                      int act_kind, const float* g_logits, const float* g_dist, void* g_x, hipStream_t stream);
+int launch_bwd_pw_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const float* protos, const void* img,
+                       float eps, int act_kind, const float* g_logits, const float* g_dist, float* g_protos,
+                       float* g_w, float* ws, hipStream_t stream);
 
 }  // namespace protoseg

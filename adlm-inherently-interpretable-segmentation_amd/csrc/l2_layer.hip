@@ -20,6 +20,10 @@
 //                      partial slabs, reduced by l2_bwd_reduce_kernel in a fixed order
 //                      (bitwise reproducible, no atomics).
 #include "protoseg_device.h"
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "l2_launch.h"
 #include "protoseg_host.h"
 
@@ -579,6 +583,47 @@ Geometry geometry_of(int B, int C, int H, int W, int P, int K) {
 
 using namespace protoseg;
 
+namespace {
+// Scratch for the bf16 family's operand images (a few hundred KiB): one block per (device,
+// stream), allocated on first use at a size that covers every supported shape, then reused.
+// Kernels on one stream are ordered, so a call's prep kernel never overwrites images that an
+// earlier call's kernels still read. No per-call allocation: the launch sequence is only
+// kernel launches and can be captured in a HIP graph once the block exists.
+constexpr size_t kImageBlockMin = 512 * 1024;
+
+struct ImageBlock {
+  void* ptr = nullptr;
+  int build(const Geometry& g, int terms, const float* protos, const float* w_last, hipStream_t s) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> blocks;
+    const size_t need = bf16_image_bytes(g, terms);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return check_launch("hipGetDevice");
+    {
+      std::lock_guard<std::mutex> lock(mu);
+      auto& b = blocks[{dev, s}];
+      if (b.second < need) {
+        if (b.first) {  // never for supported shapes (kImageBlockMin covers Pp <= 384, T = 3)
+          if (hipStreamSynchronize(s) != hipSuccess || hipFree(b.first) != hipSuccess)
+            return check_launch("image block regrow");
+          b = {nullptr, 0};
+        }
+        const size_t bytes = need > kImageBlockMin ? need : kImageBlockMin;
+        const hipError_t e = hipMalloc(&b.first, bytes);
+        if (e != hipSuccess) {
+          (void)hipGetLastError();
+          b = {nullptr, 0};
+          return fail(PROTOSEG_ERR_HIP, "hipMalloc (operand images, %zu B): %s", bytes, hipGetErrorString(e));
+        }
+        b.second = bytes;
+      }
+      ptr = b.first;
+    }
+    return launch_prep_bf16(g, terms, protos, w_last, ptr, s);
+  }
+};
+}  // namespace
+
 extern "C" int protoseg_l2_supported(int C, int P, int K) {
   if (nc_of(C) == 0 || P <= 0 || K < 0 || K > 32) return 0;
   return layer_lds_bytes(C, padded_protos(P)) <= kMaxLds ? 1 : 0;
@@ -593,9 +638,12 @@ extern "C" int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, 
   if (!dist_out && !act_out && !logits_out) return PROTOSEG_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int terms = terms_of(precision);
-  if (terms && bf16_fwd_fits(geo, terms))
-    return launch_fwd_bf16(geo, x_dtype == PROTOSEG_BF16, terms, x, protos, w_last, eps, act_kind, dist_out, act_out,
+  if (terms && bf16_fwd_fits(geo, terms)) {
+    ImageBlock img;
+    if (int st = img.build(geo, terms, protos, logits_out ? w_last : nullptr, s)) return st;
+    return launch_fwd_bf16(geo, x_dtype == PROTOSEG_BF16, terms, x, img.ptr, eps, act_kind, dist_out, act_out,
                            logits_out, s);
+  }
   return dispatch(x_dtype, C, [&](auto tx, auto nc) {
     using TX = std::remove_pointer_t<decltype(tx)>;
     return launch_fwd<TX, decltype(nc)::value>(geo, x, protos, w_last, eps, act_kind, dist_out, act_out,
@@ -638,10 +686,15 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
   const int terms = terms_of(precision);
   const bool xb = x_dtype == PROTOSEG_BF16;
   float* ws = static_cast<float*>(workspace);
+  const bool bf16_x = g_x && terms && bf16_bwd_x_fits(geo, terms);
+  const bool bf16_pw = (g_protos || g_w) && terms && bf16_bwd_pw_fits(geo, terms);
+  ImageBlock img;
+  if (bf16_x || bf16_pw)
+    if (int st = img.build(geo, terms, protos, g_logits ? w_last : nullptr, s)) return st;
   if (g_x) {
     int st;
-    if (terms && bf16_bwd_x_fits(geo, terms))
-      st = launch_bwd_x_bf16(geo, xb, terms, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_x, s);
+    if (bf16_x)
+      st = launch_bwd_x_bf16(geo, xb, terms, x, img.ptr, eps, act_kind, g_logits, g_dist, g_x, s);
     else
       st = dispatch(x_dtype, C, [&](auto tx, auto nc) {
         using TX = std::remove_pointer_t<decltype(tx)>;
@@ -650,8 +703,8 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
     if (st) return st;
   }
   if (g_protos || g_w) {
-    if (terms && bf16_bwd_pw_fits(geo, terms))
-      return launch_bwd_pw_bf16(geo, xb, terms, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_protos, g_w, ws,
+    if (bf16_pw)
+      return launch_bwd_pw_bf16(geo, xb, terms, x, protos, img.ptr, eps, act_kind, g_logits, g_dist, g_protos, g_w, ws,
                                 s);
     return dispatch(x_dtype, C, [&](auto tx, auto nc) {
       using TX = std::remove_pointer_t<decltype(tx)>;

@@ -61,7 +61,7 @@ template <> struct XIO<uint16_t> {
 __device__ __forceinline__ float l2_distance(float x2, float p2, float xp) {
   const float inter = p2 - 2.f * xp;
   const float s = x2 + inter;
-  return s > 0.f ? s : 0.f;  // F.relu: threshold(s, 0, 0) -> +0.0 for s <= 0
+  return __builtin_fmaxf(s, 0.f);  // F.relu (v_max_f32; NaN inputs are out of scope)
 }
 
 // model.py:231-237

@@ -33,4 +33,26 @@ int ensure_lds() {
 
 inline long long ceil_div(long long a, long long b) { return (a + b - 1) / b; }
 
+// Workgroups of `kernel` resident on the whole device at (threads, lds): CUs x blocks per CU
+// from the occupancy calculator (VGPRs and LDS), at least the CU count. Cached per
+// (kernel, threads, lds) of the first call — the launchers use one configuration per shape.
+template <auto kernel>
+int resident_blocks(int threads, size_t lds) {
+  static std::mutex mu;
+  static int cached_threads = -1, cached = 0;
+  static size_t cached_lds = 0;
+  std::lock_guard<std::mutex> lock(mu);
+  if (threads == cached_threads && lds == cached_lds) return cached;
+  int dev = 0, cus = 256, per_cu = 1;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kernel), threads, lds) !=
+          hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  cached_threads = threads;
+  cached_lds = lds;
+  cached = cus * per_cu;
+  return cached;
+}
+
 }  // namespace protoseg

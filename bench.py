@@ -154,33 +154,61 @@ def pmc_traffic(kernel: str, config_key: str):
         return None
 
 
-def time_layer(step: LayerStep, steps: int, warmup: int, world: int):
-    for _ in range(warmup):
-        step.fwd()
-        step.bwd_x()
-        step.bwd_pw()
-        step.allreduce(world)
-    torch.cuda.synchronize()
+def capture(fn, stream):
+    """HIP graph of fn()'s launches on `stream` (the C ABI launches on torch's current stream)."""
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=stream):
+        fn()
+    return g
+
+
+def time_layer(step: LayerStep, steps: int, warmup: int, world: int, use_graph: bool):
+    """Times `steps` training steps of the prototype layer (fwd + bwd_x + bwd_pw [+ all-reduce]).
+
+    With use_graph the three C-ABI calls of a step are captured once into a HIP graph and each
+    step is one replay (no host launch gaps); the all-reduce stays outside the graph. Per-call
+    device times come from HIP events around one graph per call, replayed on the same stream."""
     names = step.kernel_names()
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for s in range(steps):
-        e = ev[s]
-        e[0].record()
-        step.fwd()
-        e[1].record()
-        step.bwd_x()
-        e[2].record()
-        step.bwd_pw()
-        e[3].record()
-        step.allreduce(world)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    calls = [step.fwd, step.bwd_x, step.bwd_pw]
+    stream = torch.cuda.Stream(step.device)
+    with torch.cuda.stream(stream):
+        for _ in range(max(1, warmup)):
+            for c in calls:
+                c()
+            step.allreduce(world)
+        torch.cuda.synchronize()
+        if use_graph:
+            g_step = capture(lambda: [c() for c in calls], stream)
+            g_calls = [capture(c, stream) for c in calls]
+            run_step = g_step.replay
+            run_calls = [g.replay for g in g_calls]
+            for _ in range(warmup):
+                run_step()
+                step.allreduce(world)
+        else:
+            run_step = lambda: [c() for c in calls]  # noqa: E731
+            run_calls = calls
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            run_step()
+            step.allreduce(world)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        # per-call device time: events on this stream around each call's graph
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
+        for s in range(steps):
+            e = ev[s]
+            e[0].record(stream)
+            for i, rc in enumerate(run_calls):
+                rc()
+                e[i + 1].record(stream)
+        torch.cuda.synchronize()
     per_kernel = {n: [] for n in names}
     for e in ev:
         for i, n in enumerate(names):
@@ -295,6 +323,8 @@ def main():
     ap.add_argument("--no-push", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--launch", choices=["graph", "eager"], default="graph",
+                    help="graph: each step is one HIP graph replay of the three C-ABI calls")
     args = ap.parse_args()
 
     rank, local_rank, world = init_from_env()
@@ -306,7 +336,7 @@ def main():
 
     step = LayerStep(args.batch, args.channels, args.fmap, args.fmap, args.protos, args.classes, x_dtype, device,
                      SEED + rank, args.precision)
-    elapsed, per_kernel = time_layer(step, args.steps, args.warmup, world)
+    elapsed, per_kernel = time_layer(step, args.steps, args.warmup, world, args.launch == "graph")
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -348,7 +378,7 @@ def main():
                                    "when N>1), 513x513 crop -> 65x65 map",
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "channels": args.channels, "prototypes": args.protos, "classes": args.classes,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}", "launch": args.launch},
             "roofline": roof,
             "kernels": kernels,
         }
