@@ -505,6 +505,8 @@ __global__ __launch_bounds__(pw_max_threads<NPTC>()) void l2_bwd_pw_bf16_kernel(
   bf16* Pimg = reinterpret_cast<bf16*>(smem_raw);      // [T][Pp][64]  CPR 8 (chan_of order)
   bf16* WTimg = Pimg + T * Pp * kC;                    // [T][Pp][32]  CPR 4
   unsigned char* stage_root = reinterpret_cast<unsigned char*>(WTimg + T * Pp * 32);
+  STAMP(0);
+  STAMP_RT(7);
   lds_copy(Pimg, img + io.p, io.p2 - io.p);  // P and W^T images are adjacent in the block
   float *Xf, *Gf, *x2s;
   unsigned* rowoff;
@@ -550,10 +552,12 @@ __global__ __launch_bounds__(pw_max_threads<NPTC>()) void l2_bwd_pw_bf16_kernel(
       gr[i] = BufIO<float>::load(rg, (r0 + i * rstep < lim) ? go : kOOB, i * gs_step);
   };
 
+  STAMP(1);
   stage_load(0);
   for (int it = 0; it < iters; ++it) {
     const int t = blockIdx.x * streams + stream + it * total_streams;
     __syncthreads();  // previous tile's operand reads are done
+    if (it == 1) STAMP(2);
     // ---- prefetched registers -> fp32 LDS staging ----
 #pragma unroll
     for (int i = 0; i < kNX; ++i)
@@ -569,6 +573,7 @@ __global__ __launch_bounds__(pw_max_threads<NPTC>()) void l2_bwd_pw_bf16_kernel(
       rowoff[tid_s] = ok ? static_cast<unsigned>((b * P * HW + (g - b * HW)) * 4) : kOOB;
     }
     __syncthreads();
+    if (it == 1) STAMP(3);
     // ---- convert to split bf16 operand images ----
     for (int idx = tid_s; idx < 32 * 8; idx += nt_stream) {  // XA: row n, chunk e8 = (q, h)
       const int nn = idx >> 3, e8 = idx & 7, q = e8 >> 1, hh = e8 & 1;
@@ -616,6 +621,7 @@ __global__ __launch_bounds__(pw_max_threads<NPTC>()) void l2_bwd_pw_bf16_kernel(
       x2s[nn] = s0 + s1;
     }
     __syncthreads();
+    if (it == 1) STAMP(4);
 
     // ---- compute: this wave's prototype tile against the staged pixel tile ----
     // Rows past npix hold x = 0 and g_logits = 0 (out-of-range loads), so they contribute exact
@@ -679,6 +685,7 @@ __global__ __launch_bounds__(pw_max_threads<NPTC>()) void l2_bwd_pw_bf16_kernel(
         gw = mma_split<T>(gt, actb, gw);
       }
     }
+    if (it == 1) STAMP(5);
   }
 
   // ---- workgroup reduction over streams (fixed order) and slab write ----
@@ -687,6 +694,7 @@ __global__ __launch_bounds__(pw_max_threads<NPTC>()) void l2_bwd_pw_bf16_kernel(
   float* red = reinterpret_cast<float*>(smem_raw);  // [streams-1][npt][32*64 + 32*32 + 32]
   constexpr int kPerWave = 32 * kC + 32 * 32 + 32;
   __syncthreads();
+  STAMP(6);
   gsum += __shfl_xor(gsum, 32);
   if (stream > 0) {
     float* dst = red + static_cast<size_t>((stream - 1) * npt + w) * kPerWave;
