@@ -19,6 +19,8 @@
 // Memory ops go through buffer resources (out-of-range lanes read 0 / drop their store), the
 // activation is a template parameter, and every kernel uses the channel order chan_of() for
 // the distance GEMM, so all three compute bit-identical distances for the same inputs.
+#include <type_traits>
+
 #include "bf16_split.h"
 #include "l2_launch.h"
 #include "protoseg_host.h"
@@ -448,70 +450,89 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
 }
 
 // ---- bwd_pw ----------------------------------------------------------------------------------
-template <int T>
+// Per pixel stream: the raw tile (x [64 c][32 n] in the input dtype, g_logits [32 n][32 k] f32)
+// is brought into LDS by LDS-DMA (buffer_load ... lds: no VGPRs, out-of-range lanes land as 0)
+// while the previous tile is computed, then split into the bf16 operand images. Rows are
+// stored in pairs (row 2r at +0, 2r+1 at +32 elements, pair stride kPair) so one DMA
+// wave-instruction fills one pair; the stride keeps the conversion reads conflict-free.
+// A 2-byte LDS-DMA lands zero-extended in a dword per lane, so bf16 x is staged as uint32 words
+// holding the bf16 bits in their low half.
+template <typename TX>
+struct PwRaw {
+  using XS = std::conditional_t<sizeof(TX) == 4, float, uint32_t>;
+  static constexpr int kPairX = 72;
+  static constexpr int kPairG = 72;
+  static constexpr int kXs = 32 * kPairX;                    // dwords
+  static constexpr int kGs = 16 * kPairG;                    // floats
+  static constexpr int kBytes = (kXs + kGs + 64) * 4;        // + x2[32], rowoff[32]
+};
+template <typename TX, int T>
 struct PwStage {
-  static constexpr int kXf = kC * kLdf;        // fp32 [64][33]
-  static constexpr int kGf = 32 * kLdf;        // fp32 [32][33]
-  static constexpr int kXA = T * 32 * kC;      // bf16 [T][32 n][64 c]   CPR 8, chan_of order
-  static constexpr int kXB = T * kC * 32;      // bf16 [T][64 c][32 n~]  CPR 4, permuted n
-  static constexpr int kGA = T * 32 * 32;      // bf16 [T][32 n][32 k]   CPR 4
-  static constexpr int kGT = T * 32 * 32;      // bf16 [T][32 k][32 n~]  CPR 4, permuted n
-  // byte layout: Xf | Gf | x2[32] | rowoff[32] | XA | XB | GA | GT
-  static constexpr int kBytes = (kXf + kGf + 32) * 4 + 32 * 4 + (kXA + kXB + kGA + kGT) * 2;
+  static constexpr int kXA = T * 32 * kC;   // bf16 [T][32 n][64 c]   CPR 8, chan_of order
+  static constexpr int kXB = T * kC * 32;   // bf16 [T][64 c][32 n~]  CPR 4, permuted n, x * -2
+  static constexpr int kGA = T * 32 * 32;   // bf16 [T][32 n][32 k]   CPR 4
+  static constexpr int kGT = T * 32 * 32;   // bf16 [T][32 k][32 n~]  CPR 4, permuted n
+  static constexpr int kBytes = PwRaw<TX>::kBytes + (kXA + kXB + kGA + kGT) * 2;
 };
 
-template <int T>
-__device__ __forceinline__ void pw_carve(unsigned char* base, float*& Xf, float*& Gf, float*& x2s,
-                                         unsigned*& rowoff, bf16*& XA, bf16*& XB, bf16*& GA, bf16*& GT) {
-  using S = PwStage<T>;
-  Xf = reinterpret_cast<float*>(base);
-  Gf = Xf + S::kXf;
-  x2s = Gf + S::kGf;
-  rowoff = reinterpret_cast<unsigned*>(x2s + 32);
-  XA = reinterpret_cast<bf16*>(rowoff + 32);
-  XB = XA + S::kXA;
-  GA = XB + S::kXB;
-  GT = GA + S::kGA;
+template <int PAIR>
+__device__ __forceinline__ int pair_off(int row, int col) { return (row >> 1) * PAIR + (row & 1) * 32 + col; }
+
+__device__ __forceinline__ float lds_val(const float* p) { return *p; }
+__device__ __forceinline__ float lds_val(const uint32_t* p) { return __uint_as_float(*p << 16); }
+// Four consecutive elements (16-B / 8-B aligned).
+__device__ __forceinline__ void lds_val4(const float* p, float* v) {
+  const float4 q = *reinterpret_cast<const float4*>(p);
+  v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+}
+__device__ __forceinline__ void lds_val4(const uint32_t* p, float* v) {
+  const uint4 q = *reinterpret_cast<const uint4*>(p);
+  v[0] = __uint_as_float(q.x << 16), v[1] = __uint_as_float(q.y << 16);
+  v[2] = __uint_as_float(q.z << 16), v[3] = __uint_as_float(q.w << 16);
 }
 
-// Staging: the npt*64 threads of a stream load that stream's next tile into registers one tile
-// ahead — x[c][pixel] (2048 elements) and g_logits[pixel][class] (1024). Thread ts covers
-// pixel ts&31 (x) / class ts&31 (g_logits) and rows (ts>>5) + i*2npt, so the per-i part of
-// every address is wave-uniform. NPTC is a lower bound on npt that sizes the register arrays.
-template <int NPTC>
-struct PwLoads {
-  static constexpr int kNX = (kC * 32 + NPTC * 64 - 1) / (NPTC * 64);
-  static constexpr int kNG = (32 * 32 + NPTC * 64 - 1) / (NPTC * 64);
-};
+// One LDS-DMA wave-instruction: lane l's element (byte offset voff + soff of the buffer) lands
+// in the dword at lds + 4 l (zero-extended); out-of-range lanes land as 0.
+template <typename TX>
+__device__ __forceinline__ void dma(rsrc_t r, void* lds, unsigned voff, unsigned soff) {
+  if constexpr (sizeof(TX) == 4)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 4,
+                                             static_cast<int>(voff), static_cast<int>(soff), 0, 0);
+  else
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 2,
+                                             static_cast<int>(voff), static_cast<int>(soff), 0, 0);
+}
 
-// Launch bound per class: npt 1 -> 2 streams x 1 wave; 2..3 -> <= 6 waves; 4..5 -> <= 10; 6..12 -> <= 12.
-template <int NPTC>
-constexpr int pw_max_threads() { return NPTC == 1 ? 128 : NPTC == 2 ? 384 : NPTC == 4 ? 640 : 768; }
-
-template <typename TX, int T, int ACT, int NPTC, bool GD>
-__global__ __launch_bounds__(pw_max_threads<NPTC>()) void l2_bwd_pw_bf16_kernel(
+template <typename TX, int T, int ACT, int MAXT, bool GD>
+__global__ __launch_bounds__(MAXT) void l2_bwd_pw_bf16_kernel(
     const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const unsigned char* __restrict__ img, int P, int Pp,
     int K, float eps, const float* __restrict__ g_logits, unsigned gl_bytes,
     const float* __restrict__ g_dist, unsigned gd_bytes, int streams, float* __restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  constexpr int kNX = PwLoads<NPTC>::kNX, kNG = PwLoads<NPTC>::kNG;
+  using R = PwRaw<TX>;
+  using S = PwStage<TX, T>;
   const int npt = Pp / 32;
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
   const int stream = wave / npt;                 // which pixel stream this wave computes on
   const int w = wave - stream * npt;             // prototype tile owned by this wave
 
-  // LDS: [P image | W^T image | stream staging areas]
+  // LDS: [P image | W^T image | per stream: Xs | Gs | x2[32] | rowoff[32] | XA | XB | GA | GT]
   const ImgOffsets io = img_offsets(Pp, T);
   bf16* Pimg = reinterpret_cast<bf16*>(smem_raw);      // [T][Pp][64]  CPR 8 (chan_of order)
   bf16* WTimg = Pimg + T * Pp * kC;                    // [T][Pp][32]  CPR 4
-  unsigned char* stage_root = reinterpret_cast<unsigned char*>(WTimg + T * Pp * 32);
+  unsigned char* sbase = reinterpret_cast<unsigned char*>(WTimg + T * Pp * 32) + stream * S::kBytes;
+  using XS = typename R::XS;
+  XS* Xs = reinterpret_cast<XS*>(sbase);
+  float* Gs = reinterpret_cast<float*>(sbase + R::kXs * 4);
+  float* x2s = Gs + R::kGs;
+  unsigned* rowoff = reinterpret_cast<unsigned*>(x2s + 32);
+  bf16* XA = reinterpret_cast<bf16*>(rowoff + 32);
+  bf16* XB = XA + S::kXA;
+  bf16* GA = XB + S::kXB;
+  bf16* GT = GA + S::kGA;
   STAMP(0);
   STAMP_RT(7);
   lds_copy(Pimg, img + io.p, io.p2 - io.p);  // P and W^T images are adjacent in the block
-  float *Xf, *Gf, *x2s;
-  unsigned* rowoff;
-  bf16 *XA, *XB, *GA, *GT;
-  pw_carve<T>(stage_root + static_cast<size_t>(stream) * PwStage<T>::kBytes, Xf, Gf, x2s, rowoff, XA, XB, GA, GT);
 
   const rsrc_t rx = make_rsrc(x, x_bytes), rg = make_rsrc(g_logits, gl_bytes), rgd = make_rsrc(g_dist, gd_bytes);
   const int p = w * 32 + j;  // this lane's prototype column
@@ -528,104 +549,103 @@ __global__ __launch_bounds__(pw_max_threads<NPTC>()) void l2_bwd_pw_bf16_kernel(
   const int iters = (ntiles + total_streams - 1) / total_streams;  // uniform across the workgroup
   const int tid_s = threadIdx.x - stream * npt * 64;
   const int nt_stream = npt * 64;
-  const int rstep = 2 * npt;            // rows advanced per load index i
-  const int r0 = tid_s >> 5, col = tid_s & 31;
-  const unsigned xs_step = static_cast<unsigned>(rstep * HW) * sizeof(TX);
-  const unsigned gs_step = static_cast<unsigned>(rstep * K) * 4u;
 
-  float xr[kNX], gr[kNG];
-  auto stage_load = [&](int it) {
-    const int t = blockIdx.x * streams + stream + it * total_streams;
-    const int g = t * 32 + col;
+  // DMA of tile t: instruction i < 32 moves x channels 2i, 2i+1 (lane = pixel l&31 of channel
+  // 2i + (l>>5)); instruction 32 + i2 moves g_logits pixels 2i2, 2i2+1 (lane = class l&31).
+  // The stream's waves take instructions w, w + npt, ...
+  auto dma_tile = [&](int t) {
+    const int g = t * 32 + j;
     unsigned xo = kOOB;
     if (t < ntiles && g < npix) {
       const int b = g / HW;
-      xo = static_cast<unsigned>(((b * kC + r0) * HW + (g - b * HW)) * static_cast<int>(sizeof(TX)));
+      xo = static_cast<unsigned>(((b * kC + h) * HW + (g - b * HW)) * static_cast<int>(sizeof(TX)));
     }
-    const int lim = t < ntiles ? min(32, npix - t * 32) : 0;  // valid pixel rows of g_logits
-    const unsigned go = (t < ntiles && col < K) ? static_cast<unsigned>(((t * 32 + r0) * K + col) * 4) : kOOB;
-#pragma unroll
-    for (int i = 0; i < kNX; ++i)
-      xr[i] = BufIO<TX>::load(rx, (r0 + i * rstep < kC) ? xo : kOOB, i * xs_step);
-#pragma unroll
-    for (int i = 0; i < kNG; ++i)
-      gr[i] = BufIO<float>::load(rg, (r0 + i * rstep < lim) ? go : kOOB, i * gs_step);
+    const int lim = t < ntiles ? min(32, npix - t * 32) : 0;  // valid pixels of this tile
+    const unsigned go = j < K ? static_cast<unsigned>(((t * 32 + h) * K + j) * 4) : kOOB;
+    for (int i = w; i < 48; i += npt) {
+      if (i < 32) {
+        dma<TX>(rx, Xs + i * R::kPairX, xo, static_cast<unsigned>(2 * i * HW) * sizeof(TX));
+      } else {
+        const int i2 = i - 32;
+        dma<float>(rg, Gs + i2 * R::kPairG, (2 * i2 + h < lim) ? go : kOOB, static_cast<unsigned>(2 * i2 * K * 4));
+      }
+    }
   };
 
-  STAMP(1);
-  stage_load(0);
-  for (int it = 0; it < iters; ++it) {
-    const int t = blockIdx.x * streams + stream + it * total_streams;
-    __syncthreads();  // previous tile's operand reads are done
-    if (it == 1) STAMP(2);
-    // ---- prefetched registers -> fp32 LDS staging ----
+  // Raw tile -> split images. Wave 0 of the stream: XA and ||x||^2 (lane = (pixel, half), the
+  // x_frags chain of the forward, so the distances match it bit for bit); the other waves (all
+  // of them when npt == 1): XB (x * -2, exact), GA, GT.
+  auto convert = [&](int t) {
+    if (w == 0) {
+      float s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < kNX; ++i)
-      if (r0 + i * rstep < kC) Xf[(r0 + i * rstep) * kLdf + col] = xr[i];
-#pragma unroll
-    for (int i = 0; i < kNG; ++i)
-      if (r0 + i * rstep < 32) Gf[(r0 + i * rstep) * kLdf + col] = gr[i];
-    stage_load(it + 1);  // prefetch the next tile while this one is converted and computed
-    if (tid_s < 32) {    // per-row g_dist offset (b, n) of this tile
-      const int g = t * 32 + tid_s;
-      const bool ok = t < ntiles && g < npix;
-      const int b = ok ? g / HW : 0;
-      rowoff[tid_s] = ok ? static_cast<unsigned>((b * P * HW + (g - b * HW)) * 4) : kOOB;
-    }
-    __syncthreads();
-    if (it == 1) STAMP(3);
-    // ---- convert to split bf16 operand images ----
-    for (int idx = tid_s; idx < 32 * 8; idx += nt_stream) {  // XA: row n, chunk e8 = (q, h)
-      const int nn = idx >> 3, e8 = idx & 7, q = e8 >> 1, hh = e8 & 1;
-      float v[8];
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) v[jj] = Xf[chan_of(q, hh, jj) * kLdf + nn];
-      bf16x8 f[T];
-      split8<T>(v, f);
-      store_frag<T>(XA, 32 * kC, img_off<8>(nn, e8), f);
-    }
-    for (int idx = tid_s; idx < kC * 4; idx += nt_stream) {  // XB: row c, permuted pixels
-      const int c = idx >> 2, e8 = idx & 3;
-      float v[8];
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) v[jj] = Xf[c * kLdf + perm_of(e8 * 8 + jj)];
-      bf16x8 f[T];
-      split8<T>(v, f);
-      store_frag<T>(XB, kC * 32, img_off<4>(c, e8), f);
-    }
-    for (int idx = tid_s; idx < 32 * 4; idx += nt_stream) {  // GA: row n, classes; GT: row k, permuted n
-      const int r = idx >> 2, e8 = idx & 3;
-      float v[8], u[8];
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        v[jj] = Gf[r * kLdf + e8 * 8 + jj];
-        u[jj] = Gf[perm_of(e8 * 8 + jj) * kLdf + r];
-      }
-      bf16x8 f[T], ft[T];
-      split8<T>(v, f);
-      split8<T>(u, ft);
-      store_frag<T>(GA, 32 * 32, img_off<4>(r, e8), f);
-      store_frag<T>(GT, 32 * 32, img_off<4>(r, e8), ft);
-    }
-    if (tid_s < 32) {  // ||x||^2 per pixel: the chain of x_frags (half 0, half 1, then the sum)
-      const int nn = tid_s;
-      float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-      for (int q = 0; q < kNQ; ++q)
+      for (int q = 0; q < kNQ; ++q) {
+        float v[8];
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) {
-          const float a = Xf[chan_of(q, 0, jj) * kLdf + nn], c = Xf[chan_of(q, 1, jj) * kLdf + nn];
-          s0 = fmaf(a, a, s0);
-          s1 = fmaf(c, c, s1);
+          v[jj] = lds_val(Xs + pair_off<R::kPairX>(chan_of(q, h, jj), j));
+          s2 = fmaf(v[jj], v[jj], s2);
         }
-      x2s[nn] = s0 + s1;
+        bf16x8 f[T];
+        split8<T>(v, f);
+        store_frag<T>(XA, 32 * kC, img_off<8>(j, 2 * q + h), f);
+      }
+      const float x2 = s2 + __shfl_xor(s2, 32);
+      if (h == 0) x2s[j] = x2;
     }
-    __syncthreads();
-    if (it == 1) STAMP(4);
+    const int nthr = npt > 1 ? nt_stream - 64 : nt_stream;
+    for (int idx = npt > 1 ? tid_s - 64 : tid_s; idx >= 0 && idx < 512; idx += nthr) {
+      float v[8];
+      if (idx < 256) {  // XB row c, chunk e8 = (s, hp): pixels 16s + 4hp + {0..3} and + 8
+        const int c = idx >> 2, e8 = idx & 3, sb = 16 * (e8 >> 1) + 4 * (e8 & 1);
+        lds_val4(Xs + pair_off<R::kPairX>(c, sb), v);
+        lds_val4(Xs + pair_off<R::kPairX>(c, sb + 8), v + 4);
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) v[jj] *= -2.f;
+        bf16x8 f[T];
+        split8<T>(v, f);
+        store_frag<T>(XB, kC * 32, img_off<4>(c, e8), f);
+      } else if (idx < 384) {  // GA row n, classes 8e8..8e8+7
+        const int n = (idx - 256) >> 2, e8 = idx & 3;
+        lds_val4(Gs + pair_off<R::kPairG>(n, 8 * e8), v);
+        lds_val4(Gs + pair_off<R::kPairG>(n, 8 * e8 + 4), v + 4);
+        bf16x8 f[T];
+        split8<T>(v, f);
+        store_frag<T>(GA, 32 * 32, img_off<4>(n, e8), f);
+      } else {  // GT row k, permuted pixels
+        const int k = (idx - 384) >> 2, e8 = idx & 3;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) v[jj] = Gs[pair_off<R::kPairG>(perm_of(e8 * 8 + jj), k)];
+        bf16x8 f[T];
+        split8<T>(v, f);
+        store_frag<T>(GT, 32 * 32, img_off<4>(k, e8), f);
+      }
+    }
+    if constexpr (GD) {
+      if (w == npt - 1 && lane < 32) {  // per-row g_dist offset (b, n) of this tile
+        const int g = t * 32 + lane;
+        const bool ok = t < ntiles && g < npix;
+        const int b = ok ? g / HW : 0;
+        rowoff[lane] = ok ? static_cast<unsigned>((b * P * HW + (g - b * HW)) * 4) : kOOB;
+      }
+    }
+  };
+
+  int t = blockIdx.x * streams + stream;
+  dma_tile(t);
+  STAMP(1);
+  for (int it = 0; it < iters; ++it, t += total_streams) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile t has landed
+    __syncthreads();                                   // ... and every wave's; images are free
+    if (it == 1) STAMP(2);
+    convert(t);
+    __syncthreads();  // images ready; the raw tile area is free
+    if (it == 1) STAMP(3);
+    if (it + 1 < iters) dma_tile(t + total_streams);  // lands while this tile is computed
 
     // ---- compute: this wave's prototype tile against the staged pixel tile ----
-    // Rows past npix hold x = 0 and g_logits = 0 (out-of-range loads), so they contribute exact
-    // zeros to g_P and g_W; columns p >= P have zero W^T rows, so g_s = 0 there.
+    // Rows past npix hold x = 0 and g_logits = 0, so they contribute exact zeros to g_P and g_W;
+    // columns p >= P have zero W^T rows, so g_s = 0 there.
     float x2r[16], gdv[16];
     load_rows16(x2s + 4 * h, x2r);
     if constexpr (GD) {
@@ -665,7 +685,7 @@ __global__ __launch_bounds__(pw_max_threads<NPTC>()) void l2_bwd_pw_bf16_kernel(
       if constexpr (GD) gd += gdv[r];
       const float gs = d > 0.f ? gd : 0.f;
       gsum += gs;
-      acc[r] = -2.f * gs;
+      acc[r] = gs;  // XB holds -2x
       gacc[r] = act_fast<ACT>(d, eps);
     }
 #pragma unroll
@@ -796,24 +816,23 @@ size_t fwd_lds(const Geometry& g, int terms) { return static_cast<size_t>(g.Pp) 
 size_t bwd_x_lds(const Geometry& g, int terms) {
   return static_cast<size_t>(g.Pp) * terms * (2 * kC + 32) * 2 + p2_pad(g);
 }
-// Pixel streams per workgroup: 2 when 2*npt waves fit the 768-thread launch bound.
-int pw_streams(const Geometry& g) { return (g.Pp / 32) * 2 <= 12 ? 2 : 1; }
-size_t pw_lds(const Geometry& g, int terms) {
-  const size_t stage = terms == 2 ? PwStage<2>::kBytes : PwStage<3>::kBytes;
-  const int streams = pw_streams(g);
+size_t pw_lds_for(const Geometry& g, int terms, bool x_bf16, int streams) {
+  const size_t stage = x_bf16 ? (terms == 2 ? PwStage<uint16_t, 2>::kBytes : PwStage<uint16_t, 3>::kBytes)
+                              : (terms == 2 ? PwStage<float, 2>::kBytes : PwStage<float, 3>::kBytes);
   const size_t red = static_cast<size_t>(streams - 1) * (g.Pp / 32) * (32 * kC + 32 * 32 + 32) * sizeof(float);
   const size_t st = static_cast<size_t>(g.Pp) * terms * (kC + 32) * 2 + stage * streams;
   return st > red ? st : red;
 }
-int pw_grid(const Geometry& g) {
-  const int streams = pw_streams(g);
+// Pixel streams per workgroup: 2 when 2*npt waves fit the 768-thread launch bound and LDS.
+int pw_streams(const Geometry& g, int terms, bool x_bf16) {
+  return (g.Pp / 32) * 2 <= 12 && pw_lds_for(g, terms, x_bf16, 2) <= kMaxLds ? 2 : 1;
+}
+size_t pw_lds(const Geometry& g, int terms, bool x_bf16) {
+  return pw_lds_for(g, terms, x_bf16, pw_streams(g, terms, x_bf16));
+}
+int pw_grid(const Geometry& g, int streams) {
   const int need = static_cast<int>(ceil_div(g.ntiles, streams));
   return need < 256 ? need : 256;
-}
-// npt class sizing the staging registers: the largest of {1, 2, 4, 6} not above npt.
-int pw_nptc(const Geometry& g) {
-  const int npt = g.Pp / 32;
-  return npt >= 6 ? 6 : npt >= 4 ? 4 : npt >= 2 ? 2 : 1;
 }
 
 struct Bytes {
@@ -848,17 +867,16 @@ int bwd_x_t(const Geometry& g, const Bytes& nb, const void* x, const unsigned ch
   return check_launch("l2_bwd_x_bf16_kernel");
 }
 
-template <typename TX, int T, int ACT, int NPTC, bool GD>
-int bwd_pw_nptc(const Geometry& g, const Bytes& nb, const void* x, const float* protos, const unsigned char* img,
-                float eps, const float* g_logits, const float* g_dist, float* g_protos, float* g_w, float* ws,
-                hipStream_t stream) {
-  if (int st = ensure_lds<l2_bwd_pw_bf16_kernel<TX, T, ACT, NPTC, GD>>()) return st;
-  const int streams = pw_streams(g);
-  const int grid = pw_grid(g);
+template <typename TX, int T, int ACT, int MAXT, bool GD>
+int bwd_pw_launch(const Geometry& g, const Bytes& nb, const void* x, const float* protos, const unsigned char* img,
+                  float eps, const float* g_logits, const float* g_dist, float* g_protos, float* g_w, float* ws,
+                  int streams, hipStream_t stream) {
+  if (int st = ensure_lds<l2_bwd_pw_bf16_kernel<TX, T, ACT, MAXT, GD>>()) return st;
+  const int grid = pw_grid(g, streams);
   const int threads = streams * (g.Pp / 32) * 64;
-  hipLaunchKernelGGL((l2_bwd_pw_bf16_kernel<TX, T, ACT, NPTC, GD>), dim3(grid), dim3(threads), pw_lds(g, T), stream,
-                     static_cast<const TX*>(x), nb.x, g.HW, g.npix, img, g.P, g.Pp, g.K, eps, g_logits, nb.gl, g_dist,
-                     nb.gd, streams, ws);
+  hipLaunchKernelGGL((l2_bwd_pw_bf16_kernel<TX, T, ACT, MAXT, GD>), dim3(grid), dim3(threads),
+                     pw_lds(g, T, sizeof(TX) == 2), stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, img, g.P,
+                     g.Pp, g.K, eps, g_logits, nb.gl, g_dist, nb.gd, streams, ws);
   if (int st = check_launch("l2_bwd_pw_bf16_kernel")) return st;
   const int elems = g.Pp * kC + 32 * g.Pp;
   hipLaunchKernelGGL(l2_bwd_reduce_bf16_kernel, dim3(static_cast<unsigned>(ceil_div(elems, 64))), dim3(256), 0,
@@ -870,16 +888,12 @@ template <typename TX, int T, int ACT, bool GD>
 int bwd_pw_t(const Geometry& g, const Bytes& nb, const void* x, const float* protos, const unsigned char* img,
              float eps, const float* g_logits, const float* g_dist, float* g_protos, float* g_w, float* ws,
              hipStream_t stream) {
-  switch (pw_nptc(g)) {
-    case 6:
-      return bwd_pw_nptc<TX, T, ACT, 6, GD>(g, nb, x, protos, img, eps, g_logits, g_dist, g_protos, g_w, ws, stream);
-    case 4:
-      return bwd_pw_nptc<TX, T, ACT, 4, GD>(g, nb, x, protos, img, eps, g_logits, g_dist, g_protos, g_w, ws, stream);
-    case 2:
-      return bwd_pw_nptc<TX, T, ACT, 2, GD>(g, nb, x, protos, img, eps, g_logits, g_dist, g_protos, g_w, ws, stream);
-    default:
-      return bwd_pw_nptc<TX, T, ACT, 1, GD>(g, nb, x, protos, img, eps, g_logits, g_dist, g_protos, g_w, ws, stream);
-  }
+  const int streams = pw_streams(g, T, sizeof(TX) == 2);
+  if (streams * (g.Pp / 32) * 64 > 384)
+    return bwd_pw_launch<TX, T, ACT, 768, GD>(g, nb, x, protos, img, eps, g_logits, g_dist, g_protos, g_w, ws, streams,
+                                              stream);
+  return bwd_pw_launch<TX, T, ACT, 384, GD>(g, nb, x, protos, img, eps, g_logits, g_dist, g_protos, g_w, ws, streams,
+                                            stream);
 }
 
 template <typename Fn>
@@ -930,10 +944,12 @@ bool bf16_bwd_x_fits(const Geometry& g, int terms) {
   return g.C == kC && bwd_x_lds(g, terms) <= kMaxLds && bf16_sizes_ok(g);
 }
 bool bf16_bwd_pw_fits(const Geometry& g, int terms) {
-  return g.C == kC && g.Pp <= 384 && pw_lds(g, terms) <= kMaxLds && bf16_sizes_ok(g);
+  return g.C == kC && g.Pp <= 384 && pw_lds(g, terms, false) <= kMaxLds && pw_lds(g, terms, true) <= kMaxLds &&
+         bf16_sizes_ok(g);
 }
 size_t bf16_bwd_pw_workspace(const Geometry& g) {
-  return static_cast<size_t>(pw_grid(g)) * (static_cast<size_t>(g.Pp) * kC + 32 * g.Pp + g.Pp) * sizeof(float);
+  // the largest slab count of any stream configuration (one stream per workgroup)
+  return static_cast<size_t>(pw_grid(g, 1)) * (static_cast<size_t>(g.Pp) * kC + 32 * g.Pp + g.Pp) * sizeof(float);
 }
 
 size_t bf16_image_bytes(const Geometry& g, int terms) {

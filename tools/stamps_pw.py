@@ -1,7 +1,7 @@
 """Per-wave phase timing of l2_bwd_pw_bf16_kernel from a `make stamps` build (second tile).
 
-Slots: 0 start, 1 prologue (LDS images) done, 2 tile-1 first barrier passed, 3 fp32 staging
-visible, 4 split images ready, 5 tile-1 compute done, 6 after the stream reduction; 7 realtime.
+Slots: 0 start, 1 prologue issued (image copy + first DMA), 2 tile-1 barrier A passed (raw tile
+landed), 3 barrier B passed (split images ready), 5 tile-1 compute done, 6 after the loop; 7 realtime.
 """
 import ctypes
 import os
@@ -47,12 +47,13 @@ def main():
     print(f"waves recorded: {len(st)}")
     rt = (st[:, 7] - st[:, 7].min()) * 10
     print(f"start spread: p50 {np.percentile(rt, 50):.0f} max {rt.max():.0f} ns")
-    names = ["prologue", "to tile-1 barrier", "fp32 staging", "split images", "compute", "rest+reduce"]
-    for a in range(6):
-        ok = (st[:, a + 1] != 0) & (st[:, a] != 0)
-        d = (st[:, a + 1] - st[:, a])[ok]
+    phases = [("prologue", 0, 1), ("tile 0 (+wait)", 1, 2), ("convert", 2, 3), ("compute", 3, 5),
+              ("remaining tiles", 5, 6)]
+    for name, a, b in phases:
+        ok = (st[:, b] != 0) & (st[:, a] != 0)
+        d = (st[:, b] - st[:, a])[ok]
         if len(d):
-            print(f"{names[a]:18s} cycles: p10 {np.percentile(d, 10):8.0f} p50 {np.percentile(d, 50):8.0f} "
+            print(f"{name:18s} cycles: p10 {np.percentile(d, 10):8.0f} p50 {np.percentile(d, 50):8.0f} "
                   f"p90 {np.percentile(d, 90):8.0f} max {d.max():8.0f}")
     tot = st[:, 6] - st[:, 0]
     print(f"{'wave total':18s} cycles: p50 {np.percentile(tot, 50):8.0f} max {tot.max():8.0f}")
