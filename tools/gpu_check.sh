@@ -16,5 +16,5 @@ step() {  # step <name> <seconds> <cmd...>
   return 0
 }
 step smoke 400 python __graft_entry__.py smoke
-step pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:randomly
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:randomly --timeout 120 --timeout-method thread
 step bench 600 python bench.py --steps 20 --warmup 5 --cpu-seconds 8
