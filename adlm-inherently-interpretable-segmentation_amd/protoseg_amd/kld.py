@@ -1,0 +1,149 @@
+"""KLD similarity loss of segmentation/module.py:167-208 on the HIP kernels, with autograd.
+
+The reference computes, per image and per class present in the (resized) label map, the
+log_softmax of every prototype's distances over the class's pixels and the symmetric KL of
+every prototype pair of the class, in a Python loop with host syncs; the loss is the mean
+over all pairs of exp(-kld). ``kld_loss`` returns the same scalar from three kernels and
+its backward produces d loss / d distances in one kernel, which then flows into the
+prototype layer's backward as ``g_dist`` (protoseg_l2_bwd).
+
+Reference quirks kept (oracle/kld_oracle.py): ``target_img`` holds raw label values with
+0 = void and the prototype column for label value c is c itself, so void pixels pair with
+class-0 prototypes and label value ``num_classes`` is skipped (module.py:170-178).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from . import _lib
+
+MAX_PER_CLASS = 32  # prototypes per class the kernels hold (kld.hip kKldMaxPerClass)
+
+_LABEL_DTYPES = {torch.int64: _lib.I64, torch.int32: _lib.I32, torch.uint8: _lib.U8}
+
+
+def _labels(target_img: Tensor, B: int) -> Tuple[Tensor, int]:
+    t = target_img.reshape(B, -1)
+    if t.dtype not in _LABEL_DTYPES:
+        t = t.to(torch.int64)
+    return t.contiguous(), _LABEL_DTYPES[t.dtype]
+
+
+@torch.library.custom_op("protoseg::kld_forward", mutates_args=(), device_types="cuda")
+def kld_forward(distances: Tensor, target_img: Tensor, proto_class: Tensor, num_classes: int,
+                max_per_class: int) -> Tuple[Tensor, Tensor, Tensor]:
+    """Returns (loss [] f32, n_pairs [] int32, workspace [bytes] uint8 for the backward)."""
+    dev = _lib.require_device(distances, target_img, proto_class)
+    d = distances.contiguous().float()
+    B, P = d.shape[0], d.shape[1]
+    HW = d[0, 0].numel()
+    t, ldt = _labels(target_img, B)
+    if t.shape[1] != HW:
+        raise _lib.ProtosegError(f"target_img has {t.shape[1]} pixels per image, distances {HW}")
+    pc = proto_class.to(torch.int32).contiguous()
+    lib = _lib.load()
+    ws = torch.empty(lib.protoseg_kld_workspace_size(B, P, num_classes), device=dev, dtype=torch.uint8)
+    loss = torch.empty((), device=dev, dtype=torch.float32)
+    npairs = torch.empty((), device=dev, dtype=torch.int32)
+    with torch.cuda.device(dev):
+        _lib.call("protoseg_kld_forward", _lib.ptr(d), B, P, HW, _lib.ptr(t), ldt, _lib.ptr(pc), int(num_classes),
+                  int(max_per_class), _lib.ptr(loss), _lib.ptr(npairs), _lib.ptr(ws), ws.numel(), _lib.stream_of(dev))
+    return loss, npairs, ws
+
+
+@kld_forward.register_fake
+def _(distances, target_img, proto_class, num_classes, max_per_class):
+    B, P = distances.shape[0], distances.shape[1]
+    n = _lib.load().protoseg_kld_workspace_size(B, P, num_classes)
+    return (distances.new_empty((), dtype=torch.float32), distances.new_empty((), dtype=torch.int32),
+            distances.new_empty((n,), dtype=torch.uint8))
+
+
+@torch.library.custom_op("protoseg::kld_backward", mutates_args=(), device_types="cuda")
+def kld_backward(distances: Tensor, target_img: Tensor, proto_class: Tensor, num_classes: int, max_per_class: int,
+                 workspace: Tensor, g_loss: Tensor) -> Tensor:
+    """d(g_loss * loss) / d distances, dense, shaped like ``distances``."""
+    dev = _lib.require_device(distances, target_img, proto_class, workspace, g_loss)
+    d = distances.contiguous().float()
+    B, P = d.shape[0], d.shape[1]
+    HW = d[0, 0].numel()
+    t, ldt = _labels(target_img, B)
+    pc = proto_class.to(torch.int32).contiguous()
+    g = g_loss.to(torch.float32).contiguous()
+    g_dist = torch.empty_like(d)
+    with torch.cuda.device(dev):
+        _lib.call("protoseg_kld_backward", _lib.ptr(d), B, P, HW, _lib.ptr(t), ldt, _lib.ptr(pc), int(num_classes),
+                  int(max_per_class), _lib.ptr(g), _lib.ptr(workspace), workspace.numel(), _lib.ptr(g_dist),
+                  _lib.stream_of(dev))
+    return g_dist
+
+
+@kld_backward.register_fake
+def _(distances, target_img, proto_class, num_classes, max_per_class, workspace, g_loss):
+    return torch.empty_like(distances, dtype=torch.float32)
+
+
+def _setup_context(ctx, inputs, output):
+    distances, target_img, proto_class, num_classes, max_per_class = inputs
+    _, _, ws = output
+    ctx.save_for_backward(distances, target_img, proto_class, ws)
+    ctx.num_classes = num_classes
+    ctx.max_per_class = max_per_class
+    ctx.mark_non_differentiable(output[1], output[2])
+
+
+def _backward(ctx, g_loss, g_npairs, g_ws):
+    distances, target_img, proto_class, ws = ctx.saved_tensors
+    if g_loss is None or not ctx.needs_input_grad[0]:
+        return None, None, None, None, None
+    g = kld_backward(distances, target_img, proto_class, ctx.num_classes, ctx.max_per_class, ws, g_loss)
+    return g.to(distances.dtype), None, None, None, None
+
+
+torch.library.register_autograd("protoseg::kld_forward", _backward, setup_context=_setup_context)
+
+_class_cache: dict = {}
+
+
+def prototype_columns(prototype_class_identity: Tensor, device) -> Tuple[Tensor, int]:
+    """(class column of each prototype as int32 on ``device``, max prototypes per class).
+
+    module.py:173 selects the prototypes of class c as nonzero(identity[:, c]); with the
+    reference's one-hot identity (model.py:66-71) that is argmax(identity[p]) == c. Cached per
+    identity tensor version, so a training loop pays the host reduction once."""
+    ident = prototype_class_identity
+    key = (id(ident), ident._version, ident.data_ptr(), str(device))
+    hit = _class_cache.get(key)
+    if hit is not None:
+        return hit
+    host = ident.detach().to("cpu")
+    if host.dim() != 2 or not bool(((host != 0).sum(1) == 1).all()):
+        raise _lib.ProtosegError("prototype_class_identity must be one-hot per prototype (model.py:66-71)")
+    counts = (host != 0).sum(0)
+    mpc = max(1, int(counts.max()))
+    if mpc > MAX_PER_CLASS:
+        raise _lib.ProtosegError(f"{mpc} prototypes in one class; the KLD kernels hold at most {MAX_PER_CLASS}")
+    cols = host.abs().argmax(1).to(torch.int32).to(device)
+    if len(_class_cache) > 16:
+        _class_cache.clear()
+    _class_cache[key] = (cols, mpc)
+    return cols, mpc
+
+
+def kld_loss(distances: Tensor, target_img: Tensor, prototype_class_identity: Tensor,
+             max_per_class: Optional[int] = None) -> Tensor:
+    """module.py:167-208: mean over (image, class, prototype pair) of exp(-symmetric KL) of the
+    per-prototype log_softmax of the distances over the class's pixels. 0-dim f32 tensor
+    (0 when no pair exists), differentiable with respect to ``distances``.
+
+    distances [B, P, h, w] (PPNet.forward's second output); target_img [B, h*w] or [B, h, w]
+    label values (0 = void); prototype_class_identity [P, K] one-hot."""
+    cols, mpc = prototype_columns(prototype_class_identity, distances.device)
+    if max_per_class is not None:
+        mpc = int(max_per_class)
+    loss, _, _ = torch.ops.protoseg.kld_forward(distances, target_img, cols, int(prototype_class_identity.shape[1]),
+                                                mpc)
+    return loss

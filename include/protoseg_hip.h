@@ -151,6 +151,41 @@ int protoseg_push_merge(const uint64_t* img_keys, int n_img, int64_t first_img,
                         float* global_dist, int64_t* global_img, int32_t* global_patch,
                         float* global_fmap, protoseg_stream_t stream);
 
+/*
+ * KLD similarity loss. Replaces segmentation/module.py:167-208 (the Python loop over images x
+ * classes x prototype pairs: masked_select -> log_softmax -> two kl_div per pair -> mean of
+ * exp(-kld)) and, in protoseg_kld_backward, its autograd. Semantics of the reference kept:
+ * label value c selects the prototypes of class column c (void = 0 pairs with class 0, value
+ * K is skipped, module.py:170-178); a class with < 2 prototypes or < 2 pixels adds no pair;
+ * loss = 0 without pairs.
+ *
+ *   dist        [B, P, HW] f32: the distances of protoseg_l2_fwd (model.py:283, NCHW)
+ *   label       [B, HW] label_dtype (PROTOSEG_I64 | I32 | U8): target_img of module.py:150
+ *               (the resized label map before the void shift)
+ *   proto_class [P] int32: class column of each prototype (argmax of prototype_class_identity;
+ *               the identity is one-hot in the reference, model.py:66-71)
+ *   K           num_classes (prototype_class_identity.shape[1]), K <= 63
+ *   max_per_class  bound on prototypes per class, 1..32 (sizes LDS); a class holding more
+ *               makes the loss NaN
+ *   loss_out    [1] f32 device: mean over pairs of exp(-kld)
+ *   npairs_out  [1] int32 device or NULL: number of pairs
+ *   workspace   protoseg_kld_workspace_size(B, P, K) bytes; the forward fills it and the
+ *               backward of the same inputs reads it
+ * Backward:
+ *   g_loss      [1] f32 device or NULL (= 1): upstream gradient of the loss
+ *   g_dist      [B, P, HW] f32 out: d(g_loss * loss)/d dist (overwritten, dense; zero off each
+ *               prototype's class pixels) — pass it to protoseg_l2_bwd as g_dist
+ */
+size_t protoseg_kld_workspace_size(int B, int P, int K);
+int protoseg_kld_forward(const float* dist, int B, int P, int HW, const void* label, int label_dtype,
+                         const int32_t* proto_class, int K, int max_per_class, float* loss_out,
+                         int32_t* npairs_out, void* workspace, size_t workspace_bytes,
+                         protoseg_stream_t stream);
+int protoseg_kld_backward(const float* dist, int B, int P, int HW, const void* label, int label_dtype,
+                          const int32_t* proto_class, int K, int max_per_class, const float* g_loss,
+                          const void* workspace, size_t workspace_bytes, float* g_dist,
+                          protoseg_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -18,6 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 
 from oracle import protoseg_oracle as po  # noqa: E402
+from oracle import kld_oracle as ko  # noqa: E402
 from oracle import push_oracle as pu  # noqa: E402
 
 SEED = 20220227
@@ -67,15 +68,33 @@ def push_case(n_img, C, H, W, h, w, P, K, seed):
                 duplicate_idx=np.asarray(duplicate_idx, dtype=np.int64))
 
 
+def kld_case(B, h, w, P, K, seed):
+    """module.py:167-208 on the distances of a trained-looking layer: labels in blocks with
+    void, every class value and the skipped value K present; one class with a single pixel."""
+    x, protos, _ = po.synthetic_inputs(B, 64, h, w, P, K, seed)
+    dist = po.l2_convolution(x, protos[:, :, None, None], torch.ones(P, 64, 1, 1))
+    target = ko.synthetic_targets(B, h, w, K, seed + 1, block=3)
+    absent = [c for c in range(1, K) if int((target[1] == c).sum()) == 0]
+    if absent:
+        target[1, 0] = absent[0]  # a class with a single pixel: no distribution (module.py:186)
+    identity = po.class_identity(P, K)
+    loss, n_pairs, g_dist = ko.kld_loss_and_grad(dist, target, identity, g_loss=1.0)
+    return dict(dist=dist.numpy(), target=target.numpy(), proto_class=torch.argmax(identity, 1).numpy().astype(np.int32),
+                num_classes=np.int64(K), loss=np.float32(loss), n_pairs=np.int64(n_pairs), g_dist=g_dist.numpy())
+
+
 CASES = {
     "l2_small": lambda: l2_case(2, 64, 17, 17, 38, 19, SEED),
     "l2_ragged": lambda: l2_case(3, 32, 7, 11, 21, 3, SEED + 7),
     "push_small": lambda: push_case(3, 64, 64, 128, 8, 16, 38, 19, SEED),
+    "kld_small": lambda: kld_case(2, 13, 17, 38, 19, SEED + 11),
 }
 
 
-def main():
+def main(only=None):
     for name, fn in CASES.items():
+        if only and name not in only:
+            continue
         arrays = fn()
         path = os.path.join(HERE, f"{name}.npz")
         np.savez_compressed(path, **arrays)
@@ -83,4 +102,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])
