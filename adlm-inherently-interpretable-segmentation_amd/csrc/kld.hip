@@ -31,6 +31,7 @@ constexpr int kKldMaxPerClass = 32;  // prototypes of one class held per workgro
 constexpr int kKldMaxClasses = 63;   // K + 1 buckets handled by one wave
 constexpr int kKldThreads = 256;     // = pixels per staged chunk
 constexpr int kKldPair = kKldMaxPerClass * kKldMaxPerClass;
+constexpr size_t kKldMaxDynLds = 2 * kKldMaxPerClass * kKldThreads * sizeof(float);  // p | log p chunks
 
 size_t align256(size_t v) { return (v + 255) & ~static_cast<size_t>(255); }
 
@@ -420,7 +421,7 @@ extern "C" int protoseg_kld_forward(const float* dist, int B, int P, int HW, con
   const size_t lds = static_cast<size_t>(2) * max_per_class * kKldThreads * sizeof(float);
   const int st = by_label(label_dtype, [&](auto tl) {
     using TL = std::remove_pointer_t<decltype(tl)>;
-    if (int e = ensure_lds<kld_pairs_kernel<TL>>()) return e;
+    if (int e = ensure_lds<kld_pairs_kernel<TL>, kKldMaxDynLds>()) return e;
     hipLaunchKernelGGL(kld_pairs_kernel<TL>, dim3(K, B), dim3(kKldThreads), lds, s, dist, P, HW,
                        static_cast<const TL*>(label), K, max_per_class, w.off, w.idx, w.cnt, w.mx, w.lse, w.kl);
     return check_launch("kld_pairs_kernel");
@@ -445,7 +446,7 @@ extern "C" int protoseg_kld_backward(const float* dist, int B, int P, int HW, co
   const dim3 grid(static_cast<unsigned>(ceil_div(HW, kKldThreads)), K + 1, B);
   return by_label(label_dtype, [&](auto tl) {
     using TL = std::remove_pointer_t<decltype(tl)>;
-    if (int e = ensure_lds<kld_grad_kernel<TL>>()) return e;
+    if (int e = ensure_lds<kld_grad_kernel<TL>, kKldMaxDynLds>()) return e;
     hipLaunchKernelGGL(kld_grad_kernel<TL>, grid, dim3(kKldThreads), lds, s, dist, P, HW,
                        static_cast<const TL*>(label), K, max_per_class, w.off, w.idx, w.cnt, w.mx, w.lse, w.kl, w.stat,
                        g_loss, g_dist);

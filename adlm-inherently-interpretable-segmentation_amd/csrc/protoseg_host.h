@@ -17,15 +17,16 @@ int check_launch(const char* what);
 // gfx950 has 160 KiB of LDS per CU; a kernel opts in once to dynamic LDS above 64 KiB.
 constexpr size_t kMaxLds = 160 * 1024;
 
-// One flag per kernel (the template parameter is the kernel itself).
-template <auto kernel>
+// One flag per kernel (the template parameter is the kernel itself). `bytes` is the largest
+// dynamic LDS the kernel is launched with; static LDS plus `bytes` must fit the 160 KiB.
+template <auto kernel, size_t bytes = kMaxLds>
 int ensure_lds() {
   static std::once_flag once;
   static hipError_t status = hipSuccess;
   std::call_once(once, [] {
     status = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 static_cast<int>(kMaxLds));
+                                 static_cast<int>(bytes));
   });
   if (status != hipSuccess) return fail(PROTOSEG_ERR_HIP, "hipFuncSetAttribute: %s", hipGetErrorString(status));
   return PROTOSEG_OK;
