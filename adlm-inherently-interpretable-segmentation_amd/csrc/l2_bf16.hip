@@ -178,11 +178,16 @@ __global__ __launch_bounds__(256) void l2_prep_bf16_kernel(const float* __restri
   }
 }
 
+// Wave index as a provably wave-uniform value (SGPR): threadIdx.x / 64 is uniform but the
+// compiler cannot prove it, and a "divergent" LDS-DMA base or buffer soffset derived from it
+// makes hipcc wrap every such memory op in a waterfall loop (cdna_hip_programming.md T20).
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)); }
+
 // Workgroup-wide copy of `bytes` (a multiple of 1 KiB) from global to LDS by 16-B LDS-DMA
 // (global_load_lds_dwordx4: one wave-instruction moves 1 KiB, lane-linear). The caller's
 // __syncthreads() waits for it.
 __device__ __forceinline__ void lds_copy(void* lds, const unsigned char* src, int bytes) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, wave = wave_id(), nw = blockDim.x >> 6;
   for (int off = wave * 1024; off < bytes; off += nw * 1024)
     __builtin_amdgcn_global_load_lds(
         (const __attribute__((address_space(1))) void*)(src + off + lane * 16),
@@ -225,7 +230,39 @@ __device__ __forceinline__ float x_frags(const float (&raw)[kNQ * 8], bf16x8 (&x
   return x2 + __shfl_xor(x2, 32);
 }
 
-template <typename TX, int T, int ACT, bool ACTS>
+// S = P . X for prototype tile pt (layout A: rows p, cols the wave's 32 pixels), T-term split.
+template <int T>
+__device__ __forceinline__ f32x16 s_tile(const bf16* Pimg, int Pp, int pt, const bf16x8 (&xb)[kNQ][T]) {
+  const int j = threadIdx.x & 31, h = (threadIdx.x & 63) >> 5;
+  f32x16 acc = zero16();
+#pragma unroll
+  for (int q = 0; q < kNQ; ++q) {
+    bf16x8 pa[T];
+    load_frag<T>(Pimg, Pp * kC, img_off<8>(pt * 32 + j, 2 * q + h), pa);
+    acc = mma_split<T>(pa, xb[q], acc);
+  }
+  return acc;
+}
+
+// Tile schedule shared by the layout-A kernels (forward, x-backward). The ntiles pixel tiles are
+// split into R = ntiles / W full rounds (W = resident waves; wave g takes tiles g, g + W, ...,
+// every wave the same count) and a remainder of m < W tiles. A remainder tile is processed
+// by one whole workgroup, its waves splitting the prototype tiles (wave w: pt = w, w + 8, ...),
+// so the remainder costs about one prototype tile of time instead of one pixel tile — with
+// one tile per wave per round, a remainder handled the plain way would leave most of the chip
+// idle for a whole extra round.
+struct TileSchedule {
+  int full_end;  // tiles [0, full_end) are done in full rounds
+  __device__ TileSchedule(int ntiles) {
+    const int W = static_cast<int>(gridDim.x) * kWavesA;
+    full_end = (ntiles / W) * W;
+  }
+};
+
+// Forward, one pixel tile per wave per round: distances (NCHW stores), activation in registers,
+// logits = W . act with the accumulator as B operand. Remainder tiles: see TileSchedule; the
+// per-wave logits partials are summed in LDS in a fixed order (deterministic).
+template <typename TX, int T, int ACT, bool ACTS, bool LOGITS>
 __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
     const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const unsigned char* __restrict__ img, int P, int Pp,
     int K, float eps, float* __restrict__ dist, unsigned d_bytes,
@@ -237,9 +274,9 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
   bf16* Pimg = reinterpret_cast<bf16*>(smem_raw);                // [T][Pp][64]
   bf16* Wimg = Pimg + T * Pp * kC;                               // [T][Pp][32]
   float* p2s = reinterpret_cast<float*>(Wimg + T * Pp * 32);     // [Pp]
-  const bool do_logits = logits != nullptr;
+  float* lpart = p2s + (io.pt - io.p2) / 4;                      // [kWavesA][16][64] remainder logits
   lds_copy(Pimg, img + io.p, io.wt - io.p);
-  lds_copy(Wimg, img + io.w, io.total - io.w);
+  if constexpr (LOGITS) lds_copy(Wimg, img + io.w, io.total - io.w);
   lds_copy(p2s, img + io.p2, io.pt - io.p2);
   __syncthreads();
   STAMP(1);
@@ -247,58 +284,42 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
   const rsrc_t rx = make_rsrc(x, x_bytes), rd = make_rsrc(dist, d_bytes);
   const rsrc_t ra = make_rsrc(act_out, a_bytes), rl = make_rsrc(logits, l_bytes);
   const unsigned cs = static_cast<unsigned>(HW) * sizeof(TX);
-  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = wave_id();
   const int ntiles = (npix + 31) / 32;
   const int npt = Pp / 32;
   const int stride = gridDim.x * kWavesA;
-  int t = blockIdx.x * kWavesA + wave;
-  float raw[kNQ * 8];
-  load_x_raw<TX>(rx, x_lane_off<TX>(t, ntiles, npix, HW), cs, raw);
-  for (; t < ntiles; t += stride) {
+  const TileSchedule sched(ntiles);
+
+  // Prototype tiles pt0, pt0 + dpt, ... of pixel tile t (x already in raw); returns the
+  // tile's logits accumulator over those prototype tiles.
+  auto run_tile = [&](int t, const float (&raw)[kNQ * 8], int pt0, int dpt) {
     bf16x8 xb[kNQ][T];
     const float x2 = x_frags<T>(raw, xb);
-    const bool first = t == static_cast<int>(blockIdx.x) * kWavesA + wave;
-    if (first) STAMP(2);
-    load_x_raw<TX>(rx, x_lane_off<TX>(t + stride, ntiles, npix, HW), cs, raw);  // prefetch next tile
-
     const int g = t * 32 + j;
     const bool valid = g < npix;
     const int b = valid ? g / HW : 0;
     const int n = valid ? g - b * HW : 0;
     const unsigned dbase = valid ? static_cast<unsigned>(((b * P + 4 * h) * HW + n) * 4) : kOOB;
     const unsigned abase = valid ? static_cast<unsigned>((g * P + 4 * h) * 4) : kOOB;
-
     f32x16 lacc = zero16();
 #pragma unroll 1
-    for (int pt = 0; pt < npt; ++pt) {
-      f32x16 acc = zero16();
-#pragma unroll
-      for (int q = 0; q < kNQ; ++q) {
-        bf16x8 pa[T];
-        load_frag<T>(Pimg, Pp * kC, img_off<8>(pt * 32 + j, 2 * q + h), pa);
-        acc = mma_split<T>(pa, xb[q], acc);
-      }
+    for (int pt = pt0; pt < npt; pt += dpt) {
+      f32x16 acc = s_tile<T>(Pimg, Pp, pt, xb);
       const int prem = P - pt * 32 - 4 * h;  // rows of this tile (and half) below P
       float p2r[16];
       load_rows16(p2s + pt * 32 + 4 * h, p2r);
-      // Distances / activations: no branches per element (a null output has a zero-size
-      // buffer resource, so its stores are dropped); full prototype tiles skip the row test.
-      auto epilogue = [&](auto full) {
+      // No branches per element: a null output has a zero-size buffer resource (its stores are
+      // dropped), rows past P get an out-of-range offset.
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float d = l2_distance(x2, p2r[r], acc[r]);
-          const bool pin = decltype(full)::value || row_of(r) < prem;
-          BufIO<float>::store(rd, d, pin ? dbase : kOOB, static_cast<unsigned>((pt * 32 + row_of(r)) * HW * 4));
-          const float a = act_fast<ACT>(d, eps);
-          if constexpr (ACTS) BufIO<float>::store(ra, a, pin ? abase : kOOB, static_cast<unsigned>((pt * 32 + row_of(r)) * 4));
-          acc[r] = a;
-        }
-      };
-      if ((pt + 1) * 32 <= P)
-        epilogue(std::true_type());
-      else
-        epilogue(std::false_type());
-      if (do_logits) {
+      for (int r = 0; r < 16; ++r) {
+        const float d = l2_distance(x2, p2r[r], acc[r]);
+        const unsigned row_ok = row_of(r) < prem ? 0u : kOOB;
+        BufIO<float>::store(rd, d, dbase | row_ok, static_cast<unsigned>((pt * 32 + row_of(r)) * HW * 4));
+        const float a = act_fast<ACT>(d, eps);
+        if constexpr (ACTS) BufIO<float>::store(ra, a, abase | row_ok, static_cast<unsigned>((pt * 32 + row_of(r)) * 4));
+        acc[r] = a;
+      }
+      if constexpr (LOGITS) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           bf16x8 ab[T], wa[T];
@@ -307,17 +328,55 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
           lacc = mma_split<T>(wa, ab, lacc);
         }
       }
-      if (pt == 0 && first) STAMP(3);
     }
-    if (first) STAMP(4);
-    if (do_logits) {
-      const unsigned lbase = valid ? static_cast<unsigned>((g * K + 4 * h) * 4) : kOOB;
-      const int krem = K - 4 * h;
+    return lacc;
+  };
+  auto store_logits = [&](int t, const f32x16& lacc) {
+    const int g = t * 32 + j;
+    const unsigned lbase = g < npix ? static_cast<unsigned>((g * K + 4 * h) * 4) : kOOB;
+    const int krem = K - 4 * h;
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        BufIO<float>::store(rl, lacc[r], row_of(r) < krem ? lbase : kOOB, static_cast<unsigned>(row_of(r) * 4));
+    for (int r = 0; r < 16; ++r)
+      BufIO<float>::store(rl, lacc[r], row_of(r) < krem ? lbase : kOOB, static_cast<unsigned>(row_of(r) * 4));
+  };
+
+  // ---- full rounds: one tile per wave per round, the next tile's x prefetched into registers
+  int t = blockIdx.x * kWavesA + wave;
+  float raw[kNQ * 8];
+  load_x_raw<TX>(rx, x_lane_off<TX>(t < sched.full_end ? t : ntiles, ntiles, npix, HW), cs, raw);
+  for (; t < sched.full_end; t += stride) {
+    float cur[kNQ * 8];
+#pragma unroll
+    for (int i = 0; i < kNQ * 8; ++i) cur[i] = raw[i];
+    const int tn = t + stride;
+    load_x_raw<TX>(rx, x_lane_off<TX>(tn < sched.full_end ? tn : ntiles, ntiles, npix, HW), cs, raw);
+    if (t == static_cast<int>(blockIdx.x) * kWavesA + wave) STAMP(2);
+    const f32x16 lacc = run_tile(t, cur, 0, 1);
+    if constexpr (LOGITS) store_logits(t, lacc);
+    if (t == static_cast<int>(blockIdx.x) * kWavesA + wave) STAMP(3);
+  }
+  STAMP(4);
+
+  // ---- remainder: one tile per workgroup, prototype tiles split over the waves
+  for (int tt = sched.full_end + static_cast<int>(blockIdx.x); tt < ntiles; tt += gridDim.x) {
+    float rt[kNQ * 8];
+    load_x_raw<TX>(rx, x_lane_off<TX>(tt, ntiles, npix, HW), cs, rt);
+    const f32x16 lacc = run_tile(tt, rt, wave, kWavesA);
+    if constexpr (LOGITS) {
+      float* mine = lpart + wave * 16 * 64;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mine[r * 64 + lane] = lacc[r];
+      __syncthreads();
+      if (wave == 0) {
+        f32x16 sum = zero16();
+        const int nw = npt < kWavesA ? npt : kWavesA;
+        for (int w = 0; w < nw; ++w)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sum[r] += lpart[(w * 16 + r) * 64 + lane];
+        store_logits(tt, sum);
+      }
+      __syncthreads();
     }
-    if (first) STAMP(5);
   }
   STAMP(6);
 }
@@ -342,10 +401,9 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
   const rsrc_t rx = make_rsrc(x, x_bytes), rg = make_rsrc(g_logits, gl_bytes);
   const rsrc_t rgd = make_rsrc(g_dist, gd_bytes), rgx = make_rsrc(g_x, x_bytes);
   const unsigned cs = static_cast<unsigned>(HW) * sizeof(TX);
-  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = wave_id();
   const int ntiles = (npix + 31) / 32;
   const int npt = Pp / 32;
-  const int KS = (K + 15) / 16;  // class k-steps of 16
   for (int t = blockIdx.x * kWavesA + wave; t < ntiles; t += gridDim.x * kWavesA) {
     const unsigned xoff = x_lane_off<TX>(t, ntiles, npix, HW);
     float raw[kNQ * 8];
@@ -392,16 +450,14 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
         load_frag<T>(Pimg, Pp * kC, img_off<8>(pt * 32 + j, 2 * q + h), pa);
         acc = mma_split<T>(pa, xb[q], acc);
       }
+      // Both class k-steps always run (W^T rows >= K are zero, and g_logits reads as 0 when
+      // absent), so the loop body stays one basic block.
       f32x16 gacc = zero16();
-      if (g_logits) {
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          if (s < KS) {
-            bf16x8 wa[T];
-            load_frag<T>(WTimg, Pp * 32, img_off<4>(pt * 32 + j, 2 * s + h), wa);
-            gacc = mma_split<T>(wa, glb[s], gacc);
-          }
-        }
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 wa[T];
+        load_frag<T>(WTimg, Pp * 32, img_off<4>(pt * 32 + j, 2 * s + h), wa);
+        gacc = mma_split<T>(wa, glb[s], gacc);
       }
       const int prem = P - pt * 32 - 4 * h;
       float p2r[16];
@@ -493,14 +549,25 @@ __device__ __forceinline__ void lds_val4(const uint32_t* p, float* v) {
 
 // One LDS-DMA wave-instruction: lane l's element (byte offset voff + soff of the buffer) lands
 // in the dword at lds + 4 l (zero-extended); out-of-range lanes land as 0.
+// Written as inline asm on purpose (cdna_hip_programming.md §5.7): hipcc counts a builtin
+// LDS-DMA as an LDS write of unknown extent and drains it (vmcnt(0)) before the next ds_read,
+// which here would stall the compute of tile t on the prefetch of tile t+1. The kernel waits
+// for its DMA itself (s_waitcnt vmcnt(0) + barrier at the top of each tile). `lds` and `soff`
+// must be wave-uniform.
 template <typename TX>
 __device__ __forceinline__ void dma(rsrc_t r, void* lds, unsigned voff, unsigned soff) {
+  const unsigned dst = static_cast<unsigned>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)lds));
+  unsigned keep;
   if constexpr (sizeof(TX) == 4)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 4,
-                                             static_cast<int>(voff), static_cast<int>(soff), 0, 0);
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %1, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(__builtin_amdgcn_readfirstlane(dst)), "s"(r), "s"(__builtin_amdgcn_readfirstlane(soff))
+                 : "memory");
   else
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 2,
-                                             static_cast<int>(voff), static_cast<int>(soff), 0, 0);
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_ushort %1, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(__builtin_amdgcn_readfirstlane(dst)), "s"(r), "s"(__builtin_amdgcn_readfirstlane(soff))
+                 : "memory");
 }
 
 template <typename TX, int T, int ACT, int MAXT, bool GD>
@@ -512,7 +579,7 @@ __global__ __launch_bounds__(MAXT) void l2_bwd_pw_bf16_kernel(
   using R = PwRaw<TX>;
   using S = PwStage<TX, T>;
   const int npt = Pp / 32;
-  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = wave_id();
   const int stream = wave / npt;                 // which pixel stream this wave computes on
   const int w = wave - stream * npt;             // prototype tile owned by this wave
 
@@ -538,7 +605,6 @@ __global__ __launch_bounds__(MAXT) void l2_bwd_pw_bf16_kernel(
   const int p = w * 32 + j;  // this lane's prototype column
   const bool pvalid = p < P;
   const float p2 = reinterpret_cast<const float*>(img + io.p2)[p];
-  const int KS = (K + 15) / 16;
 
   f32x16 gp[2] = {zero16(), zero16()};
   f32x16 gw = zero16();
@@ -666,17 +732,13 @@ __global__ __launch_bounds__(MAXT) void l2_bwd_pw_bf16_kernel(
       load_frag<T>(Pimg, Pp * kC, img_off<8>(p, 2 * q + h), pb);
       acc = mma_split<T>(xa, pb, acc);
     }
-    f32x16 gacc = zero16();
-    if (g_logits) {
+    f32x16 gacc = zero16();  // both class k-steps always run: zero W^T rows / GA columns past K
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        if (s < KS) {
-          bf16x8 ga[T], wb[T];
-          load_frag<T>(GA, 32 * 32, img_off<4>(j, 2 * s + h), ga);
-          load_frag<T>(WTimg, Pp * 32, img_off<4>(p, 2 * s + h), wb);
-          gacc = mma_split<T>(ga, wb, gacc);
-        }
-      }
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 ga[T], wb[T];
+      load_frag<T>(GA, 32 * 32, img_off<4>(j, 2 * s + h), ga);
+      load_frag<T>(WTimg, Pp * 32, img_off<4>(p, 2 * s + h), wb);
+      gacc = mma_split<T>(ga, wb, gacc);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -699,11 +761,9 @@ __global__ __launch_bounds__(MAXT) void l2_bwd_pw_bf16_kernel(
         load_frag<T>(XB, kC * 32, img_off<4>(ct * 32 + j, 2 * s + h), xbf);
         gp[ct] = mma_split<T>(gsa, xbf, gp[ct]);
       }
-      if (g_logits) {
-        bf16x8 gt[T];
-        load_frag<T>(GT, 32 * 32, img_off<4>(j, 2 * s + h), gt);
-        gw = mma_split<T>(gt, actb, gw);
-      }
+      bf16x8 gt[T];
+      load_frag<T>(GT, 32 * 32, img_off<4>(j, 2 * s + h), gt);
+      gw = mma_split<T>(gt, actb, gw);
     }
     if (it == 1) STAMP(5);
   }
@@ -812,7 +872,9 @@ __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __
 
 // ---- host side ---------------------------------------------------------------------------------
 size_t p2_pad(const Geometry& g) { return (static_cast<size_t>(g.Pp) * 4 + 1023) & ~static_cast<size_t>(1023); }
-size_t fwd_lds(const Geometry& g, int terms) { return static_cast<size_t>(g.Pp) * terms * (kC + 32) * 2 + p2_pad(g); }
+size_t fwd_lds(const Geometry& g, int terms) {
+  return static_cast<size_t>(g.Pp) * terms * (kC + 32) * 2 + p2_pad(g) + static_cast<size_t>(kWavesA) * 16 * 64 * 4;
+}
 size_t bwd_x_lds(const Geometry& g, int terms) {
   return static_cast<size_t>(g.Pp) * terms * (2 * kC + 32) * 2 + p2_pad(g);
 }
@@ -839,16 +901,16 @@ struct Bytes {
   unsigned x, d, a, l, gl, gd;
 };
 
-template <typename TX, int T, int ACT, bool ACTS>
+template <typename TX, int T, int ACT, bool ACTS, bool LOGITS>
 int fwd_t(const Geometry& g, const Bytes& nb, const void* x, const unsigned char* img, float eps, float* dist,
           float* act, float* logits, hipStream_t stream) {
-  if (int st = ensure_lds<l2_fwd_bf16_kernel<TX, T, ACT, ACTS>>()) return st;
+  if (int st = ensure_lds<l2_fwd_bf16_kernel<TX, T, ACT, ACTS, LOGITS>>()) return st;
   const size_t lds = fwd_lds(g, T);
   // Persistent: one generation of resident workgroups; waves stride over the tiles and
   // prefetch their next tile.
-  const int cap = resident_blocks<l2_fwd_bf16_kernel<TX, T, ACT, ACTS>>(kWavesA * 64, lds);
+  const int cap = resident_blocks<l2_fwd_bf16_kernel<TX, T, ACT, ACTS, LOGITS>>(kWavesA * 64, lds);
   const int want = static_cast<int>(ceil_div(g.ntiles, kWavesA));
-  hipLaunchKernelGGL((l2_fwd_bf16_kernel<TX, T, ACT, ACTS>), dim3(want < cap ? want : cap), dim3(kWavesA * 64), lds,
+  hipLaunchKernelGGL((l2_fwd_bf16_kernel<TX, T, ACT, ACTS, LOGITS>), dim3(want < cap ? want : cap), dim3(kWavesA * 64), lds,
                      stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, img, g.P, g.Pp, g.K, eps, dist, nb.d, act,
                      nb.a, logits, nb.l);
   return check_launch("l2_fwd_bf16_kernel");
@@ -975,8 +1037,12 @@ int launch_fwd_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, co
   return by_type(x_bf16, terms, act_kind, [&](auto tx, auto tt, auto aa) {
     using TX = std::remove_pointer_t<decltype(tx)>;
     constexpr int kT = decltype(tt)::value, kA = decltype(aa)::value;
-    if (act) return fwd_t<TX, kT, kA, true>(g, nb, x, blk, eps, dist, act, logits, stream);
-    return fwd_t<TX, kT, kA, false>(g, nb, x, blk, eps, dist, act, logits, stream);
+    if (act) {
+      if (logits) return fwd_t<TX, kT, kA, true, true>(g, nb, x, blk, eps, dist, act, logits, stream);
+      return fwd_t<TX, kT, kA, true, false>(g, nb, x, blk, eps, dist, act, logits, stream);
+    }
+    if (logits) return fwd_t<TX, kT, kA, false, true>(g, nb, x, blk, eps, dist, act, logits, stream);
+    return fwd_t<TX, kT, kA, false, false>(g, nb, x, blk, eps, dist, act, logits, stream);
   });
 }
 

@@ -104,6 +104,14 @@ class LayerStep:
                   ctypes.c_void_p(None), ctypes.c_void_p(None), _lib.ptr(self.g_p), _lib.ptr(self.g_w),
                   _lib.ptr(self.ws), self.ws_bytes, self._stream())
 
+    def bwd(self):
+        """One backward call for g_x, g_prototypes and g_last_layer, as the autograd op makes it
+        (ops.l2_backward): one operand-image prep shared by the two backward kernels."""
+        _lib.call("protoseg_l2_bwd", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w, _lib.ptr(self.protos),
+                  self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec, _lib.ptr(self.g_logits),
+                  ctypes.c_void_p(None), _lib.ptr(self.g_x), _lib.ptr(self.g_p), _lib.ptr(self.g_w),
+                  _lib.ptr(self.ws), self.ws_bytes, self._stream())
+
     def allreduce(self, world):
         if world > 1:
             self.grad_flat[: self.P * self.C].copy_(self.g_p.view(-1))
@@ -163,22 +171,26 @@ def capture(fn, stream):
 
 
 def time_layer(step: LayerStep, steps: int, warmup: int, world: int, use_graph: bool):
-    """Times `steps` training steps of the prototype layer (fwd + bwd_x + bwd_pw [+ all-reduce]).
+    """Times `steps` training steps of the prototype layer (fwd + bwd [+ all-reduce]).
 
-    With use_graph the three C-ABI calls of a step are captured once into a HIP graph and each
-    step is one replay (no host launch gaps); the all-reduce stays outside the graph. Per-call
-    device times come from HIP events around one graph per call, replayed on the same stream."""
+    A step is the forward call and one backward call (g_x, g_P, g_W), as the autograd op
+    issues them. With use_graph the step's C-ABI calls are captured once into a HIP graph and
+    each step is one replay (no host launch gaps); the all-reduce stays outside the graph.
+    Per-kernel device times come from HIP events around one graph per kernel family (fwd,
+    bwd_x, bwd_pw: each call there includes its own operand-image prep), replayed on the same
+    stream."""
     names = step.kernel_names()
+    step_calls = [step.fwd, step.bwd]
     calls = [step.fwd, step.bwd_x, step.bwd_pw]
     stream = torch.cuda.Stream(step.device)
     with torch.cuda.stream(stream):
         for _ in range(max(1, warmup)):
-            for c in calls:
+            for c in step_calls + calls:
                 c()
             step.allreduce(world)
         torch.cuda.synchronize()
         if use_graph:
-            g_step = capture(lambda: [c() for c in calls], stream)
+            g_step = capture(lambda: [c() for c in step_calls], stream)
             g_calls = [capture(c, stream) for c in calls]
             run_step = g_step.replay
             run_calls = [g.replay for g in g_calls]
@@ -186,7 +198,7 @@ def time_layer(step: LayerStep, steps: int, warmup: int, world: int, use_graph: 
                 run_step()
                 step.allreduce(world)
         else:
-            run_step = lambda: [c() for c in calls]  # noqa: E731
+            run_step = lambda: [c() for c in step_calls]  # noqa: E731
             run_calls = calls
         torch.cuda.synchronize()
         if world > 1:

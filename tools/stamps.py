@@ -1,8 +1,8 @@
 """Per-wave phase timing of the bf16 prototype-layer kernels from a `make stamps` build.
 
 Run on the GPU box: PROTOSEG_HIP_LIB=<csrc>/build_stamps/libprotoseg_hip.so python3 tools/stamps.py
-Slots (fwd): 0 start, 1 prologue done, 2 x tile ready, 3 first prototype tile done, 4 all
-prototype tiles done, 5 logits stored, 6 end (s_memtime, shader clock); 7 start (s_memrealtime,
+Slots (fwd): 0 start, 1 prologue done, 2 tile 1 started (x ready), 3 tile 1 done, 4 full
+rounds done, 6 end (remainder tiles done) (s_memtime, shader clock); 7 start (s_memrealtime,
 100 MHz, comparable across CUs).
 """
 import ctypes
@@ -49,10 +49,11 @@ def main():
     rt = (st[:, 7] - st[:, 7].min()) * 10  # ns (100 MHz)
     print(f"start (realtime) spread: p0 {np.percentile(rt, 0):.0f} p50 {np.percentile(rt, 50):.0f} "
           f"p90 {np.percentile(rt, 90):.0f} max {rt.max():.0f} ns")
-    names = ["prologue", "x tile", "first p-tile", "rest p-tiles", "logits st", "tail/end"]
+    names = ["prologue", "x tile 1", "tile 1", "rounds 2+", "-", "remainder"]
     for a in range(6):
-        d = st[:, a + 1] - st[:, a]
-        ok = st[:, a + 1] != 0
+        lo, hi = (4, 6) if a == 5 else (a, a + 1)
+        d = st[:, hi] - st[:, lo]
+        ok = (st[:, hi] != 0) & (st[:, lo] != 0)
         d = d[ok]
         if len(d):
             print(f"{names[a]:14s} cycles: p10 {np.percentile(d, 10):8.0f} p50 {np.percentile(d, 50):8.0f} "
