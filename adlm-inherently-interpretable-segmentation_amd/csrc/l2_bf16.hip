@@ -50,7 +50,7 @@ __device__ void stage_p_rows(bf16* img, const float* __restrict__ protos, int P,
   }
 }
 
-// P^T image [T][npt][64 c][32 p-permuted] (CPR 4) — A operand of g_x^T = P^T g_s.
+// (-2 P)^T image [T][npt][64 c][32 p-permuted] (CPR 4) — A operand of g_x^T = -2 P^T g_s.
 template <int T>
 __device__ void stage_pt_perm(bf16* img, const float* __restrict__ protos, int P, int Pp, int tid, int nth) {
   const int plane = Pp * kC;
@@ -60,7 +60,7 @@ __device__ void stage_pt_perm(bf16* img, const float* __restrict__ protos, int P
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
       const int p = pt * 32 + perm_of(e8 * 8 + jj);
-      v[jj] = p < P ? protos[static_cast<size_t>(p) * kC + c] : 0.f;
+      v[jj] = p < P ? -2.f * protos[static_cast<size_t>(p) * kC + c] : 0.f;  // -2 folded in (exact)
     }
     bf16x8 f[T];
     split8<T>(v, f);
@@ -381,6 +381,12 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
   STAMP(6);
 }
 
+// x-backward (layout A): per pixel tile, recompute S and g_act = W^T g_logits^T for every
+// prototype tile, g_s, and g_x^T = (-2 P^T) g_s with the accumulator as B operand (the -2 is
+// folded into the P^T image), plus 2x * sum_p g_s. Rows p >= P need no predicate: their W^T
+// rows and g_dist reads are zero, so g_s = 0 there. Same tile schedule as the forward; the
+// remainder tiles' g_x partials are summed in LDS in a fixed order, 8 registers at a time.
+constexpr int kXPartRegs = 8;
 template <typename TX, int T, int ACT, bool GD>
 __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
     const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const unsigned char* __restrict__ img, int P, int Pp,
@@ -392,6 +398,7 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
   bf16* PTimg = Pimg + T * Pp * kC;                               // [T][npt*64][32]
   bf16* WTimg = PTimg + T * Pp * kC;                              // [T][Pp][32]
   float* p2s = reinterpret_cast<float*>(WTimg + T * Pp * 32);     // [Pp]
+  float* part = p2s + (io.pt - io.p2) / 4;                        // [kWavesA][kXPartRegs + 1][64]
   lds_copy(Pimg, img + io.p, io.wt - io.p);
   lds_copy(PTimg, img + io.pt, io.w - io.pt);
   lds_copy(WTimg, img + io.wt, io.p2 - io.wt);
@@ -404,10 +411,11 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = wave_id();
   const int ntiles = (npix + 31) / 32;
   const int npt = Pp / 32;
-  for (int t = blockIdx.x * kWavesA + wave; t < ntiles; t += gridDim.x * kWavesA) {
-    const unsigned xoff = x_lane_off<TX>(t, ntiles, npix, HW);
-    float raw[kNQ * 8];
-    load_x_raw<TX>(rx, xoff, cs, raw);
+  const TileSchedule sched(ntiles);
+
+  // Prototype tiles pt0, pt0 + dpt, ... of pixel tile t: accumulates this wave's part of
+  // (-2 P^T) g_s into gx and of sum_p g_s into gsum (this half-wave's rows only).
+  auto run_tile = [&](int t, const float (&raw)[kNQ * 8], int pt0, int dpt, f32x16 (&gx)[2], float& gsum) {
     const int g = t * 32 + j;
     const bool valid = g < npix;
     const int b = valid ? g / HW : 0;
@@ -430,11 +438,8 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
     bf16x8 xb[kNQ][T];
     const float x2 = x_frags<T>(raw, xb);
     const unsigned gdbase = valid ? static_cast<unsigned>(((b * P + 4 * h) * HW + n) * 4) : kOOB;
-
-    f32x16 gx[2] = {zero16(), zero16()};
-    float gsum = 0.f;
 #pragma unroll 1
-    for (int pt = 0; pt < npt; ++pt) {
+    for (int pt = pt0; pt < npt; pt += dpt) {
       float gdv[16];  // upstream distance gradient of this tile, loaded before the MFMAs
       if constexpr (GD) {
         const int prem_gd = P - pt * 32 - 4 * h;
@@ -443,15 +448,8 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
           gdv[r] = BufIO<float>::load(rgd, row_of(r) < prem_gd ? gdbase : kOOB,
                                       static_cast<unsigned>((pt * 32 + row_of(r)) * HW * 4));
       }
-      f32x16 acc = zero16();
-#pragma unroll
-      for (int q = 0; q < kNQ; ++q) {
-        bf16x8 pa[T];
-        load_frag<T>(Pimg, Pp * kC, img_off<8>(pt * 32 + j, 2 * q + h), pa);
-        acc = mma_split<T>(pa, xb[q], acc);
-      }
-      // Both class k-steps always run (W^T rows >= K are zero, and g_logits reads as 0 when
-      // absent), so the loop body stays one basic block.
+      f32x16 acc = s_tile<T>(Pimg, Pp, pt, xb);
+      // Both class k-steps always run (W^T rows >= K are zero, g_logits reads 0 when absent).
       f32x16 gacc = zero16();
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -459,25 +457,17 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
         load_frag<T>(WTimg, Pp * 32, img_off<4>(pt * 32 + j, 2 * s + h), wa);
         gacc = mma_split<T>(wa, glb[s], gacc);
       }
-      const int prem = P - pt * 32 - 4 * h;
       float p2r[16];
       load_rows16(p2s + pt * 32 + 4 * h, p2r);
-      auto epilogue = [&](auto full) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float d = l2_distance(x2, p2r[r], acc[r]);
-          const bool pin = decltype(full)::value || row_of(r) < prem;
-          float gd = gacc[r] * act_grad_fast<ACT>(d, eps);  // gacc is 0 without g_logits
-          if constexpr (GD) gd += gdv[r];
-          const float gs = (d > 0.f && pin) ? gd : 0.f;  // relu backward: grad * (out > 0)
-          gsum += gs;
-          acc[r] = -2.f * gs;
-        }
-      };
-      if ((pt + 1) * 32 <= P)
-        epilogue(std::true_type());
-      else
-        epilogue(std::false_type());
+      for (int r = 0; r < 16; ++r) {
+        const float d = l2_distance(x2, p2r[r], acc[r]);
+        float gd = gacc[r] * act_grad_fast<ACT>(d, eps);  // gacc is 0 without g_logits
+        if constexpr (GD) gd += gdv[r];
+        const float gs = d > 0.f ? gd : 0.f;  // relu backward: grad * (out > 0)
+        gsum += gs;
+        acc[r] = gs;
+      }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         bf16x8 gsb[T];
@@ -490,9 +480,10 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
         }
       }
     }
-    gsum += __shfl_xor(gsum, 32);
-    // gx[ct] register 8s+jj is channel chan_of(2ct+s, h, jj) — the channel of raw[(2ct+s)*8+jj].
-    // conv(x^2, ones) backward then pow backward: gsum * (2x); plus the xp branch in gx.
+  };
+  // gx[ct] register 8s+jj is channel chan_of(2ct+s, h, jj) — the channel of raw[(2ct+s)*8+jj].
+  // conv(x^2, ones) backward then pow backward: gsum * (2x); plus the xp branch in gx.
+  auto store_gx = [&](unsigned xoff, const float (&raw)[kNQ * 8], const f32x16 (&gx)[2], float gsum_all) {
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
@@ -500,8 +491,51 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) {
           const int q = 2 * ct + s;
-          BufIO<TX>::store(rgx, gx[ct][8 * s + jj] + gsum * (2.f * raw[q * 8 + jj]), xoff, chan_base(q, jj) * cs);
+          BufIO<TX>::store(rgx, gx[ct][8 * s + jj] + gsum_all * (2.f * raw[q * 8 + jj]), xoff, chan_base(q, jj) * cs);
         }
+  };
+
+  // ---- full rounds
+  for (int t = blockIdx.x * kWavesA + wave; t < sched.full_end; t += gridDim.x * kWavesA) {
+    const unsigned xoff = x_lane_off<TX>(t, ntiles, npix, HW);
+    float raw[kNQ * 8];
+    load_x_raw<TX>(rx, xoff, cs, raw);
+    f32x16 gx[2] = {zero16(), zero16()};
+    float gsum = 0.f;
+    run_tile(t, raw, 0, 1, gx, gsum);
+    store_gx(xoff, raw, gx, gsum + __shfl_xor(gsum, 32));
+  }
+
+  // ---- remainder: one tile per workgroup, prototype tiles split over the waves
+  const int nw = npt < kWavesA ? npt : kWavesA;
+  for (int tt = sched.full_end + static_cast<int>(blockIdx.x); tt < ntiles; tt += gridDim.x) {
+    const unsigned xoff = x_lane_off<TX>(tt, ntiles, npix, HW);
+    float raw[kNQ * 8];
+    load_x_raw<TX>(rx, xoff, cs, raw);
+    f32x16 gx[2] = {zero16(), zero16()};
+    float gsum = 0.f;
+    run_tile(tt, raw, wave, kWavesA, gx, gsum);
+    gsum += __shfl_xor(gsum, 32);
+    float* mine = part + wave * (kXPartRegs + 1) * 64;
+    mine[kXPartRegs * 64 + lane] = gsum;
+    f32x16 tot[2] = {zero16(), zero16()};
+    float gsum_all = 0.f;
+#pragma unroll
+    for (int c8 = 0; c8 < 4; ++c8) {  // registers 8*c8 .. 8*c8+7 of (gx[0] | gx[1])
+#pragma unroll
+      for (int r = 0; r < kXPartRegs; ++r) mine[r * 64 + lane] = gx[c8 >> 1][8 * (c8 & 1) + r];
+      __syncthreads();
+      if (wave == 0) {
+        for (int w = 0; w < nw; ++w) {
+          const float* src = part + w * (kXPartRegs + 1) * 64;
+#pragma unroll
+          for (int r = 0; r < kXPartRegs; ++r) tot[c8 >> 1][8 * (c8 & 1) + r] += src[r * 64 + lane];
+          if (c8 == 0) gsum_all += src[kXPartRegs * 64 + lane];
+        }
+      }
+      __syncthreads();
+    }
+    if (wave == 0) store_gx(xoff, raw, tot, gsum_all);
   }
 }
 
@@ -876,7 +910,8 @@ size_t fwd_lds(const Geometry& g, int terms) {
   return static_cast<size_t>(g.Pp) * terms * (kC + 32) * 2 + p2_pad(g) + static_cast<size_t>(kWavesA) * 16 * 64 * 4;
 }
 size_t bwd_x_lds(const Geometry& g, int terms) {
-  return static_cast<size_t>(g.Pp) * terms * (2 * kC + 32) * 2 + p2_pad(g);
+  return static_cast<size_t>(g.Pp) * terms * (2 * kC + 32) * 2 + p2_pad(g) +
+         static_cast<size_t>(kWavesA) * (kXPartRegs + 1) * 64 * 4;
 }
 size_t pw_lds_for(const Geometry& g, int terms, bool x_bf16, int streams) {
   const size_t stage = x_bf16 ? (terms == 2 ? PwStage<uint16_t, 2>::kBytes : PwStage<uint16_t, 3>::kBytes)
