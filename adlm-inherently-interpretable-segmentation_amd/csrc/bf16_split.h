@@ -150,27 +150,33 @@ template <> struct BufIO<uint16_t> {
   }
 };
 
-// Fast activation for the bf16 family: v_rcp_f32 + v_log_f32 (log2) instead of the IEEE
-// division and the denormal-safe logf sequence. The ratio (d+1)/(d+eps) lies in (1, 1e4],
-// where v_log_f32 is accurate to ~1 ulp.
+// Activations of the bf16 family, with their constant factors folded into the operand images
+// (l2_prep_bf16_kernel) instead of applied per element:
+//   act  = act_unit * act_base(d):   log: ln2 * log2((d+1)/(d+eps))   (ln2 is in the W image)
+//                                    linear: 1 * (-d)
+//   act' = grad_unit * grad_base(d): log: (eps-1) * 1/((d+1)(d+eps))   ((eps-1) is in W^T)
+//                                    linear: -1 * 1                   (-1 is in W^T)
+// v_rcp_f32 + v_log_f32 replace the IEEE division and the denormal-safe logf: the ratio
+// (d+1)/(d+eps) lies in (1, 1e4], where v_log_f32 is accurate to ~1 ulp.
+constexpr float kLn2 = 0.6931471805599453f;
 template <int ACT>
-__device__ __forceinline__ float act_fast(float d, float eps) {
+__device__ __forceinline__ float act_base(float d, float eps) {
   if constexpr (ACT == 0) {
-    const float r = (d + 1.f) * __builtin_amdgcn_rcpf(d + eps);
-    return __builtin_amdgcn_logf(r) * 0.6931471805599453f;
+    return __builtin_amdgcn_logf((d + 1.f) * __builtin_amdgcn_rcpf(d + eps));
   } else {
     return -d;
   }
 }
-// d act / d d ; log: (eps - 1) / ((d + 1)(d + eps))
 template <int ACT>
-__device__ __forceinline__ float act_grad_fast(float d, float eps) {
+__device__ __forceinline__ float act_grad_base(float d, float eps) {
   if constexpr (ACT == 0) {
-    return (eps - 1.f) * __builtin_amdgcn_rcpf((d + 1.f) * (d + eps));
+    return __builtin_amdgcn_rcpf((d + 1.f) * (d + eps));
   } else {
-    return -1.f;
+    return 1.f;
   }
 }
+__host__ __device__ inline float act_unit(int act_kind) { return act_kind == 0 ? kLn2 : 1.f; }
+__host__ __device__ inline float act_grad_unit(int act_kind, float eps) { return act_kind == 0 ? eps - 1.f : -1.f; }
 
 // Channel of k-step q, element jj, half h in the shared channel order of the bf16 family:
 // chan_of(q, h, jj) = 32*(q>>1) + perm_row(q&1, h, jj). With it the x fragments a lane loads

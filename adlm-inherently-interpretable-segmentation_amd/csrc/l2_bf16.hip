@@ -34,8 +34,9 @@ constexpr int kNQ = kC / 16;   // channel k-steps of 16
 constexpr int kWavesA = 8;     // layout-A kernels: 8 waves, one 32-pixel tile each at a time
 constexpr int kLdf = 33;       // padded fp32 staging rows
 
-// P image [T][Pp][64]: row p, chunk 2q+h = channels chan_of(q, h, 0..7) (CPR 8).
-// Operand of S in every kernel: A in layout A (lane = p), B in layout B (lane = p).
+// (-2 P) image [T][Pp][64]: row p, chunk 2q+h = channels chan_of(q, h, 0..7) (CPR 8). Operand
+// of the distance GEMM in every kernel: A in layout A (lane = p), B in layout B (lane = p). The
+// accumulator starts at ||x||^2 + ||p||^2, so d = relu(acc) directly (the -2 scaling is exact).
 template <int T>
 __device__ void stage_p_rows(bf16* img, const float* __restrict__ protos, int P, int Pp, int tid, int nth) {
   const int plane = Pp * kC;
@@ -43,7 +44,8 @@ __device__ void stage_p_rows(bf16* img, const float* __restrict__ protos, int P,
     const int p = idx >> 3, e8 = idx & 7, q = e8 >> 1, h = e8 & 1;
     float v[8];
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) v[jj] = p < P ? protos[static_cast<size_t>(p) * kC + chan_of(q, h, jj)] : 0.f;
+    for (int jj = 0; jj < 8; ++jj)
+      v[jj] = p < P ? -2.f * protos[static_cast<size_t>(p) * kC + chan_of(q, h, jj)] : 0.f;
     bf16x8 f[T];
     split8<T>(v, f);
     store_frag<T>(img, plane, img_off<8>(p, e8), f);
@@ -68,9 +70,10 @@ __device__ void stage_pt_perm(bf16* img, const float* __restrict__ protos, int P
   }
 }
 
-// W image [T][npt][32 k][32 p-permuted] (CPR 4) — A operand of logits = W . act.
+// (act_unit W) image [T][npt][32 k][32 p-permuted] (CPR 4) — A operand of logits = W . act.
 template <int T>
-__device__ void stage_w_perm(bf16* img, const float* __restrict__ w, int K, int P, int Pp, int tid, int nth) {
+__device__ void stage_w_perm(bf16* img, const float* __restrict__ w, int K, int P, int Pp, float scale, int tid,
+                             int nth) {
   const int plane = Pp * 32;
   for (int idx = tid; idx < Pp * 4; idx += nth) {
     const int row = idx >> 2, e8 = idx & 3;  // row = pt*32 + k
@@ -79,7 +82,7 @@ __device__ void stage_w_perm(bf16* img, const float* __restrict__ w, int K, int 
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
       const int p = pt * 32 + perm_of(e8 * 8 + jj);
-      v[jj] = (k < K && p < P) ? w[static_cast<size_t>(k) * P + p] : 0.f;
+      v[jj] = (k < K && p < P) ? scale * w[static_cast<size_t>(k) * P + p] : 0.f;
     }
     bf16x8 f[T];
     split8<T>(v, f);
@@ -87,10 +90,11 @@ __device__ void stage_w_perm(bf16* img, const float* __restrict__ w, int K, int 
   }
 }
 
-// W^T image [T][Pp][32 k] natural classes (CPR 4) — operand of g_act: A in layout A
+// (grad_unit W)^T image [T][Pp][32 k] natural classes (CPR 4) — operand of g_act: A in layout A
 // (lane = p), B in layout B (lane = p).
 template <int T>
-__device__ void stage_wt_rows(bf16* img, const float* __restrict__ w, int K, int P, int Pp, int tid, int nth) {
+__device__ void stage_wt_rows(bf16* img, const float* __restrict__ w, int K, int P, int Pp, float scale, int tid,
+                              int nth) {
   const int plane = Pp * 32;
   for (int idx = tid; idx < Pp * 4; idx += nth) {
     const int p = idx >> 2, e8 = idx & 3;
@@ -98,7 +102,7 @@ __device__ void stage_wt_rows(bf16* img, const float* __restrict__ w, int K, int
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
       const int k = e8 * 8 + jj;
-      v[jj] = (k < K && p < P) ? w[static_cast<size_t>(k) * P + p] : 0.f;
+      v[jj] = (k < K && p < P) ? scale * w[static_cast<size_t>(k) * P + p] : 0.f;
     }
     bf16x8 f[T];
     split8<T>(v, f);
@@ -154,8 +158,8 @@ __host__ __device__ inline ImgOffsets img_offsets(int Pp, int T) {
 // blockIdx.y selects the image, so the five loops (each a few load round trips) run concurrently.
 template <int T>
 __global__ __launch_bounds__(256) void l2_prep_bf16_kernel(const float* __restrict__ protos, int P, int Pp,
-                                                           const float* __restrict__ w_last, int K,
-                                                           unsigned char* __restrict__ block) {
+                                                           const float* __restrict__ w_last, int K, float w_scale,
+                                                           float wt_scale, unsigned char* __restrict__ block) {
   const ImgOffsets o = img_offsets(Pp, T);
   const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
   switch (blockIdx.y) {
@@ -163,13 +167,13 @@ __global__ __launch_bounds__(256) void l2_prep_bf16_kernel(const float* __restri
       stage_p_rows<T>(reinterpret_cast<bf16*>(block + o.p), protos, P, Pp, tid, nth);
       break;
     case 1:
-      stage_wt_rows<T>(reinterpret_cast<bf16*>(block + o.wt), w_last, w_last ? K : 0, P, Pp, tid, nth);
+      stage_wt_rows<T>(reinterpret_cast<bf16*>(block + o.wt), w_last, w_last ? K : 0, P, Pp, wt_scale, tid, nth);
       break;
     case 2:
       stage_pt_perm<T>(reinterpret_cast<bf16*>(block + o.pt), protos, P, Pp, tid, nth);
       break;
     case 3:
-      stage_w_perm<T>(reinterpret_cast<bf16*>(block + o.w), w_last, w_last ? K : 0, P, Pp, tid, nth);
+      stage_w_perm<T>(reinterpret_cast<bf16*>(block + o.w), w_last, w_last ? K : 0, P, Pp, w_scale, tid, nth);
       break;
     default: {
       float* p2 = reinterpret_cast<float*>(block + o.p2);
@@ -230,11 +234,15 @@ __device__ __forceinline__ float x_frags(const float (&raw)[kNQ * 8], bf16x8 (&x
   return x2 + __shfl_xor(x2, 32);
 }
 
-// S = P . X for prototype tile pt (layout A: rows p, cols the wave's 32 pixels), T-term split.
+// ||x||^2 + ||p||^2 - 2 P . X for prototype tile pt (layout A: rows p, cols the wave's 32
+// pixels): the accumulator starts at x2 + p2 (per element) and the (-2 P) image does the rest.
 template <int T>
-__device__ __forceinline__ f32x16 s_tile(const bf16* Pimg, int Pp, int pt, const bf16x8 (&xb)[kNQ][T]) {
+__device__ __forceinline__ f32x16 s_tile(const bf16* Pimg, int Pp, int pt, const bf16x8 (&xb)[kNQ][T], float x2,
+                                         const float (&p2r)[16]) {
   const int j = threadIdx.x & 31, h = (threadIdx.x & 63) >> 5;
-  f32x16 acc = zero16();
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = x2 + p2r[r];
 #pragma unroll
   for (int q = 0; q < kNQ; ++q) {
     bf16x8 pa[T];
@@ -304,19 +312,20 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
     f32x16 lacc = zero16();
 #pragma unroll 1
     for (int pt = pt0; pt < npt; pt += dpt) {
-      f32x16 acc = s_tile<T>(Pimg, Pp, pt, xb);
-      const int prem = P - pt * 32 - 4 * h;  // rows of this tile (and half) below P
       float p2r[16];
       load_rows16(p2s + pt * 32 + 4 * h, p2r);
+      f32x16 acc = s_tile<T>(Pimg, Pp, pt, xb, x2, p2r);
+      const int prem = P - pt * 32 - 4 * h;  // rows of this tile (and half) below P
       // No branches per element: a null output has a zero-size buffer resource (its stores are
       // dropped), rows past P get an out-of-range offset.
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float d = l2_distance(x2, p2r[r], acc[r]);
+        const float d = __builtin_fmaxf(acc[r], 0.f);  // F.relu (model.py:219)
         const unsigned row_ok = row_of(r) < prem ? 0u : kOOB;
         BufIO<float>::store(rd, d, dbase | row_ok, static_cast<unsigned>((pt * 32 + row_of(r)) * HW * 4));
-        const float a = act_fast<ACT>(d, eps);
-        if constexpr (ACTS) BufIO<float>::store(ra, a, abase | row_ok, static_cast<unsigned>((pt * 32 + row_of(r)) * 4));
+        const float a = act_base<ACT>(d, eps);  // act_unit lives in the W image
+        if constexpr (ACTS)
+          BufIO<float>::store(ra, a * act_unit(ACT), abase | row_ok, static_cast<unsigned>((pt * 32 + row_of(r)) * 4));
         acc[r] = a;
       }
       if constexpr (LOGITS) {
@@ -448,7 +457,9 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
           gdv[r] = BufIO<float>::load(rgd, row_of(r) < prem_gd ? gdbase : kOOB,
                                       static_cast<unsigned>((pt * 32 + row_of(r)) * HW * 4));
       }
-      f32x16 acc = s_tile<T>(Pimg, Pp, pt, xb);
+      float p2r[16];
+      load_rows16(p2s + pt * 32 + 4 * h, p2r);
+      f32x16 acc = s_tile<T>(Pimg, Pp, pt, xb, x2, p2r);
       // Both class k-steps always run (W^T rows >= K are zero, g_logits reads 0 when absent).
       f32x16 gacc = zero16();
 #pragma unroll
@@ -457,12 +468,10 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
         load_frag<T>(WTimg, Pp * 32, img_off<4>(pt * 32 + j, 2 * s + h), wa);
         gacc = mma_split<T>(wa, glb[s], gacc);
       }
-      float p2r[16];
-      load_rows16(p2s + pt * 32 + 4 * h, p2r);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float d = l2_distance(x2, p2r[r], acc[r]);
-        float gd = gacc[r] * act_grad_fast<ACT>(d, eps);  // gacc is 0 without g_logits
+        const float d = __builtin_fmaxf(acc[r], 0.f);
+        float gd = gacc[r] * act_grad_base<ACT>(d, eps);  // gacc holds grad_unit * g_act (W^T image)
         if constexpr (GD) gd += gdv[r];
         const float gs = d > 0.f ? gd : 0.f;  // relu backward: grad * (out > 0)
         gsum += gs;
@@ -758,7 +767,9 @@ __global__ __launch_bounds__(MAXT) void l2_bwd_pw_bf16_kernel(
         gdv[r] = BufIO<float>::load(rgd, (ro != kOOB && pvalid) ? ro + pcol : kOOB, 0);
       }
     }
-    f32x16 acc = zero16();
+    f32x16 acc;  // starts at ||x||^2 + ||p||^2; the (-2 P) image does the rest
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = x2r[r] + p2;
 #pragma unroll
     for (int q = 0; q < kNQ; ++q) {
       bf16x8 xa[T], pb[T];
@@ -776,13 +787,13 @@ __global__ __launch_bounds__(MAXT) void l2_bwd_pw_bf16_kernel(
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float d = l2_distance(x2r[r], p2, acc[r]);
-      float gd = gacc[r] * act_grad_fast<ACT>(d, eps);
+      const float d = __builtin_fmaxf(acc[r], 0.f);
+      float gd = gacc[r] * act_grad_base<ACT>(d, eps);  // grad_unit is in the W^T image
       if constexpr (GD) gd += gdv[r];
       const float gs = d > 0.f ? gd : 0.f;
       gsum += gs;
       acc[r] = gs;  // XB holds -2x
-      gacc[r] = act_fast<ACT>(d, eps);
+      gacc[r] = act_base<ACT>(d, eps);  // act_unit is applied to g_W in the slab reduce
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -853,7 +864,7 @@ __global__ __launch_bounds__(MAXT) void l2_bwd_pw_bf16_kernel(
 // thread keeps 8 independent loads in flight.
 __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __restrict__ slab, int S, int P,
                                                                   int Pp, int K, const float* __restrict__ protos,
-                                                                  float* __restrict__ g_protos,
+                                                                  float w_unit, float* __restrict__ g_protos,
                                                                   float* __restrict__ g_w) {
   __shared__ float part[4][64];
   __shared__ float gpart[4][64];
@@ -900,7 +911,7 @@ __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __
   } else {
     const int e2 = e - Pp * kC;
     const int k = e2 / Pp, pp = e2 - k * Pp;
-    if (g_w && k < K && pp < P) g_w[static_cast<size_t>(k) * P + pp] = tot;
+    if (g_w && k < K && pp < P) g_w[static_cast<size_t>(k) * P + pp] = tot * w_unit;  // act = act_unit * act_base
   }
 }
 
@@ -977,7 +988,7 @@ int bwd_pw_launch(const Geometry& g, const Bytes& nb, const void* x, const float
   if (int st = check_launch("l2_bwd_pw_bf16_kernel")) return st;
   const int elems = g.Pp * kC + 32 * g.Pp;
   hipLaunchKernelGGL(l2_bwd_reduce_bf16_kernel, dim3(static_cast<unsigned>(ceil_div(elems, 64))), dim3(256), 0,
-                     stream, ws, grid, g.P, g.Pp, g.K, protos, g_protos, g_logits ? g_w : nullptr);
+                     stream, ws, grid, g.P, g.Pp, g.K, protos, act_unit(ACT), g_protos, g_logits ? g_w : nullptr);
   return check_launch("l2_bwd_reduce_bf16_kernel");
 }
 
@@ -1053,15 +1064,16 @@ size_t bf16_image_bytes(const Geometry& g, int terms) {
   return static_cast<size_t>(img_offsets(g.Pp, terms).total);
 }
 
-int launch_prep_bf16(const Geometry& g, int terms, const float* protos, const float* w_last, void* img,
-                     hipStream_t stream) {
+int launch_prep_bf16(const Geometry& g, int terms, const float* protos, const float* w_last, int act_kind, float eps,
+                     void* img, hipStream_t stream) {
   const int items = g.Pp * 8;  // the largest image loop (P rows x 8 chunks)
   const dim3 grid(static_cast<unsigned>(ceil_div(items, 256)), 5);
   unsigned char* blk = static_cast<unsigned char*>(img);
+  const float ws = act_unit(act_kind), wts = act_grad_unit(act_kind, eps);
   if (terms == 2)
-    hipLaunchKernelGGL(l2_prep_bf16_kernel<2>, grid, dim3(256), 0, stream, protos, g.P, g.Pp, w_last, g.K, blk);
+    hipLaunchKernelGGL(l2_prep_bf16_kernel<2>, grid, dim3(256), 0, stream, protos, g.P, g.Pp, w_last, g.K, ws, wts, blk);
   else
-    hipLaunchKernelGGL(l2_prep_bf16_kernel<3>, grid, dim3(256), 0, stream, protos, g.P, g.Pp, w_last, g.K, blk);
+    hipLaunchKernelGGL(l2_prep_bf16_kernel<3>, grid, dim3(256), 0, stream, protos, g.P, g.Pp, w_last, g.K, ws, wts, blk);
   return check_launch("l2_prep_bf16_kernel");
 }
 

@@ -21,8 +21,9 @@ size_t bf16_bwd_pw_workspace(const Geometry& g);
 // Operand-image block (split P, P^T, W, W^T images and ||p||^2 in the kernels' LDS layout),
 // built once per call by launch_prep_bf16 and shared by the kernels of that call.
 size_t bf16_image_bytes(const Geometry& g, int terms);
-int launch_prep_bf16(const Geometry& g, int terms, const float* protos, const float* w_last, void* img,
-                     hipStream_t stream);
+// act_kind / eps select the constant factors folded into the W and W^T images (bf16_split.h).
+int launch_prep_bf16(const Geometry& g, int terms, const float* protos, const float* w_last, int act_kind, float eps,
+                     void* img, hipStream_t stream);
 
 int launch_fwd_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const void* img, float eps, int act_kind,
                     float* dist, float* act, float* logits, hipStream_t stream);

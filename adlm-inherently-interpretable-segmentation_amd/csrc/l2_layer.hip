@@ -593,7 +593,8 @@ constexpr size_t kImageBlockMin = 512 * 1024;
 
 struct ImageBlock {
   void* ptr = nullptr;
-  int build(const Geometry& g, int terms, const float* protos, const float* w_last, hipStream_t s) {
+  int build(const Geometry& g, int terms, const float* protos, const float* w_last, int act_kind, float eps,
+            hipStream_t s) {
     static std::mutex mu;
     static std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> blocks;
     const size_t need = bf16_image_bytes(g, terms);
@@ -619,7 +620,7 @@ struct ImageBlock {
       }
       ptr = b.first;
     }
-    return launch_prep_bf16(g, terms, protos, w_last, ptr, s);
+    return launch_prep_bf16(g, terms, protos, w_last, act_kind, eps, ptr, s);
   }
 };
 }  // namespace
@@ -640,7 +641,7 @@ extern "C" int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, 
   const int terms = terms_of(precision);
   if (terms && bf16_fwd_fits(geo, terms)) {
     ImageBlock img;
-    if (int st = img.build(geo, terms, protos, logits_out ? w_last : nullptr, s)) return st;
+    if (int st = img.build(geo, terms, protos, logits_out ? w_last : nullptr, act_kind, eps, s)) return st;
     return launch_fwd_bf16(geo, x_dtype == PROTOSEG_BF16, terms, x, img.ptr, eps, act_kind, dist_out, act_out,
                            logits_out, s);
   }
@@ -690,7 +691,7 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
   const bool bf16_pw = (g_protos || g_w) && terms && bf16_bwd_pw_fits(geo, terms);
   ImageBlock img;
   if (bf16_x || bf16_pw)
-    if (int st = img.build(geo, terms, protos, g_logits ? w_last : nullptr, s)) return st;
+    if (int st = img.build(geo, terms, protos, g_logits ? w_last : nullptr, act_kind, eps, s)) return st;
   if (g_x) {
     int st;
     if (bf16_x)
