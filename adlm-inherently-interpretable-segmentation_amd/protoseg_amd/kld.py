@@ -45,7 +45,7 @@ def kld_forward(distances: Tensor, target_img: Tensor, proto_class: Tensor, num_
         raise _lib.ProtosegError(f"target_img has {t.shape[1]} pixels per image, distances {HW}")
     pc = proto_class.to(torch.int32).contiguous()
     lib = _lib.load()
-    ws = torch.empty(lib.protoseg_kld_workspace_size(B, P, num_classes), device=dev, dtype=torch.uint8)
+    ws = torch.empty(lib.protoseg_kld_workspace_size(B, P, HW, num_classes), device=dev, dtype=torch.uint8)
     loss = torch.empty((), device=dev, dtype=torch.float32)
     npairs = torch.empty((), device=dev, dtype=torch.int32)
     with torch.cuda.device(dev):
@@ -57,12 +57,12 @@ def kld_forward(distances: Tensor, target_img: Tensor, proto_class: Tensor, num_
 @kld_forward.register_fake
 def _(distances, target_img, proto_class, num_classes, max_per_class):
     B, P = distances.shape[0], distances.shape[1]
-    n = _lib.load().protoseg_kld_workspace_size(B, P, num_classes)
+    n = _lib.load().protoseg_kld_workspace_size(B, P, distances[0, 0].numel(), num_classes)
     return (distances.new_empty((), dtype=torch.float32), distances.new_empty((), dtype=torch.int32),
             distances.new_empty((n,), dtype=torch.uint8))
 
 
-@torch.library.custom_op("protoseg::kld_backward", mutates_args=(), device_types="cuda")
+@torch.library.custom_op("protoseg::kld_backward", mutates_args=("workspace",), device_types="cuda")
 def kld_backward(distances: Tensor, target_img: Tensor, proto_class: Tensor, num_classes: int, max_per_class: int,
                  workspace: Tensor, g_loss: Tensor) -> Tensor:
     """d(g_loss * loss) / d distances, dense, shaped like ``distances``."""

@@ -112,6 +112,39 @@ class LayerStep:
                   ctypes.c_void_p(None), _lib.ptr(self.g_x), _lib.ptr(self.g_p), _lib.ptr(self.g_w),
                   _lib.ptr(self.ws), self.ws_bytes, self._stream())
 
+    # ---- KLD training step (BASELINE configs[2], cityscapes_kld_imnet: loss_weight_kld = 0.25) ----
+    def setup_kld(self, seed, weight=0.25):
+        gen = torch.Generator(device="cpu").manual_seed(seed + 1)
+        blocks = torch.randint(0, self.K + 1, (self.B, (self.h + 7) // 8, (self.w + 7) // 8), generator=gen)
+        tgt = blocks.repeat_interleave(8, 1).repeat_interleave(8, 2)[:, :self.h, :self.w]
+        self.target = tgt.reshape(self.B, -1).contiguous().to(self.device)  # resized labels, 0 = void
+        per = self.P // self.K
+        self.proto_class = torch.clamp(torch.arange(self.P) // per, max=self.K - 1).to(torch.int32).to(self.device)
+        self.mpc = int(torch.bincount(self.proto_class.cpu().long()).max())
+        lib = _lib.load()
+        self.kld_ws_bytes = lib.protoseg_kld_workspace_size(self.B, self.P, self.h * self.w, self.K)
+        self.kld_ws = torch.empty(self.kld_ws_bytes, device=self.device, dtype=torch.uint8)
+        self.kld_loss = torch.empty((), device=self.device, dtype=torch.float32)
+        self.kld_gloss = torch.full((), weight, device=self.device, dtype=torch.float32)
+        self.g_dist = torch.empty_like(self.dist)
+
+    def kld_fwd(self):
+        _lib.call("protoseg_kld_forward", _lib.ptr(self.dist), self.B, self.P, self.h * self.w, _lib.ptr(self.target),
+                  _lib.I64, _lib.ptr(self.proto_class), self.K, self.mpc, _lib.ptr(self.kld_loss), ctypes.c_void_p(None),
+                  _lib.ptr(self.kld_ws), self.kld_ws_bytes, self._stream())
+
+    def kld_bwd(self):
+        _lib.call("protoseg_kld_backward", _lib.ptr(self.dist), self.B, self.P, self.h * self.w, _lib.ptr(self.target),
+                  _lib.I64, _lib.ptr(self.proto_class), self.K, self.mpc, _lib.ptr(self.kld_gloss),
+                  _lib.ptr(self.kld_ws), self.kld_ws_bytes, _lib.ptr(self.g_dist), self._stream())
+
+    def bwd_gd(self):
+        """Backward with the KLD distance gradient (protoseg_l2_bwd g_dist)."""
+        _lib.call("protoseg_l2_bwd", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w, _lib.ptr(self.protos),
+                  self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec, _lib.ptr(self.g_logits),
+                  _lib.ptr(self.g_dist), _lib.ptr(self.g_x), _lib.ptr(self.g_p), _lib.ptr(self.g_w),
+                  _lib.ptr(self.ws), self.ws_bytes, self._stream())
+
     def allreduce(self, world):
         if world > 1:
             self.grad_flat[: self.P * self.C].copy_(self.g_p.view(-1))
@@ -228,6 +261,47 @@ def time_layer(step: LayerStep, steps: int, warmup: int, world: int, use_graph: 
     return elapsed, {n: float(np.mean(v)) for n, v in per_kernel.items()}
 
 
+def time_kld_step(step: LayerStep, steps: int, warmup: int):
+    """BASELINE configs[2] step on one GPU: forward, KLD loss (module.py:167-208) forward and
+    backward, layer backward with g_logits and the KLD g_dist, as one HIP graph per step.
+    Returns ms per step and the per-launch event times of the two KLD calls."""
+    calls = [step.fwd, step.kld_fwd, step.kld_bwd, step.bwd_gd]
+    stream = torch.cuda.Stream(step.device)
+    with torch.cuda.stream(stream):
+        for _ in range(max(1, warmup)):
+            for c in calls:
+                c()
+        torch.cuda.synchronize()
+        g = capture(lambda: [c() for c in calls], stream)
+        g_kf, g_kb = capture(step.kld_fwd, stream), capture(step.kld_bwd, stream)
+        for _ in range(warmup):
+            g.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            g.replay()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ms_f, ms_b = [], []
+        for _ in range(steps):
+            ev[0].record(stream)
+            g_kf.replay()
+            ev[1].record(stream)
+            g_kb.replay()
+            ev[2].record(stream)
+            torch.cuda.synchronize()
+            ms_f.append(ev[0].elapsed_time(ev[1]))
+            ms_b.append(ev[1].elapsed_time(ev[2]))
+    loss = float(step.kld_loss)
+    n = step.B * step.h * step.w
+    kb = float(np.mean(ms_b)) * 1e-3
+    return {"workload": "cityscapes_kld_imnet step on 1 GPU: fwd + KLD fwd/bwd (loss_weight_kld 0.25) + bwd with g_dist",
+            "ms_per_step": round(elapsed / steps * 1e3, 4), "img_per_s": round(step.B * steps / elapsed, 1),
+            "kld_forward_ms": round(float(np.mean(ms_f)), 4), "kld_backward_ms": round(kb * 1e3, 4),
+            "kld_backward_gbps": round(n * step.P * 4 / kb / 1e9, 1), "loss": round(loss, 6)}
+
+
 def cpu_layer_baseline(C, h, w, P, K, budget_s):
     """Oracle (op-for-op torch-CPU restatement of model.py) fwd+bwd per image, host threads."""
     from oracle import protoseg_oracle as po
@@ -333,6 +407,7 @@ def main():
     ap.add_argument("--push-images", type=int, default=8)
     ap.add_argument("--push-steps", type=int, default=5)
     ap.add_argument("--no-push", action="store_true")
+    ap.add_argument("--no-kld", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--launch", choices=["graph", "eager"], default="graph",
@@ -355,6 +430,11 @@ def main():
         elapsed = t.item()
     images = args.batch * world * args.steps
     value = images / elapsed
+
+    kld = None
+    if not args.no_kld and world == 1:
+        step.setup_kld(SEED + rank)
+        kld = time_kld_step(step, max(5, args.steps // 4), 3)
 
     push = None
     if not args.no_push:
@@ -394,6 +474,8 @@ def main():
             "roofline": roof,
             "kernels": kernels,
         }
+        if kld is not None:
+            out["kld_step"] = kld
         if push is not None:
             out["push"] = push
         if not args.no_cpu_baseline and world == 1:

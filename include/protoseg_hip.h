@@ -169,21 +169,21 @@ int protoseg_push_merge(const uint64_t* img_keys, int n_img, int64_t first_img,
  *               makes the loss NaN
  *   loss_out    [1] f32 device: mean over pairs of exp(-kld)
  *   npairs_out  [1] int32 device or NULL: number of pairs
- *   workspace   protoseg_kld_workspace_size(B, P, K) bytes; the forward fills it and the
- *               backward of the same inputs reads it
+ *   workspace   protoseg_kld_workspace_size(B, P, HW, K) bytes; the forward fills it and the
+ *               backward of the same inputs reads it (and reuses its scratch part)
  * Backward:
  *   g_loss      [1] f32 device or NULL (= 1): upstream gradient of the loss
  *   g_dist      [B, P, HW] f32 out: d(g_loss * loss)/d dist (overwritten, dense; zero off each
  *               prototype's class pixels) — pass it to protoseg_l2_bwd as g_dist
  */
-size_t protoseg_kld_workspace_size(int B, int P, int K);
+size_t protoseg_kld_workspace_size(int B, int P, int HW, int K);
 int protoseg_kld_forward(const float* dist, int B, int P, int HW, const void* label, int label_dtype,
                          const int32_t* proto_class, int K, int max_per_class, float* loss_out,
                          int32_t* npairs_out, void* workspace, size_t workspace_bytes,
                          protoseg_stream_t stream);
 int protoseg_kld_backward(const float* dist, int B, int P, int HW, const void* label, int label_dtype,
                           const int32_t* proto_class, int K, int max_per_class, const float* g_loss,
-                          const void* workspace, size_t workspace_bytes, float* g_dist,
+                          void* workspace, size_t workspace_bytes, float* g_dist,
                           protoseg_stream_t stream);
 
 #ifdef __cplusplus

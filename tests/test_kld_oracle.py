@@ -88,9 +88,9 @@ def test_kld_abi_validation_without_gpu():
     from protoseg_amd import _lib
     lib = _lib.load()
     null, dummy = ctypes.c_void_p(None), ctypes.c_void_p(256)
-    n = lib.protoseg_kld_workspace_size(32, 190, 19)
+    n = lib.protoseg_kld_workspace_size(32, 190, 4225, 19)
     assert n > 0 and n % 256 == 0
-    assert lib.protoseg_kld_workspace_size(0, 190, 19) == 0
+    assert lib.protoseg_kld_workspace_size(0, 190, 4225, 19) == 0
     st = lib.protoseg_kld_forward(null, 2, 38, 10, dummy, _lib.I64, dummy, 19, 2, dummy, null, dummy, n, null)
     assert st == _lib.ERR_INVALID
     st = lib.protoseg_kld_forward(dummy, 2, 38, 10, dummy, _lib.I64, dummy, 19, 33, dummy, null, dummy, n, null)

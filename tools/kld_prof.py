@@ -1,0 +1,20 @@
+"""Runs the KLD forward/backward at the bench shape (B=32, 65x65, P=190, K=19) a few times, for
+rocprofv3 --kernel-trace --stats."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "adlm-inherently-interpretable-segmentation_amd"))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+import torch  # noqa: E402
+
+dev = torch.device("cuda:0")
+st = bench.LayerStep(32, 64, 65, 65, 190, 19, torch.float32, dev, bench.SEED)
+st.setup_kld(bench.SEED)
+st.fwd()
+for _ in range(10):
+    st.kld_fwd()
+    st.kld_bwd()
+torch.cuda.synchronize()
+print("loss", float(st.kld_loss))
