@@ -47,6 +47,7 @@ SIGNATURES = {
     "protoseg_kld_workspace_size": (_sz, [_i, _i, _i, _i]),
     "protoseg_kld_forward": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _vp, _sz, _vp]),
     "protoseg_kld_backward": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _sz, _vp, _vp]),
+    "protoseg_eval_counts": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _vp, _i, _vp, _vp, _vp]),
 }
 
 

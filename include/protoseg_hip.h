@@ -186,6 +186,26 @@ int protoseg_kld_backward(const float* dist, int B, int P, int HW, const void* l
                           void* workspace, size_t workspace_bytes, float* g_dist,
                           protoseg_stream_t stream);
 
+/*
+ * Segmentation evaluation counts. Replaces segmentation/eval_valid.py:159-197: bilinear upsample
+ * (F.interpolate, align_corners=False) of logits and distances to the label resolution, argmax /
+ * argmin, and the numpy counts per class and per prototype — without materialising the
+ * upsampled tensors. Counts are ADDED to `counts` (zero it once per evaluation run, then call
+ * per batch, as the reference accumulates its Counters).
+ *
+ *   logits      [B, h, w, K] f32 (PPNet.forward's logits, NHWC, model.py:278)
+ *   dist        [B, P, h, w] f32 or NULL (distances, model.py:283): NULL skips the per-prototype counts
+ *   ann         [B, H, W] ann_dtype (PROTOSEG_I64 | I32 | U8): labels after CLS_CONVERT (0 = void),
+ *               or raw ids mapped through `lut` [lut_size] int32 (ids outside -> void)
+ *   proto_class [P] int32 (argmax of prototype_class_identity), required with dist
+ *   counts      [2 + 2K + P] int64 in/out: correct, total, I[K], U[K], per-prototype counts
+ *               (pixels whose nearest prototype is p and whose prediction is p's class)
+ * K <= 64, P <= 4096.
+ */
+int protoseg_eval_counts(const float* logits, const float* dist, int B, int h, int w, int K, int P,
+                         const void* ann, int ann_dtype, int H, int W, const int32_t* lut, int lut_size,
+                         const int32_t* proto_class, int64_t* counts, protoseg_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -101,3 +101,19 @@ def test_kld_abi_validation_without_gpu():
     assert st == _lib.ERR_UNSUPPORTED
     st = lib.protoseg_kld_backward(dummy, 2, 38, 10, dummy, _lib.I64, dummy, 19, 2, null, dummy, 16, dummy, null)
     assert st == _lib.ERR_INVALID and b"workspace" in lib.protoseg_last_error()
+
+
+def test_eval_oracle_metrics_and_abi():
+    """eval_valid.py:216-219 formulas on hand counts; the eval C ABI validates without a GPU."""
+    from oracle import eval_oracle as eo
+    from protoseg_amd import _lib
+    acc, miou, ious = eo.metrics(30, 40, np.array([10, 0, 5]), np.array([20, 0, 10]))
+    assert acc == 75.0 and ious == {0: 50.0, 2: 50.0} and miou == 50.0
+    lib = _lib.load()
+    null, dummy = ctypes.c_void_p(None), ctypes.c_void_p(256)
+    st = lib.protoseg_eval_counts(null, null, 1, 4, 4, 19, 0, dummy, _lib.I64, 8, 8, null, 0, null, dummy, null)
+    assert st == _lib.ERR_INVALID
+    st = lib.protoseg_eval_counts(dummy, dummy, 1, 4, 4, 19, 10, dummy, _lib.I64, 8, 8, null, 0, null, dummy, null)
+    assert st == _lib.ERR_INVALID and b"proto_class" in lib.protoseg_last_error()
+    st = lib.protoseg_eval_counts(dummy, null, 1, 4, 4, 65, 0, dummy, _lib.I64, 8, 8, null, 0, null, dummy, null)
+    assert st == _lib.ERR_UNSUPPORTED
