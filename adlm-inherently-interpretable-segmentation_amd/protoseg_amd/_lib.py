@@ -48,6 +48,11 @@ SIGNATURES = {
     "protoseg_kld_forward": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _vp, _sz, _vp]),
     "protoseg_kld_backward": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _sz, _vp, _vp]),
     "protoseg_eval_counts": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _vp, _i, _vp, _vp, _vp]),
+    "protoseg_resize_label": (_i, [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp]),
+    "protoseg_knn_image_min": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
+    "protoseg_knn_patch_label": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp]),
+    "protoseg_knn_heap_push": (_i, [_vp, _vp, _vp, _i, _i64, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "protoseg_knn_finalize": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
 }
 
 

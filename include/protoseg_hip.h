@@ -206,6 +206,68 @@ int protoseg_eval_counts(const float* logits, const float* dist, int B, int h, i
                          const void* ann, int ann_dtype, int H, int W, const int32_t* lut, int lut_size,
                          const int32_t* proto_class, int64_t* counts, protoseg_stream_t stream);
 
+/*
+ * Label resize with PIL Image.resize(NEAREST) semantics. Replaces segmentation/dataset.py:23-31
+ * (resize_label), used by find_nearest.py:128-130 (void mask of the k-NN search) and by
+ * module.py:145 (KLD targets). out[y, x] = label[sy(y), sx(x)] where the source index follows
+ * PIL's f64 accumulation (start scale/2, += scale per step, truncate): bit-exact to PIL.
+ *   label [n_img, H, W] label_dtype (PROTOSEG_I64 | I32 | U8), mapped through `lut` when given
+ *   out   [n_img, h, w] int32
+ */
+int protoseg_resize_label(const void* label, int label_dtype, int n_img, int H, int W, int h, int w,
+                          const int32_t* lut, int lut_size, int32_t* out, protoseg_stream_t stream);
+
+/*
+ * k-nearest-patch search, step 1 of 3 per batch. Replaces find_nearest.py:132 and 140-145:
+ * per image and prototype, np.amin / first np.argmin of dist + 10e6 * (label == void), the sum
+ * formed in f64 as numpy broadcasts it.
+ *   dist        [n_img, P, h, w] f32 (push_forward distances, find_nearest.py:103-104)
+ *   small_label [n_img, h, w] int32 converted labels at map size (protoseg_resize_label), 0 = void;
+ *               NULL = no void patches
+ *   min_dist    [n_img, P] f64 out;  min_idx [n_img, P] int32 out (flat patch index r * w + c)
+ */
+int protoseg_knn_image_min(const float* dist, int n_img, int P, int h, int w, const int32_t* small_label,
+                           double* min_dist, int32_t* min_idx, protoseg_stream_t stream);
+
+/*
+ * k-NN step 2: label of each winning patch. Replaces find_nearest.py:159-166 and 202-211: the
+ * patch's pixel box int(r * H/h) .. int((r+1) * H/h) (f64) and the label of its pixels
+ * (search_y = converted label - 1): the prototype's class when any pixel has it, else the most
+ * common value (smallest on ties). An empty box yields INT32_MIN (the image is skipped,
+ * find_nearest.py:179-180). Labels outside [-256, 255] after conversion set status bit 0.
+ *   label  [n_img, H, W] label_dtype, raw ids mapped through `lut` when given
+ *   proto_class [P] int32; patch_label [n_img, P] int32 out; status [1] int32 in/out
+ */
+int protoseg_knn_patch_label(const int32_t* min_idx, int n_img, int P, int h, int w, const void* label,
+                             int label_dtype, int H, int W, const int32_t* lut, int lut_size,
+                             const int32_t* proto_class, int32_t* patch_label, int32_t* status,
+                             protoseg_stream_t stream);
+
+/*
+ * k-NN step 3: offers the batch's images, in order, to the per-prototype heaps. Replaces
+ * find_nearest.py:224-230 (heapq.heappush while fewer than k, else heappushpop) with CPython
+ * heapq's exact sift sequence, so ties resolve as the reference's do. Heap state persists across
+ * calls: heap_neg [P, k] f64 (negative distances), heap_label / heap_patch [P, k] int32,
+ * heap_img [P, k] int64 (first_img + image index), heap_size [P] int32 (zero it before the
+ * first batch). k <= 64.
+ */
+int protoseg_knn_heap_push(const double* min_dist, const int32_t* min_idx, const int32_t* patch_label, int n_img,
+                           int64_t first_img, int P, int k, double* heap_neg, int32_t* heap_label,
+                           int32_t* heap_patch, int64_t* heap_img, int32_t* heap_size, protoseg_stream_t stream);
+
+/*
+ * k-NN finalisation and the pruning rule. Replaces find_nearest.py:227-232 (heaps[j].sort(),
+ * [::-1]: ascending distance, stable) and prune.py:35-43: class_count[p] = number of the k
+ * nearest patches labelled with p's class; prune[p] = class_count[p] < prune_threshold.
+ * Outputs [P, k]: out_dist f64, out_label int32, out_img int64, out_patch int32; slots past a
+ * heap's size hold inf / INT32_MIN / -1 / -1.
+ */
+int protoseg_knn_finalize(const double* heap_neg, const int32_t* heap_label, const int32_t* heap_patch,
+                          const int64_t* heap_img, const int32_t* heap_size, int P, int k,
+                          const int32_t* proto_class, int prune_threshold, double* out_dist, int32_t* out_label,
+                          int64_t* out_img, int32_t* out_patch, int32_t* class_count, int32_t* prune,
+                          protoseg_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

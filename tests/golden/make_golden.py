@@ -20,6 +20,7 @@ sys.path.insert(0, ROOT)
 from oracle import protoseg_oracle as po  # noqa: E402
 from oracle import kld_oracle as ko  # noqa: E402
 from oracle import push_oracle as pu  # noqa: E402
+from oracle import knn_oracle as kn  # noqa: E402
 
 SEED = 20220227
 
@@ -83,11 +84,33 @@ def kld_case(B, h, w, P, K, seed):
                 num_classes=np.int64(K), loss=np.float32(loss), n_pairs=np.int64(n_pairs), g_dist=g_dist.numpy())
 
 
+def knn_case(n_img, C, H, W, h, w, P, K, k, seed):
+    """find_nearest.py:87-232 + prune.py:35-43 on l2 distance maps of seeded features; image 4
+    is all void (the 10e6 mask decides alone), image 5 repeats image 1 (exact ties across
+    images: heapq keeps the earlier one)."""
+    dists = []
+    for i in range(n_img):
+        x, protos, _ = po.synthetic_inputs(1, C, h, w, P, K, seed)  # same prototypes every image
+        x = po.synthetic_inputs(1, C, h, w, P, K, seed + 100 + i)[0]
+        dists.append(po.l2_convolution(x, protos[:, :, None, None], torch.ones(P, C, 1, 1))[0].numpy())
+    _, labels = kn.synthetic_search(n_img, 1, 1, 1, H, W, K, seed + 1)
+    labels[4][:] = 0
+    dists[5] = dists[1].copy()
+    labels[5] = labels[1].copy()
+    proto_class = (np.arange(P) * K // P).astype(np.int32)
+    res = kn.find_k_nearest(dists, [y - 1 for y in labels], proto_class, k)
+    pruned = kn.prune_list(res["label"], proto_class, 3)
+    return dict(dist=np.stack(dists), labels=np.stack(labels), proto_class=proto_class, k=np.int64(k),
+                prune_threshold=np.int64(3), out_dist=res["dist"], out_label=res["label"], out_img=res["img"],
+                out_patch=res["patch"], pruned=np.array(pruned, np.int64))
+
+
 CASES = {
     "l2_small": lambda: l2_case(2, 64, 17, 17, 38, 19, SEED),
     "l2_ragged": lambda: l2_case(3, 32, 7, 11, 21, 3, SEED + 7),
     "push_small": lambda: push_case(3, 64, 64, 128, 8, 16, 38, 19, SEED),
     "kld_small": lambda: kld_case(2, 13, 17, 38, 19, SEED + 11),
+    "knn_small": lambda: knn_case(7, 32, 60, 110, 9, 13, 38, 4, 5, SEED + 13),
 }
 
 
