@@ -51,6 +51,13 @@ __device__ __forceinline__ void wave_count(unsigned* counter, int key, bool vali
   }
 }
 
+// Adds the wave's sum of v to counter[key] (one LDS atomic per wave).
+__device__ __forceinline__ void wave_sum_to(unsigned* counter, int key, unsigned v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(&counter[key], v);
+}
+
 // counts (int64): [0] correct, [1] total, [2, 2+K) I, [2+K, 2+2K) U, [2+2K, 2+2K+P) per-prototype.
 template <typename TL>
 __global__ __launch_bounds__(kEvalThreads) void eval_seg_kernel(const float* __restrict__ logits,
@@ -125,6 +132,168 @@ __global__ __launch_bounds__(kEvalThreads) void eval_seg_kernel(const float* __r
     if (s_cnt[i]) atomicAdd(&counts[i], static_cast<unsigned long long>(s_cnt[i]));
 }
 
+// Row-group variant for upsampling (H >= h): every output row y with the same top source row
+// i0 shares the two horizontally interpolated source rows, so a thread (one output column)
+// computes a = w0 * v(i0, j0) + w1 * v(i0, j1) and b = (the same on row i0 + di) once per class
+// / prototype and evaluates h0 * a + h1 * b — torch's expression, term for term — for up to
+// kEvalRows output rows at once: 4 loads per class serve kEvalRows pixels instead of one.
+// Grid: (column tiles, source rows h, images); a group with more rows runs in chunks.
+constexpr int kEvalRows = 8;
+
+template <typename TL>
+__global__ __launch_bounds__(kEvalThreads) void eval_rows_kernel(const float* __restrict__ logits,
+                                                                 const float* __restrict__ dist, int h, int w, int K,
+                                                                 int P, const TL* __restrict__ ann, int H, int W,
+                                                                 const int32_t* __restrict__ lut, int lut_size,
+                                                                 const int32_t* __restrict__ proto_class,
+                                                                 unsigned long long* __restrict__ counts) {
+  __shared__ unsigned s_cnt[2 + 2 * kEvalMaxK + kEvalMaxP];
+  const int ncnt = 2 + 2 * K + (dist ? P : 0);
+  for (int i = threadIdx.x; i < ncnt; i += kEvalThreads) s_cnt[i] = 0u;
+  __syncthreads();
+  const int b = blockIdx.z, i0 = blockIdx.y;
+  const int x = blockIdx.x * kEvalThreads + threadIdx.x;
+  const bool inside = x < W;
+  const float sy = static_cast<float>(h) / static_cast<float>(H);
+  // output rows whose top source row is i0 (monotone in y): a guess, then exact lin_of checks
+  int y0 = static_cast<int>((static_cast<float>(i0) + 0.5f) / sy - 0.5f) - 2;
+  y0 = y0 < 0 ? 0 : y0;
+  while (y0 > 0 && lin_of(sy, y0, h).i0 >= i0) --y0;
+  while (y0 < H && lin_of(sy, y0, h).i0 < i0) ++y0;
+  int y1 = y0;
+  while (y1 < H && lin_of(sy, y1, h).i0 == i0) ++y1;
+  const int di = i0 < h - 1 ? 1 : 0;
+  const Lin lx = lin_of(static_cast<float>(w) / static_cast<float>(W), inside ? x : 0, w);
+  const int c0 = lx.i0, c1 = lx.i0 + lx.di;
+  unsigned n_hit = 0, n_lab = 0;
+  for (int ya = y0; ya < y1; ya += kEvalRows) {
+    const int nr = y1 - ya < kEvalRows ? y1 - ya : kEvalRows;
+    float l0[kEvalRows], l1[kEvalRows];
+#pragma unroll
+    for (int r = 0; r < kEvalRows; ++r) {
+      const Lin ly = lin_of(sy, r < nr ? ya + r : ya, h);
+      l0[r] = ly.l0;
+      l1[r] = ly.l1;
+    }
+    int pred[kEvalRows];
+    {
+      // wave-uniform class base + 32-bit per-lane offsets; next class prefetched
+      const float* lb = logits + static_cast<size_t>(b) * h * w * K;
+      const unsigned q00 = static_cast<unsigned>((i0 * w + c0) * K), q01 = static_cast<unsigned>((i0 * w + c1) * K);
+      const unsigned q10 = static_cast<unsigned>(((i0 + di) * w + c0) * K);
+      const unsigned q11 = static_cast<unsigned>(((i0 + di) * w + c1) * K);
+      float best[kEvalRows];
+      float u00 = lb[q00], u01 = lb[q01], u10 = lb[q10], u11 = lb[q11];
+      {
+        const float a = lx.l0 * u00 + lx.l1 * u01;
+        const float bb = lx.l0 * u10 + lx.l1 * u11;
+#pragma unroll
+        for (int r = 0; r < kEvalRows; ++r) {
+          best[r] = l0[r] * a + l1[r] * bb;
+          pred[r] = 0;
+        }
+      }
+      if (K > 1) {
+        u00 = lb[q00 + 1];
+        u01 = lb[q01 + 1];
+        u10 = lb[q10 + 1];
+        u11 = lb[q11 + 1];
+      }
+      for (int k = 1; k < K; ++k) {
+        const float a = lx.l0 * u00 + lx.l1 * u01;
+        const float bb = lx.l0 * u10 + lx.l1 * u11;
+        if (k + 1 < K) {
+          const float* ln = lb + k + 1;
+          u00 = ln[q00];
+          u01 = ln[q01];
+          u10 = ln[q10];
+          u11 = ln[q11];
+        }
+#pragma unroll
+        for (int r = 0; r < kEvalRows; ++r) {
+          const float v = l0[r] * a + l1[r] * bb;
+          if (v > best[r]) {  // torch.argmax: first maximal index
+            best[r] = v;
+            pred[r] = k;
+          }
+        }
+      }
+    }
+    int near[kEvalRows];
+    if (dist) {
+      // wave-uniform plane base + 32-bit per-lane offsets (saddr loads); the next prototype's
+      // four values are loaded before the current one is evaluated
+      const float* db = dist + static_cast<size_t>(b) * P * h * w;
+      const unsigned o00 = static_cast<unsigned>(i0 * w + c0), o01 = static_cast<unsigned>(i0 * w + c1);
+      const unsigned o10 = static_cast<unsigned>((i0 + di) * w + c0), o11 = static_cast<unsigned>((i0 + di) * w + c1);
+      const size_t plane = static_cast<size_t>(h) * w;
+      float best[kEvalRows];
+      float v00 = db[o00], v01 = db[o01], v10 = db[o10], v11 = db[o11];
+      {
+        const float a = lx.l0 * v00 + lx.l1 * v01;
+        const float bb = lx.l0 * v10 + lx.l1 * v11;
+#pragma unroll
+        for (int r = 0; r < kEvalRows; ++r) {
+          best[r] = l0[r] * a + l1[r] * bb;
+          near[r] = 0;
+        }
+      }
+      if (P > 1) {
+        const float* dp = db + plane;
+        v00 = dp[o00];
+        v01 = dp[o01];
+        v10 = dp[o10];
+        v11 = dp[o11];
+      }
+      for (int p = 1; p < P; ++p) {
+        const float a = lx.l0 * v00 + lx.l1 * v01;
+        const float bb = lx.l0 * v10 + lx.l1 * v11;
+        if (p + 1 < P) {
+          const float* dn = db + static_cast<size_t>(p + 1) * plane;
+          v00 = dn[o00];
+          v01 = dn[o01];
+          v10 = dn[o10];
+          v11 = dn[o11];
+        }
+#pragma unroll
+        for (int r = 0; r < kEvalRows; ++r) {
+          const float v = l0[r] * a + l1[r] * bb;
+          if (v < best[r]) {  // torch.argmin: first minimal index
+            best[r] = v;
+            near[r] = p;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kEvalRows; ++r) {
+      if (r >= nr) break;  // nr is block-uniform
+      const int y = ya + r;
+      long long a = 0;
+      if (inside) {
+        a = static_cast<long long>(ann[(static_cast<size_t>(b) * H + y) * W + x]);
+        if (lut) a = (a >= 0 && a < lut_size) ? lut[a] : 0;
+      }
+      const bool labelled = inside && a != 0;
+      const bool hit = labelled && a - 1 == pred[r];
+      n_hit += hit;
+      n_lab += labelled;
+      const int gt = static_cast<int>(a - 1);
+      // keyed counts: one LDS atomic per lane (same-key lanes serialise in the LDS unit; measured
+      // cheaper than a ballot loop over the wave's distinct keys and than per-thread key runs)
+      if (hit) atomicAdd(&s_cnt[2 + pred[r]], 1u);
+      if (labelled) atomicAdd(&s_cnt[2 + K + pred[r]], 1u);
+      if (labelled && gt != pred[r] && gt >= 0 && gt < K) atomicAdd(&s_cnt[2 + K + gt], 1u);
+      if (dist && inside && proto_class[near[r]] == pred[r]) atomicAdd(&s_cnt[2 + 2 * K + near[r]], 1u);
+    }
+  }
+  wave_sum_to(s_cnt, 0, n_hit);
+  wave_sum_to(s_cnt, 1, n_lab);
+  __syncthreads();
+  for (int i = threadIdx.x; i < ncnt; i += kEvalThreads)
+    if (s_cnt[i]) atomicAdd(&counts[i], static_cast<unsigned long long>(s_cnt[i]));
+}
+
 }  // namespace
 
 }  // namespace protoseg
@@ -143,8 +312,28 @@ extern "C" int protoseg_eval_counts(const float* logits, const float* dist, int 
   if (lut && lut_size <= 0) return fail(PROTOSEG_ERR_INVALID, "lut_size must be > 0");
   if (H > 65535 || B > 65535) return fail(PROTOSEG_ERR_UNSUPPORTED, "H=%d / B=%d per call", H, B);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const dim3 grid(static_cast<unsigned>(ceil_div(W, kEvalThreads)), H, B);
   auto* c = reinterpret_cast<unsigned long long*>(counts);
+  if (H >= h && h <= 65535) {  // upsampling: row-group kernel, one workgroup per (column tile, source row)
+    const dim3 grid(static_cast<unsigned>(ceil_div(W, kEvalThreads)), h, B);
+    switch (ann_dtype) {
+      case PROTOSEG_I64:
+        hipLaunchKernelGGL(eval_rows_kernel<int64_t>, grid, dim3(kEvalThreads), 0, s, logits, dist, h, w, K, P,
+                           static_cast<const int64_t*>(ann), H, W, lut, lut_size, proto_class, c);
+        break;
+      case PROTOSEG_I32:
+        hipLaunchKernelGGL(eval_rows_kernel<int32_t>, grid, dim3(kEvalThreads), 0, s, logits, dist, h, w, K, P,
+                           static_cast<const int32_t*>(ann), H, W, lut, lut_size, proto_class, c);
+        break;
+      case PROTOSEG_U8:
+        hipLaunchKernelGGL(eval_rows_kernel<uint8_t>, grid, dim3(kEvalThreads), 0, s, logits, dist, h, w, K, P,
+                           static_cast<const uint8_t*>(ann), H, W, lut, lut_size, proto_class, c);
+        break;
+      default:
+        return fail(PROTOSEG_ERR_UNSUPPORTED, "ann_dtype %d", ann_dtype);
+    }
+    return check_launch("eval_rows_kernel");
+  }
+  const dim3 grid(static_cast<unsigned>(ceil_div(W, kEvalThreads)), H, B);
   switch (ann_dtype) {
     case PROTOSEG_I64:
       hipLaunchKernelGGL(eval_seg_kernel<int64_t>, grid, dim3(kEvalThreads), 0, s, logits, dist, h, w, K, P,

@@ -32,7 +32,6 @@ namespace {
 constexpr int kC = 64;         // channels of the bf16 family
 constexpr int kNQ = kC / 16;   // channel k-steps of 16
 constexpr int kWavesA = 8;     // layout-A kernels: 8 waves, one 32-pixel tile each at a time
-constexpr int kLdf = 33;       // padded fp32 staging rows
 
 // (-2 P) image [T][Pp][64]: row p, chunk 2q+h = channels chan_of(q, h, 0..7) (CPR 8). Operand
 // of the distance GEMM in every kernel: A in layout A (lane = p), B in layout B (lane = p). The

@@ -391,6 +391,95 @@ def cpu_push_baseline(budget_s, C=64, H=1024, W=2048, h=129, w=257, P=190, K=19)
                       f"{H}x{W} labels, {C}x{h}x{w} map, P={P}"}
 
 
+def _timed_calls(run, steps, warmup):
+    """Runs run(ev) `steps` times after `warmup`; returns (wall s per call, mean event s per call
+    of the bracketed kernel). Events are recorded on torch's current stream, which is the stream
+    the C ABI launches on."""
+    for _ in range(warmup):
+        run(None)
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps)]
+    t0 = time.perf_counter()
+    for s in range(steps):
+        run(evs[s])
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps
+    return wall, float(np.mean([e[0].elapsed_time(e[1]) for e in evs])) * 1e-3
+
+
+def time_knn(n_img, steps, warmup, device, H=1024, W=2048, h=129, w=257, P=190, K=19, k=5):
+    """k-NN search (find_nearest.py:87-230) over batches of push_forward distance maps: label
+    resize -> masked f64 image minima -> patch labels -> heap push. The dominant kernel
+    (knn_image_min_kernel) streams the [n, P, h, w] f32 maps once: algorithmic bytes = maps +
+    the int32 small labels."""
+    from protoseg_amd import knn as dknn
+    gen = torch.Generator().manual_seed(SEED + 3)
+    dmaps = (torch.rand(n_img, P, h, w, generator=gen) * 40).to(device)
+    rng = np.random.default_rng(SEED + 3)
+    blocks = rng.integers(0, K + 1, size=(n_img, H // 16, W // 16)).astype(np.uint8)
+    labels = torch.from_numpy(np.repeat(np.repeat(blocks, 16, 1), 16, 2)).to(device)
+    pc = (torch.arange(P) // (P // K)).to(torch.int32).to(device)
+    state = dknn.KnnState.create(P, k, device)
+    small = torch.empty((n_img, h, w), device=device, dtype=torch.int32)
+    min_dist = torch.empty((n_img, P), device=device, dtype=torch.float64)
+    min_idx = torch.empty((n_img, P), device=device, dtype=torch.int32)
+    plab = torch.empty((n_img, P), device=device, dtype=torch.int32)
+    stream = _lib.stream_of(device)
+    null = ctypes.c_void_p(None)
+
+    def run(ev):
+        _lib.call("protoseg_resize_label", _lib.ptr(labels), _lib.U8, n_img, H, W, h, w, null, 0, _lib.ptr(small),
+                  stream)
+        if ev is not None:
+            ev[0].record()
+        _lib.call("protoseg_knn_image_min", _lib.ptr(dmaps), n_img, P, h, w, _lib.ptr(small), _lib.ptr(min_dist),
+                  _lib.ptr(min_idx), stream)
+        if ev is not None:
+            ev[1].record()
+        _lib.call("protoseg_knn_patch_label", _lib.ptr(min_idx), n_img, P, h, w, _lib.ptr(labels), _lib.U8, H, W,
+                  null, 0, _lib.ptr(pc), _lib.ptr(plab), _lib.ptr(state.status), stream)
+        _lib.call("protoseg_knn_heap_push", _lib.ptr(min_dist), _lib.ptr(min_idx), _lib.ptr(plab), n_img, 0, P, k,
+                  _lib.ptr(state.neg), _lib.ptr(state.label), _lib.ptr(state.patch), _lib.ptr(state.img),
+                  _lib.ptr(state.size), stream)
+
+    wall, kern = _timed_calls(run, steps, warmup)
+    nbytes = n_img * (P * h * w * 4 + h * w * 4)
+    return {"ms_per_img": round(wall / n_img * 1e3, 4), "images_per_call": n_img, "k": k,
+            "workload": f"k-NN search: labels {H}x{W} u8, maps {P}x{h}x{w} f32, K={K}",
+            "image_min_kernel_ms_per_img": round(kern / n_img * 1e3, 4),
+            "roofline": roofline_entry(0.0, nbytes, kern) | {"kernel": "knn_image_min_kernel"}}
+
+
+def time_eval(n_img, steps, warmup, device, H=1024, W=2048, h=129, w=257, P=190, K=19):
+    """mIoU evaluation counts (eval_valid.py:159-197) at Cityscapes eval resolution: bilinear
+    upsample + argmax of K logits + argmin of P distances per output pixel, fused. Algorithmic
+    bytes = the low-resolution logits and distances + the u8 labels (each read once)."""
+    gen = torch.Generator().manual_seed(SEED + 5)
+    logits = (torch.randn(n_img, h, w, K, generator=gen) * 3).to(device)
+    dmaps = (torch.rand(n_img, P, h, w, generator=gen) * 40).to(device)
+    rng = np.random.default_rng(SEED + 5)
+    blocks = rng.integers(0, K + 1, size=(n_img, H // 16, W // 16)).astype(np.uint8)
+    anns = torch.from_numpy(np.repeat(np.repeat(blocks, 16, 1), 16, 2)).to(device)
+    pc = (torch.arange(P) // (P // K)).to(torch.int32).to(device)
+    counts = torch.zeros(2 + 2 * K + P, device=device, dtype=torch.int64)
+    stream = _lib.stream_of(device)
+    null = ctypes.c_void_p(None)
+
+    def run(ev):
+        if ev is not None:
+            ev[0].record()
+        _lib.call("protoseg_eval_counts", _lib.ptr(logits), _lib.ptr(dmaps), n_img, h, w, K, P, _lib.ptr(anns),
+                  _lib.U8, H, W, null, 0, _lib.ptr(pc), _lib.ptr(counts), stream)
+        if ev is not None:
+            ev[1].record()
+
+    wall, kern = _timed_calls(run, steps, warmup)
+    nbytes = n_img * ((K + P) * h * w * 4 + H * W)
+    return {"ms_per_img": round(wall / n_img * 1e3, 4), "images_per_call": n_img,
+            "workload": f"eval counts: labels {H}x{W} u8, logits {h}x{w}x{K}, distances {P}x{h}x{w} f32",
+            "roofline": roofline_entry(0.0, nbytes, kern) | {"kernel": "eval_seg_kernel"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -408,6 +497,8 @@ def main():
     ap.add_argument("--push-steps", type=int, default=5)
     ap.add_argument("--no-push", action="store_true")
     ap.add_argument("--no-kld", action="store_true")
+    ap.add_argument("--no-knn", action="store_true")
+    ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--launch", choices=["graph", "eager"], default="graph",
@@ -439,6 +530,12 @@ def main():
     push = None
     if not args.no_push:
         push = time_push(args.push_images, args.push_steps, 1, device)
+
+    knn = evaluation = None
+    if not args.no_knn and world == 1:
+        knn = time_knn(args.push_images, args.push_steps, 1, device)
+    if not args.no_eval and world == 1:
+        evaluation = time_eval(2, 3, 1, device)
 
     if rank == 0:
         work = step.work()
@@ -478,6 +575,10 @@ def main():
             out["kld_step"] = kld
         if push is not None:
             out["push"] = push
+        if knn is not None:
+            out["knn_search"] = knn
+        if evaluation is not None:
+            out["eval"] = evaluation
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_layer_baseline(args.channels, args.fmap, args.fmap, args.protos, args.classes,
                                                      args.cpu_seconds)
