@@ -175,6 +175,24 @@ __device__ __forceinline__ float act_grad_base(float d, float eps) {
     return 1.f;
   }
 }
+// Both at once from one reciprocal (the bwd_pw epilogue needs the pair): with u = d+1 and
+// r = 1/(u(d+eps)), (d+1)/(d+eps) = u*u*r — two multiplies instead of a second v_rcp_f32.
+template <int ACT>
+__device__ __forceinline__ float act_grad_and_base(float d, float eps, float& act) {
+  if constexpr (ACT == 0) {
+    const float u = d + 1.f;
+    const float r = __builtin_amdgcn_rcpf(u * (d + eps));
+    act = __builtin_amdgcn_logf((u * u) * r);
+    return r;
+  } else {
+    act = -d;
+    return 1.f;
+  }
+}
+// F.relu on an accumulator value as one v_med3_f32 (distances are finite, so the FLT_MAX bound
+// never binds). fmaxf(x, 0), or med3 with +inf (folded back to fmaxnum), also emits a NaN-quieting
+// v_max_f32 x, x: IEEE mode cannot prove that an MFMA result is not a signalling NaN.
+__device__ __forceinline__ float relu_f(float x) { return __builtin_amdgcn_fmed3f(x, 0.f, 3.402823466e38f); }
 __host__ __device__ inline float act_unit(int act_kind) { return act_kind == 0 ? kLn2 : 1.f; }
 __host__ __device__ inline float act_grad_unit(int act_kind, float eps) { return act_kind == 0 ? eps - 1.f : -1.f; }
 

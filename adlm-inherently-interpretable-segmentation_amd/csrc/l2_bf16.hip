@@ -309,8 +309,10 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
     const unsigned dbase = valid ? static_cast<unsigned>(((b * P + 4 * h) * HW + n) * 4) : kOOB;
     const unsigned abase = valid ? static_cast<unsigned>((g * P + 4 * h) * 4) : kOOB;
     f32x16 lacc = zero16();
-#pragma unroll 1
-    for (int pt = pt0; pt < npt; pt += dpt) {
+    // Prototype tiles entirely below P store without a row predicate; only the last one (when
+    // P is not a multiple of 32) pays for it. The body is instantiated for both cases.
+    auto proto_tile = [&](int pt, auto full_tag) {
+      constexpr bool kFull = decltype(full_tag)::value;
       float p2r[16];
       load_rows16(p2s + pt * 32 + 4 * h, p2r);
       f32x16 acc = s_tile<T>(Pimg, Pp, pt, xb, x2, p2r);
@@ -319,8 +321,8 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
       // dropped), rows past P get an out-of-range offset.
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float d = __builtin_fmaxf(acc[r], 0.f);  // F.relu (model.py:219)
-        const unsigned row_ok = row_of(r) < prem ? 0u : kOOB;
+        const float d = relu_f(acc[r]);  // F.relu (model.py:219)
+        const unsigned row_ok = (kFull || row_of(r) < prem) ? 0u : kOOB;
         BufIO<float>::store(rd, d, dbase | row_ok, static_cast<unsigned>((pt * 32 + row_of(r)) * HW * 4));
         const float a = act_base<ACT>(d, eps);  // act_unit lives in the W image
         if constexpr (ACTS)
@@ -336,6 +338,14 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
           lacc = mma_split<T>(wa, ab, lacc);
         }
       }
+    };
+    const int npt_full = P / 32;  // tiles whose 32 rows are all below P
+#pragma unroll 1
+    for (int pt = pt0; pt < npt; pt += dpt) {
+      if (pt < npt_full)
+        proto_tile(pt, std::true_type());
+      else
+        proto_tile(pt, std::false_type());
     }
     return lacc;
   };
@@ -469,7 +479,7 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float d = __builtin_fmaxf(acc[r], 0.f);
+        const float d = relu_f(acc[r]);
         float gd = gacc[r] * act_grad_base<ACT>(d, eps);  // gacc holds grad_unit * g_act (W^T image)
         if constexpr (GD) gd += gdv[r];
         const float gs = d > 0.f ? gd : 0.f;  // relu backward: grad * (out > 0)
@@ -786,13 +796,14 @@ __global__ __launch_bounds__(MAXT) void l2_bwd_pw_bf16_kernel(
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float d = __builtin_fmaxf(acc[r], 0.f);
-      float gd = gacc[r] * act_grad_base<ACT>(d, eps);  // grad_unit is in the W^T image
+      const float d = relu_f(acc[r]);
+      float a;
+      float gd = gacc[r] * act_grad_and_base<ACT>(d, eps, a);  // grad_unit is in the W^T image
       if constexpr (GD) gd += gdv[r];
       const float gs = d > 0.f ? gd : 0.f;
       gsum += gs;
       acc[r] = gs;  // XB holds -2x
-      gacc[r] = act_base<ACT>(d, eps);  // act_unit is applied to g_W in the slab reduce
+      gacc[r] = a;  // act_unit is applied to g_W in the slab reduce
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
