@@ -31,7 +31,8 @@ namespace {
 
 constexpr int kC = 64;         // channels of the bf16 family
 constexpr int kNQ = kC / 16;   // channel k-steps of 16
-constexpr int kWavesA = 8;     // layout-A kernels: 8 waves, one 32-pixel tile each at a time
+constexpr int kWavesA = 8;     // x-backward: 8 waves, one 32-pixel tile each at a time
+constexpr int kWavesF = 8;     // forward: 8 waves (12 would need <= 168 VGPRs: 80+ spill today)
 
 // (-2 P) image [T][Pp][64]: row p, chunk 2q+h = channels chan_of(q, h, 0..7) (CPR 8). Operand
 // of the distance GEMM in every kernel: A in layout A (lane = p), B in layout B (lane = p). The
@@ -260,8 +261,8 @@ __device__ __forceinline__ f32x16 s_tile(const bf16* Pimg, int Pp, int pt, const
 // idle for a whole extra round.
 struct TileSchedule {
   int full_end;  // tiles [0, full_end) are done in full rounds
-  __device__ TileSchedule(int ntiles) {
-    const int W = static_cast<int>(gridDim.x) * kWavesA;
+  __device__ TileSchedule(int ntiles, int waves_per_block) {
+    const int W = static_cast<int>(gridDim.x) * waves_per_block;
     full_end = (ntiles / W) * W;
   }
 };
@@ -270,7 +271,7 @@ struct TileSchedule {
 // logits = W . act with the accumulator as B operand. Remainder tiles: see TileSchedule; the
 // per-wave logits partials are summed in LDS in a fixed order (deterministic).
 template <typename TX, int T, int ACT, bool ACTS, bool LOGITS>
-__global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
+__global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
     const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const unsigned char* __restrict__ img, int P, int Pp,
     int K, float eps, float* __restrict__ dist, unsigned d_bytes,
     float* __restrict__ act_out, unsigned a_bytes, float* __restrict__ logits, unsigned l_bytes) {
@@ -281,7 +282,7 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
   bf16* Pimg = reinterpret_cast<bf16*>(smem_raw);                // [T][Pp][64]
   bf16* Wimg = Pimg + T * Pp * kC;                               // [T][Pp][32]
   float* p2s = reinterpret_cast<float*>(Wimg + T * Pp * 32);     // [Pp]
-  float* lpart = p2s + (io.pt - io.p2) / 4;                      // [kWavesA][16][64] remainder logits
+  float* lpart = p2s + (io.pt - io.p2) / 4;                      // [kWavesF][8][64] remainder logits
   lds_copy(Pimg, img + io.p, io.wt - io.p);
   if constexpr (LOGITS) lds_copy(Wimg, img + io.w, io.total - io.w);
   lds_copy(p2s, img + io.p2, io.pt - io.p2);
@@ -294,8 +295,8 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = wave_id();
   const int ntiles = (npix + 31) / 32;
   const int npt = Pp / 32;
-  const int stride = gridDim.x * kWavesA;
-  const TileSchedule sched(ntiles);
+  const int stride = gridDim.x * kWavesF;
+  const TileSchedule sched(ntiles, kWavesF);
 
   // Prototype tiles pt0, pt0 + dpt, ... of pixel tile t (x already in raw); returns the
   // tile's logits accumulator over those prototype tiles.
@@ -358,20 +359,27 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
       BufIO<float>::store(rl, lacc[r], row_of(r) < krem ? lbase : kOOB, static_cast<unsigned>(row_of(r) * 4));
   };
 
-  // ---- full rounds: one tile per wave per round, the next tile's x prefetched into registers
-  int t = blockIdx.x * kWavesA + wave;
+  // ---- full rounds: one tile per wave per round. At 2 waves per SIMD the next tile's x is
+  // prefetched into registers; at 3 the other waves cover the load and the 32 VGPRs go.
+  constexpr bool kPrefetch = kWavesF <= 8;
+  int t = blockIdx.x * kWavesF + wave;
   float raw[kNQ * 8];
-  load_x_raw<TX>(rx, x_lane_off<TX>(t < sched.full_end ? t : ntiles, ntiles, npix, HW), cs, raw);
+  if constexpr (kPrefetch)
+    load_x_raw<TX>(rx, x_lane_off<TX>(t < sched.full_end ? t : ntiles, ntiles, npix, HW), cs, raw);
   for (; t < sched.full_end; t += stride) {
     float cur[kNQ * 8];
+    if constexpr (kPrefetch) {
 #pragma unroll
-    for (int i = 0; i < kNQ * 8; ++i) cur[i] = raw[i];
-    const int tn = t + stride;
-    load_x_raw<TX>(rx, x_lane_off<TX>(tn < sched.full_end ? tn : ntiles, ntiles, npix, HW), cs, raw);
-    if (t == static_cast<int>(blockIdx.x) * kWavesA + wave) STAMP(2);
+      for (int i = 0; i < kNQ * 8; ++i) cur[i] = raw[i];
+      const int tn = t + stride;
+      load_x_raw<TX>(rx, x_lane_off<TX>(tn < sched.full_end ? tn : ntiles, ntiles, npix, HW), cs, raw);
+    } else {
+      load_x_raw<TX>(rx, x_lane_off<TX>(t, ntiles, npix, HW), cs, cur);
+    }
+    if (t == static_cast<int>(blockIdx.x) * kWavesF + wave) STAMP(2);
     const f32x16 lacc = run_tile(t, cur, 0, 1);
     if constexpr (LOGITS) store_logits(t, lacc);
-    if (t == static_cast<int>(blockIdx.x) * kWavesA + wave) STAMP(3);
+    if (t == static_cast<int>(blockIdx.x) * kWavesF + wave) STAMP(3);
   }
   STAMP(4);
 
@@ -379,21 +387,24 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_fwd_bf16_kernel(
   for (int tt = sched.full_end + static_cast<int>(blockIdx.x); tt < ntiles; tt += gridDim.x) {
     float rt[kNQ * 8];
     load_x_raw<TX>(rx, x_lane_off<TX>(tt, ntiles, npix, HW), cs, rt);
-    const f32x16 lacc = run_tile(tt, rt, wave, kWavesA);
-    if constexpr (LOGITS) {
-      float* mine = lpart + wave * 16 * 64;
+    const f32x16 lacc = run_tile(tt, rt, wave, kWavesF);
+    if constexpr (LOGITS) {  // fixed-order sum of the waves' partials, 8 registers at a time
+      const int nw = npt < kWavesF ? npt : kWavesF;
+      float* mine = lpart + wave * 8 * 64;
+      f32x16 sum = zero16();
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mine[r * 64 + lane] = lacc[r];
-      __syncthreads();
-      if (wave == 0) {
-        f32x16 sum = zero16();
-        const int nw = npt < kWavesA ? npt : kWavesA;
-        for (int w = 0; w < nw; ++w)
+      for (int hf = 0; hf < 2; ++hf) {
+        if (wave < nw)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) sum[r] += lpart[(w * 16 + r) * 64 + lane];
-        store_logits(tt, sum);
+          for (int r = 0; r < 8; ++r) mine[r * 64 + lane] = lacc[8 * hf + r];
+        __syncthreads();
+        if (wave == 0)
+          for (int w = 0; w < nw; ++w)
+#pragma unroll
+            for (int r = 0; r < 8; ++r) sum[8 * hf + r] += lpart[(w * 8 + r) * 64 + lane];
+        __syncthreads();
       }
-      __syncthreads();
+      if (wave == 0) store_logits(tt, sum);
     }
   }
   STAMP(6);
@@ -429,7 +440,7 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = wave_id();
   const int ntiles = (npix + 31) / 32;
   const int npt = Pp / 32;
-  const TileSchedule sched(ntiles);
+  const TileSchedule sched(ntiles, kWavesA);
 
   // Prototype tiles pt0, pt0 + dpt, ... of pixel tile t: accumulates this wave's part of
   // (-2 P^T) g_s into gx and of sum_p g_s into gsum (this half-wave's rows only).
@@ -928,7 +939,7 @@ __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __
 // ---- host side ---------------------------------------------------------------------------------
 size_t p2_pad(const Geometry& g) { return (static_cast<size_t>(g.Pp) * 4 + 1023) & ~static_cast<size_t>(1023); }
 size_t fwd_lds(const Geometry& g, int terms) {
-  return static_cast<size_t>(g.Pp) * terms * (kC + 32) * 2 + p2_pad(g) + static_cast<size_t>(kWavesA) * 16 * 64 * 4;
+  return static_cast<size_t>(g.Pp) * terms * (kC + 32) * 2 + p2_pad(g) + static_cast<size_t>(kWavesF) * 8 * 64 * 4;
 }
 size_t bwd_x_lds(const Geometry& g, int terms) {
   return static_cast<size_t>(g.Pp) * terms * (2 * kC + 32) * 2 + p2_pad(g) +
@@ -964,9 +975,9 @@ int fwd_t(const Geometry& g, const Bytes& nb, const void* x, const unsigned char
   const size_t lds = fwd_lds(g, T);
   // Persistent: one generation of resident workgroups; waves stride over the tiles and
   // prefetch their next tile.
-  const int cap = resident_blocks<l2_fwd_bf16_kernel<TX, T, ACT, ACTS, LOGITS>>(kWavesA * 64, lds);
-  const int want = static_cast<int>(ceil_div(g.ntiles, kWavesA));
-  hipLaunchKernelGGL((l2_fwd_bf16_kernel<TX, T, ACT, ACTS, LOGITS>), dim3(want < cap ? want : cap), dim3(kWavesA * 64), lds,
+  const int cap = resident_blocks<l2_fwd_bf16_kernel<TX, T, ACT, ACTS, LOGITS>>(kWavesF * 64, lds);
+  const int want = static_cast<int>(ceil_div(g.ntiles, kWavesF));
+  hipLaunchKernelGGL((l2_fwd_bf16_kernel<TX, T, ACT, ACTS, LOGITS>), dim3(want < cap ? want : cap), dim3(kWavesF * 64), lds,
                      stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, img, g.P, g.Pp, g.K, eps, dist, nb.d, act,
                      nb.a, logits, nb.l);
   return check_launch("l2_fwd_bf16_kernel");
