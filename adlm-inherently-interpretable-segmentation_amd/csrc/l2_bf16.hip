@@ -42,11 +42,15 @@ __device__ void stage_p_rows(bf16* img, const float* __restrict__ protos, int P,
   const int plane = Pp * kC;
   for (int idx = tid; idx < Pp * 8; idx += nth) {
     const int p = idx >> 3, e8 = idx & 7, q = e8 >> 1, h = e8 & 1;
+    const int pc = p < P ? p : P - 1;  // clamped: every load is issued unconditionally
     float v[8];
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj)
-      v[jj] = p < P ? -2.f * protos[static_cast<size_t>(p) * kC + chan_of(q, h, jj)] : 0.f;
+      v[jj] = -2.f * protos[static_cast<size_t>(pc) * kC + chan_of(q, h, jj)];
     bf16x8 f[T];
+    if (p >= P)
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) v[jj] = 0.f;
     split8<T>(v, f);
     store_frag<T>(img, plane, img_off<8>(p, e8), f);
   }
@@ -62,7 +66,8 @@ __device__ void stage_pt_perm(bf16* img, const float* __restrict__ protos, int P
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
       const int p = pt * 32 + perm_of(e8 * 8 + jj);
-      v[jj] = p < P ? -2.f * protos[static_cast<size_t>(p) * kC + c] : 0.f;  // -2 folded in (exact)
+      const float t = -2.f * protos[static_cast<size_t>(p < P ? p : P - 1) * kC + c];  // -2 folded in (exact)
+      v[jj] = p < P ? t : 0.f;
     }
     bf16x8 f[T];
     split8<T>(v, f);
@@ -78,12 +83,14 @@ __device__ void stage_w_perm(bf16* img, const float* __restrict__ w, int K, int 
   for (int idx = tid; idx < Pp * 4; idx += nth) {
     const int row = idx >> 2, e8 = idx & 3;  // row = pt*32 + k
     const int pt = row >> 5, k = row & 31;
-    float v[8];
+    float v[8] = {};
+    if (K > 0)  // w is null iff K = 0 (uniform)
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const int p = pt * 32 + perm_of(e8 * 8 + jj);
-      v[jj] = (k < K && p < P) ? scale * w[static_cast<size_t>(k) * P + p] : 0.f;
-    }
+      for (int jj = 0; jj < 8; ++jj) {
+        const int p = pt * 32 + perm_of(e8 * 8 + jj);
+        const float t = w[static_cast<size_t>(k < K ? k : 0) * P + (p < P ? p : P - 1)];
+        v[jj] = (k < K && p < P) ? scale * t : 0.f;
+      }
     bf16x8 f[T];
     split8<T>(v, f);
     store_frag<T>(img, plane, img_off<4>(row, e8), f);
@@ -98,12 +105,14 @@ __device__ void stage_wt_rows(bf16* img, const float* __restrict__ w, int K, int
   const int plane = Pp * 32;
   for (int idx = tid; idx < Pp * 4; idx += nth) {
     const int p = idx >> 2, e8 = idx & 3;
-    float v[8];
+    float v[8] = {};
+    if (K > 0)  // w is null iff K = 0 (uniform)
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const int k = e8 * 8 + jj;
-      v[jj] = (k < K && p < P) ? scale * w[static_cast<size_t>(k) * P + p] : 0.f;
-    }
+      for (int jj = 0; jj < 8; ++jj) {
+        const int k = e8 * 8 + jj;
+        const float t = w[static_cast<size_t>(k < K ? k : 0) * P + (p < P ? p : P - 1)];
+        v[jj] = (k < K && p < P) ? scale * t : 0.f;
+      }
     bf16x8 f[T];
     split8<T>(v, f);
     store_frag<T>(img, plane, img_off<4>(p, e8), f);
@@ -126,14 +135,14 @@ __device__ __forceinline__ void load_rows16(const float* rows, float (&v)[16]) {
 // ||p||^2 exactly as the f32 family (sequential, no contraction).
 __device__ float proto_norm2_64(const float* __restrict__ protos, int p, bool valid) {
 #pragma clang fp contract(off)
+  const float* row = protos + static_cast<size_t>(valid ? p : 0) * kC;
+  float v[kC];
+#pragma unroll
+  for (int c = 0; c < kC; ++c) v[c] = row[c];  // all loads in flight, then the ordered sum
   float s = 0.f;
-  if (valid) {
-    for (int c = 0; c < kC; ++c) {
-      const float v = protos[static_cast<size_t>(p) * kC + c];
-      s += v * v;
-    }
-  }
-  return s;
+#pragma unroll
+  for (int c = 0; c < kC; ++c) s += v[c] * v[c];
+  return valid ? s : 0.f;
 }
 
 // Operand images of the prototypes and the last layer, built once per call by
