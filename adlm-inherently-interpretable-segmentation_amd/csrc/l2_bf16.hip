@@ -292,11 +292,6 @@ __global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
   bf16* Wimg = Pimg + T * Pp * kC;                               // [T][Pp][32]
   float* p2s = reinterpret_cast<float*>(Wimg + T * Pp * 32);     // [Pp]
   float* lpart = p2s + (io.pt - io.p2) / 4;                      // [kWavesF][8][64] remainder logits
-  lds_copy(Pimg, img + io.p, io.wt - io.p);
-  if constexpr (LOGITS) lds_copy(Wimg, img + io.w, io.total - io.w);
-  lds_copy(p2s, img + io.p2, io.pt - io.p2);
-  __syncthreads();
-  STAMP(1);
 
   const rsrc_t rx = make_rsrc(x, x_bytes), rd = make_rsrc(dist, d_bytes);
   const rsrc_t ra = make_rsrc(act_out, a_bytes), rl = make_rsrc(logits, l_bytes);
@@ -306,6 +301,19 @@ __global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
   const int npt = Pp / 32;
   const int stride = gridDim.x * kWavesF;
   const TileSchedule sched(ntiles, kWavesF);
+
+  // The first tile's x loads are issued before the operand-image DMA, so the barrier's wait
+  // covers both round trips at once instead of one after the other.
+  constexpr bool kPrefetch = kWavesF <= 8;
+  int t = blockIdx.x * kWavesF + wave;
+  float raw[kNQ * 8];
+  if constexpr (kPrefetch)
+    load_x_raw<TX>(rx, x_lane_off<TX>(t < sched.full_end ? t : ntiles, ntiles, npix, HW), cs, raw);
+  lds_copy(Pimg, img + io.p, io.wt - io.p);
+  if constexpr (LOGITS) lds_copy(Wimg, img + io.w, io.total - io.w);
+  lds_copy(p2s, img + io.p2, io.pt - io.p2);
+  __syncthreads();
+  STAMP(1);
 
   // Prototype tiles pt0, pt0 + dpt, ... of pixel tile t (x already in raw); returns the
   // tile's logits accumulator over those prototype tiles.
@@ -370,11 +378,6 @@ __global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
 
   // ---- full rounds: one tile per wave per round. At 2 waves per SIMD the next tile's x is
   // prefetched into registers; at 3 the other waves cover the load and the 32 VGPRs go.
-  constexpr bool kPrefetch = kWavesF <= 8;
-  int t = blockIdx.x * kWavesF + wave;
-  float raw[kNQ * 8];
-  if constexpr (kPrefetch)
-    load_x_raw<TX>(rx, x_lane_off<TX>(t < sched.full_end ? t : ntiles, ntiles, npix, HW), cs, raw);
   for (; t < sched.full_end; t += stride) {
     float cur[kNQ * 8];
     if constexpr (kPrefetch) {
@@ -437,12 +440,6 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
   bf16* WTimg = PTimg + T * Pp * kC;                              // [T][Pp][32]
   float* p2s = reinterpret_cast<float*>(WTimg + T * Pp * 32);     // [Pp]
   float* part = p2s + (io.pt - io.p2) / 4;                        // [kWavesA][kXPartRegs + 1][64]
-  lds_copy(Pimg, img + io.p, io.wt - io.p);
-  lds_copy(PTimg, img + io.pt, io.w - io.pt);
-  lds_copy(WTimg, img + io.wt, io.p2 - io.wt);
-  lds_copy(p2s, img + io.p2, io.pt - io.p2);
-  __syncthreads();
-
   const rsrc_t rx = make_rsrc(x, x_bytes), rg = make_rsrc(g_logits, gl_bytes);
   const rsrc_t rgd = make_rsrc(g_dist, gd_bytes), rgx = make_rsrc(g_x, x_bytes);
   const unsigned cs = static_cast<unsigned>(HW) * sizeof(TX);
@@ -450,6 +447,15 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
   const int ntiles = (npix + 31) / 32;
   const int npt = Pp / 32;
   const TileSchedule sched(ntiles, kWavesA);
+  // The first tile's x loads go out before the operand-image DMA (one combined wait).
+  const int t0 = static_cast<int>(blockIdx.x) * kWavesA + wave;
+  float raw[kNQ * 8];
+  load_x_raw<TX>(rx, x_lane_off<TX>(t0 < sched.full_end ? t0 : ntiles, ntiles, npix, HW), cs, raw);
+  lds_copy(Pimg, img + io.p, io.wt - io.p);
+  lds_copy(PTimg, img + io.pt, io.w - io.pt);
+  lds_copy(WTimg, img + io.wt, io.p2 - io.wt);
+  lds_copy(p2s, img + io.p2, io.pt - io.p2);
+  __syncthreads();
 
   // Prototype tiles pt0, pt0 + dpt, ... of pixel tile t: accumulates this wave's part of
   // (-2 P^T) g_s into gx and of sum_p g_s into gsum (this half-wave's rows only).
@@ -534,10 +540,9 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
   };
 
   // ---- full rounds
-  for (int t = blockIdx.x * kWavesA + wave; t < sched.full_end; t += gridDim.x * kWavesA) {
+  for (int t = t0; t < sched.full_end; t += gridDim.x * kWavesA) {
     const unsigned xoff = x_lane_off<TX>(t, ntiles, npix, HW);
-    float raw[kNQ * 8];
-    load_x_raw<TX>(rx, xoff, cs, raw);
+    if (t != t0) load_x_raw<TX>(rx, xoff, cs, raw);
     f32x16 gx[2] = {zero16(), zero16()};
     float gsum = 0.f;
     run_tile(t, raw, 0, 1, gx, gsum);
