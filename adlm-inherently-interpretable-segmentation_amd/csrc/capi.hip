@@ -1,6 +1,9 @@
 // capi.hip — library-wide C ABI entry points: version and error reporting.
 #include <cstdarg>
 #include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
 
 #include "protoseg_host.h"
 
@@ -24,7 +27,49 @@ int check_launch(const char* what) {
   return PROTOSEG_OK;
 }
 
+namespace {
+std::mutex g_timer_mu;
+std::string g_timer_kernel;
+hipEvent_t g_timer_start = nullptr, g_timer_stop = nullptr;
+}  // namespace
+
+namespace {
+// Eager launches only: under graph capture the hook stays silent (a plain record there would only
+// order streams), so capturing a call with the hook set is harmless.
+hipError_t record(hipEvent_t e, hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return hipErrorNotReady;
+  return hipEventRecord(e, s);
+}
+}  // namespace
+
+KernelTimer::KernelTimer(const char* kernel, hipStream_t s) {
+  std::lock_guard<std::mutex> lock(g_timer_mu);
+  if (!g_timer_start || g_timer_kernel != kernel) return;
+  if (record(g_timer_start, s) == hipSuccess) {
+    stop_ = g_timer_stop;
+    s_ = s;
+  }
+}
+
+KernelTimer::~KernelTimer() {
+  if (stop_) (void)record(stop_, s_);
+}
+
 }  // namespace protoseg
+
+extern "C" int protoseg_timing_events(const char* kernel, void* start_event, void* stop_event) {
+  std::lock_guard<std::mutex> lock(protoseg::g_timer_mu);
+  if (!kernel || !start_event || !stop_event) {
+    protoseg::g_timer_kernel.clear();
+    protoseg::g_timer_start = protoseg::g_timer_stop = nullptr;
+    return PROTOSEG_OK;
+  }
+  protoseg::g_timer_kernel = kernel;
+  protoseg::g_timer_start = static_cast<hipEvent_t>(start_event);
+  protoseg::g_timer_stop = static_cast<hipEvent_t>(stop_event);
+  return PROTOSEG_OK;
+}
 
 extern "C" int protoseg_version(void) { return 1 * 10000 + 0 * 100 + 0; }
 

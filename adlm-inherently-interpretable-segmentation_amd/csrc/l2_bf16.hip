@@ -991,6 +991,7 @@ int fwd_t(const Geometry& g, const Bytes& nb, const void* x, const unsigned char
   // prefetch their next tile.
   const int cap = resident_blocks<l2_fwd_bf16_kernel<TX, T, ACT, ACTS, LOGITS>>(kWavesF * 64, lds);
   const int want = static_cast<int>(ceil_div(g.ntiles, kWavesF));
+  KernelTimer timer("l2_fwd_bf16_kernel", stream);
   hipLaunchKernelGGL((l2_fwd_bf16_kernel<TX, T, ACT, ACTS, LOGITS>), dim3(want < cap ? want : cap), dim3(kWavesF * 64), lds,
                      stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, img, g.P, g.Pp, g.K, eps, dist, nb.d, act,
                      nb.a, logits, nb.l);
@@ -1004,6 +1005,7 @@ int bwd_x_t(const Geometry& g, const Bytes& nb, const void* x, const unsigned ch
   const size_t lds = bwd_x_lds(g, T);
   const int cap = resident_blocks<l2_bwd_x_bf16_kernel<TX, T, ACT, GD>>(kWavesA * 64, lds);
   const int want = static_cast<int>(ceil_div(g.ntiles, kWavesA));
+  KernelTimer timer("l2_bwd_x_bf16_kernel", stream);
   hipLaunchKernelGGL((l2_bwd_x_bf16_kernel<TX, T, ACT, GD>), dim3(want < cap ? want : cap), dim3(kWavesA * 64), lds,
                      stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, img, g.P, g.Pp, g.K, eps, g_logits, nb.gl,
                      g_dist, nb.gd, static_cast<TX*>(g_x));
@@ -1017,9 +1019,12 @@ int bwd_pw_launch(const Geometry& g, const Bytes& nb, const void* x, const float
   if (int st = ensure_lds<l2_bwd_pw_bf16_kernel<TX, T, ACT, MAXT, GD>>()) return st;
   const int grid = pw_grid(g, streams);
   const int threads = streams * (g.Pp / 32) * 64;
-  hipLaunchKernelGGL((l2_bwd_pw_bf16_kernel<TX, T, ACT, MAXT, GD>), dim3(grid), dim3(threads),
-                     pw_lds(g, T, sizeof(TX) == 2), stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, img, g.P,
-                     g.Pp, g.K, eps, g_logits, nb.gl, g_dist, nb.gd, streams, ws);
+  {
+    KernelTimer timer("l2_bwd_pw_bf16_kernel", stream);
+    hipLaunchKernelGGL((l2_bwd_pw_bf16_kernel<TX, T, ACT, MAXT, GD>), dim3(grid), dim3(threads),
+                       pw_lds(g, T, sizeof(TX) == 2), stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, img,
+                       g.P, g.Pp, g.K, eps, g_logits, nb.gl, g_dist, nb.gd, streams, ws);
+  }
   if (int st = check_launch("l2_bwd_pw_bf16_kernel")) return st;
   const int elems = g.Pp * kC + 32 * g.Pp;
   hipLaunchKernelGGL(l2_bwd_reduce_bf16_kernel, dim3(static_cast<unsigned>(ceil_div(elems, 64))), dim3(256), 0,

@@ -34,6 +34,22 @@ int ensure_lds() {
 
 inline long long ceil_div(long long a, long long b) { return (a + b - 1) / b; }
 
+// Measurement hook (protoseg_timing_events): when events are registered for `kernel`, its
+// launcher records them on the launch stream around that one kernel, so a caller times the
+// kernel alone (not the call's prep / reduce launches) with HIP events, the figure rocprofv3
+// reports per dispatch. The scope is a no-op for every other kernel and when nothing is set.
+class KernelTimer {
+ public:
+  KernelTimer(const char* kernel, hipStream_t s);
+  ~KernelTimer();
+  KernelTimer(const KernelTimer&) = delete;
+  KernelTimer& operator=(const KernelTimer&) = delete;
+
+ private:
+  hipEvent_t stop_ = nullptr;
+  hipStream_t s_ = nullptr;
+};
+
 // Workgroups of `kernel` resident on the whole device at (threads, lds): CUs x blocks per CU
 // from the occupancy calculator (VGPRs and LDS), at least the CU count. Cached per
 // (kernel, threads, lds) of the first call — the launchers use one configuration per shape.

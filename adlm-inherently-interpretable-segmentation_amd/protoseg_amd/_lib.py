@@ -36,6 +36,7 @@ _vp, _i, _f, _sz, _i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c
 SIGNATURES = {
     "protoseg_version": (_i, []),
     "protoseg_last_error": (ctypes.c_char_p, []),
+    "protoseg_timing_events": (_i, [ctypes.c_char_p, _vp, _vp]),
     "protoseg_l2_supported": (_i, [_i, _i, _i]),
     "protoseg_l2_fwd": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _i, _vp, _vp, _vp, _vp]),
     "protoseg_l2_bwd_workspace_size": (_sz, [_i, _i, _i, _i, _i, _i]),

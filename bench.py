@@ -209,9 +209,8 @@ def time_layer(step: LayerStep, steps: int, warmup: int, world: int, use_graph: 
     A step is the forward call and one backward call (g_x, g_P, g_W), as the autograd op
     issues them. With use_graph the step's C-ABI calls are captured once into a HIP graph and
     each step is one replay (no host launch gaps); the all-reduce stays outside the graph.
-    Per-kernel device times come from HIP events around one graph per kernel family (fwd,
-    bwd_x, bwd_pw: each call there includes its own operand-image prep), replayed on the same
-    stream."""
+    Per-kernel device times come from HIP events the library records around the named kernel
+    alone (protoseg_timing_events) during eager calls on the same stream."""
     names = step.kernel_names()
     step_calls = [step.fwd, step.bwd]
     calls = [step.fwd, step.bwd_x, step.bwd_pw]
@@ -224,15 +223,12 @@ def time_layer(step: LayerStep, steps: int, warmup: int, world: int, use_graph: 
         torch.cuda.synchronize()
         if use_graph:
             g_step = capture(lambda: [c() for c in step_calls], stream)
-            g_calls = [capture(c, stream) for c in calls]
             run_step = g_step.replay
-            run_calls = [g.replay for g in g_calls]
             for _ in range(warmup):
                 run_step()
                 step.allreduce(world)
         else:
             run_step = lambda: [c() for c in step_calls]  # noqa: E731
-            run_calls = calls
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -245,19 +241,24 @@ def time_layer(step: LayerStep, steps: int, warmup: int, world: int, use_graph: 
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
-        # per-call device time: events on this stream around each call's graph
-        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
-        for s in range(steps):
-            e = ev[s]
-            e[0].record(stream)
-            for i, rc in enumerate(run_calls):
-                rc()
-                e[i + 1].record(stream)
+        # per-kernel device time: the library records a start/stop event pair around the one
+        # named kernel (protoseg_timing_events) of an eager call on this stream, so the figure
+        # is the kernel alone, as rocprofv3 reports it (not the call's prep / reduce launches).
+        lib = _lib.load()
+        per_kernel = {n: [] for n in names}
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        for ev in e:
+            ev.record(stream)  # creates the HIP events
         torch.cuda.synchronize()
-    per_kernel = {n: [] for n in names}
-    for e in ev:
-        for i, n in enumerate(names):
-            per_kernel[n].append(e[i].elapsed_time(e[i + 1]) * 1e-3)
+        for n, c in zip(names, calls):
+            lib.protoseg_timing_events(n.encode(), ctypes.c_void_p(e[0].cuda_event), ctypes.c_void_p(e[1].cuda_event))
+            try:
+                for _ in range(steps):
+                    c()
+                    torch.cuda.synchronize()
+                    per_kernel[n].append(e[0].elapsed_time(e[1]) * 1e-3)
+            finally:
+                lib.protoseg_timing_events(None, None, None)
     return elapsed, {n: float(np.mean(v)) for n, v in per_kernel.items()}
 
 
@@ -477,7 +478,7 @@ def time_eval(n_img, steps, warmup, device, H=1024, W=2048, h=129, w=257, P=190,
     nbytes = n_img * ((K + P) * h * w * 4 + H * W)
     return {"ms_per_img": round(wall / n_img * 1e3, 4), "images_per_call": n_img,
             "workload": f"eval counts: labels {H}x{W} u8, logits {h}x{w}x{K}, distances {P}x{h}x{w} f32",
-            "roofline": roofline_entry(0.0, nbytes, kern) | {"kernel": "eval_seg_kernel"}}
+            "roofline": roofline_entry(0.0, nbytes, kern) | {"kernel": "eval_rows_kernel"}}
 
 
 def main():

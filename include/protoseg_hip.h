@@ -56,6 +56,14 @@ enum protoseg_precision { PROTOSEG_PREC_BF16X3 = 0, PROTOSEG_PREC_BF16X6 = 1, PR
 int protoseg_version(void);                 /* MAJOR*10000 + MINOR*100 + PATCH */
 const char* protoseg_last_error(void);      /* thread-local text of the last failure */
 
+/* Measurement only (no reference counterpart): while set, every launch of the kernel named
+ * `kernel` (e.g. "l2_bwd_pw_bf16_kernel") is bracketed by hipEventRecord(start_event) /
+ * hipEventRecord(stop_event) on its launch stream, so a caller (bench.py) times that kernel
+ * alone, as rocprofv3 does, instead of the whole call. The events are caller-owned
+ * hipEvent_t handles; eager launches only (silent under graph capture). A null argument
+ * clears the hook. */
+int protoseg_timing_events(const char* kernel, void* start_event, void* stop_event);
+
 /*
  * Prototype layer forward. Replaces model.py:203-221 (_l2_convolution), 231-237
  * (distance_2_similarity) and 259-283 (forward_from_conv_features, patch-classification
