@@ -25,9 +25,10 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--precision", default="bf16x3")
     ap.add_argument("--only", default="", help="comma-separated variant names (default: all)")
+    ap.add_argument("--fmap", type=int, default=65, help="feature-map side")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
-    B, C, h, w, P, K = args.batch, 64, 65, 65, args.protos, 19
+    B, C, h, w, P, K = args.batch, 64, args.fmap, args.fmap, args.protos, 19
     gen = torch.Generator().manual_seed(0)
     x = torch.sigmoid(2 * torch.randn(B, C, h, w, generator=gen)).to(dev)
     protos = torch.rand(P, C, generator=gen).to(dev)
@@ -53,6 +54,12 @@ def main():
                                              prec, null, null, P_(logits), s()),
         "fwd_dist_only": lambda: _lib.call("protoseg_l2_fwd", P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 0,
                                            prec, P_(dist), null, null, s()),
+        "fwd_linear": lambda: _lib.call("protoseg_l2_fwd", P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 1,
+                                        prec, P_(dist), null, P_(logits), s()),
+        "bwd_x_linear": lambda: _lib.call("protoseg_l2_bwd", P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 1,
+                                          prec, P_(gl), null, P_(gx), null, null, null, 0, s()),
+        "bwd_pw_linear": lambda: _lib.call("protoseg_l2_bwd", P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 1,
+                                           prec, P_(gl), null, null, P_(gp), P_(gw), P_(ws), ws_b, s()),
         "bwd_x": lambda: _lib.call("protoseg_l2_bwd", P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 0, prec,
                                    P_(gl), null, P_(gx), null, null, null, 0, s()),
         "bwd_pw": lambda: _lib.call("protoseg_l2_bwd", P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 0, prec,
