@@ -200,3 +200,44 @@ def test_cpu_tensors_fail_loudly():
     x, protos, w_last = po.synthetic_inputs(1, 64, 2, 2, 19, 19)
     with pytest.raises((RuntimeError, NotImplementedError)):
         ops.prototype_layer(x, protos, w_last)
+
+
+def test_timing_events_bracket_one_kernel():
+    """protoseg_timing_events (bench.py's roofline timer) brackets the named kernel only: its
+    interval is positive, no longer than the whole call's, and it is silent once cleared."""
+    import ctypes
+
+    from protoseg_amd import _lib
+
+    dev = torch.device("cuda:0")
+    x, protos, w_last = po.synthetic_inputs(8, 64, 33, 33, 190, 19, seed=5)
+    x, protos, w_last = x.to(dev), protos.to(dev), w_last.to(dev)
+    dist = torch.empty(8, 190, 33, 33, device=dev)
+    logits = torch.empty(8, 33, 33, 19, device=dev)
+    lib = _lib.load()
+    stream = _lib.stream_of(dev)
+    null = ctypes.c_void_p(None)
+
+    def fwd():
+        _lib.call("protoseg_l2_fwd", _lib.ptr(x), _lib.F32, 8, 64, 33, 33, _lib.ptr(protos), 190, _lib.ptr(w_last), 19,
+                  1e-4, _lib.ACT_LOG, _lib.PREC_BF16X3, _lib.ptr(dist), null, _lib.ptr(logits), stream)
+
+    fwd()
+    k0, k1, c0, c1 = (torch.cuda.Event(enable_timing=True) for _ in range(4))
+    for e in (k0, k1):
+        e.record()
+    torch.cuda.synchronize()
+    assert lib.protoseg_timing_events(b"l2_fwd_bf16_kernel", ctypes.c_void_p(k0.cuda_event),
+                                      ctypes.c_void_p(k1.cuda_event)) == 0
+    try:
+        c0.record()
+        fwd()
+        c1.record()
+        torch.cuda.synchronize()
+    finally:
+        assert lib.protoseg_timing_events(None, None, None) == 0
+    kern, call = k0.elapsed_time(k1), c0.elapsed_time(c1)
+    assert 0.0 < kern <= call, (kern, call)
+    fwd()  # cleared: the kernel events keep their last interval
+    torch.cuda.synchronize()
+    assert k0.elapsed_time(k1) == kern
