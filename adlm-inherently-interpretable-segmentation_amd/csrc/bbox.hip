@@ -1,0 +1,369 @@
+// bbox.hip — high-activation bound boxes of the pushed prototypes on gfx950.
+//
+// Reference: segmentation/push.py:309-353 (inside update_prototypes_on_image) and
+// helpers.py:48-82 (find_continuous_high_activation_crop). Per pushed prototype the reference
+//   1. turns the winning image's distance map into activations (push.py:310-316),
+//   2. cv2.resize(..., INTER_CUBIC) to the full image (push.py:318-319),
+//   3. threshold = np.percentile(upsampled, 95) (push.py:322),
+//   4. multiplies by the ground-truth mask of the prototype's class (push.py:325-326),
+//   5. grows the receptive-field box greedily over pixels >= threshold, then adds a 5-px
+//      margin (push.py:328-329, helpers.py:48-82).
+// Here: act_kernel (1), cubic_upsample_kernel (2: one thread per output pixel, OpenCV's
+// separable H-then-V INTER_CUBIC with A = -0.75, half-pixel centres, replicated border, every
+// product and sum rounded separately as the scalar OpenCV code writes them), and
+// bound_box_kernel (3-5: one 1024-thread workgroup per prototype map — an LDS radix select of
+// the two order statistics numpy's 'linear' percentile interpolates between, in numpy's f32
+// arithmetic, then the greedy walk with every row/column probe a workgroup-wide OR).
+#include "protoseg_device.h"
+#include "protoseg_host.h"
+
+// The restated arithmetic rounds every product and sum separately: no FMA contraction in this
+// file (the pragma, plus -ffp-contract=off for bbox.o in the Makefile; HIP's __fmul_rn et al.
+// are header inlines that the default fast contraction would still fuse).
+#pragma clang fp contract(off)
+
+namespace protoseg {
+
+namespace {
+
+constexpr int kBoxThreads = 1024;
+constexpr int kUpThreads = 256;
+constexpr int kHistBins = 2048;
+
+__device__ __forceinline__ float fmul(float a, float b) { return a * b; }
+__device__ __forceinline__ float fadd(float a, float b) { return a + b; }
+__device__ __forceinline__ float fsub(float a, float b) { return a - b; }
+
+// OpenCV imgproc resize.cpp interpolateCubic, A = -0.75, f32.
+__device__ __forceinline__ void cubic_coeffs(float x, float c[4]) {
+  const float A = -0.75f;
+  const float x1 = fadd(x, 1.0f);
+  c[0] = fsub(fmul(fadd(fmul(fsub(fmul(A, x1), 5.0f * A), x1), 8.0f * A), x1), 4.0f * A);
+  c[1] = fadd(fmul(fmul(fsub(fmul(A + 2.0f, x), A + 3.0f), x), x), 1.0f);
+  const float omx = fsub(1.0f, x);
+  c[2] = fadd(fmul(fmul(fsub(fmul(A + 2.0f, omx), A + 3.0f), omx), omx), 1.0f);
+  c[3] = fsub(fsub(fsub(1.0f, c[0]), c[1]), c[2]);
+}
+
+// Source taps of output index d: fx = (float)((d + 0.5) * scale - 0.5) in f64 (scale =
+// 1 / (dsize / ssize) as cv::resize forms it), sx = floor(fx), taps sx-1 .. sx+2 clamped.
+__device__ __forceinline__ void cubic_taps(int d, double scale, int n_src, int idx[4], float c[4]) {
+  const float f = static_cast<float>((static_cast<double>(d) + 0.5) * scale - 0.5);
+  const float fl = floorf(f);
+  const int s = static_cast<int>(fl);
+  cubic_coeffs(fsub(f, fl), c);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    int t = s + k - 1;
+    t = t < 0 ? 0 : t;
+    idx[k] = t > n_src - 1 ? n_src - 1 : t;
+  }
+}
+
+// push.py:312-316 on the f32 numpy map: log -> np.log((d + 1) / (d + eps)) (f32 ops; the log
+// rounded from f64), linear -> max_dist - d, identity -> the caller passed activations.
+__global__ __launch_bounds__(256) void act_kernel(const float* __restrict__ dist, size_t n, int kind, float eps,
+                                                  float max_dist, float* __restrict__ act) {
+  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<size_t>(gridDim.x) * blockDim.x) {
+    const float d = dist[i];
+    float a;
+    if (kind == PROTOSEG_ACT_LOG) {
+      const float q = fadd(d, 1.0f) / fadd(d, eps);
+      a = static_cast<float>(log(static_cast<double>(q)));
+    } else if (kind == PROTOSEG_ACT_LINEAR) {
+      a = fsub(max_dist, d);
+    } else {
+      a = d;
+    }
+    act[i] = a;
+  }
+}
+
+// grid (ceil(W / 256), H, m): one output row segment of one map per workgroup.
+__global__ __launch_bounds__(kUpThreads) void cubic_upsample_kernel(const float* __restrict__ act, int h, int w,
+                                                                    int H, int W, double scale_y, double scale_x,
+                                                                    float* __restrict__ up) {
+  const int dx = blockIdx.x * kUpThreads + threadIdx.x;
+  const int dy = blockIdx.y;
+  const int map = blockIdx.z;
+  if (dx >= W) return;
+  int xi[4], yi[4];
+  float a[4], b[4];
+  cubic_taps(dx, scale_x, w, xi, a);
+  cubic_taps(dy, scale_y, h, yi, b);
+  const float* S = act + static_cast<size_t>(map) * h * w;
+  float rows[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // HResizeCubic: S[x0]*a0 + S[x1]*a1 + S[x2]*a2 + S[x3]*a3
+    const float* R = S + static_cast<size_t>(yi[k]) * w;
+    rows[k] = fadd(fadd(fadd(fmul(R[xi[0]], a[0]), fmul(R[xi[1]], a[1])), fmul(R[xi[2]], a[2])),
+                   fmul(R[xi[3]], a[3]));
+  }
+  // VResizeCubic: S0*b0 + S1*b1 + S2*b2 + S3*b3
+  const float v = fadd(fadd(fadd(fmul(rows[0], b[0]), fmul(rows[1], b[1])), fmul(rows[2], b[2])),
+                       fmul(rows[3], b[3]));
+  up[(static_cast<size_t>(map) * H + dy) * W + dx] = v;
+}
+
+// Order-preserving f32 <-> u32 (NaN sorts last, as np.sort puts it).
+__device__ __forceinline__ uint32_t fkey(float f) {
+  const uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float fkey_inv(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+struct Select {
+  uint32_t key;    // key of the element of the requested rank
+  uint32_t below;  // elements with a smaller key
+  uint32_t equal;  // elements with this key
+};
+
+// Histogram of the keys matching (prefix, pmask), bin = (key >> sh) & bm. Four float4 loads
+// in flight per thread per iteration; the scalar tail covers n % 4 and unaligned maps.
+__device__ void key_histogram(const float* __restrict__ a, size_t n, uint32_t prefix, uint32_t pmask, int sh,
+                              uint32_t bm, uint32_t* hist) {
+  const int t = threadIdx.x;
+  const bool aligned = (reinterpret_cast<uintptr_t>(a) & 15u) == 0;
+  size_t n4 = aligned ? n / 4 : 0;
+  const float4* a4 = reinterpret_cast<const float4*>(a);
+  auto put = [&](float f) {
+    const uint32_t k = fkey(f);
+    if ((k & pmask) == prefix) atomicAdd(&hist[(k >> sh) & bm], 1u);
+  };
+  size_t i = t;
+  for (; i + 3 * kBoxThreads < n4; i += 4 * kBoxThreads) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = a4[i + u * kBoxThreads];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { put(v[u].x); put(v[u].y); put(v[u].z); put(v[u].w); }
+  }
+  for (; i < n4; i += kBoxThreads) {
+    const float4 v = a4[i];
+    put(v.x); put(v.y); put(v.z); put(v.w);
+  }
+  for (size_t j = n4 * 4 + t; j < n; j += kBoxThreads) put(a[j]);
+}
+
+// Key of the element of rank `rank` (0-based, ascending) of a[0..n): three LDS histogram passes
+// over 11 + 11 + 10 key bits; bins scanned by the whole workgroup (2 bins per thread).
+__device__ Select block_select(const float* __restrict__ a, size_t n, uint32_t rank, uint32_t* hist,
+                               uint32_t* scan, uint32_t* bcast) {
+  const int t = threadIdx.x;
+  uint32_t prefix = 0, pmask = 0, below = 0, equal = 0;
+  const int shifts[3] = {21, 10, 0};
+  const int widths[3] = {11, 11, 10};
+  for (int pass = 0; pass < 3; ++pass) {
+    const int sh = shifts[pass];
+    const uint32_t bm = (1u << widths[pass]) - 1u;
+    for (int i = t; i < kHistBins; i += kBoxThreads) hist[i] = 0u;
+    __syncthreads();
+    key_histogram(a, n, prefix, pmask, sh, bm, hist);
+    __syncthreads();
+    const uint32_t h0 = hist[2 * t], h1 = hist[2 * t + 1];
+    const uint32_t s = h0 + h1;
+    scan[t] = s;
+    __syncthreads();
+    for (int off = 1; off < kBoxThreads; off <<= 1) {
+      const uint32_t v = t >= off ? scan[t - off] : 0u;
+      __syncthreads();
+      scan[t] += v;
+      __syncthreads();
+    }
+    const uint32_t incl = scan[t], excl = incl - s;
+    if (excl <= rank && rank < incl) {
+      const uint32_t r = rank - excl;
+      if (r < h0) {
+        bcast[0] = 2u * t; bcast[1] = excl; bcast[2] = h0;
+      } else {
+        bcast[0] = 2u * t + 1u; bcast[1] = excl + h0; bcast[2] = h1;
+      }
+    }
+    __syncthreads();
+    const uint32_t b = bcast[0];
+    below += bcast[1];
+    rank -= bcast[1];
+    equal = bcast[2];
+    prefix |= b << sh;
+    pmask |= bm << sh;
+    __syncthreads();
+  }
+  return {prefix, below, equal};
+}
+
+// Smallest key strictly above `key` (the next order statistic when `key` is unique).
+__device__ uint32_t block_min_above(const float* __restrict__ a, size_t n, uint32_t key, uint32_t* bcast) {
+  uint32_t m = 0xffffffffu;
+  for (size_t i = threadIdx.x; i < n; i += kBoxThreads) {
+    const uint32_t k = fkey(a[i]);
+    if (k > key && k < m) m = k;
+  }
+  if (threadIdx.x == 0) bcast[3] = 0xffffffffu;
+  __syncthreads();
+  atomicMin(&bcast[3], m);
+  __syncthreads();
+  const uint32_t r = bcast[3];
+  __syncthreads();
+  return r;
+}
+
+template <typename TL>
+__device__ __forceinline__ long long label_value(const TL* L, size_t i, const int32_t* lut, int lut_size) {
+  const long long raw = static_cast<long long>(L[i]);
+  if (!lut) return raw;
+  if (raw < 0 || raw >= lut_size) return -1;
+  return lut[raw];
+}
+
+// grid (m), 1024 threads. rf [m, 4] = (start_h, end_h, start_w, end_w) of push.py:288-294;
+// box [m, 4] = (start_h, end_h + 1, start_w, end_w + 1) of helpers.py:82; -1 rows for maps whose
+// label index or rf box is out of range.
+template <typename TL>
+__global__ __launch_bounds__(kBoxThreads) void bound_box_kernel(
+    const float* __restrict__ up, int H, int W, const TL* __restrict__ label, int n_label, const int32_t* label_index,
+    const int32_t* __restrict__ lut, int lut_size, const int32_t* __restrict__ target_class,
+    const int32_t* __restrict__ rf, float percentile, int margin, float* __restrict__ thr_out,
+    int32_t* __restrict__ box_out) {
+  __shared__ uint32_t hist[kHistBins];
+  __shared__ uint32_t scan[kBoxThreads];
+  __shared__ uint32_t bcast[4];
+  const int map = blockIdx.x;
+  const size_t n = static_cast<size_t>(H) * W;
+  const float* U = up + static_cast<size_t>(map) * n;
+  int sh = rf[4 * map + 0], eh = rf[4 * map + 1], sw = rf[4 * map + 2], ew = rf[4 * map + 3];
+  const int li = label_index ? label_index[map] : 0;
+  if (li < 0 || li >= n_label || sh < 0 || sh >= H || sw < 0 || sw >= W || eh < sh || ew < sw) {
+    if (threadIdx.x < 4) box_out[4 * map + threadIdx.x] = -1;
+    if (threadIdx.x == 0) thr_out[map] = __uint_as_float(0x7fc00000u);
+    return;
+  }
+
+  // push.py:322 np.percentile(upsampled, q): numpy 'linear' on f32 — q / 100 in f32,
+  // virtual index (n - 1) * q in f32, lerp between the two neighbouring order statistics with
+  // numpy's _lerp (a + (b - a) * g, or b - (b - a) * (1 - g) when g >= 0.5), all f32.
+  const float qq = percentile / 100.0f;
+  const float vidx = fmul(static_cast<float>(n - 1), qq);
+  uint32_t lo, hi;
+  if (vidx >= static_cast<float>(n - 1)) {
+    lo = hi = static_cast<uint32_t>(n - 1);
+  } else {
+    const float fl = floorf(vidx < 0.f ? 0.f : vidx);
+    lo = static_cast<uint32_t>(fl);
+    hi = lo + 1u;
+  }
+  const float g = vidx < 0.f ? 0.f : fsub(vidx, floorf(vidx));
+  const Select s = block_select(U, n, lo, hist, scan, bcast);
+  uint32_t key_hi = s.key;
+  if (hi != lo && hi >= s.below + s.equal) key_hi = block_min_above(U, n, s.key, bcast);
+  const float A = fkey_inv(s.key), B = fkey_inv(key_hi);
+  const float diff = fsub(B, A);
+  const float thr = g >= 0.5f ? fsub(B, fmul(diff, fsub(1.0f, g))) : fadd(A, fmul(diff, g));
+
+  // push.py:325-326 upsampled * (img_y == target_class + 1); helpers.py:51 mask = map >= thr.
+  const TL* L = label + static_cast<size_t>(li) * n;
+  const long long cls = static_cast<long long>(target_class[map]) + 1;
+  auto hit = [&](int r, int c) -> bool {
+    const size_t i = static_cast<size_t>(r) * W + c;
+    const float u = U[i];
+    const float v = label_value(L, i, lut, lut_size) == cls ? u : fmul(u, 0.0f);
+    return v >= thr;
+  };
+  auto row_any = [&](int r, int c0, int c1) -> bool {  // np.amax(mask[r, c0:c1]) > 0.5
+    c1 = c1 > W ? W : c1;
+    bool f = false;
+    for (int c = c0 + static_cast<int>(threadIdx.x); c < c1; c += kBoxThreads) f = f || hit(r, c);
+    return __syncthreads_or(f) != 0;
+  };
+  auto col_any = [&](int c, int r0, int r1) -> bool {  // np.amax(mask[r0:r1, c]) > 0.5
+    r1 = r1 > H ? H : r1;
+    bool f = false;
+    for (int r = r0 + static_cast<int>(threadIdx.x); r < r1; r += kBoxThreads) f = f || hit(r, c);
+    return __syncthreads_or(f) != 0;
+  };
+  // helpers.py:53-75: the four sides in order, each re-tested until it fails once.
+  bool st0 = false, st1 = false, st2 = false, st3 = false;
+  while (!(st0 && st1 && st2 && st3)) {
+    if (!st0 && sh > 0 && row_any(sh - 1, sw, ew + 1)) --sh; else st0 = true;
+    if (!st1 && eh < H - 1 && row_any(eh + 1, sw, ew + 1)) ++eh; else st1 = true;
+    if (!st2 && sw > 0 && col_any(sw - 1, sh, eh + 1)) --sw; else st2 = true;
+    if (!st3 && ew < W - 1 && col_any(ew + 1, sh, eh + 1)) ++ew; else st3 = true;
+  }
+  // helpers.py:77-82
+  sh = sh - margin > 0 ? sh - margin : 0;
+  sw = sw - margin > 0 ? sw - margin : 0;
+  eh = eh + margin < H - 1 ? eh + margin : H - 1;
+  ew = ew + margin < W - 1 ? ew + margin : W - 1;
+  if (threadIdx.x == 0) {
+    thr_out[map] = thr;
+    box_out[4 * map + 0] = sh;
+    box_out[4 * map + 1] = eh + 1;
+    box_out[4 * map + 2] = sw;
+    box_out[4 * map + 3] = ew + 1;
+  }
+}
+
+}  // namespace
+
+}  // namespace protoseg
+
+using namespace protoseg;
+
+extern "C" int protoseg_act_upsample(const float* dist, int m, int h, int w, int H, int W, int act_kind, float eps,
+                                     float max_dist, float* act, float* up, protoseg_stream_t stream) {
+  if (!dist || !act || !up) return fail(PROTOSEG_ERR_INVALID, "dist, act and up must be non-null");
+  if (m <= 0 || h <= 0 || w <= 0 || H <= 0 || W <= 0)
+    return fail(PROTOSEG_ERR_INVALID, "bad shape m=%d h=%d w=%d H=%d W=%d", m, h, w, H, W);
+  if (m > 65535 || H > 65535) return fail(PROTOSEG_ERR_UNSUPPORTED, "m=%d H=%d above the grid limit", m, H);
+  if (act_kind < PROTOSEG_ACT_LOG || act_kind > PROTOSEG_ACT_IDENTITY)
+    return fail(PROTOSEG_ERR_INVALID, "act_kind %d", act_kind);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const size_t n = static_cast<size_t>(m) * h * w;
+  const int blocks = static_cast<int>(ceil_div(static_cast<long long>(n), 256) < 4096 ? ceil_div(n, 256) : 4096);
+  hipLaunchKernelGGL(act_kernel, dim3(blocks), dim3(256), 0, s, dist, n, act_kind, eps, max_dist, act);
+  int rc = check_launch("act_kernel");
+  if (rc) return rc;
+  // cv::resize: inv_scale = dsize / ssize, scale = 1 / inv_scale (both f64).
+  const double scale_x = 1.0 / (static_cast<double>(W) / static_cast<double>(w));
+  const double scale_y = 1.0 / (static_cast<double>(H) / static_cast<double>(h));
+  const dim3 grid(static_cast<unsigned>(ceil_div(W, kUpThreads)), H, m);
+  hipLaunchKernelGGL(cubic_upsample_kernel, grid, dim3(kUpThreads), 0, s, act, h, w, H, W, scale_y, scale_x, up);
+  return check_launch("cubic_upsample_kernel");
+}
+
+extern "C" int protoseg_bound_boxes(const float* up, int m, int H, int W, const void* label, int label_dtype,
+                                    int n_label, const int32_t* label_index, const int32_t* lut, int lut_size,
+                                    const int32_t* target_class, const int32_t* rf_box, float percentile, int margin,
+                                    float* threshold, int32_t* box, protoseg_stream_t stream) {
+  if (!up || !label || !target_class || !rf_box || !threshold || !box)
+    return fail(PROTOSEG_ERR_INVALID, "up, label, target_class, rf_box, threshold and box must be non-null");
+  if (m <= 0 || H <= 0 || W <= 0 || n_label <= 0)
+    return fail(PROTOSEG_ERR_INVALID, "bad shape m=%d H=%d W=%d n_label=%d", m, H, W, n_label);
+  if (static_cast<long long>(H) * W >= (1ll << 32)) return fail(PROTOSEG_ERR_UNSUPPORTED, "map too large");
+  if (!(percentile >= 0.f && percentile <= 100.f)) return fail(PROTOSEG_ERR_INVALID, "percentile must be in [0, 100]");
+  if (margin < 0) return fail(PROTOSEG_ERR_INVALID, "margin must be >= 0");
+  if (lut && lut_size <= 0) return fail(PROTOSEG_ERR_INVALID, "lut_size must be > 0");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  switch (label_dtype) {
+    case PROTOSEG_I64:
+      hipLaunchKernelGGL(bound_box_kernel<int64_t>, dim3(m), dim3(kBoxThreads), 0, s, up, H, W,
+                         static_cast<const int64_t*>(label), n_label, label_index, lut, lut_size, target_class, rf_box,
+                         percentile, margin, threshold, box);
+      break;
+    case PROTOSEG_I32:
+      hipLaunchKernelGGL(bound_box_kernel<int32_t>, dim3(m), dim3(kBoxThreads), 0, s, up, H, W,
+                         static_cast<const int32_t*>(label), n_label, label_index, lut, lut_size, target_class, rf_box,
+                         percentile, margin, threshold, box);
+      break;
+    case PROTOSEG_U8:
+      hipLaunchKernelGGL(bound_box_kernel<uint8_t>, dim3(m), dim3(kBoxThreads), 0, s, up, H, W,
+                         static_cast<const uint8_t*>(label), n_label, label_index, lut, lut_size, target_class, rf_box,
+                         percentile, margin, threshold, box);
+      break;
+    default:
+      return fail(PROTOSEG_ERR_UNSUPPORTED, "label_dtype %d", label_dtype);
+  }
+  return check_launch("bound_box_kernel");
+}

@@ -25,7 +25,7 @@ OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_HIP = 0, 1, 2, 3
 # enum protoseg_dtype
 F32, BF16, I64, I32, U8 = 0, 1, 2, 3, 4
 # enum protoseg_act
-ACT_LOG, ACT_LINEAR = 0, 1
+ACT_LOG, ACT_LINEAR, ACT_IDENTITY = 0, 1, 2
 # enum protoseg_precision
 PREC_BF16X3, PREC_BF16X6, PREC_F32 = 0, 1, 2
 PRECISIONS = {"bf16x3": PREC_BF16X3, "bf16x6": PREC_BF16X6, "f32": PREC_F32}
@@ -54,6 +54,8 @@ SIGNATURES = {
     "protoseg_knn_patch_label": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp]),
     "protoseg_knn_heap_push": (_i, [_vp, _vp, _vp, _i, _i64, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     "protoseg_knn_finalize": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "protoseg_act_upsample": (_i, [_vp, _i, _i, _i, _i, _i, _i, _f, _f, _vp, _vp, _vp]),
+    "protoseg_bound_boxes": (_i, [_vp, _i, _i, _i, _vp, _i, _i, _vp, _vp, _i, _vp, _vp, _f, _i, _vp, _vp, _vp]),
 }
 
 

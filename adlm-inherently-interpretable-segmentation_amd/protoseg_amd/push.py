@@ -12,12 +12,15 @@ Semantics kept from the reference:
     the image are skipped (push.py:255-256);
   * a prototype moves only on a strictly smaller distance; images are visited in
     ``dataset.img_ids`` order, so an earlier image wins a tie (push.py:101, 265);
-  * receptive-field boxes push.py:288-307, dedup push.py:147-155, prune model.py:311-336.
+  * receptive-field boxes push.py:288-307, dedup push.py:147-155, prune model.py:311-336;
+  * high-activation bound boxes push.py:309-343 + helpers.py:48-82 (bbox.hip), computed once
+    per prototype on its final winning image — the reference recomputes them on every image
+    that improves the prototype and keeps the last, i.e. the same image.
 Ties between patches of ONE image resolve to the lowest patch index; the reference's order
 there is the iteration order of a Python set (push.py:214, 230). See DESIGN.md.
 
-Out of scope (host-side visualisation, needs cv2/matplotlib): the PNG outputs and the
-high-activation bound boxes of push.py:309-481 (``proto_bound_boxes`` stay -1).
+Out of scope (host-side visualisation, needs cv2/matplotlib): the PNG outputs of
+push.py:344-481.
 """
 from __future__ import annotations
 
@@ -124,6 +127,81 @@ def push_update(state: PushState, x: Tensor, labels: Tensor, protos: Tensor, pro
     H, W = labels.shape[-2:]
     for i in range(n):
         state.geometry[first_img + i] = (int(H), int(W), int(h), int(w))
+
+
+_ACT_KINDS = {"log": _lib.ACT_LOG, "linear": _lib.ACT_LINEAR, "identity": _lib.ACT_IDENTITY}
+
+
+def act_upsample(dist: Tensor, H: int, W: int, act: str = "log", eps: float = 1e-4, max_dist: float = 0.0):
+    """push.py:309-319: activation of each [h, w] distance map, then cv2.resize INTER_CUBIC to
+    (H, W). ``dist`` [m, h, w] f32 on the device; returns (act [m, h, w], up [m, H, W])."""
+    _lib.require_device(dist)
+    if dist.dim() == 2:
+        dist = dist.unsqueeze(0)
+    dist = dist.float().contiguous()
+    m, h, w = dist.shape
+    if act not in _ACT_KINDS:
+        raise ValueError(f"act {act!r}: one of {sorted(_ACT_KINDS)}")
+    act_t = torch.empty_like(dist)
+    up = torch.empty((m, int(H), int(W)), device=dist.device, dtype=torch.float32)
+    with torch.cuda.device(dist.device):
+        _lib.call("protoseg_act_upsample", _lib.ptr(dist), m, h, w, int(H), int(W), _ACT_KINDS[act], float(eps),
+                  float(max_dist), _lib.ptr(act_t), _lib.ptr(up), _lib.stream_of(dist.device))
+    return act_t, up
+
+
+def bound_boxes(up: Tensor, labels: Tensor, target_class: Tensor, rf: Tensor, label_index: Optional[Tensor] = None,
+                lut: Optional[Tensor] = None, percentile: float = 95.0, margin: int = 5):
+    """push.py:321-343 + helpers.py:48-82 on the device. ``up`` [m, H, W] f32; ``labels``
+    [n, H, W] (or [H, W]) int64/int32/uint8; ``target_class`` [m]; ``rf`` [m, 4] =
+    (start_h, end_h, start_w, end_w). Returns (threshold [m] f32, box [m, 4] int32)."""
+    _lib.require_device(up, labels, target_class, rf, label_index, lut)
+    if labels.dim() == 2:
+        labels = labels.unsqueeze(0)
+    labels = labels.contiguous()
+    dt = _label_dtype(labels)
+    if dt < 0:
+        labels, dt = labels.to(torch.int64), _lib.I64
+    m, H, W = up.shape
+    if tuple(labels.shape[1:]) != (H, W):
+        raise ValueError(f"labels {tuple(labels.shape)} do not match maps {tuple(up.shape)}")
+    tc = target_class.to(torch.int32).contiguous()
+    rf32 = rf.to(torch.int32).contiguous()
+    li = label_index.to(torch.int32).contiguous() if label_index is not None else None
+    lut32 = lut.to(torch.int32).contiguous() if lut is not None else None
+    if tc.numel() != m or rf32.shape != (m, 4) or (li is not None and li.numel() != m):
+        raise ValueError("target_class [m], rf [m, 4] and label_index [m] must match up [m, H, W]")
+    thr = torch.empty(m, device=up.device, dtype=torch.float32)
+    box = torch.empty((m, 4), device=up.device, dtype=torch.int32)
+    with torch.cuda.device(up.device):
+        _lib.call("protoseg_bound_boxes", _lib.ptr(up.contiguous()), m, H, W, _lib.ptr(labels), dt, labels.shape[0],
+                  _lib.ptr(li), _lib.ptr(lut32), 0 if lut32 is None else lut32.numel(), _lib.ptr(tc), _lib.ptr(rf32),
+                  float(percentile), int(margin), _lib.ptr(thr), _lib.ptr(box), _lib.stream_of(up.device))
+    return thr, box
+
+
+def image_bound_boxes(x: Tensor, labels: Tensor, protos: Tensor, proto_ids: np.ndarray, proto_class: np.ndarray,
+                      rf_rows: np.ndarray, act: str = "log", eps: float = 1e-4, act_fn: Optional[Callable] = None,
+                      lut: Optional[Tensor] = None) -> np.ndarray:
+    """Bound boxes of the prototypes ``proto_ids`` that won on one image (push.py:309-343).
+    ``x`` [1, C, h, w] features of that image, ``labels`` [H, W]; ``rf_rows`` [m, 5] their
+    receptive-field boxes. Returns [m, 4] (start_h, end_h, start_w, end_w)."""
+    from .ops import l2_distances
+    ids = torch.as_tensor(np.asarray(proto_ids, dtype=np.int64), device=x.device)
+    dist = l2_distances(x.float(), protos.detach()[ids], eps, precision="f32")[0]  # [m, h, w]
+    max_dist = float(protos.shape[1])  # push.py:229 prototype_shape[1] * [2] * [3]
+    if act not in ("log", "linear"):
+        if act_fn is None:
+            raise ValueError(f"activation {act!r} needs prototype_activation_function_in_numpy")
+        dist = torch.as_tensor(np.ascontiguousarray(act_fn(dist.cpu().numpy())), dtype=torch.float32,
+                               device=x.device)
+        act = "identity"
+    H, W = labels.shape[-2:]
+    _, up = act_upsample(dist, H, W, act, eps, max_dist)
+    tc = torch.as_tensor(np.asarray(proto_class, dtype=np.int32)[np.asarray(proto_ids)], device=x.device)
+    rf = torch.as_tensor(np.asarray(rf_rows)[:, 1:5].astype(np.int32), device=x.device)
+    _, box = bound_boxes(up, labels, tc, rf, lut=lut)
+    return box.cpu().numpy().astype(np.int64)
 
 
 def prototype_classes(ppnet) -> Tensor:
@@ -235,22 +313,25 @@ def push_prototypes(dataset, prototype_network_parallel, prototype_layer_stride=
     rank, world = world_info(process_group)
     lo, hi = shard_bounds(len(dataset.img_ids), rank, world)
 
+    def load(push_iter):
+        img_id = dataset.img_ids[push_iter]
+        with open(dataset.get_img_path(img_id), "rb") as f:
+            img = Image.open(f).convert("RGB")
+        margin = dataset.image_margin_size
+        img = img.crop((margin, margin, img.width - margin, img.height - margin))
+        gt_ann = np.load(os.path.join(dataset.annotations_dir, img_id + ".npy"))
+        if convert is not None and lut is None:
+            gt_ann = convert(gt_ann)
+        labels = torch.as_tensor(np.ascontiguousarray(gt_ann)).to(device)
+        if labels.dtype not in (torch.int64, torch.int32, torch.uint8):
+            labels = labels.to(torch.int64)
+        img_tensor = to_normalized_tensor(img, mean, std).unsqueeze(0).to(device)
+        return ppnet.conv_features(img_tensor), labels
+
     log("Updating prototypes...")
     with torch.no_grad():
         for push_iter in range(lo, hi):
-            img_id = dataset.img_ids[push_iter]
-            with open(dataset.get_img_path(img_id), "rb") as f:
-                img = Image.open(f).convert("RGB")
-            margin = dataset.image_margin_size
-            img = img.crop((margin, margin, img.width - margin, img.height - margin))
-            gt_ann = np.load(os.path.join(dataset.annotations_dir, img_id + ".npy"))
-            if convert is not None and lut is None:
-                gt_ann = convert(gt_ann)
-            labels = torch.as_tensor(np.ascontiguousarray(gt_ann)).to(device)
-            if labels.dtype not in (torch.int64, torch.int32, torch.uint8):
-                labels = labels.to(torch.int64)
-            img_tensor = to_normalized_tensor(img, mean, std).unsqueeze(0).to(device)
-            conv_features = ppnet.conv_features(img_tensor)
+            conv_features, labels = load(push_iter)
             push_update(state, conv_features, labels, ppnet.prototype_vectors, proto_class_t, push_iter, lut)
 
     if world > 1:
@@ -258,7 +339,25 @@ def push_prototypes(dataset, prototype_network_parallel, prototype_layer_stride=
 
     with_class = bool(save_prototype_class_identity)
     proto_rf_boxes = rf_boxes(state, proto_class, with_class)
+    # push.py:309-343: bound boxes on each prototype's winning image (this rank's shard only).
     proto_bound_boxes = np.full_like(proto_rf_boxes, -1)
+    winners = proto_rf_boxes[:, 0]
+    with torch.no_grad():
+        for img_idx in np.unique(winners[(winners >= lo) & (winners < hi)]):
+            ids = np.nonzero(winners == img_idx)[0]
+            conv_features, labels = load(int(img_idx))
+            box = image_bound_boxes(conv_features, labels, ppnet.prototype_vectors, ids, proto_class,
+                                    proto_rf_boxes[ids], ppnet.prototype_activation_function, ppnet.epsilon,
+                                    prototype_activation_function_in_numpy, lut)
+            proto_bound_boxes[ids, 0] = img_idx
+            proto_bound_boxes[ids, 1:5] = box
+            if with_class:
+                proto_bound_boxes[ids, 5] = proto_class[ids]
+    if world > 1:
+        import torch.distributed as tdist
+        t = torch.as_tensor(proto_bound_boxes, device=device)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX, group=process_group)
+        proto_bound_boxes = t.cpu().numpy()
     if proto_epoch_dir is not None and proto_bound_boxes_filename_prefix is not None:
         np.save(os.path.join(proto_epoch_dir, f"{proto_bound_boxes_filename_prefix}-receptive_field{epoch_number}.npy"),
                 proto_rf_boxes)

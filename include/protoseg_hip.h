@@ -43,8 +43,10 @@ enum protoseg_dtype {
   PROTOSEG_U8 = 4
 };
 
-/* model.py:231-237 distance_2_similarity: 'log' -> log((d+1)/(d+eps)); 'linear' -> -d */
-enum protoseg_act { PROTOSEG_ACT_LOG = 0, PROTOSEG_ACT_LINEAR = 1 };
+/* model.py:231-237 distance_2_similarity: 'log' -> log((d+1)/(d+eps)); 'linear' -> -d.
+ * IDENTITY (protoseg_act_upsample only): the input already holds activations, e.g. from the
+ * caller's prototype_activation_function_in_numpy (push.py:317-318). */
+enum protoseg_act { PROTOSEG_ACT_LOG = 0, PROTOSEG_ACT_LINEAR = 1, PROTOSEG_ACT_IDENTITY = 2 };
 
 /* Arithmetic of the x.p / W.act / gradient products (always f32 accumulation):
  *  BF16X3  operands split in 2 bf16 terms, 3 bf16 MFMAs per product (|rel err| ~ 1e-5 on d)
@@ -275,6 +277,37 @@ int protoseg_knn_finalize(const double* heap_neg, const int32_t* heap_label, con
                           const int32_t* proto_class, int prune_threshold, double* out_dist, int32_t* out_label,
                           int64_t* out_img, int32_t* out_patch, int32_t* class_count, int32_t* prune,
                           protoseg_stream_t stream);
+
+/*
+ * Push outputs, high-activation bound boxes, step 1. Replaces segmentation/push.py:309-319:
+ * the prototype's activation map on the winning image (log: np.log((d+1)/(d+eps)) in f32;
+ * linear: max_dist - d, max_dist = C; identity: dist already holds activations) and
+ * cv2.resize(act, (W, H), interpolation=cv2.INTER_CUBIC) (A = -0.75, half-pixel centres,
+ * replicated border, horizontal then vertical pass, unfused f32).
+ *   dist [m, h, w] f32   one distance map per pushed prototype (gathered by the caller)
+ *   act  [m, h, w] f32 out;  up [m, H, W] f32 out
+ */
+int protoseg_act_upsample(const float* dist, int m, int h, int w, int H, int W, int act_kind, float eps,
+                          float max_dist, float* act, float* up, protoseg_stream_t stream);
+
+/*
+ * Bound boxes, step 2. Replaces push.py:321-343 and helpers.py:48-82: threshold =
+ * np.percentile(up, percentile) (numpy 'linear', f32), mask = up * (label == class + 1) >=
+ * threshold, the receptive-field box grown greedily over the mask, a `margin`-pixel border
+ * added (find_continuous_high_activation_crop, add_margin = 5).
+ *   up [m, H, W] f32 from protoseg_act_upsample
+ *   label [n_label, H, W] label_dtype (raw ids through `lut` when given); label_index [m] int32
+ *         picks each map's image (NULL = image 0)
+ *   target_class [m] int32 (push.py:251);  rf_box [m, 4] int32 (start_h, end_h, start_w, end_w)
+ *         as push.py:288-294
+ *   threshold [m] f32 out;  box [m, 4] int32 out = (start_h, end_h, start_w, end_w) as
+ *         proto_bound_boxes[j, 1:5] (push.py:338-342); -1 (threshold NaN) when label_index or
+ *         rf_box is out of range
+ */
+int protoseg_bound_boxes(const float* up, int m, int H, int W, const void* label, int label_dtype, int n_label,
+                         const int32_t* label_index, const int32_t* lut, int lut_size, const int32_t* target_class,
+                         const int32_t* rf_box, float percentile, int margin, float* threshold, int32_t* box,
+                         protoseg_stream_t stream);
 
 #ifdef __cplusplus
 }
