@@ -80,30 +80,61 @@ __global__ __launch_bounds__(256) void act_kernel(const float* __restrict__ dist
   }
 }
 
-// grid (ceil(W / 256), H, m): one output row segment of one map per workgroup.
+// Output tile: kUpThreads columns x `rows` output rows of one map per workgroup (grid
+// (ceil(W / 256), ceil(H / rows), m)). Phase 1: the horizontal pass for every source row the
+// tile touches, one column per thread (its x taps computed once), into LDS. Phase 2: the
+// vertical pass per output row from LDS, coalesced row stores. Each H-value is formed once per
+// tile instead of once per output pixel; the arithmetic is the same sequence as OpenCV's.
+constexpr int kUpMaxSrcRows = 72;
+constexpr int kUpMaxRows = 64;
+
 __global__ __launch_bounds__(kUpThreads) void cubic_upsample_kernel(const float* __restrict__ act, int h, int w,
-                                                                    int H, int W, double scale_y, double scale_x,
-                                                                    float* __restrict__ up) {
-  const int dx = blockIdx.x * kUpThreads + threadIdx.x;
-  const int dy = blockIdx.y;
+                                                                    int H, int W, int rows, double scale_y,
+                                                                    double scale_x, float* __restrict__ up) {
+  __shared__ float hr[kUpMaxSrcRows][kUpThreads];
+  __shared__ float ycoef[kUpMaxRows][4];
+  __shared__ int yrow[kUpMaxRows][4];
+  const int t = threadIdx.x;
+  const int dx = blockIdx.x * kUpThreads + t;
+  const int dy0 = blockIdx.y * rows;
+  const int dy1 = dy0 + rows < H ? dy0 + rows : H;
   const int map = blockIdx.z;
-  if (dx >= W) return;
-  int xi[4], yi[4];
-  float a[4], b[4];
-  cubic_taps(dx, scale_x, w, xi, a);
-  cubic_taps(dy, scale_y, h, yi, b);
-  const float* S = act + static_cast<size_t>(map) * h * w;
-  float rows[4];
+  // Source row window [r0, r1] of this tile (taps are monotone in dy).
+  int i0[4], i1[4];
+  float c_unused[4];
+  cubic_taps(dy0, scale_y, h, i0, c_unused);
+  cubic_taps(dy1 - 1, scale_y, h, i1, c_unused);
+  const int r0 = i0[0], r1 = i1[3];
+  if (t < dy1 - dy0) {
+    int yi[4];
+    float b[4];
+    cubic_taps(dy0 + t, scale_y, h, yi, b);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {  // HResizeCubic: S[x0]*a0 + S[x1]*a1 + S[x2]*a2 + S[x3]*a3
-    const float* R = S + static_cast<size_t>(yi[k]) * w;
-    rows[k] = fadd(fadd(fadd(fmul(R[xi[0]], a[0]), fmul(R[xi[1]], a[1])), fmul(R[xi[2]], a[2])),
-                   fmul(R[xi[3]], a[3]));
+    for (int k = 0; k < 4; ++k) {
+      ycoef[t][k] = b[k];
+      yrow[t][k] = yi[k] - r0;
+    }
   }
-  // VResizeCubic: S0*b0 + S1*b1 + S2*b2 + S3*b3
-  const float v = fadd(fadd(fadd(fmul(rows[0], b[0]), fmul(rows[1], b[1])), fmul(rows[2], b[2])),
-                       fmul(rows[3], b[3]));
-  up[(static_cast<size_t>(map) * H + dy) * W + dx] = v;
+  const float* S = act + static_cast<size_t>(map) * h * w;
+  if (dx < W) {
+    int xi[4];
+    float a[4];
+    cubic_taps(dx, scale_x, w, xi, a);
+    for (int r = r0; r <= r1; ++r) {  // HResizeCubic: S[x0]*a0 + S[x1]*a1 + S[x2]*a2 + S[x3]*a3
+      const float* R = S + static_cast<size_t>(r) * w;
+      hr[r - r0][t] = fadd(fadd(fadd(fmul(R[xi[0]], a[0]), fmul(R[xi[1]], a[1])), fmul(R[xi[2]], a[2])),
+                           fmul(R[xi[3]], a[3]));
+    }
+  }
+  __syncthreads();
+  if (dx >= W) return;
+  float* out = up + (static_cast<size_t>(map) * H + dy0) * W + dx;
+  for (int j = 0; j < dy1 - dy0; ++j) {  // VResizeCubic: S0*b0 + S1*b1 + S2*b2 + S3*b3
+    const float v = fadd(fadd(fadd(fmul(hr[yrow[j][0]][t], ycoef[j][0]), fmul(hr[yrow[j][1]][t], ycoef[j][1])),
+                              fmul(hr[yrow[j][2]][t], ycoef[j][2])),
+                         fmul(hr[yrow[j][3]][t], ycoef[j][3]));
+    out[static_cast<size_t>(j) * W] = v;
+  }
 }
 
 // Order-preserving f32 <-> u32 (NaN sorts last, as np.sort puts it).
@@ -316,7 +347,7 @@ extern "C" int protoseg_act_upsample(const float* dist, int m, int h, int w, int
   if (!dist || !act || !up) return fail(PROTOSEG_ERR_INVALID, "dist, act and up must be non-null");
   if (m <= 0 || h <= 0 || w <= 0 || H <= 0 || W <= 0)
     return fail(PROTOSEG_ERR_INVALID, "bad shape m=%d h=%d w=%d H=%d W=%d", m, h, w, H, W);
-  if (m > 65535 || H > 65535) return fail(PROTOSEG_ERR_UNSUPPORTED, "m=%d H=%d above the grid limit", m, H);
+  if (m > 65535) return fail(PROTOSEG_ERR_UNSUPPORTED, "m=%d H=%d above the grid limit", m, H);
   if (act_kind < PROTOSEG_ACT_LOG || act_kind > PROTOSEG_ACT_IDENTITY)
     return fail(PROTOSEG_ERR_INVALID, "act_kind %d", act_kind);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -328,8 +359,12 @@ extern "C" int protoseg_act_upsample(const float* dist, int m, int h, int w, int
   // cv::resize: inv_scale = dsize / ssize, scale = 1 / inv_scale (both f64).
   const double scale_x = 1.0 / (static_cast<double>(W) / static_cast<double>(w));
   const double scale_y = 1.0 / (static_cast<double>(H) / static_cast<double>(h));
-  const dim3 grid(static_cast<unsigned>(ceil_div(W, kUpThreads)), H, m);
-  hipLaunchKernelGGL(cubic_upsample_kernel, grid, dim3(kUpThreads), 0, s, act, h, w, H, W, scale_y, scale_x, up);
+  // Output rows per tile: the source rows they touch (<= rows * h / H + 5) must fit the LDS window.
+  long long rows = (static_cast<long long>(kUpMaxSrcRows - 6) * H) / h;
+  rows = rows < 1 ? 1 : rows > kUpMaxRows ? kUpMaxRows : rows;
+  const dim3 grid(static_cast<unsigned>(ceil_div(W, kUpThreads)), static_cast<unsigned>(ceil_div(H, rows)), m);
+  hipLaunchKernelGGL(cubic_upsample_kernel, grid, dim3(kUpThreads), 0, s, act, h, w, H, W, static_cast<int>(rows),
+                     scale_y, scale_x, up);
   return check_launch("cubic_upsample_kernel");
 }
 

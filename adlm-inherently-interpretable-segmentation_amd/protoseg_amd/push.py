@@ -180,28 +180,44 @@ def bound_boxes(up: Tensor, labels: Tensor, target_class: Tensor, rf: Tensor, la
     return thr, box
 
 
-def image_bound_boxes(x: Tensor, labels: Tensor, protos: Tensor, proto_ids: np.ndarray, proto_class: np.ndarray,
-                      rf_rows: np.ndarray, act: str = "log", eps: float = 1e-4, act_fn: Optional[Callable] = None,
-                      lut: Optional[Tensor] = None) -> np.ndarray:
-    """Bound boxes of the prototypes ``proto_ids`` that won on one image (push.py:309-343).
-    ``x`` [1, C, h, w] features of that image, ``labels`` [H, W]; ``rf_rows`` [m, 5] their
-    receptive-field boxes. Returns [m, 4] (start_h, end_h, start_w, end_w)."""
+def batch_bound_boxes(items, protos: Tensor, proto_class: np.ndarray, rf_boxes_all: np.ndarray, act: str = "log",
+                      eps: float = 1e-4, act_fn: Optional[Callable] = None, lut: Optional[Tensor] = None):
+    """Bound boxes (push.py:309-343) of every pushed prototype in one act_upsample + one
+    bound_boxes launch per image geometry. ``items`` yields (proto_ids, x [1, C, h, w],
+    labels [H, W]) per winning image. Returns {prototype id: (start_h, end_h, start_w, end_w)}."""
     from .ops import l2_distances
-    ids = torch.as_tensor(np.asarray(proto_ids, dtype=np.int64), device=x.device)
-    dist = l2_distances(x.float(), protos.detach()[ids], eps, precision="f32")[0]  # [m, h, w]
+    groups: Dict[tuple, dict] = {}
+    for ids, x, labels in items:
+        idt = torch.as_tensor(np.asarray(ids, dtype=np.int64), device=x.device)
+        dist = l2_distances(x.float(), protos.detach()[idt], eps, precision="f32")[0]  # [m_i, h, w]
+        key = (tuple(dist.shape[1:]), tuple(labels.shape[-2:]), labels.dtype)
+        g = groups.setdefault(key, {"ids": [], "dist": [], "labels": [], "li": []})
+        g["li"].extend([len(g["labels"])] * len(ids))
+        g["ids"].extend(int(j) for j in ids)
+        g["dist"].append(dist)
+        g["labels"].append(labels.reshape(labels.shape[-2:]))
     max_dist = float(protos.shape[1])  # push.py:229 prototype_shape[1] * [2] * [3]
-    if act not in ("log", "linear"):
-        if act_fn is None:
-            raise ValueError(f"activation {act!r} needs prototype_activation_function_in_numpy")
-        dist = torch.as_tensor(np.ascontiguousarray(act_fn(dist.cpu().numpy())), dtype=torch.float32,
-                               device=x.device)
-        act = "identity"
-    H, W = labels.shape[-2:]
-    _, up = act_upsample(dist, H, W, act, eps, max_dist)
-    tc = torch.as_tensor(np.asarray(proto_class, dtype=np.int32)[np.asarray(proto_ids)], device=x.device)
-    rf = torch.as_tensor(np.asarray(rf_rows)[:, 1:5].astype(np.int32), device=x.device)
-    _, box = bound_boxes(up, labels, tc, rf, lut=lut)
-    return box.cpu().numpy().astype(np.int64)
+    out: Dict[int, tuple] = {}
+    for (_, (H, W), _), g in groups.items():
+        dist = torch.cat(g["dist"], 0)
+        kind = act
+        if kind not in ("log", "linear"):
+            if act_fn is None:
+                raise ValueError(f"activation {act!r} needs prototype_activation_function_in_numpy")
+            dist = torch.as_tensor(np.ascontiguousarray(act_fn(dist.cpu().numpy())), dtype=torch.float32,
+                                   device=dist.device)
+            kind = "identity"
+        _, up = act_upsample(dist, H, W, kind, eps, max_dist)
+        ids = np.asarray(g["ids"])
+        dev = dist.device
+        tc = torch.as_tensor(np.asarray(proto_class, dtype=np.int32)[ids], device=dev)
+        rf = torch.as_tensor(np.asarray(rf_boxes_all)[ids, 1:5].astype(np.int32), device=dev)
+        li = torch.as_tensor(np.asarray(g["li"], dtype=np.int32), device=dev)
+        _, box = bound_boxes(up, torch.stack(g["labels"], 0), tc, rf, li, lut=lut)
+        del up
+        for j, b in zip(ids, box.cpu().numpy().astype(np.int64)):
+            out[int(j)] = tuple(int(v) for v in b)
+    return out
 
 
 def prototype_classes(ppnet) -> Tensor:
@@ -342,17 +358,20 @@ def push_prototypes(dataset, prototype_network_parallel, prototype_layer_stride=
     # push.py:309-343: bound boxes on each prototype's winning image (this rank's shard only).
     proto_bound_boxes = np.full_like(proto_rf_boxes, -1)
     winners = proto_rf_boxes[:, 0]
+    mine = np.unique(winners[(winners >= lo) & (winners < hi)])
     with torch.no_grad():
-        for img_idx in np.unique(winners[(winners >= lo) & (winners < hi)]):
-            ids = np.nonzero(winners == img_idx)[0]
-            conv_features, labels = load(int(img_idx))
-            box = image_bound_boxes(conv_features, labels, ppnet.prototype_vectors, ids, proto_class,
-                                    proto_rf_boxes[ids], ppnet.prototype_activation_function, ppnet.epsilon,
-                                    prototype_activation_function_in_numpy, lut)
-            proto_bound_boxes[ids, 0] = img_idx
-            proto_bound_boxes[ids, 1:5] = box
-            if with_class:
-                proto_bound_boxes[ids, 5] = proto_class[ids]
+        def items():
+            for img_idx in mine:
+                conv_features, labels = load(int(img_idx))
+                yield np.nonzero(winners == img_idx)[0], conv_features, labels
+        boxes = batch_bound_boxes(items(), ppnet.prototype_vectors, proto_class, proto_rf_boxes,
+                                  ppnet.prototype_activation_function, ppnet.epsilon,
+                                  prototype_activation_function_in_numpy, lut)
+    for j, b in boxes.items():
+        proto_bound_boxes[j, 0] = winners[j]
+        proto_bound_boxes[j, 1:5] = b
+        if with_class:
+            proto_bound_boxes[j, 5] = proto_class[j]
     if world > 1:
         import torch.distributed as tdist
         t = torch.as_tensor(proto_bound_boxes, device=device)

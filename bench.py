@@ -481,6 +481,47 @@ def time_eval(n_img, steps, warmup, device, H=1024, W=2048, h=129, w=257, P=190,
             "roofline": roofline_entry(0.0, nbytes, kern) | {"kernel": "eval_rows_kernel"}}
 
 
+def time_bound_boxes(steps, warmup, device, H=1024, W=2048, h=129, w=257, P=190, K=19):
+    """Push post-step, high-activation bound boxes of all P prototypes (push.py:309-343) in one
+    act_upsample + bound_boxes pair. The dominant cost is cubic_upsample_kernel, an HBM-write
+    stream: algorithmic bytes = P * H * W * 4 (upsampled maps written once) + the P low-res
+    activation maps read."""
+    from protoseg_amd import push as dpush
+    gen = torch.Generator().manual_seed(SEED + 7)
+    dmaps = (torch.rand(P, h, w, generator=gen) * 6).to(device)
+    rng = np.random.default_rng(SEED + 7)
+    blocks = rng.integers(0, K + 1, size=(1, H // 16, W // 16)).astype(np.uint8)
+    labels = torch.from_numpy(np.repeat(np.repeat(blocks, 16, 1), 16, 2)).to(device)
+    tc = (torch.arange(P) // (P // K)).to(torch.int32).to(device)
+    r, c = rng.integers(0, h, P), rng.integers(0, w, P)
+    rf = torch.as_tensor(np.stack([r * H // h, r * H // h + 9, c * W // w, c * W // w + 9], 1).astype(np.int32),
+                         device=device)
+    act = torch.empty_like(dmaps)
+    up = torch.empty((P, H, W), device=device, dtype=torch.float32)
+    thr = torch.empty(P, device=device, dtype=torch.float32)
+    box = torch.empty((P, 4), device=device, dtype=torch.int32)
+    stream = _lib.stream_of(device)
+    null = ctypes.c_void_p(None)
+    t_box = []
+
+    def run(ev):
+        if ev is not None:
+            ev[0].record()
+        _lib.call("protoseg_act_upsample", _lib.ptr(dmaps), P, h, w, H, W, _lib.ACT_LOG, 1e-4, float(64),
+                  _lib.ptr(act), _lib.ptr(up), stream)
+        if ev is not None:
+            ev[1].record()
+        _lib.call("protoseg_bound_boxes", _lib.ptr(up), P, H, W, _lib.ptr(labels), _lib.U8, 1, null, null, 0,
+                  _lib.ptr(tc), _lib.ptr(rf), 95.0, 5, _lib.ptr(thr), _lib.ptr(box), stream)
+
+    wall, kern = _timed_calls(run, steps, warmup)
+    nbytes = P * (H * W * 4 + h * w * 4)
+    return {"ms_per_push": round(wall * 1e3, 4), "prototypes": P,
+            "workload": f"bound boxes: {P} maps {h}x{w} -> {H}x{W} cubic, 95th percentile, greedy crop",
+            "act_upsample_ms": round(kern * 1e3, 4), "bound_boxes_ms": round((wall - kern) * 1e3, 4),
+            "roofline": roofline_entry(0.0, nbytes, kern) | {"kernel": "act_kernel + cubic_upsample_kernel"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -537,6 +578,9 @@ def main():
         knn = time_knn(args.push_images, args.push_steps, 1, device)
     if not args.no_eval and world == 1:
         evaluation = time_eval(2, 3, 1, device)
+    bboxes = None
+    if not args.no_push and world == 1:
+        bboxes = time_bound_boxes(3, 1, device)
 
     if rank == 0:
         work = step.work()
@@ -580,6 +624,8 @@ def main():
             out["knn_search"] = knn
         if evaluation is not None:
             out["eval"] = evaluation
+        if bboxes is not None:
+            out["push"]["bound_boxes"] = bboxes
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_layer_baseline(args.channels, args.fmap, args.fmap, args.protos, args.classes,
                                                      args.cpu_seconds)
