@@ -38,6 +38,7 @@ from protoseg_amd import _lib  # noqa: E402
 from protoseg_amd.distributed import init_from_env  # noqa: E402
 
 PEAK_HBM_GBPS = 8000.0       # MI355X_MICROARCH.md chip table (spec)
+PEAK_F32_VALU_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 (vector), spec
 PEAK_F32_MFMA_TFLOPS = 157.3  # dense f32-input MFMA (v_mfma_f32_32x32x2_f32), MI355X_MICROARCH.md
 PEAK_BF16_MFMA_TFLOPS = 2500.0  # dense bf16 MFMA (spec, no sparsity), MI355X_MICROARCH.md
 # Peak rate of f32-product FLOPs per precision mode: the bf16 split modes execute 3 or 6
@@ -476,9 +477,17 @@ def time_eval(n_img, steps, warmup, device, H=1024, W=2048, h=129, w=257, P=190,
 
     wall, kern = _timed_calls(run, steps, warmup)
     nbytes = n_img * ((K + P) * h * w * 4 + H * W)
+    # VALU-bound: per output pixel and class/prototype, torch's bilinear form
+    # h0*(w0*v00 + w1*v01) + h1*(w0*v10 + w1*v11) (6 mul + 3 add) and one compare = 10 flops,
+    # against the f32 vector peak; the HBM figure is reported beside it.
+    flops = n_img * 10.0 * (K + P) * H * W
+    valu = flops / kern / 1e12
+    hbm = roofline_entry(0.0, nbytes, kern)
     return {"ms_per_img": round(wall / n_img * 1e3, 4), "images_per_call": n_img,
             "workload": f"eval counts: labels {H}x{W} u8, logits {h}x{w}x{K}, distances {P}x{h}x{w} f32",
-            "roofline": roofline_entry(0.0, nbytes, kern) | {"kernel": "eval_rows_kernel"}}
+            "roofline": {"bound": "valu", "achieved": round(valu, 2), "peak": PEAK_F32_VALU_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(valu / PEAK_F32_VALU_TFLOPS, 4),
+                         "hbm_gbps": hbm["achieved"], "hbm_frac": hbm["frac"], "kernel": "eval_rows_kernel"}}
 
 
 def time_bound_boxes(steps, warmup, device, H=1024, W=2048, h=129, w=257, P=190, K=19):
