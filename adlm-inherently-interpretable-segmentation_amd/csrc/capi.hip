@@ -30,6 +30,7 @@ int check_launch(const char* what) {
 namespace {
 std::mutex g_timer_mu;
 std::string g_timer_kernel;
+std::string g_timer_last;  // full name of the last kernel the hook bracketed
 hipEvent_t g_timer_start = nullptr, g_timer_stop = nullptr;
 }  // namespace
 
@@ -45,8 +46,15 @@ hipError_t record(hipEvent_t e, hipStream_t s) {
 
 KernelTimer::KernelTimer(const char* kernel, hipStream_t s) {
   std::lock_guard<std::mutex> lock(g_timer_mu);
-  if (!g_timer_start || g_timer_kernel != kernel) return;
+  // Match the exact kernel name, or a family prefix: "l2_fwd" brackets l2_fwd_kernel and
+  // l2_fwd_bf16_kernel, whichever family serves the call.
+  if (!g_timer_start) return;
+  const size_t n = g_timer_kernel.size();
+  const bool match = g_timer_kernel == kernel ||
+                     (std::strncmp(kernel, g_timer_kernel.c_str(), n) == 0 && kernel[n] == '_');
+  if (!match) return;
   if (record(g_timer_start, s) == hipSuccess) {
+    g_timer_last = kernel;
     stop_ = g_timer_stop;
     s_ = s;
   }
@@ -57,6 +65,11 @@ KernelTimer::~KernelTimer() {
 }
 
 }  // namespace protoseg
+
+extern "C" const char* protoseg_timing_kernel(void) {
+  std::lock_guard<std::mutex> lock(protoseg::g_timer_mu);
+  return protoseg::g_timer_last.c_str();
+}
 
 extern "C" int protoseg_timing_events(const char* kernel, void* start_event, void* stop_event) {
   std::lock_guard<std::mutex> lock(protoseg::g_timer_mu);

@@ -33,6 +33,9 @@ constexpr int kC = 64;         // channels of the bf16 family
 constexpr int kNQ = kC / 16;   // channel k-steps of 16
 constexpr int kWavesA = 8;     // x-backward: 8 waves, one 32-pixel tile each at a time
 constexpr int kWavesF = 8;     // forward: 8 waves (12 would need <= 168 VGPRs: 80+ spill today)
+// Remainder-tile logits partials go through LDS 4 registers at a time (8 KB for 8 waves), so the
+// forward's LDS (P and W images + partials) fits 160 KiB up to Pp = 384 (19 prototypes/class).
+constexpr int kFwdPartRegs = 4;
 
 // (-2 P) image [T][Pp][64]: row p, chunk 2q+h = channels chan_of(q, h, 0..7) (CPR 8). Operand
 // of the distance GEMM in every kernel: A in layout A (lane = p), B in layout B (lane = p). The
@@ -291,7 +294,7 @@ __global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
   bf16* Pimg = reinterpret_cast<bf16*>(smem_raw);                // [T][Pp][64]
   bf16* Wimg = Pimg + T * Pp * kC;                               // [T][Pp][32]
   float* p2s = reinterpret_cast<float*>(Wimg + T * Pp * 32);     // [Pp]
-  float* lpart = p2s + (io.pt - io.p2) / 4;                      // [kWavesF][8][64] remainder logits
+  float* lpart = p2s + (io.pt - io.p2) / 4;                      // [kWavesF][kFwdPartRegs][64] remainder logits
 
   const rsrc_t rx = make_rsrc(x, x_bytes), rd = make_rsrc(dist, d_bytes);
   const rsrc_t ra = make_rsrc(act_out, a_bytes), rl = make_rsrc(logits, l_bytes);
@@ -400,20 +403,21 @@ __global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
     float rt[kNQ * 8];
     load_x_raw<TX>(rx, x_lane_off<TX>(tt, ntiles, npix, HW), cs, rt);
     const f32x16 lacc = run_tile(tt, rt, wave, kWavesF);
-    if constexpr (LOGITS) {  // fixed-order sum of the waves' partials, 8 registers at a time
+    if constexpr (LOGITS) {  // fixed-order sum of the waves' partials, kFwdPartRegs registers at a time
       const int nw = npt < kWavesF ? npt : kWavesF;
-      float* mine = lpart + wave * 8 * 64;
+      float* mine = lpart + wave * kFwdPartRegs * 64;
       f32x16 sum = zero16();
 #pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
+      for (int hf = 0; hf < 16 / kFwdPartRegs; ++hf) {
         if (wave < nw)
 #pragma unroll
-          for (int r = 0; r < 8; ++r) mine[r * 64 + lane] = lacc[8 * hf + r];
+          for (int r = 0; r < kFwdPartRegs; ++r) mine[r * 64 + lane] = lacc[kFwdPartRegs * hf + r];
         __syncthreads();
         if (wave == 0)
           for (int w = 0; w < nw; ++w)
 #pragma unroll
-            for (int r = 0; r < 8; ++r) sum[8 * hf + r] += lpart[(w * 8 + r) * 64 + lane];
+            for (int r = 0; r < kFwdPartRegs; ++r)
+              sum[kFwdPartRegs * hf + r] += lpart[(w * kFwdPartRegs + r) * 64 + lane];
         __syncthreads();
       }
       if (wave == 0) store_logits(tt, sum);
@@ -953,7 +957,8 @@ __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __
 // ---- host side ---------------------------------------------------------------------------------
 size_t p2_pad(const Geometry& g) { return (static_cast<size_t>(g.Pp) * 4 + 1023) & ~static_cast<size_t>(1023); }
 size_t fwd_lds(const Geometry& g, int terms) {
-  return static_cast<size_t>(g.Pp) * terms * (kC + 32) * 2 + p2_pad(g) + static_cast<size_t>(kWavesF) * 8 * 64 * 4;
+  return static_cast<size_t>(g.Pp) * terms * (kC + 32) * 2 + p2_pad(g) +
+         static_cast<size_t>(kWavesF) * kFwdPartRegs * 64 * 4;
 }
 size_t bwd_x_lds(const Geometry& g, int terms) {
   return static_cast<size_t>(g.Pp) * terms * (2 * kC + 32) * 2 + p2_pad(g) +

@@ -502,6 +502,7 @@ int launch_fwd(const Geometry& geo, const void* x, const float* protos, const fl
                int act_kind, float* dist, float* act, float* logits, hipStream_t stream) {
   if (int st = ensure_lds<l2_fwd_kernel<TX, NC>>()) return st;
   const size_t lds = layer_lds_bytes(geo.C, geo.Pp);
+  KernelTimer timer("l2_fwd_kernel", stream);
   hipLaunchKernelGGL((l2_fwd_kernel<TX, NC>), dim3(layer_grid(geo)), dim3(kFwdWaves * 64), lds, stream,
                      static_cast<const TX*>(x), geo.HW, geo.npix, protos, geo.P, geo.Pp, w_last, geo.K, eps,
                      act_kind, dist, act, logits);
@@ -512,6 +513,7 @@ template <typename TX, int NC>
 int launch_bwd_x(const Geometry& geo, const void* x, const float* protos, const float* w_last, float eps,
                  int act_kind, const float* g_logits, const float* g_dist, void* g_x, hipStream_t stream) {
   if (int st = ensure_lds<l2_bwd_x_kernel<TX, NC>>()) return st;
+  KernelTimer timer("l2_bwd_x_kernel", stream);
   hipLaunchKernelGGL((l2_bwd_x_kernel<TX, NC>), dim3(layer_grid(geo)), dim3(kFwdWaves * 64),
                      layer_lds_bytes(geo.C, geo.Pp), stream, static_cast<const TX*>(x), geo.HW, geo.npix, protos,
                      geo.P, geo.Pp, w_last, geo.K, eps, act_kind, g_logits, g_dist, static_cast<TX*>(g_x));
@@ -534,10 +536,13 @@ int launch_bwd_pw(const Geometry& geo, const void* x, const float* protos, const
   const size_t lds = (static_cast<size_t>(geo.C) * 32 + 32 * 32 + static_cast<size_t>(kPwWaves) * geo.C * kLdx) *
                      sizeof(float);
   if (int st = ensure_lds<l2_bwd_pw_kernel<TX, NC>>()) return st;
-  hipLaunchKernelGGL((l2_bwd_pw_kernel<TX, NC>), dim3(geo.Pp / 32, S), dim3(kPwWaves * 64), lds, stream,
-                     static_cast<const TX*>(x), geo.HW, geo.npix, protos, geo.P, geo.Pp, w_last, geo.K, eps, act_kind,
-                     g_logits, g_dist, slab_gp, slab_gw, slab_gs);
-  if (int st = check_launch("l2_bwd_pw_kernel")) return st;
+  {
+    KernelTimer timer("l2_bwd_pw_kernel", stream);
+    hipLaunchKernelGGL((l2_bwd_pw_kernel<TX, NC>), dim3(geo.Pp / 32, S), dim3(kPwWaves * 64), lds, stream,
+                       static_cast<const TX*>(x), geo.HW, geo.npix, protos, geo.P, geo.Pp, w_last, geo.K, eps,
+                       act_kind, g_logits, g_dist, slab_gp, slab_gw, slab_gs);
+    if (int st = check_launch("l2_bwd_pw_kernel")) return st;
+  }
   const long long n = static_cast<long long>(geo.P) * (geo.C > geo.K ? geo.C : geo.K);
   hipLaunchKernelGGL(l2_bwd_reduce_kernel, dim3(static_cast<unsigned>(ceil_div(n, 256))), dim3(256), 0, stream,
                      slab_gp, slab_gw, slab_gs, S, geo.P, geo.Pp, geo.C, geo.K, protos, g_protos,

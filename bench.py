@@ -153,10 +153,11 @@ class LayerStep:
             dist.all_reduce(self.grad_flat)
 
     def kernel_names(self):
-        """rocprof names of the kernels behind the fwd / bwd_x / bwd_pw calls (bwd_pw's call
-        also runs the slab-reduce kernel, timed inside its segment)."""
-        sfx = "" if self.prec == _lib.PREC_F32 or self.C != 64 else "_bf16"
-        return [f"l2_fwd{sfx}_kernel", f"l2_bwd_x{sfx}_kernel", f"l2_bwd_pw{sfx}_kernel"]
+        """Kernel families behind the fwd / bwd_x / bwd_pw calls. The library's timing hook
+        matches a family prefix (l2_fwd -> l2_fwd_bf16_kernel or l2_fwd_kernel, whichever the
+        shape and precision select) and reports the full name it bracketed; bwd_pw's call also
+        runs the slab-reduce kernel, outside the bracket."""
+        return ["l2_fwd", "l2_bwd_x", "l2_bwd_pw"]
 
     # algorithmic work per launch (unpadded P, K; SURVEY.md §8d)
     def work(self):
@@ -247,6 +248,7 @@ def time_layer(step: LayerStep, steps: int, warmup: int, world: int, use_graph: 
         # is the kernel alone, as rocprofv3 reports it (not the call's prep / reduce launches).
         lib = _lib.load()
         per_kernel = {n: [] for n in names}
+        actual = {}
         e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         for ev in e:
             ev.record(stream)  # creates the HIP events
@@ -258,9 +260,12 @@ def time_layer(step: LayerStep, steps: int, warmup: int, world: int, use_graph: 
                     c()
                     torch.cuda.synchronize()
                     per_kernel[n].append(e[0].elapsed_time(e[1]) * 1e-3)
+                actual[n] = lib.protoseg_timing_kernel().decode()
+                if not actual[n].startswith(n + "_"):
+                    raise RuntimeError(f"timing hook did not bracket a {n}* kernel (got {actual[n]!r})")
             finally:
                 lib.protoseg_timing_events(None, None, None)
-    return elapsed, {n: float(np.mean(v)) for n, v in per_kernel.items()}
+    return elapsed, {n: float(np.mean(v)) for n, v in per_kernel.items()}, actual
 
 
 def time_kld_step(step: LayerStep, steps: int, warmup: int):
@@ -565,7 +570,7 @@ def main():
 
     step = LayerStep(args.batch, args.channels, args.fmap, args.fmap, args.protos, args.classes, x_dtype, device,
                      SEED + rank, args.precision)
-    elapsed, per_kernel = time_layer(step, args.steps, args.warmup, world, args.launch == "graph")
+    elapsed, per_kernel, actual = time_layer(step, args.steps, args.warmup, world, args.launch == "graph")
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -595,15 +600,17 @@ def main():
         work = step.work()
         dominant = max(per_kernel, key=per_kernel.get)
         flops, nbytes = work[dominant]
-        roof = roofline_entry(flops, nbytes, per_kernel[dominant], args.precision)
+        prec = args.precision if "_bf16" in actual[dominant] else "f32"  # the family that ran
+        roof = roofline_entry(flops, nbytes, per_kernel[dominant], prec)
         config_key = (f"B{args.batch}_C{args.channels}_{args.fmap}x{args.fmap}_P{args.protos}_K{args.classes}"
                       f"_{args.x_dtype}_{args.precision}")
-        roof["traffic"] = pmc_traffic(dominant, config_key)
-        roof["kernel"] = dominant
+        roof["traffic"] = pmc_traffic(actual[dominant], config_key)
+        roof["kernel"] = actual[dominant]
         kernels = {}
         for n, s in per_kernel.items():
             f, b = work[n]
-            kernels[n] = {"ms": round(s * 1e3, 4), "tflops": round(f / s / 1e12, 2), "gbps": round(b / s / 1e9, 1)}
+            kernels[actual[n]] = {"ms": round(s * 1e3, 4), "tflops": round(f / s / 1e12, 2),
+                                  "gbps": round(b / s / 1e9, 1)}
         out = {
             "metric": baseline_metric(),
             "value": round(value, 1),

@@ -65,6 +65,10 @@ const char* protoseg_last_error(void);      /* thread-local text of the last fai
  * hipEvent_t handles; eager launches only (silent under graph capture). A null argument
  * clears the hook. */
 int protoseg_timing_events(const char* kernel, void* start_event, void* stop_event);
+/* `kernel` may also name a kernel family by prefix ("l2_fwd" matches l2_fwd_kernel and
+ * l2_fwd_bf16_kernel); protoseg_timing_kernel() returns the full name of the last kernel the
+ * hook bracketed ("" if none), i.e. which family served the call. */
+const char* protoseg_timing_kernel(void);
 
 /*
  * Prototype layer forward. Replaces model.py:203-221 (_l2_convolution), 231-237

@@ -238,6 +238,45 @@ def test_timing_events_bracket_one_kernel():
         assert lib.protoseg_timing_events(None, None, None) == 0
     kern, call = k0.elapsed_time(k1), c0.elapsed_time(c1)
     assert 0.0 < kern <= call, (kern, call)
+    assert lib.protoseg_timing_kernel() == b"l2_fwd_bf16_kernel"
     fwd()  # cleared: the kernel events keep their last interval
     torch.cuda.synchronize()
     assert k0.elapsed_time(k1) == kern
+
+
+def test_timing_events_family_prefix_reports_the_family_that_ran():
+    """bench.py times kernels by family prefix: at P = 361 the x-backward runs on the f32
+    family (its bf16 LDS images do not fit), and the hook names that kernel."""
+    import ctypes
+
+    from protoseg_amd import _lib
+
+    dev = torch.device("cuda:0")
+    B, h, w, P, K = 2, 17, 17, 361, 19
+    x, protos, w_last = (t.to(dev) for t in po.synthetic_inputs(B, 64, h, w, P, K, seed=6))
+    g_logits = torch.randn(B, h, w, K, device=dev)
+    g_x = torch.empty_like(x)
+    lib = _lib.load()
+    null = ctypes.c_void_p(None)
+    k0, k1 = (torch.cuda.Event(enable_timing=True) for _ in range(2))
+    for e in (k0, k1):
+        e.record()
+    torch.cuda.synchronize()
+    for family, expect_bf16 in (("l2_fwd", True), ("l2_bwd_x", False)):
+        assert lib.protoseg_timing_events(family.encode(), ctypes.c_void_p(k0.cuda_event),
+                                          ctypes.c_void_p(k1.cuda_event)) == 0
+        try:
+            if family == "l2_fwd":
+                dist = torch.empty(B, P, h, w, device=dev)
+                _lib.call("protoseg_l2_fwd", _lib.ptr(x), _lib.F32, B, 64, h, w, _lib.ptr(protos), P, _lib.ptr(w_last),
+                          K, 1e-4, _lib.ACT_LOG, _lib.PREC_BF16X3, _lib.ptr(dist), null, null, _lib.stream_of(dev))
+            else:
+                _lib.call("protoseg_l2_bwd", _lib.ptr(x), _lib.F32, B, 64, h, w, _lib.ptr(protos), P, _lib.ptr(w_last),
+                          K, 1e-4, _lib.ACT_LOG, _lib.PREC_BF16X3, _lib.ptr(g_logits), null, _lib.ptr(g_x), null, null,
+                          null, 0, _lib.stream_of(dev))
+            torch.cuda.synchronize()
+        finally:
+            assert lib.protoseg_timing_events(None, None, None) == 0
+        name = lib.protoseg_timing_kernel().decode()
+        assert name == (f"{family}_bf16_kernel" if expect_bf16 else f"{family}_kernel"), name
+        assert k0.elapsed_time(k1) > 0.0
