@@ -44,15 +44,40 @@ hipError_t record(hipEvent_t e, hipStream_t s) {
 }
 }  // namespace
 
+namespace {
+thread_local bool t_span_active = false;
+// Exact kernel name, or a family prefix: "l2_fwd" matches l2_fwd_kernel and l2_fwd_bf16_kernel,
+// whichever family serves the call. Caller holds g_timer_mu.
+bool hook_matches(const char* kernel) {
+  if (!g_timer_start) return false;
+  const size_t n = g_timer_kernel.size();
+  return g_timer_kernel == kernel || (std::strncmp(kernel, g_timer_kernel.c_str(), n) == 0 && kernel[n] == '_');
+}
+}  // namespace
+
+KernelSpan::KernelSpan(const char* kernel_a, const char* kernel_b, hipStream_t s) {
+  std::lock_guard<std::mutex> lock(g_timer_mu);
+  if (t_span_active || !(hook_matches(kernel_a) || hook_matches(kernel_b))) return;
+  if (record(g_timer_start, s) == hipSuccess) {
+    t_span_active = true;
+    stop_ = g_timer_stop;
+    s_ = s;
+  }
+}
+
+KernelSpan::~KernelSpan() {
+  if (!stop_) return;
+  (void)record(stop_, s_);
+  t_span_active = false;
+}
+
 KernelTimer::KernelTimer(const char* kernel, hipStream_t s) {
   std::lock_guard<std::mutex> lock(g_timer_mu);
-  // Match the exact kernel name, or a family prefix: "l2_fwd" brackets l2_fwd_kernel and
-  // l2_fwd_bf16_kernel, whichever family serves the call.
-  if (!g_timer_start) return;
-  const size_t n = g_timer_kernel.size();
-  const bool match = g_timer_kernel == kernel ||
-                     (std::strncmp(kernel, g_timer_kernel.c_str(), n) == 0 && kernel[n] == '_');
-  if (!match) return;
+  if (!hook_matches(kernel)) return;
+  if (t_span_active) {  // inside a matching span: name the kernel, leave the events to the span
+    g_timer_last = kernel;
+    return;
+  }
   if (record(g_timer_start, s) == hipSuccess) {
     g_timer_last = kernel;
     stop_ = g_timer_stop;

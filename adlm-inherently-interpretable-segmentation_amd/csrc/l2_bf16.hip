@@ -80,8 +80,8 @@ __device__ void stage_pt_perm(bf16* img, const float* __restrict__ protos, int P
 
 // (act_unit W) image [T][npt][32 k][32 p-permuted] (CPR 4) — A operand of logits = W . act.
 template <int T>
-__device__ void stage_w_perm(bf16* img, const float* __restrict__ w, int K, int P, int Pp, float scale, int tid,
-                             int nth) {
+__device__ void stage_w_perm(bf16* img, const float* __restrict__ w, int K, int P, int ldw, int Pp, float scale,
+                             int tid, int nth) {
   const int plane = Pp * 32;
   for (int idx = tid; idx < Pp * 4; idx += nth) {
     const int row = idx >> 2, e8 = idx & 3;  // row = pt*32 + k
@@ -91,7 +91,7 @@ __device__ void stage_w_perm(bf16* img, const float* __restrict__ w, int K, int 
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
         const int p = pt * 32 + perm_of(e8 * 8 + jj);
-        const float t = w[static_cast<size_t>(k < K ? k : 0) * P + (p < P ? p : P - 1)];
+        const float t = w[static_cast<size_t>(k < K ? k : 0) * ldw + (p < P ? p : P - 1)];
         v[jj] = (k < K && p < P) ? scale * t : 0.f;
       }
     bf16x8 f[T];
@@ -103,8 +103,8 @@ __device__ void stage_w_perm(bf16* img, const float* __restrict__ w, int K, int 
 // (grad_unit W)^T image [T][Pp][32 k] natural classes (CPR 4) — operand of g_act: A in layout A
 // (lane = p), B in layout B (lane = p).
 template <int T>
-__device__ void stage_wt_rows(bf16* img, const float* __restrict__ w, int K, int P, int Pp, float scale, int tid,
-                              int nth) {
+__device__ void stage_wt_rows(bf16* img, const float* __restrict__ w, int K, int P, int ldw, int Pp, float scale,
+                              int tid, int nth) {
   const int plane = Pp * 32;
   for (int idx = tid; idx < Pp * 4; idx += nth) {
     const int p = idx >> 2, e8 = idx & 3;
@@ -113,7 +113,7 @@ __device__ void stage_wt_rows(bf16* img, const float* __restrict__ w, int K, int
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
         const int k = e8 * 8 + jj;
-        const float t = w[static_cast<size_t>(k < K ? k : 0) * P + (p < P ? p : P - 1)];
+        const float t = w[static_cast<size_t>(k < K ? k : 0) * ldw + (p < P ? p : P - 1)];
         v[jj] = (k < K && p < P) ? scale * t : 0.f;
       }
     bf16x8 f[T];
@@ -170,7 +170,8 @@ __host__ __device__ inline ImgOffsets img_offsets(int Pp, int T) {
 // blockIdx.y selects the image, so the five loops (each a few load round trips) run concurrently.
 template <int T>
 __global__ __launch_bounds__(256) void l2_prep_bf16_kernel(const float* __restrict__ protos, int P, int Pp,
-                                                           const float* __restrict__ w_last, int K, float w_scale,
+                                                           const float* __restrict__ w_last, int K, int ldw,
+                                                           float w_scale,
                                                            float wt_scale, unsigned char* __restrict__ block) {
   const ImgOffsets o = img_offsets(Pp, T);
   const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
@@ -179,13 +180,13 @@ __global__ __launch_bounds__(256) void l2_prep_bf16_kernel(const float* __restri
       stage_p_rows<T>(reinterpret_cast<bf16*>(block + o.p), protos, P, Pp, tid, nth);
       break;
     case 1:
-      stage_wt_rows<T>(reinterpret_cast<bf16*>(block + o.wt), w_last, w_last ? K : 0, P, Pp, wt_scale, tid, nth);
+      stage_wt_rows<T>(reinterpret_cast<bf16*>(block + o.wt), w_last, w_last ? K : 0, P, ldw, Pp, wt_scale, tid, nth);
       break;
     case 2:
       stage_pt_perm<T>(reinterpret_cast<bf16*>(block + o.pt), protos, P, Pp, tid, nth);
       break;
     case 3:
-      stage_w_perm<T>(reinterpret_cast<bf16*>(block + o.w), w_last, w_last ? K : 0, P, Pp, w_scale, tid, nth);
+      stage_w_perm<T>(reinterpret_cast<bf16*>(block + o.w), w_last, w_last ? K : 0, P, ldw, Pp, w_scale, tid, nth);
       break;
     default: {
       float* p2 = reinterpret_cast<float*>(block + o.p2);
@@ -436,7 +437,7 @@ template <typename TX, int T, int ACT, bool GD>
 __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
     const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const unsigned char* __restrict__ img, int P, int Pp,
     int K, float eps, const float* __restrict__ g_logits, unsigned gl_bytes,
-    const float* __restrict__ g_dist, unsigned gd_bytes, TX* __restrict__ g_x) {
+    const float* __restrict__ g_dist, unsigned gd_bytes, TX* __restrict__ g_x, int accumulate) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const ImgOffsets io = img_offsets(Pp, T);
   bf16* Pimg = reinterpret_cast<bf16*>(smem_raw);                 // [T][Pp][64]
@@ -539,7 +540,9 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) {
           const int q = 2 * ct + s;
-          BufIO<TX>::store(rgx, gx[ct][8 * s + jj] + gsum_all * (2.f * raw[q * 8 + jj]), xoff, chan_base(q, jj) * cs);
+          float v = gx[ct][8 * s + jj] + gsum_all * (2.f * raw[q * 8 + jj]);
+          if (accumulate) v = BufIO<TX>::load(rgx, xoff, chan_base(q, jj) * cs) + v;  // prototype chunks
+          BufIO<TX>::store(rgx, v, xoff, chan_base(q, jj) * cs);
         }
   };
 
@@ -902,7 +905,7 @@ __global__ __launch_bounds__(MAXT) void l2_bwd_pw_bf16_kernel(
 // Slab sum: 64 elements x 4 slab groups per workgroup, groups combined in fixed order; each
 // thread keeps 8 independent loads in flight.
 __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __restrict__ slab, int S, int P,
-                                                                  int Pp, int K, const float* __restrict__ protos,
+                                                                  int Pp, int K, int ldw, const float* __restrict__ protos,
                                                                   float w_unit, float* __restrict__ g_protos,
                                                                   float* __restrict__ g_w) {
   __shared__ float part[4][64];
@@ -950,7 +953,7 @@ __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __
   } else {
     const int e2 = e - Pp * kC;
     const int k = e2 / Pp, pp = e2 - k * Pp;
-    if (g_w && k < K && pp < P) g_w[static_cast<size_t>(k) * P + pp] = tot * w_unit;  // act = act_unit * act_base
+    if (g_w && k < K && pp < P) g_w[static_cast<size_t>(k) * ldw + pp] = tot * w_unit;  // act = act_unit * act_base
   }
 }
 
@@ -1005,7 +1008,7 @@ int fwd_t(const Geometry& g, const Bytes& nb, const void* x, const unsigned char
 
 template <typename TX, int T, int ACT, bool GD>
 int bwd_x_t(const Geometry& g, const Bytes& nb, const void* x, const unsigned char* img, float eps,
-            const float* g_logits, const float* g_dist, void* g_x, hipStream_t stream) {
+            const float* g_logits, const float* g_dist, void* g_x, int accumulate, hipStream_t stream) {
   if (int st = ensure_lds<l2_bwd_x_bf16_kernel<TX, T, ACT, GD>>()) return st;
   const size_t lds = bwd_x_lds(g, T);
   const int cap = resident_blocks<l2_bwd_x_bf16_kernel<TX, T, ACT, GD>>(kWavesA * 64, lds);
@@ -1013,7 +1016,7 @@ int bwd_x_t(const Geometry& g, const Bytes& nb, const void* x, const unsigned ch
   KernelTimer timer("l2_bwd_x_bf16_kernel", stream);
   hipLaunchKernelGGL((l2_bwd_x_bf16_kernel<TX, T, ACT, GD>), dim3(want < cap ? want : cap), dim3(kWavesA * 64), lds,
                      stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, img, g.P, g.Pp, g.K, eps, g_logits, nb.gl,
-                     g_dist, nb.gd, static_cast<TX*>(g_x));
+                     g_dist, nb.gd, static_cast<TX*>(g_x), accumulate);
   return check_launch("l2_bwd_x_bf16_kernel");
 }
 
@@ -1033,7 +1036,7 @@ int bwd_pw_launch(const Geometry& g, const Bytes& nb, const void* x, const float
   if (int st = check_launch("l2_bwd_pw_bf16_kernel")) return st;
   const int elems = g.Pp * kC + 32 * g.Pp;
   hipLaunchKernelGGL(l2_bwd_reduce_bf16_kernel, dim3(static_cast<unsigned>(ceil_div(elems, 64))), dim3(256), 0,
-                     stream, ws, grid, g.P, g.Pp, g.K, protos, act_unit(ACT), g_protos, g_logits ? g_w : nullptr);
+                     stream, ws, grid, g.P, g.Pp, g.K, g.ldw, protos, act_unit(ACT), g_protos, g_logits ? g_w : nullptr);
   return check_launch("l2_bwd_reduce_bf16_kernel");
 }
 
@@ -1116,9 +1119,11 @@ int launch_prep_bf16(const Geometry& g, int terms, const float* protos, const fl
   unsigned char* blk = static_cast<unsigned char*>(img);
   const float ws = act_unit(act_kind), wts = act_grad_unit(act_kind, eps);
   if (terms == 2)
-    hipLaunchKernelGGL(l2_prep_bf16_kernel<2>, grid, dim3(256), 0, stream, protos, g.P, g.Pp, w_last, g.K, ws, wts, blk);
+    hipLaunchKernelGGL(l2_prep_bf16_kernel<2>, grid, dim3(256), 0, stream, protos, g.P, g.Pp, w_last, g.K, g.ldw, ws,
+                       wts, blk);
   else
-    hipLaunchKernelGGL(l2_prep_bf16_kernel<3>, grid, dim3(256), 0, stream, protos, g.P, g.Pp, w_last, g.K, ws, wts, blk);
+    hipLaunchKernelGGL(l2_prep_bf16_kernel<3>, grid, dim3(256), 0, stream, protos, g.P, g.Pp, w_last, g.K, g.ldw, ws,
+                       wts, blk);
   return check_launch("l2_prep_bf16_kernel");
 }
 
@@ -1139,14 +1144,15 @@ int launch_fwd_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, co
 }
 
 int launch_bwd_x_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const void* img, float eps,
-                      int act_kind, const float* g_logits, const float* g_dist, void* g_x, hipStream_t stream) {
+                      int act_kind, const float* g_logits, const float* g_dist, void* g_x, hipStream_t stream,
+                      int accumulate) {
   const Bytes nb = bytes_of(g, x_bf16, nullptr, nullptr, nullptr, g_logits, g_dist);
   const unsigned char* blk = static_cast<const unsigned char*>(img);
   return by_type(x_bf16, terms, act_kind, [&](auto tx, auto tt, auto aa) {
     using TX = std::remove_pointer_t<decltype(tx)>;
     constexpr int kT = decltype(tt)::value, kA = decltype(aa)::value;
-    if (g_dist) return bwd_x_t<TX, kT, kA, true>(g, nb, x, blk, eps, g_logits, g_dist, g_x, stream);
-    return bwd_x_t<TX, kT, kA, false>(g, nb, x, blk, eps, g_logits, g_dist, g_x, stream);
+    if (g_dist) return bwd_x_t<TX, kT, kA, true>(g, nb, x, blk, eps, g_logits, g_dist, g_x, accumulate, stream);
+    return bwd_x_t<TX, kT, kA, false>(g, nb, x, blk, eps, g_logits, g_dist, g_x, accumulate, stream);
   });
 }
 

@@ -10,6 +10,7 @@ namespace protoseg {
 struct Geometry {
   int C, P, Pp, K, HW;
   int npix, ntiles;  // B*H*W pixels, 32-pixel tiles
+  int ldw = 0;       // row stride of w_last / g_w (= P, or the full P for a prototype chunk)
 };
 
 // bf16 split family (C = 64). `terms` = 2 (3 products) or 3 (6 products).
@@ -27,8 +28,10 @@ int launch_prep_bf16(const Geometry& g, int terms, const float* protos, const fl
 
 int launch_fwd_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const void* img, float eps, int act_kind,
                     float* dist, float* act, float* logits, hipStream_t stream);
+// accumulate != 0: g_x += this call's gradient (prototype chunks of one backward).
 int launch_bwd_x_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const void* img, float eps,
-                      int act_kind, const float* g_logits, const float* g_dist, void* g_x, hipStream_t stream);
+                      int act_kind, const float* g_logits, const float* g_dist, void* g_x, hipStream_t stream,
+                      int accumulate = 0);
 int launch_bwd_pw_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const float* protos, const void* img,
                        float eps, int act_kind, const float* g_logits, const float* g_dist, float* g_protos,
                        float* g_w, float* ws, hipStream_t stream);

@@ -50,6 +50,22 @@ class KernelTimer {
   hipStream_t s_ = nullptr;
 };
 
+// A call that runs a kernel several times (the prototype-chunked backward) brackets the whole
+// sequence instead: while a KernelSpan that matched the hook is alive, the KernelTimers inside
+// it record nothing, and the span's events cover everything launched in between (conservative:
+// the chunks' prep and reduce launches are inside).
+class KernelSpan {
+ public:
+  KernelSpan(const char* kernel_a, const char* kernel_b, hipStream_t s);
+  ~KernelSpan();
+  KernelSpan(const KernelSpan&) = delete;
+  KernelSpan& operator=(const KernelSpan&) = delete;
+
+ private:
+  hipEvent_t stop_ = nullptr;
+  hipStream_t s_ = nullptr;
+};
+
 // Workgroups of `kernel` resident on the whole device at (threads, lds): CUs x blocks per CU
 // from the occupancy calculator (VGPRs and LDS), at least the CU count. Cached per
 // (kernel, threads, lds) of the first call — the launchers use one configuration per shape.

@@ -114,10 +114,12 @@ def test_forward_backward_vs_oracle(device, B, C, h, w, P, K, activation, precis
     assert_scaled_close(gw, ref_gw, 1e-4, "g_w")
 
 
+@pytest.mark.parametrize("P", [57, 361])
 @pytest.mark.parametrize("precision", PRECISIONS)
-def test_bf16_features(device, precision):
-    """bf16 feature maps are read exactly (bf16 -> f32 is exact) and computed in f32."""
-    x, protos, w_last = po.synthetic_inputs(2, 64, 17, 19, 57, 19, seed=3)
+def test_bf16_features(device, precision, P):
+    """bf16 feature maps are read exactly (bf16 -> f32 is exact) and computed in f32 (P = 361:
+    the backward runs over prototype chunks, g_x accumulated in bf16 — tolerance 1e-2 holds)."""
+    x, protos, w_last = po.synthetic_inputs(2, 64, 17, 19, P, 19, seed=3)
     xb = x.to(torch.bfloat16)
     dist, logits, _ = run_layer(xb, protos, w_last, device=device, precision=precision)
     ref_logits, ref_dist = po.forward_from_conv_features(xb.float(), protos[:, :, None, None], w_last)
@@ -245,8 +247,9 @@ def test_timing_events_bracket_one_kernel():
 
 
 def test_timing_events_family_prefix_reports_the_family_that_ran():
-    """bench.py times kernels by family prefix: at P = 361 the x-backward runs on the f32
-    family (its bf16 LDS images do not fit), and the hook names that kernel."""
+    """bench.py times kernels by family prefix and the hook names the kernel that ran: the
+    forward in f32 precision runs the f32 family; the P = 361 x-backward runs the bf16 family
+    over prototype chunks (the hook keeps the last chunk's launch)."""
     import ctypes
 
     from protoseg_amd import _lib
@@ -262,14 +265,14 @@ def test_timing_events_family_prefix_reports_the_family_that_ran():
     for e in (k0, k1):
         e.record()
     torch.cuda.synchronize()
-    for family, expect_bf16 in (("l2_fwd", True), ("l2_bwd_x", False)):
+    for family, expect_bf16 in (("l2_fwd", False), ("l2_bwd_x", True)):
         assert lib.protoseg_timing_events(family.encode(), ctypes.c_void_p(k0.cuda_event),
                                           ctypes.c_void_p(k1.cuda_event)) == 0
         try:
             if family == "l2_fwd":
                 dist = torch.empty(B, P, h, w, device=dev)
                 _lib.call("protoseg_l2_fwd", _lib.ptr(x), _lib.F32, B, 64, h, w, _lib.ptr(protos), P, _lib.ptr(w_last),
-                          K, 1e-4, _lib.ACT_LOG, _lib.PREC_BF16X3, _lib.ptr(dist), null, null, _lib.stream_of(dev))
+                          K, 1e-4, _lib.ACT_LOG, _lib.PREC_F32, _lib.ptr(dist), null, null, _lib.stream_of(dev))
             else:
                 _lib.call("protoseg_l2_bwd", _lib.ptr(x), _lib.F32, B, 64, h, w, _lib.ptr(protos), P, _lib.ptr(w_last),
                           K, 1e-4, _lib.ACT_LOG, _lib.PREC_BF16X3, _lib.ptr(g_logits), null, _lib.ptr(g_x), null, null,
