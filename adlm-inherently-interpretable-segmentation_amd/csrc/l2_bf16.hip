@@ -437,7 +437,7 @@ template <typename TX, int T, int ACT, bool GD>
 __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
     const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const unsigned char* __restrict__ img, int P, int Pp,
     int K, float eps, const float* __restrict__ g_logits, unsigned gl_bytes,
-    const float* __restrict__ g_dist, unsigned gd_bytes, TX* __restrict__ g_x, int accumulate) {
+    const float* __restrict__ g_dist, unsigned gd_bytes, int gd_ld, int gd_p0, TX* __restrict__ g_x, int accumulate) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const ImgOffsets io = img_offsets(Pp, T);
   bf16* Pimg = reinterpret_cast<bf16*>(smem_raw);                 // [T][Pp][64]
@@ -486,7 +486,7 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
     }
     bf16x8 xb[kNQ][T];
     const float x2 = x_frags<T>(raw, xb);
-    const unsigned gdbase = valid ? static_cast<unsigned>(((b * P + 4 * h) * HW + n) * 4) : kOOB;
+    const unsigned gdbase = valid ? static_cast<unsigned>(((b * gd_ld + gd_p0 + 4 * h) * HW + n) * 4) : kOOB;
 #pragma unroll 1
     for (int pt = pt0; pt < npt; pt += dpt) {
       float gdv[16];  // upstream distance gradient of this tile, loaded before the MFMAs
@@ -658,7 +658,8 @@ template <typename TX, int T, int ACT, int MAXT, bool GD>
 __global__ __launch_bounds__(MAXT) void l2_bwd_pw_bf16_kernel(
     const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const unsigned char* __restrict__ img, int P, int Pp,
     int K, float eps, const float* __restrict__ g_logits, unsigned gl_bytes,
-    const float* __restrict__ g_dist, unsigned gd_bytes, int streams, float* __restrict__ slab) {
+    const float* __restrict__ g_dist, unsigned gd_bytes, int gd_ld, int gd_p0, int streams,
+    float* __restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   using R = PwRaw<TX>;
   using S = PwStage<TX, T>;
@@ -776,7 +777,7 @@ __global__ __launch_bounds__(MAXT) void l2_bwd_pw_bf16_kernel(
         const int g = t * 32 + lane;
         const bool ok = t < ntiles && g < npix;
         const int b = ok ? g / HW : 0;
-        rowoff[lane] = ok ? static_cast<unsigned>((b * P * HW + (g - b * HW)) * 4) : kOOB;
+        rowoff[lane] = ok ? static_cast<unsigned>(((b * gd_ld + gd_p0) * HW + (g - b * HW)) * 4) : kOOB;
       }
     }
   };
@@ -1016,7 +1017,7 @@ int bwd_x_t(const Geometry& g, const Bytes& nb, const void* x, const unsigned ch
   KernelTimer timer("l2_bwd_x_bf16_kernel", stream);
   hipLaunchKernelGGL((l2_bwd_x_bf16_kernel<TX, T, ACT, GD>), dim3(want < cap ? want : cap), dim3(kWavesA * 64), lds,
                      stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, img, g.P, g.Pp, g.K, eps, g_logits, nb.gl,
-                     g_dist, nb.gd, static_cast<TX*>(g_x), accumulate);
+                     g_dist, nb.gd, g.ldd, g.p0, static_cast<TX*>(g_x), accumulate);
   return check_launch("l2_bwd_x_bf16_kernel");
 }
 
@@ -1031,7 +1032,7 @@ int bwd_pw_launch(const Geometry& g, const Bytes& nb, const void* x, const float
     KernelTimer timer("l2_bwd_pw_bf16_kernel", stream);
     hipLaunchKernelGGL((l2_bwd_pw_bf16_kernel<TX, T, ACT, MAXT, GD>), dim3(grid), dim3(threads),
                        pw_lds(g, T, sizeof(TX) == 2), stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, img,
-                       g.P, g.Pp, g.K, eps, g_logits, nb.gl, g_dist, nb.gd, streams, ws);
+                       g.P, g.Pp, g.K, eps, g_logits, nb.gl, g_dist, nb.gd, g.ldd, g.p0, streams, ws);
   }
   if (int st = check_launch("l2_bwd_pw_bf16_kernel")) return st;
   const int elems = g.Pp * kC + 32 * g.Pp;
@@ -1080,7 +1081,7 @@ Bytes bytes_of(const Geometry& g, bool x_bf16, const void* dist, const void* act
   nb.a = act ? d : 0u;
   nb.l = logits ? l : 0u;
   nb.gl = g_logits ? l : 0u;
-  nb.gd = g_dist ? d : 0u;
+  nb.gd = g_dist ? static_cast<unsigned>(npix * g.ldd * 4) : 0u;
   return nb;
 }
 

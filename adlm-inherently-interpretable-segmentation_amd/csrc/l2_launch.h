@@ -11,10 +11,13 @@ struct Geometry {
   int C, P, Pp, K, HW;
   int npix, ntiles;  // B*H*W pixels, 32-pixel tiles
   int ldw = 0;       // row stride of w_last / g_w (= P, or the full P for a prototype chunk)
+  int ldd = 0, p0 = 0;  // g_dist: prototypes per image (= P, or the full P) and the chunk's first
 };
 
 // bf16 split family (C = 64). `terms` = 2 (3 products) or 3 (6 products).
 bool bf16_fwd_fits(const Geometry& g, int terms);
+// Every [npix, max(P, C)] f32 buffer below 2^31 bytes (buffer-resource offsets are 32-bit).
+bool bf16_sizes_ok(const Geometry& g);
 bool bf16_bwd_x_fits(const Geometry& g, int terms);
 bool bf16_bwd_pw_fits(const Geometry& g, int terms);
 size_t bf16_bwd_pw_workspace(const Geometry& g);

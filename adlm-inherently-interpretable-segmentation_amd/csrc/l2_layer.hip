@@ -477,6 +477,8 @@ int validate(const void* x, int x_dtype, int B, int C, int H, int W, const float
   geo->npix = static_cast<int>(npix);
   geo->ntiles = static_cast<int>(ceil_div(npix, 32));
   geo->ldw = P;
+  geo->ldd = P;
+  geo->p0 = 0;
   return PROTOSEG_OK;
 }
 
@@ -581,6 +583,8 @@ Geometry geometry_of(int B, int C, int H, int W, int P, int K) {
   g.npix = B * H * W;
   g.ntiles = static_cast<int>(ceil_div(g.npix, 32));
   g.ldw = P;
+  g.ldd = P;
+  g.p0 = 0;
   return g;
 }
 
@@ -696,27 +700,28 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
   float* ws = static_cast<float*>(workspace);
   // P too large for the bf16 backward's LDS images (e.g. P = 361, 19 prototypes/class): run it
   // over prototype chunks of <= 192. g_P rows and g_W columns are per prototype; g_x is a sum
-  // over prototypes, so chunk c > 0 adds to it. (With g_dist the f32 family below serves.)
-  if (terms && !g_dist && C == 64 && !bf16_bwd_x_fits(geo, terms)) {
+  // over prototypes, so chunk c > 0 adds to it; g_dist rows are read at (b * P + p0 + p).
+  if (terms && C == 64 && !bf16_bwd_x_fits(geo, terms)) {
     const int nchunk = static_cast<int>(ceil_div(P, 192));
     const int per = static_cast<int>(ceil_div(P, nchunk));
     Geometry gc = geometry_of(B, C, H, W, per, K);
-    gc.ldw = P;
-    if (nchunk > 1 && bf16_bwd_x_fits(gc, terms) && bf16_bwd_pw_fits(gc, terms)) {
+    gc.ldw = gc.ldd = P;
+    if (nchunk > 1 && bf16_bwd_x_fits(gc, terms) && bf16_bwd_pw_fits(gc, terms) && bf16_sizes_ok(geo)) {
       KernelSpan span(g_x ? "l2_bwd_x_bf16_kernel" : "", (g_protos || g_w) ? "l2_bwd_pw_bf16_kernel" : "", s);
       for (int c = 0; c < nchunk; ++c) {
         const int p0 = c * per, pc = P - p0 < per ? P - p0 : per;
         gc = geometry_of(B, C, H, W, pc, K);
-        gc.ldw = P;
+        gc.ldw = gc.ldd = P;
+        gc.p0 = p0;
         const float* wc = g_logits ? w_last + p0 : nullptr;
         ImageBlock img;
         if (int st = img.build(gc, terms, protos + static_cast<size_t>(p0) * C, wc, act_kind, eps, s)) return st;
         if (g_x)
-          if (int st = launch_bwd_x_bf16(gc, xb, terms, x, img.ptr, eps, act_kind, g_logits, nullptr, g_x, s, c > 0))
+          if (int st = launch_bwd_x_bf16(gc, xb, terms, x, img.ptr, eps, act_kind, g_logits, g_dist, g_x, s, c > 0))
             return st;
         if (g_protos || g_w)
           if (int st = launch_bwd_pw_bf16(gc, xb, terms, x, protos + static_cast<size_t>(p0) * C, img.ptr, eps,
-                                          act_kind, g_logits, nullptr,
+                                          act_kind, g_logits, g_dist,
                                           g_protos ? g_protos + static_cast<size_t>(p0) * C : nullptr,
                                           g_w ? g_w + p0 : nullptr, ws, s))
             return st;

@@ -283,3 +283,24 @@ def test_timing_events_family_prefix_reports_the_family_that_ran():
         name = lib.protoseg_timing_kernel().decode()
         assert name == (f"{family}_bf16_kernel" if expect_bf16 else f"{family}_kernel"), name
         assert k0.elapsed_time(k1) > 0.0
+
+
+@pytest.mark.parametrize("with_logits", [True, False])
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_prototype_chunked_backward_with_g_dist(device, precision, with_logits):
+    """P = 361 backward with an upstream distance gradient (the KLD path, module.py:167-208):
+    the bf16 family runs over prototype chunks reading g_dist rows at (b * P + p0 + p)."""
+    B, h, w, P, K = 2, 23, 29, 361, 19
+    x, protos, w_last = po.synthetic_inputs(B, 64, h, w, P, K, seed=361)
+    gen = torch.Generator().manual_seed(8)
+    g_logits = torch.randn(B, h, w, K, generator=gen) if with_logits else None
+    g_dist = torch.randn(B, P, h, w, generator=gen) * 0.1
+    _, _, ref_gx, ref_gp, ref_gw = po.forward_backward(x, protos, w_last, g_logits, g_dist)
+    ops = _ops()
+    gx, gp, gw = ops.l2_backward(x.to(device), protos.to(device), w_last.to(device),
+                                 g_logits.to(device) if with_logits else None, g_dist.to(device), 1e-4, 0,
+                                 prec(precision), True, True, with_logits)
+    assert_scaled_close(gx, ref_gx, 1e-4, "g_x(+g_dist, chunked)")
+    assert_scaled_close(gp, ref_gp, 1e-4, "g_protos(+g_dist, chunked)")
+    if with_logits:
+        assert_scaled_close(gw, ref_gw, 1e-4, "g_w(chunked)")
