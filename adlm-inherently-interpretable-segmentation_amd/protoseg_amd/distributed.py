@@ -75,6 +75,17 @@ def reduce_push_state(state, group=None) -> None:
         state.geometry.update(g)
 
 
+def reduce_bound_boxes(boxes, device="cpu", group=None):
+    """Merges per-rank push bound boxes (push.py:338-343): each rank fills the rows of the
+    prototypes whose winning image lies in its shard and leaves -1 elsewhere, so one MAX
+    all-reduce gives every rank the full table. Returns a numpy int64 array."""
+    import numpy as np
+    t = torch.as_tensor(np.asarray(boxes, dtype=np.int64), device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return t.cpu().numpy()
+
+
 class GradientBuckets:
     """Sums .grad of ``params`` over ranks with a few large asynchronous all-reduces.
 

@@ -300,7 +300,7 @@ def push_prototypes(dataset, prototype_network_parallel, prototype_layer_stride=
     are merged exactly (distributed.reduce_push_state): the result equals the serial scan."""
     from PIL import Image
 
-    from .distributed import reduce_push_state, shard_bounds, world_info
+    from .distributed import reduce_bound_boxes, reduce_push_state, shard_bounds, world_info
 
     ppnet = prototype_network_parallel.module if hasattr(prototype_network_parallel, "module") \
         else prototype_network_parallel
@@ -373,10 +373,7 @@ def push_prototypes(dataset, prototype_network_parallel, prototype_layer_stride=
         if with_class:
             proto_bound_boxes[j, 5] = proto_class[j]
     if world > 1:
-        import torch.distributed as tdist
-        t = torch.as_tensor(proto_bound_boxes, device=device)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX, group=process_group)
-        proto_bound_boxes = t.cpu().numpy()
+        proto_bound_boxes = reduce_bound_boxes(proto_bound_boxes, device, process_group)
     if proto_epoch_dir is not None and proto_bound_boxes_filename_prefix is not None:
         np.save(os.path.join(proto_epoch_dir, f"{proto_bound_boxes_filename_prefix}-receptive_field{epoch_number}.npy"),
                 proto_rf_boxes)

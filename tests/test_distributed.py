@@ -9,7 +9,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from protoseg_amd.distributed import GradientBuckets, reduce_push_state, shard_bounds
+from protoseg_amd.distributed import GradientBuckets, reduce_bound_boxes, reduce_push_state, shard_bounds
 from protoseg_amd.push import PushState
 
 
@@ -70,7 +70,13 @@ def _worker(rank, world, port, n_img, P, C, result_q):
         gb.allreduce()
         gb.wait()
         grads = [p.grad.clone() for p in params]
-        result_q.put((rank, st.dist, st.img, st.patch, st.fmap, len(st.geometry), grads, len(gb.buckets)))
+        # bound boxes: rank r owns the prototypes whose winning image lies in its shard
+        boxes = torch.full((P, 6), -1, dtype=torch.int64)
+        for j in range(P):
+            if lo <= int(st.img[j]) < hi:
+                boxes[j] = torch.tensor([int(st.img[j]), j, j + 3, 2 * j, 2 * j + 5, j % 4])
+        merged = reduce_bound_boxes(boxes.numpy())
+        result_q.put((rank, st.dist, st.img, st.patch, st.fmap, len(st.geometry), grads, len(gb.buckets), merged))
     finally:
         dist.destroy_process_group()
 
@@ -89,8 +95,11 @@ def test_sharded_push_reduction_equals_serial_scan(n_img):
         p.join(timeout=60)
         assert p.exitcode == 0
     best, img, patch, fmap = _serial_truth(_make_images(n_img, P, C))
-    for rank, d, im, pa, fm, ngeo, grads, nbuckets in results:
+    for rank, d, im, pa, fm, ngeo, grads, nbuckets, boxes in results:
         assert ngeo == n_img
+        for j in range(P):  # every rank holds the union of the per-shard bound boxes
+            exp = [-1] * 6 if img[j] < 0 else [img[j], j, j + 3, 2 * j, 2 * j + 5, j % 4]
+            assert list(boxes[j]) == exp
         for j in range(P):
             if img[j] < 0:
                 assert im[j].item() == -1 and math.isinf(d[j].item())
