@@ -287,7 +287,8 @@ template <typename TX, int T, int ACT, bool ACTS, bool LOGITS>
 __global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
     const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const unsigned char* __restrict__ img, int P, int Pp,
     int K, float eps, float* __restrict__ dist, unsigned d_bytes,
-    float* __restrict__ act_out, unsigned a_bytes, float* __restrict__ logits, unsigned l_bytes) {
+    float* __restrict__ act_out, unsigned a_bytes, float* __restrict__ logits, unsigned l_bytes, int ld, int p0,
+    int accumulate) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   STAMP(0);
   STAMP_RT(7);
@@ -328,8 +329,10 @@ __global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
     const bool valid = g < npix;
     const int b = valid ? g / HW : 0;
     const int n = valid ? g - b * HW : 0;
-    const unsigned dbase = valid ? static_cast<unsigned>(((b * P + 4 * h) * HW + n) * 4) : kOOB;
-    const unsigned abase = valid ? static_cast<unsigned>((g * P + 4 * h) * 4) : kOOB;
+    // ld = prototypes per image / pixel row of the outputs (= P, or the full P for a chunk
+    // starting at prototype p0)
+    const unsigned dbase = valid ? static_cast<unsigned>(((b * ld + p0 + 4 * h) * HW + n) * 4) : kOOB;
+    const unsigned abase = valid ? static_cast<unsigned>((g * ld + p0 + 4 * h) * 4) : kOOB;
     f32x16 lacc = zero16();
     // Prototype tiles entirely below P store without a row predicate; only the last one (when
     // P is not a multiple of 32) pays for it. The body is instantiated for both cases.
@@ -376,8 +379,12 @@ __global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
     const unsigned lbase = g < npix ? static_cast<unsigned>((g * K + 4 * h) * 4) : kOOB;
     const int krem = K - 4 * h;
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
-      BufIO<float>::store(rl, lacc[r], row_of(r) < krem ? lbase : kOOB, static_cast<unsigned>(row_of(r) * 4));
+    for (int r = 0; r < 16; ++r) {
+      const unsigned off = row_of(r) < krem ? lbase : kOOB;
+      float v = lacc[r];
+      if (accumulate) v = BufIO<float>::load(rl, off, static_cast<unsigned>(row_of(r) * 4)) + v;  // chunk c > 0
+      BufIO<float>::store(rl, v, off, static_cast<unsigned>(row_of(r) * 4));
+    }
   };
 
   // ---- full rounds: one tile per wave per round. At 2 waves per SIMD the next tile's x is
@@ -993,7 +1000,7 @@ struct Bytes {
 
 template <typename TX, int T, int ACT, bool ACTS, bool LOGITS>
 int fwd_t(const Geometry& g, const Bytes& nb, const void* x, const unsigned char* img, float eps, float* dist,
-          float* act, float* logits, hipStream_t stream) {
+          float* act, float* logits, int accumulate, hipStream_t stream) {
   if (int st = ensure_lds<l2_fwd_bf16_kernel<TX, T, ACT, ACTS, LOGITS>>()) return st;
   const size_t lds = fwd_lds(g, T);
   // Persistent: one generation of resident workgroups; waves stride over the tiles and
@@ -1003,7 +1010,7 @@ int fwd_t(const Geometry& g, const Bytes& nb, const void* x, const unsigned char
   KernelTimer timer("l2_fwd_bf16_kernel", stream);
   hipLaunchKernelGGL((l2_fwd_bf16_kernel<TX, T, ACT, ACTS, LOGITS>), dim3(want < cap ? want : cap), dim3(kWavesF * 64), lds,
                      stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, img, g.P, g.Pp, g.K, eps, dist, nb.d, act,
-                     nb.a, logits, nb.l);
+                     nb.a, logits, nb.l, g.ldd, g.p0, accumulate);
   return check_launch("l2_fwd_bf16_kernel");
 }
 
@@ -1075,13 +1082,13 @@ Bytes bytes_of(const Geometry& g, bool x_bf16, const void* dist, const void* act
                const void* g_logits, const void* g_dist) {
   Bytes nb;
   const unsigned long long npix = static_cast<unsigned long long>(g.npix);
-  const unsigned d = static_cast<unsigned>(npix * g.P * 4), l = static_cast<unsigned>(npix * g.K * 4);
+  const unsigned d = static_cast<unsigned>(npix * g.ldd * 4), l = static_cast<unsigned>(npix * g.K * 4);
   nb.x = static_cast<unsigned>(npix * kC * (x_bf16 ? 2 : 4));
   nb.d = dist ? d : 0u;
   nb.a = act ? d : 0u;
   nb.l = logits ? l : 0u;
   nb.gl = g_logits ? l : 0u;
-  nb.gd = g_dist ? static_cast<unsigned>(npix * g.ldd * 4) : 0u;
+  nb.gd = g_dist ? d : 0u;
   return nb;
 }
 
@@ -1129,18 +1136,18 @@ int launch_prep_bf16(const Geometry& g, int terms, const float* protos, const fl
 }
 
 int launch_fwd_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const void* img, float eps, int act_kind,
-                    float* dist, float* act, float* logits, hipStream_t stream) {
+                    float* dist, float* act, float* logits, hipStream_t stream, int accumulate) {
   const Bytes nb = bytes_of(g, x_bf16, dist, act, logits, nullptr, nullptr);
   const unsigned char* blk = static_cast<const unsigned char*>(img);
   return by_type(x_bf16, terms, act_kind, [&](auto tx, auto tt, auto aa) {
     using TX = std::remove_pointer_t<decltype(tx)>;
     constexpr int kT = decltype(tt)::value, kA = decltype(aa)::value;
     if (act) {
-      if (logits) return fwd_t<TX, kT, kA, true, true>(g, nb, x, blk, eps, dist, act, logits, stream);
-      return fwd_t<TX, kT, kA, true, false>(g, nb, x, blk, eps, dist, act, logits, stream);
+      if (logits) return fwd_t<TX, kT, kA, true, true>(g, nb, x, blk, eps, dist, act, logits, accumulate, stream);
+      return fwd_t<TX, kT, kA, true, false>(g, nb, x, blk, eps, dist, act, logits, accumulate, stream);
     }
-    if (logits) return fwd_t<TX, kT, kA, false, true>(g, nb, x, blk, eps, dist, act, logits, stream);
-    return fwd_t<TX, kT, kA, false, false>(g, nb, x, blk, eps, dist, act, logits, stream);
+    if (logits) return fwd_t<TX, kT, kA, false, true>(g, nb, x, blk, eps, dist, act, logits, accumulate, stream);
+    return fwd_t<TX, kT, kA, false, false>(g, nb, x, blk, eps, dist, act, logits, accumulate, stream);
   });
 }
 

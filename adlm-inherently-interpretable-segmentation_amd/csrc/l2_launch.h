@@ -29,8 +29,10 @@ size_t bf16_image_bytes(const Geometry& g, int terms);
 int launch_prep_bf16(const Geometry& g, int terms, const float* protos, const float* w_last, int act_kind, float eps,
                      void* img, hipStream_t stream);
 
+// accumulate != 0: logits += this call's (prototype chunks of one forward).
 int launch_fwd_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const void* img, float eps, int act_kind,
-                    float* dist, float* act, float* logits, hipStream_t stream);
+                    float* dist, float* act, float* logits, hipStream_t stream,
+                    int accumulate = 0);
 // accumulate != 0: g_x += this call's gradient (prototype chunks of one backward).
 int launch_bwd_x_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const void* img, float eps,
                       int act_kind, const float* g_logits, const float* g_dist, void* g_x, hipStream_t stream,

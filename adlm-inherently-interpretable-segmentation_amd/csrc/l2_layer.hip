@@ -636,9 +636,15 @@ struct ImageBlock {
 };
 }  // namespace
 
+// Largest P the bf16 family serves through prototype chunks (C = 64).
+constexpr int kMaxChunkedP = 4096;
+
+bool f32_family_fits(int C, int Pp) { return layer_lds_bytes(C, Pp) <= kMaxLds; }
+
 extern "C" int protoseg_l2_supported(int C, int P, int K) {
   if (nc_of(C) == 0 || P <= 0 || K < 0 || K > 32) return 0;
-  return layer_lds_bytes(C, padded_protos(P)) <= kMaxLds ? 1 : 0;
+  if (f32_family_fits(C, padded_protos(P))) return 1;
+  return C == 64 && P <= kMaxChunkedP ? 1 : 0;  // bf16 precisions only, over prototype chunks
 }
 
 extern "C" int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P,
@@ -656,6 +662,37 @@ extern "C" int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, 
     return launch_fwd_bf16(geo, x_dtype == PROTOSEG_BF16, terms, x, img.ptr, eps, act_kind, dist_out, act_out,
                            logits_out, s);
   }
+  // P beyond the forward's LDS images (Pp > 384, e.g. 30 prototypes/class): prototype chunks of
+  // <= 384. Distance / activation rows land at (b * P + p0 + p); the logits are a sum over
+  // prototypes, so chunk c > 0 adds to them.
+  if (terms && C == 64 && bf16_sizes_ok(geo)) {
+    int nchunk = static_cast<int>(ceil_div(P, 384)), per = 0;
+    Geometry gc;
+    for (;; ++nchunk) {  // fewest chunks whose images fit (fewer rows per chunk at 3 terms)
+      per = static_cast<int>(ceil_div(P, nchunk));
+      gc = geometry_of(B, C, H, W, per, K);
+      if (bf16_fwd_fits(gc, terms) || per <= 32) break;
+    }
+    if (nchunk > 1 && bf16_fwd_fits(gc, terms)) {
+      KernelSpan span("l2_fwd_bf16_kernel", "", s);
+      for (int c = 0; c < nchunk; ++c) {
+        const int p0 = c * per, pc = P - p0 < per ? P - p0 : per;
+        gc = geometry_of(B, C, H, W, pc, K);
+        gc.ldw = gc.ldd = P;
+        gc.p0 = p0;
+        ImageBlock img;
+        if (int st = img.build(gc, terms, protos + static_cast<size_t>(p0) * C, logits_out ? w_last + p0 : nullptr,
+                               act_kind, eps, s))
+          return st;
+        if (int st = launch_fwd_bf16(gc, x_dtype == PROTOSEG_BF16, terms, x, img.ptr, eps, act_kind, dist_out,
+                                     act_out, logits_out, s, c > 0))
+          return st;
+      }
+      return PROTOSEG_OK;
+    }
+  }
+  if (!f32_family_fits(C, geo.Pp))
+    return fail(PROTOSEG_ERR_UNSUPPORTED, "C=%d P=%d: served by the bf16 precisions only (prototype chunks)", C, P);
   return dispatch(x_dtype, C, [&](auto tx, auto nc) {
     using TX = std::remove_pointer_t<decltype(tx)>;
     return launch_fwd<TX, decltype(nc)::value>(geo, x, protos, w_last, eps, act_kind, dist_out, act_out,
@@ -702,10 +739,13 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
   // over prototype chunks of <= 192. g_P rows and g_W columns are per prototype; g_x is a sum
   // over prototypes, so chunk c > 0 adds to it; g_dist rows are read at (b * P + p0 + p).
   if (terms && C == 64 && !bf16_bwd_x_fits(geo, terms)) {
-    const int nchunk = static_cast<int>(ceil_div(P, 192));
-    const int per = static_cast<int>(ceil_div(P, nchunk));
-    Geometry gc = geometry_of(B, C, H, W, per, K);
-    gc.ldw = gc.ldd = P;
+    int nchunk = static_cast<int>(ceil_div(P, 192)), per = 0;
+    Geometry gc;
+    for (;; ++nchunk) {  // fewest chunks whose images fit (fewer rows per chunk at 3 terms)
+      per = static_cast<int>(ceil_div(P, nchunk));
+      gc = geometry_of(B, C, H, W, per, K);
+      if ((bf16_bwd_x_fits(gc, terms) && bf16_bwd_pw_fits(gc, terms)) || per <= 32) break;
+    }
     if (nchunk > 1 && bf16_bwd_x_fits(gc, terms) && bf16_bwd_pw_fits(gc, terms) && bf16_sizes_ok(geo)) {
       KernelSpan span(g_x ? "l2_bwd_x_bf16_kernel" : "", (g_protos || g_w) ? "l2_bwd_pw_bf16_kernel" : "", s);
       for (int c = 0; c < nchunk; ++c) {
@@ -729,6 +769,8 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
       return PROTOSEG_OK;
     }
   }
+  if (!f32_family_fits(C, geo.Pp))
+    return fail(PROTOSEG_ERR_UNSUPPORTED, "C=%d P=%d: served by the bf16 precisions only (prototype chunks)", C, P);
   const bool bf16_x = g_x && terms && bf16_bwd_x_fits(geo, terms);
   const bool bf16_pw = (g_protos || g_w) && terms && bf16_bwd_pw_fits(geo, terms);
   ImageBlock img;

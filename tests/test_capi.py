@@ -35,7 +35,9 @@ def test_version_and_supported_shapes():
     assert lib.protoseg_l2_supported(128, 64, 32) == 1
     assert lib.protoseg_l2_supported(48, 190, 19) == 0    # C outside the kernel family
     assert lib.protoseg_l2_supported(64, 190, 33) == 0    # more than 32 classes
-    assert lib.protoseg_l2_supported(64, 1000, 19) == 0   # prototypes exceed LDS
+    assert lib.protoseg_l2_supported(64, 570, 19) == 1    # 30 prototypes/class: bf16 prototype chunks
+    assert lib.protoseg_l2_supported(64, 5000, 19) == 0   # beyond the chunked bound
+    assert lib.protoseg_l2_supported(128, 1000, 19) == 0  # C = 128 has no chunked family
 
 
 def test_workspace_size_is_host_only_and_aligned():

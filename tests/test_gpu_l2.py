@@ -304,3 +304,37 @@ def test_prototype_chunked_backward_with_g_dist(device, precision, with_logits):
     assert_scaled_close(gp, ref_gp, 1e-4, "g_protos(+g_dist, chunked)")
     if with_logits:
         assert_scaled_close(gw, ref_gw, 1e-4, "g_w(chunked)")
+
+
+
+@pytest.mark.parametrize("activation", ["log", "linear"])
+@pytest.mark.parametrize("precision", ["bf16x3", "bf16x6"])
+def test_prototype_chunked_forward_backward_p570(device, precision, activation):
+    """30 prototypes/class (P = 570, the DenseNet config's prototype count): the forward runs in
+    two prototype chunks (distance / activation rows at b * P + p0 + p, logits summed), the
+    backward in three; all outputs against the oracle, g_dist included."""
+    B, h, w, P, K = 2, 16, 16, 570, 19
+    x, protos, w_last = po.synthetic_inputs(B, 64, h, w, P, K, seed=570)
+    gen = torch.Generator().manual_seed(9)
+    w_last = w_last + 0.05 * torch.randn(w_last.shape, generator=gen)
+    g_logits = torch.randn(B, h, w, K, generator=gen)
+    g_dist = torch.randn(B, P, h, w, generator=gen) * 0.1
+    dist, logits, act = run_layer(x, protos, w_last, activation, with_act=True, device=device, precision=precision)
+    ref_logits, ref_dist, ref_gx, ref_gp, ref_gw = po.forward_backward(x, protos, w_last, g_logits, g_dist, activation)
+    assert_dist_close(dist, ref_dist, x, protos)
+    assert_scaled_close(logits, ref_logits, 1e-4, "logits")
+    ref_act = po.distance_2_similarity(ref_dist.permute(0, 2, 3, 1).reshape(-1, P), activation)
+    assert_scaled_close(act.reshape(-1, P), ref_act, 1e-4, "act")
+    ops = _ops()
+    gx, gp, gw = ops.l2_backward(x.to(device), protos.to(device), w_last.to(device), g_logits.to(device),
+                                 g_dist.to(device), 1e-4, ops.ACT_KINDS[activation], prec(precision), True, True, True)
+    assert_scaled_close(gx, ref_gx, 1e-4, "g_x")
+    assert_scaled_close(gp, ref_gp, 1e-4, "g_protos")
+    assert_scaled_close(gw, ref_gw, 1e-4, "g_w")
+
+
+def test_p570_f32_precision_fails_loudly(device):
+    """The f32 family cannot hold 570 prototypes: the call reports it instead of computing."""
+    x, protos, w_last = po.synthetic_inputs(1, 64, 4, 4, 570, 19, seed=1)
+    with pytest.raises(RuntimeError):
+        run_layer(x, protos, w_last, device=device, precision="f32")
