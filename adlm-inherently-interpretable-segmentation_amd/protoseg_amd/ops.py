@@ -145,7 +145,7 @@ def prototype_layer(x: Tensor, prototype_vectors: Tensor, last_layer_weight: Ten
                     with_act: bool = False, precision: Optional[str] = None) -> Tuple[Tensor, Tensor, Tensor]:
     """Distances, logits and activations of the PPNet prototype layer (1x1 prototypes).
 
-    x: [B, C, H, W] add-on-layer output (float32 or bfloat16); prototype_vectors: [P, C, 1, 1]
+    x: [B, C, H, W] add-on-layer output (float32, bfloat16, or float16 widened to f32); prototype_vectors: [P, C, 1, 1]
     or [P, C]; last_layer_weight: [K, P]. Returns (distances [B,P,H,W], logits [B,H,W,K],
     activations [B*H*W, P]) with unrequested outputs empty.
     """
@@ -156,6 +156,10 @@ def prototype_layer(x: Tensor, prototype_vectors: Tensor, last_layer_weight: Ten
         raise _lib.ProtosegError(f"prototype depth {protos.shape[1]} != feature channels {x.shape[1]}")
     if tuple(prototype_vectors.shape[2:]) not in ((), (1, 1)):
         raise _lib.ProtosegError(f"only 1x1 prototypes are supported, got {tuple(prototype_vectors.shape)}")
+    if x.dtype == torch.float16:
+        # fp16 feature maps (BASELINE config 5, DenseNet-161 fp16): widened exactly to f32 at the
+        # boundary; the layer computes as for f32 input and autograd narrows g_x back to fp16.
+        x = x.float()
     return torch.ops.protoseg.l2_forward(x, protos, last_layer_weight, float(eps), ACT_KINDS[activation],
                                          precision_code(precision), with_dist, with_logits, with_act)
 

@@ -338,3 +338,20 @@ def test_p570_f32_precision_fails_loudly(device):
     x, protos, w_last = po.synthetic_inputs(1, 64, 4, 4, 570, 19, seed=1)
     with pytest.raises(RuntimeError):
         run_layer(x, protos, w_last, device=device, precision="f32")
+
+
+def test_fp16_features_widen_exactly(device):
+    """fp16 feature maps (DenseNet fp16 config): computed as their exact f32 widening; g_x comes
+    back in fp16 through autograd."""
+    ops = _ops()
+    x, protos, w_last = po.synthetic_inputs(2, 64, 16, 16, 570, 19, seed=16)
+    xh = x.half()
+    xd = xh.to(device).requires_grad_(True)
+    dist, logits, _ = ops.prototype_layer(xd, protos.to(device), w_last.to(device))
+    g_logits = torch.randn(2, 16, 16, 19, generator=torch.Generator().manual_seed(3))
+    logits.backward(g_logits.to(device))
+    ref_logits, ref_dist, ref_gx, _, _ = po.forward_backward(xh.float(), protos, w_last, g_logits, None)
+    assert_dist_close(dist, ref_dist, xh.float(), protos)
+    assert_scaled_close(logits.detach(), ref_logits, 1e-4, "logits")
+    assert xd.grad.dtype == torch.float16
+    assert_scaled_close(xd.grad.float(), ref_gx, 2e-3, "g_x(fp16)")
