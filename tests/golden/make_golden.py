@@ -21,6 +21,7 @@ from oracle import protoseg_oracle as po  # noqa: E402
 from oracle import kld_oracle as ko  # noqa: E402
 from oracle import push_oracle as pu  # noqa: E402
 from oracle import knn_oracle as kn  # noqa: E402
+from oracle import bbox_oracle as bo  # noqa: E402
 
 SEED = 20220227
 
@@ -105,12 +106,34 @@ def knn_case(n_img, C, H, W, h, w, P, K, k, seed):
                 out_patch=res["patch"], pruned=np.array(pruned, np.int64))
 
 
+def bbox_case(m, C, H, W, h, w, P, K, seed):
+    """push.py:309-329 + helpers.py:48-82 for m prototypes on one image: l2 distances of seeded
+    features, activation, INTER_CUBIC restatement, np.percentile(95), gt-class greedy crop."""
+    x, protos, _ = po.synthetic_inputs(1, C, h, w, P, K, seed)
+    dist = po.l2_convolution(x, protos[:, :, None, None], torch.ones(P, C, 1, 1))[0].numpy()[:m]
+    rng = np.random.default_rng(seed)
+    y = rng.integers(0, K + 1, size=(H // 8, W // 8))
+    y = np.repeat(np.repeat(y, 8, 0), 8, 1).astype(np.int64)
+    proto_class = (np.arange(m) * K // m).astype(np.int32)
+    rf = np.zeros((m, 4), np.int64)
+    thr = np.zeros(m, np.float32)
+    box = np.zeros((m, 4), np.int64)
+    up = np.zeros((m, H, W), np.float32)
+    for j in range(m):
+        i0, j0 = np.unravel_index(int(np.argmin(dist[j])), dist[j].shape)
+        rf[j] = bo.rf_box(int(i0), int(j0), H, W, h, w)
+        t, b, u = bo.bound_box(dist[j], y, int(proto_class[j]), rf[j], "log", 1e-4, C)
+        thr[j], box[j], up[j] = t, b, u
+    return dict(dist=dist, labels=y, proto_class=proto_class, rf=rf, up=up, threshold=thr, box=box)
+
+
 CASES = {
     "l2_small": lambda: l2_case(2, 64, 17, 17, 38, 19, SEED),
     "l2_ragged": lambda: l2_case(3, 32, 7, 11, 21, 3, SEED + 7),
     "push_small": lambda: push_case(3, 64, 64, 128, 8, 16, 38, 19, SEED),
     "kld_small": lambda: kld_case(2, 13, 17, 38, 19, SEED + 11),
     "knn_small": lambda: knn_case(7, 32, 60, 110, 9, 13, 38, 4, 5, SEED + 13),
+    "bbox_small": lambda: bbox_case(6, 64, 72, 136, 9, 17, 38, 19, SEED + 17),
 }
 
 

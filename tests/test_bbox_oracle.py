@@ -83,3 +83,12 @@ def test_bound_box_end_to_end_prototype_on_its_patch():
     thr, box, up = bo.bound_box(dist, y, 2, rf)
     assert up.shape == (H, W) and thr == np.percentile(up, 95)
     assert box[0] <= rf[0] and box[1] >= min(rf[1], H - 1) and box[2] <= rf[2] and box[3] >= min(rf[3], W - 1)
+
+
+def test_oracle_reproduces_committed_golden():
+    """tests/golden/bbox_small.npz (make_golden.py) is re-derived bit for bit."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "bbox_small.npz"))
+    for j in range(g["dist"].shape[0]):
+        t, b, u = bo.bound_box(g["dist"][j], g["labels"], int(g["proto_class"][j]), g["rf"][j], "log", 1e-4, 64)
+        assert np.array_equal(u, g["up"][j]) and t == g["threshold"][j] and tuple(b) == tuple(g["box"][j])

@@ -197,3 +197,20 @@ def test_push_prototypes_writes_bound_boxes(device, tmp_path):
         assert tuple(bb[j, 1:5]) == box, (j, bb[j], box)
         checked += 1
     assert checked > 10
+
+
+def test_bound_boxes_match_committed_golden(device):
+    """tests/golden/bbox_small.npz: the kernels' upsampled maps within 1e-6 of the golden ones
+    (the log differs from numpy's by <= 1 ulp), thresholds / boxes equal to the golden values."""
+    import os
+    push = _push()
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "bbox_small.npz"))
+    H, W = g["labels"].shape
+    _, up = push.act_upsample(torch.from_numpy(g["dist"]).to(device), H, W, "log", 1e-4, 64.0)
+    thr, box = push.bound_boxes(up, torch.from_numpy(g["labels"]).to(device),
+                                torch.from_numpy(g["proto_class"]).to(device),
+                                torch.from_numpy(g["rf"].astype(np.int32)).to(device))
+    up, thr, box = up.cpu().numpy(), thr.cpu().numpy(), box.cpu().numpy()
+    assert np.allclose(up, g["up"], rtol=1e-6, atol=1e-6)
+    assert np.allclose(thr, g["threshold"], rtol=1e-6, atol=0)
+    assert np.array_equal(box, g["box"])
