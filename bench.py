@@ -555,6 +555,7 @@ def main():
     ap.add_argument("--no-kld", action="store_true")
     ap.add_argument("--no-knn", action="store_true")
     ap.add_argument("--no-eval", action="store_true")
+    ap.add_argument("--no-p361", action="store_true", help="skip the 19-prototypes/class layer line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--launch", choices=["graph", "eager"], default="graph",
@@ -577,6 +578,18 @@ def main():
         elapsed = t.item()
     images = args.batch * world * args.steps
     value = images / elapsed
+
+    # BASELINE's metric names 19 prototypes/class (P = 361); configs[1] is 10/class (P = 190, the
+    # headline value). Report the P = 361 layer step beside it (same B, map, precision).
+    p361 = None
+    if world == 1 and args.protos != 361 and not args.no_p361:
+        s361 = LayerStep(args.batch, args.channels, args.fmap, args.fmap, 361, args.classes, x_dtype, device,
+                         SEED + rank, args.precision)
+        e361, k361, a361 = time_layer(s361, args.steps, args.warmup, 1, args.launch == "graph")
+        p361 = {"prototypes": 361, "img_per_s": round(args.batch * args.steps / e361, 1),
+                "ms_per_step": round(e361 / args.steps * 1e3, 4),
+                "kernels_ms": {a361[n]: round(v * 1e3, 4) for n, v in k361.items()}}
+        del s361
 
     kld = None
     if not args.no_kld and world == 1:
@@ -632,6 +645,8 @@ def main():
             "roofline": roof,
             "kernels": kernels,
         }
+        if p361 is not None:
+            out["protos_361"] = p361
         if kld is not None:
             out["kld_step"] = kld
         if push is not None:
