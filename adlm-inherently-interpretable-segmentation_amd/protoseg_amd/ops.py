@@ -124,11 +124,26 @@ def _setup_context(ctx, inputs, output):
     ctx.set_materialize_grads(False)  # unused outputs give None, not a zero-filled [B,P,H,W]
 
 
+def _act_grad_as_dist_grad(x, protos, w_last, g_act, eps, act_kind, precision):
+    """Gradient arriving at the activations (return_activations=True, model.py:280-281) as a
+    distance gradient: g_d = g_act * d act / d d, with act = log((d+1)/(d+eps)) (model.py:233):
+    1/(d+1) - 1/(d+eps) = (eps-1)/((d+1)(d+eps)); linear: -1. The distances are recomputed on the
+    GPU by the forward kernel; the relu mask is applied by the backward kernel as for g_dist."""
+    B, _, H, W = x.shape
+    P = protos.shape[0]
+    ga = g_act.reshape(B, H, W, P).permute(0, 3, 1, 2).float()
+    if act_kind == _lib.ACT_LINEAR:
+        return -ga
+    d = l2_forward(x, protos, w_last, eps, act_kind, precision, True, False, False)[0]
+    return ga * ((eps - 1.0) / ((d + 1.0) * (d + eps)))
+
+
 def _backward(ctx, g_dist, g_logits, g_act):
-    if g_act is not None:
-        raise NotImplementedError("gradient through return_activations=True outputs is not implemented")
     x, protos, w_last = ctx.saved_tensors
     need_x, need_p, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+    if g_act is not None:
+        extra = _act_grad_as_dist_grad(x, protos, w_last, g_act, ctx.eps, ctx.act_kind, ctx.precision)
+        g_dist = extra if g_dist is None else g_dist + extra
     if g_dist is None and g_logits is None:
         return None, None, None, None, None, None, None, None, None
     g_x, g_p, g_w = l2_backward(x, protos, w_last, g_logits, g_dist, ctx.eps, ctx.act_kind, ctx.precision, need_x,

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """bench.py — ProtoSeg hot path on MI355X: prototype-layer training step + prototype push.
 
-Workload (BASELINE.json configs[1], cityscapes_no_kld_imnet): 513x513 crops -> 65x65 feature
-maps, C=64, P=190 (19 classes x 10), K=19. One "step" = the prototype layer's forward
+Workload (BASELINE.json metric: 513x513, 19 prototypes/class; configs[1] cityscapes_no_kld_imnet
+otherwise): 513x513 crops -> 65x65 feature maps, C=64, P=361 (19 classes x 19), K=19; the
+P=190 (10/class, the gin files' count) step is a side line with its own roofline. One "step" = the prototype layer's forward
 (distances + logits, one fused kernel) and backward (g_x, g_prototypes, g_last_layer) over a
 batch of B images per GPU, plus the data-parallel gradient all-reduce (RCCL) when N>1.
 Synthetic data (seed 20220227): X = sigmoid(N(0, 2^2)), prototypes U[0,1),
@@ -309,24 +310,52 @@ def time_kld_step(step: LayerStep, steps: int, warmup: int):
             "kld_backward_gbps": round(n * step.P * 4 / kb / 1e9, 1), "loss": round(loss, 6)}
 
 
-def cpu_layer_baseline(C, h, w, P, K, budget_s):
-    """Oracle (op-for-op torch-CPU restatement of model.py) fwd+bwd per image, host threads."""
+def host_cores():
+    """CPUs this process may run on (the cpuset / affinity mask; os.cpu_count() is the whole
+    machine) and the cgroup CPU quota in cores if one is set (None otherwise)."""
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        cores = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        pass
+    return cores, quota
+
+
+def cpu_layer_baseline(B, C, h, w, P, K, warmup=3, reps=10):
+    """Oracle (op-for-op torch-CPU restatement of model.py:203-283 + autograd) fwd+bwd of one
+    step's batch, on every host core this process may use (3 warm-up + 10 timed
+    reps, median)."""
     from oracle import protoseg_oracle as po
-    threads = max(1, min(16, os.cpu_count() or 1))
+    cores, quota = host_cores()
+    # threads = the cores this process actually gets: the affinity mask, capped by the cgroup
+    # CPU quota when one is set (on the GPU box the quota is 16 of 256 visible CPUs; 256 torch
+    # threads there oversubscribe the quota and ran 80x slower, 7.9 s per step).
+    threads = min(cores, max(1, math.ceil(quota))) if quota else cores
+    prev = torch.get_num_threads()
     torch.set_num_threads(threads)
-    x, protos, w_last = po.synthetic_inputs(1, C, h, w, P, K, SEED)
-    g = torch.randn(1, h, w, K)
-    po.forward_backward(x, protos, w_last, g, None)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
+    x, protos, w_last = po.synthetic_inputs(B, C, h, w, P, K, SEED)
+    g = torch.randn(B, h, w, K, generator=torch.Generator().manual_seed(SEED))
+    for _ in range(warmup):
         po.forward_backward(x, protos, w_last, g, None)
-        n += 1
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 3), "unit": "img/s", "cores": threads, "kind": "port",
-            "sample": f"{n} images of the oracle fwd+bwd (torch-CPU restatement of model.py:203-283 + autograd), "
-                      f"1x{C}x{h}x{w}, P={P}, K={K}, {dt:.1f} s"}
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        po.forward_backward(x, protos, w_last, g, None)
+        times.append(time.perf_counter() - t0)
+    torch.set_num_threads(prev)
+    med = float(np.median(times))
+    return {"value": round(B / med, 3), "unit": "img/s", "cores": threads, "kind": "port",
+            "sample": f"{warmup} warm-up + {reps} timed reps (median {med * 1e3:.1f} ms) of the oracle fwd+bwd "
+                      f"(torch-CPU restatement of model.py:203-283 + autograd) over one step's batch "
+                      f"{B}x{C}x{h}x{w}, P={P}, K={K}; torch threads = {threads} = the process's CPUs "
+                      f"(affinity {cores}, os.cpu_count() {os.cpu_count()}) capped by the cgroup quota ({quota} cores)"}
 
 
 def make_push_inputs(n_img, C, H, W, h, w, P, K, device, seed):
@@ -536,13 +565,34 @@ def time_bound_boxes(steps, warmup, device, H=1024, W=2048, h=129, w=257, P=190,
             "roofline": roofline_entry(0.0, nbytes, kern) | {"kernel": "act_kernel + cubic_upsample_kernel"}}
 
 
+def layer_report(step: LayerStep, per_kernel, actual, args):
+    """Roofline of the step's dominant kernel (event-timed, algorithmic work per launch) and the
+    per-kernel table."""
+    work = step.work()
+    dominant = max(per_kernel, key=per_kernel.get)
+    flops, nbytes = work[dominant]
+    prec = args.precision if "_bf16" in actual[dominant] else "f32"  # the family that ran
+    roof = roofline_entry(flops, nbytes, per_kernel[dominant], prec)
+    config_key = (f"B{step.B}_C{step.C}_{step.h}x{step.w}_P{step.P}_K{step.K}"
+                  f"_{args.x_dtype}_{args.precision}")
+    roof["traffic"] = pmc_traffic(actual[dominant], config_key)
+    roof["kernel"] = actual[dominant]
+    kernels = {}
+    for n, s in per_kernel.items():
+        f, b = work[n]
+        kernels[actual[n]] = {"ms": round(s * 1e3, 4), "tflops": round(f / s / 1e12, 2),
+                              "gbps": round(b / s / 1e9, 1)}
+    return roof, kernels
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
-    ap.add_argument("--protos", type=int, default=190)
+    ap.add_argument("--protos", type=int, default=361, help="19 prototypes/class x 19 classes (the metric)")
+    ap.add_argument("--side-protos", type=int, default=190, help="side line: cityscapes_*_imnet.gin (10/class); 0 = off")
     ap.add_argument("--classes", type=int, default=19)
     ap.add_argument("--channels", type=int, default=64)
     ap.add_argument("--fmap", type=int, default=65, help="feature-map side (513 crop -> 65)")
@@ -555,9 +605,8 @@ def main():
     ap.add_argument("--no-kld", action="store_true")
     ap.add_argument("--no-knn", action="store_true")
     ap.add_argument("--no-eval", action="store_true")
-    ap.add_argument("--no-p361", action="store_true", help="skip the 19-prototypes/class layer line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="push CPU baseline time budget")
     ap.add_argument("--launch", choices=["graph", "eager"], default="graph",
                     help="graph: each step is one HIP graph replay of the three C-ABI calls")
     args = ap.parse_args()
@@ -579,22 +628,21 @@ def main():
     images = args.batch * world * args.steps
     value = images / elapsed
 
-    # BASELINE's metric names 19 prototypes/class (P = 361); configs[1] is 10/class (P = 190, the
-    # headline value). Report the P = 361 layer step beside it (same B, map, precision).
-    p361 = None
-    if world == 1 and args.protos != 361 and not args.no_p361:
-        s361 = LayerStep(args.batch, args.channels, args.fmap, args.fmap, 361, args.classes, x_dtype, device,
-                         SEED + rank, args.precision)
-        e361, k361, a361 = time_layer(s361, args.steps, args.warmup, 1, args.launch == "graph")
-        p361 = {"prototypes": 361, "img_per_s": round(args.batch * args.steps / e361, 1),
-                "ms_per_step": round(e361 / args.steps * 1e3, 4),
-                "kernels_ms": {a361[n]: round(v * 1e3, 4) for n, v in k361.items()}}
-        del s361
+    # The headline is BASELINE's metric config, 19 prototypes/class (P = 361). configs[1]/[2]
+    # (cityscapes_{no_kld,kld}_imnet.gin) bind 10/class (P = 190): that layer step is reported
+    # beside it with its own roofline, and the KLD step runs at P = 190.
+    side = None
+    if world == 1 and args.side_protos and args.side_protos != args.protos:
+        side = LayerStep(args.batch, args.channels, args.fmap, args.fmap, args.side_protos, args.classes, x_dtype,
+                         device, SEED + rank, args.precision)
+        e_side, k_side, a_side = time_layer(side, args.steps, args.warmup, 1, args.launch == "graph")
 
     kld = None
     if not args.no_kld and world == 1:
-        step.setup_kld(SEED + rank)
-        kld = time_kld_step(step, max(5, args.steps // 4), 3)
+        kstep = side if (side is not None and side.P == 190) else step
+        kstep.setup_kld(SEED + rank)
+        kld = time_kld_step(kstep, max(5, args.steps // 4), 3)
+        kld["prototypes"] = kstep.P
 
     push = None
     if not args.no_push:
@@ -610,20 +658,7 @@ def main():
         bboxes = time_bound_boxes(3, 1, device)
 
     if rank == 0:
-        work = step.work()
-        dominant = max(per_kernel, key=per_kernel.get)
-        flops, nbytes = work[dominant]
-        prec = args.precision if "_bf16" in actual[dominant] else "f32"  # the family that ran
-        roof = roofline_entry(flops, nbytes, per_kernel[dominant], prec)
-        config_key = (f"B{args.batch}_C{args.channels}_{args.fmap}x{args.fmap}_P{args.protos}_K{args.classes}"
-                      f"_{args.x_dtype}_{args.precision}")
-        roof["traffic"] = pmc_traffic(actual[dominant], config_key)
-        roof["kernel"] = actual[dominant]
-        kernels = {}
-        for n, s in per_kernel.items():
-            f, b = work[n]
-            kernels[actual[n]] = {"ms": round(s * 1e3, 4), "tflops": round(f / s / 1e12, 2),
-                                  "gbps": round(b / s / 1e9, 1)}
+        roof, kernels = layer_report(step, per_kernel, actual, args)
         out = {
             "metric": baseline_metric(),
             "value": round(value, 1),
@@ -637,16 +672,22 @@ def main():
             "vs_baseline": None,
             "dtype": f"{args.x_dtype} in; {args.precision} products, f32 accumulate",
             "data": "synthetic (seeded; SURVEY.md §8d shapes), inputs resident in HBM",
-            "config": {"workload": "cityscapes_no_kld_imnet prototype layer fwd+bwd (+RCCL grad all-reduce "
-                                   "when N>1), 513x513 crop -> 65x65 map",
+            "config": {"workload": f"prototype layer fwd+bwd (+RCCL grad all-reduce when N>1), 513x513 crop -> "
+                                   f"{args.fmap}x{args.fmap} map, {args.protos // max(1, args.classes)} prototypes/class "
+                                   f"(P={args.protos}, the metric's config), cityscapes_*_imnet.gin otherwise",
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "channels": args.channels, "prototypes": args.protos, "classes": args.classes,
                        "parallelism": f"dp{world}", "launch": args.launch},
             "roofline": roof,
             "kernels": kernels,
         }
-        if p361 is not None:
-            out["protos_361"] = p361
+        if side is not None:
+            roof_s, kernels_s = layer_report(side, k_side, a_side, args)
+            out[f"protos_{side.P}"] = {
+                "prototypes": side.P, "img_per_s": round(args.batch * args.steps / e_side, 1),
+                "ms_per_step": round(e_side / args.steps * 1e3, 4),
+                "workload": "cityscapes_no_kld_imnet.gin prototype layer fwd+bwd (10 prototypes/class)",
+                "roofline": roof_s, "kernels": kernels_s}
         if kld is not None:
             out["kld_step"] = kld
         if push is not None:
@@ -658,8 +699,8 @@ def main():
         if bboxes is not None:
             out["push"]["bound_boxes"] = bboxes
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_layer_baseline(args.channels, args.fmap, args.fmap, args.protos, args.classes,
-                                                     args.cpu_seconds)
+            out["cpu_baseline"] = cpu_layer_baseline(args.batch, args.channels, args.fmap, args.fmap, args.protos,
+                                                     args.classes)
             if push is not None:
                 out["push"]["cpu_baseline"] = cpu_push_baseline(args.cpu_seconds)
                 out["push"]["speedup_vs_cpu"] = round(out["push"]["cpu_baseline"]["ms_per_img"] /

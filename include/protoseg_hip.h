@@ -82,8 +82,12 @@ const char* protoseg_timing_kernel(void);
  *   dist_out   [B, P, H, W]   f32 or NULL   distances (model.py:219, NCHW)
  *   act_out    [B*H*W, P]     f32 or NULL   prototype activations (model.py:273)
  *   logits_out [B, H, W, K]   f32 or NULL   logits NHWC (model.py:278)
- * Supported: C in {32, 64, 128}; P <= 384 (C=64) — see protoseg_l2_supported(); K <= 32.
- * The bf16 family serves C = 64 (P <= 384 forward / pw-backward, P <= 224 x-backward).
+ * Supported (protoseg_l2_supported() is authoritative): K <= 32 and
+ *   - C = 64, BF16X3 / BF16X6: any P <= 4096; prototypes beyond one launch's LDS images run as
+ *     prototype chunks inside the call (forward chunks of <= 384 rows at BF16X3, fewer at BF16X6);
+ *   - C in {32, 64, 128}, F32 (and the bf16 requests the bf16 family cannot serve, C != 64):
+ *     P padded to 32 must fit the f32 family's LDS (C = 64: P <= 384), no chunking;
+ *   - every tensor addressed by the kernels (B*H*W*max(P, C)*4 bytes) below 2^31 bytes.
  */
 int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, int W,
                     const float* protos, int P, const float* w_last, int K,

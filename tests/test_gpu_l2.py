@@ -114,6 +114,33 @@ def test_forward_backward_vs_oracle(device, B, C, h, w, P, K, activation, precis
     assert_scaled_close(gw, ref_gw, 1e-4, "g_w")
 
 
+@pytest.mark.parametrize("hw", [32, 65])
+@pytest.mark.parametrize("K", [2, 3])
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_config0_mds_new_layer_shapes(device, K, hw, precision):
+    """BASELINE configs[0] (mds_new.gin:6-7: prototype_shape (30, 64, 1, 1), num_classes 3, batch 2;
+    BASELINE names 2 classes, so K = 2 too) at its 256x256 (32x32 map) and 513x513 (65x65 map)
+    crops: forward and backward against the oracle, with an upstream g_dist (the KLD-style path)."""
+    B, C, P = 2, 64, 30
+    x, protos, w_last = po.synthetic_inputs(B, C, hw, hw, P, K, seed=30 + K + hw)
+    gen = torch.Generator().manual_seed(K * 100 + hw)
+    w_last = w_last + 0.05 * torch.randn(w_last.shape, generator=gen)
+    g_logits = torch.randn(B, hw, hw, K, generator=gen)
+    g_dist = torch.randn(B, P, hw, hw, generator=gen) * 0.05
+    dist, logits, act = run_layer(x, protos, w_last, with_act=True, device=device, precision=precision)
+    ref_logits, ref_dist, ref_gx, ref_gp, ref_gw = po.forward_backward(x, protos, w_last, g_logits, g_dist)
+    assert_dist_close(dist, ref_dist, x, protos)
+    assert_scaled_close(logits, ref_logits, 1e-4, "logits")
+    ref_act = po.distance_2_similarity(ref_dist.permute(0, 2, 3, 1).reshape(-1, P))
+    assert_scaled_close(act.reshape(-1, P), ref_act, 1e-4, "act")
+    ops = _ops()
+    gx, gp, gw = ops.l2_backward(x.to(device), protos.to(device), w_last.to(device), g_logits.to(device),
+                                 g_dist.to(device), 1e-4, 0, prec(precision), True, True, True)
+    assert_scaled_close(gx, ref_gx, 1e-4, "g_x")
+    assert_scaled_close(gp, ref_gp, 1e-4, "g_protos")
+    assert_scaled_close(gw, ref_gw, 1e-4, "g_w")
+
+
 @pytest.mark.parametrize("P", [57, 361])
 @pytest.mark.parametrize("precision", PRECISIONS)
 def test_bf16_features(device, precision, P):
@@ -195,6 +222,31 @@ def test_ppnet_autograd_matches_oracle(device):
     assert_scaled_close(xd.grad, ref_gx, 1e-4, "g_x")
     assert_scaled_close(net.prototype_vectors.grad.reshape(38, 64), ref_gp, 1e-4, "g_protos")
     assert_scaled_close(net.last_layer.weight.grad, ref_gw, 1e-4, "g_w")
+
+
+@pytest.mark.parametrize("activation", ["log", "linear"])
+def test_gradient_through_return_activations(device, activation):
+    """model.py:280-281: forward_from_conv_features(..., return_activations=True) returns
+    (logits, activations); a loss on both back-propagates as the reference's autograd does."""
+    from protoseg_amd.model import PPNet
+    from protoseg_amd.deeplab import deeplabv2_resnet101_features
+    feats = deeplabv2_resnet101_features(n_blocks=(1, 1, 1, 1), scales=[])
+    net = PPNet(feats, 513, (38, 64, 1, 1), None, 19, add_on_layers_type="deeplab_simple",
+                prototype_activation_function=activation, patch_classification=True).to(device)
+    x, _, _ = po.synthetic_inputs(2, 64, 9, 10, 38, 19, seed=31)
+    coef = torch.randn(2 * 9 * 10, 38, generator=torch.Generator().manual_seed(4))
+    xd = x.to(device).requires_grad_(True)
+    logits, acts = net.forward_from_conv_features(xd, return_activations=True)
+    (logits.square().sum() + (acts * coef.to(device)).sum()).backward()
+    xr = x.clone().requires_grad_(True)
+    pr = net.prototype_vectors.detach().cpu().clone().requires_grad_(True)
+    wr = net.last_layer.weight.detach().cpu().clone().requires_grad_(True)
+    rl, ra = po.forward_from_conv_features(xr, pr, wr, activation, return_activations=True)
+    (rl.square().sum() + (ra * coef).sum()).backward()
+    assert_scaled_close(acts.detach(), ra.detach(), 1e-4, "acts")
+    assert_scaled_close(xd.grad, xr.grad, 1e-4, "g_x")
+    assert_scaled_close(net.prototype_vectors.grad, pr.grad, 1e-4, "g_protos")
+    assert_scaled_close(net.last_layer.weight.grad, wr.grad, 1e-4, "g_w")
 
 
 def test_cpu_tensors_fail_loudly():
