@@ -89,11 +89,16 @@ __device__ __forceinline__ void acc_operand(const f32x16& acc, int s, bf16x8 (&o
 // XOR swizzle of the 16-B chunk index for an LDS image whose rows hold CPR chunks, making
 // ds_read_b128 of 16 different rows at the same logical chunk conflict-free (the four
 // 16-lane groups of ds_read_b128, MI355X_MICROARCH.md §LDS).
+// CPR 8 (128-B rows, two per 256-B bank period): every ds_read_b128 group holds all 8 even and
+// all 8 odd row residues mod 16, so the swizzle must permute 0..7 over each; it is also read
+// transposed (ds_read_b64_tr_b16: 4 rows p0..p0+3, p0 = 0 mod 4, 4 chunks per 32-lane half),
+// which needs rows p0 and p0+2 (both in one bank half) in disjoint aligned chunk quads, i.e.
+// swz(p0) ^ swz(p0+2) with bit 2 set. ((row>>1)&1)<<2 | ((row>>2)&3) does both.
 template <int CPR>
 __device__ __forceinline__ constexpr int swz(int row) {
   static_assert(CPR == 4 || CPR == 8 || CPR == 16, "row length");
   if constexpr (CPR == 4) return (row >> 2) & 3;
-  if constexpr (CPR == 8) return (row >> 1) & 7;
+  if constexpr (CPR == 8) return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
   return row & 15;
 }
 
@@ -215,17 +220,21 @@ constexpr int kStampSlots = 8;
 constexpr int kStampCap = 1 << 17;
 __device__ extern unsigned long long g_stamps[kStampCap];
 }  // namespace protoseg
+// Each translation unit records into its own array (no device-side linking across TUs).
+#ifndef PROTOSEG_STAMP_ARRAY
+#define PROTOSEG_STAMP_ARRAY ::protoseg::g_stamps
+#endif
 #define STAMP(slot)                                                                                   \
   do {                                                                                                \
     const unsigned _w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);                          \
     if ((threadIdx.x & 63) == 0 && _w * ::protoseg::kStampSlots + (slot) < ::protoseg::kStampCap)      \
-      ::protoseg::g_stamps[_w * ::protoseg::kStampSlots + (slot)] = __builtin_amdgcn_s_memtime();     \
+      PROTOSEG_STAMP_ARRAY[_w * ::protoseg::kStampSlots + (slot)] = __builtin_amdgcn_s_memtime();     \
   } while (0)
 #define STAMP_RT(slot)                                                                                \
   do {                                                                                                \
     const unsigned _w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);                          \
     if ((threadIdx.x & 63) == 0 && _w * ::protoseg::kStampSlots + (slot) < ::protoseg::kStampCap)      \
-      ::protoseg::g_stamps[_w * ::protoseg::kStampSlots + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+      PROTOSEG_STAMP_ARRAY[_w * ::protoseg::kStampSlots + (slot)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
 #define STAMP_RT(slot) \

@@ -1,0 +1,507 @@
+// l2_bwd_fused.hip — the prototype layer's backward as ONE kernel on bf16 MFMA with 2-term
+// split operands (bf16x3, C = 64, up to 192 prototypes per launch; larger P runs as prototype
+// chunks). It is the autograd of reference model.py:203-221 (_l2_convolution), 231-237
+// (distance_2_similarity) and 259-283 (forward_from_conv_features), which has no explicit
+// backward upstream:
+//   S = ||x||^2 + ||p||^2 - 2 X.P^T,  d = relu(S),  act = f(d),  logits = act . W^T
+//   g_act = g_logits . W,  g_s = (g_act f'(d) + g_dist) [d > 0]
+//   g_x   = 2 x sum_p g_s - 2 g_s . P          g_P = 2 p sum_n g_s - 2 g_s^T . X
+//   g_W   = g_logits^T . act
+// The two-kernel form (l2_bf16.hip: bwd_x + bwd_pw) computes S, g_act and the epilogue twice;
+// here every (pixel tile, prototype tile) block computes them once.
+//
+// Workgroup = 8 waves, one per CU (LDS), persistent over 32-pixel tiles:
+//   waves 0..5 ("owners"): wave w owns prototype tile w. Layout B (rows = pixels n, columns =
+//     prototypes p, so the prototype is on the lane): S and g_act on MFMA, the epilogue, then
+//     g_P^T += g_s^T X and g_W += g_logits^T act with the accumulators as operands (the
+//     contraction is over their row index n), so g_P / g_W stay in registers for the whole
+//     launch: one slab per workgroup, summed by l2_bwd_reduce_bf16_kernel. g_s also goes to LDS
+//     as a [p][n] bf16 image (8-byte stores, no shuffles).
+//   waves 6, 7 ("x waves"): x wave c owns channel tile c of g_x. g_x^T[c][n] = (-2P)^T g_s^T sums
+//     over p, the accumulator's column index, so it reads both operands transposed
+//     (ds_read_b64_tr_b16) from the (-2P) image and the g_s image; sum_p g_s comes from the same
+//     fragments times a ones matrix. Output lane = pixel: coalesced NCHW stores.
+// The owners also stage the tiles (register loads one tile ahead, conversion to the split bf16
+// images + ||x||^2 one tile ahead). One barrier per iteration; the x, g_logits and g_s images
+// are double-buffered, so owners work on tile i while the x waves finish g_x of tile i-1.
+#include <type_traits>
+
+#ifdef PROTOSEG_STAMPS
+#define PROTOSEG_STAMP_ARRAY ::protoseg::g_stamps_fused
+#include <hip/hip_runtime.h>
+namespace protoseg {
+__device__ unsigned long long g_stamps_fused[1 << 17];
+}
+#endif
+#include "bf16_split.h"
+#include "l2_bf16_common.h"
+#include "l2_launch.h"
+#include "protoseg_host.h"
+
+namespace protoseg {
+
+namespace {
+
+using namespace bf16l;
+
+constexpr int kT = 2;                       // split terms (bf16x3: 3 MFMAs per product)
+constexpr int kOwners = 6;                  // prototype-tile waves
+constexpr int kXWaves = 2;                  // channel-tile waves (64 channels = 2 x 32)
+constexpr int kThreads = (kOwners + kXWaves) * 64;
+constexpr int kMaxPp = kOwners * 32;        // prototypes per launch
+
+// LDS regions (bytes). The (-2P) and W^T images are adjacent, as in the operand-image block,
+// so one LDS-DMA copy fills both.
+struct FusedLds {
+  int pimg, wtimg, xa, ga, x2s, rowoff, gs, total;
+};
+__host__ __device__ inline FusedLds fused_lds(int Pp) {
+  FusedLds o;
+  o.pimg = 0;                           // [T][Pp][64] (-2P), CPR 8, chan_of order
+  o.wtimg = kT * Pp * 128;              // [T][Pp][32] (grad_unit W)^T, CPR 4
+  o.xa = o.wtimg + kT * Pp * 64;        // [2 slots][T][32 n][64 c] bf16, CPR 8
+  o.ga = o.xa + 2 * kT * 32 * 64 * 2;   // [2 slots][T][32 n][32 k] bf16, CPR 4
+  o.x2s = o.ga + 2 * kT * 32 * 32 * 2;  // [2 slots][32] f32: ||x||^2 per pixel
+  o.rowoff = o.x2s + 2 * 32 * 4;        // [2 slots][32] u32: g_dist byte offset per pixel
+  o.gs = o.rowoff + 2 * 32 * 4;         // [2 slots][T][Pp][32 n] bf16, 8-B slots swizzled
+  o.total = o.gs + 2 * kT * Pp * 64;
+  return o;
+}
+
+// Keeps the scheduler from hoisting a later phase's LDS loads above this point (register
+// pressure: every phase's operand fragments in flight at once would spill).
+#define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p' supplies the address of row q (4 contiguous
+// elements); lane i of the group receives column i of the 4 rows (cdna_hip_programming.md T10).
+// The two reads of one fragment give elements 0..3 and 4..7.
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* lo, const bf16* hi) {
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(lo));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(hi));
+  const s16x8 v = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// g_s image: [Pp rows p][32 n] bf16, 64-B rows of eight 8-B slots (4 pixels each), slot
+// swizzle (p >> 1) & 7: the owners' 8-byte stores (16 rows per lane group) and the x waves'
+// transposed reads (4 rows x 64 B per 32-lane half) are both conflict-free.
+__device__ __forceinline__ int gs_off(int row, int slot) { return row * 32 + ((slot ^ ((row >> 1) & 7)) << 2); }
+
+// Channel of physical column u of a CPR-8 image row (chunk u>>3 holds chan_of(q, h, 0..7)).
+__device__ __forceinline__ constexpr int chan_of_col(int u) { return chan_of(u >> 4, (u >> 3) & 1, u & 7); }
+
+template <typename TX, int ACT, bool GD>
+__global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
+    const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const unsigned char* __restrict__ img, int P, int Pp,
+    int K, float eps, const float* __restrict__ g_logits, unsigned gl_bytes, const float* __restrict__ g_dist,
+    unsigned gd_bytes, int gd_ld, int gd_p0, TX* __restrict__ g_x, int accumulate, float* __restrict__ slab) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const FusedLds L = fused_lds(Pp);
+  const ImgOffsets io = img_offsets(Pp, kT);
+  bf16* Pimg = reinterpret_cast<bf16*>(smem_raw + L.pimg);
+  bf16* WTimg = reinterpret_cast<bf16*>(smem_raw + L.wtimg);
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = wave_id();
+  const int ntiles = (npix + 31) / 32;
+  const int npt = Pp / 32;
+  const int iters = (ntiles - static_cast<int>(blockIdx.x) + static_cast<int>(gridDim.x) - 1) / static_cast<int>(gridDim.x);
+  const bool owner = wave < kOwners;
+  const int xw = wave - kOwners;  // x wave index (channel tile), valid when !owner
+  const unsigned sz = sizeof(TX);
+  const rsrc_t rx = make_rsrc(x, x_bytes), rg = make_rsrc(g_logits, gl_bytes);
+  const rsrc_t rgd = make_rsrc(g_dist, gd_bytes), rgx = make_rsrc(g_x, g_x ? x_bytes : 0u);
+  auto tile_of = [&](int i) __attribute__((always_inline)) { return static_cast<int>(blockIdx.x) + i * static_cast<int>(gridDim.x); };
+  auto xa_slot = [&](int sb) __attribute__((always_inline)) { return reinterpret_cast<bf16*>(smem_raw + L.xa) + sb * kT * 32 * kC; };
+  auto ga_slot = [&](int sb) __attribute__((always_inline)) { return reinterpret_cast<bf16*>(smem_raw + L.ga) + sb * kT * 32 * 32; };
+  auto x2_slot = [&](int sb) __attribute__((always_inline)) { return reinterpret_cast<float*>(smem_raw + L.x2s) + sb * 32; };
+  auto ro_slot = [&](int sb) __attribute__((always_inline)) { return reinterpret_cast<unsigned*>(smem_raw + L.rowoff) + sb * 32; };
+  auto gs_slot = [&](int sb) __attribute__((always_inline)) { return reinterpret_cast<bf16*>(smem_raw + L.gs) + sb * kT * Pp * 32; };
+
+  // ---- owners: staging ---------------------------------------------------------------------
+  // Tile t's raw inputs are loaded into registers one iteration before they are converted into
+  // the split images (the compiler tracks the loads, so the wait is exactly the conversion's).
+  // One 8-value chunk per lane: owners 0..3 hold the XA chunks (pixel 8w + (lane >> 3), chunk
+  // lane & 7 = 2q + hh: channels chan_of(q, hh, 0..7)); owners 4, 5 the GA chunks (pixel
+  // 16 (w - 4) + (lane >> 2), classes 8 (lane & 3) .. + 7).
+  float raw[8];
+  const bool xa_lane = wave < 4;
+  const int st_n = xa_lane ? 8 * wave + (lane >> 3) : 16 * (wave - 4) + (lane >> 2);
+  const int st_c = xa_lane ? lane & 7 : lane & 3;
+  auto stage_load = [&](int t) __attribute__((always_inline)) {
+    const int g = t * 32 + st_n;
+    const bool ok = t < ntiles && g < npix;
+    if (xa_lane) {
+      unsigned off = kOOB;
+      if (ok) {
+        const int b = g / HW;
+        off = static_cast<unsigned>((b * kC + chan_of(st_c >> 1, st_c & 1, 0)) * HW + (g - b * HW)) * sz;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e)  // chan_of(q, hh, e) - chan_of(q, hh, 0) = 8 (e >> 2) + (e & 3)
+        raw[e] = BufIO<TX>::load(rx, off, static_cast<unsigned>((8 * (e >> 2) + (e & 3)) * HW) * sz);
+    } else {
+      const unsigned off = ok ? static_cast<unsigned>((g * K + 8 * st_c) * 4) : kOOB;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) raw[e] = BufIO<float>::load(rg, 8 * st_c + e < K ? off : kOOB, static_cast<unsigned>(e * 4));
+    }
+  };
+  // Registers -> split images of slot sb. ||x||^2 follows the forward's x_frags chain exactly
+  // (per channel half hh: one fma chain over q = 0..3, e = 0..7; then + the other half): four
+  // rounds, the chain value moving from chunk 2q + hh to 2(q+1) + hh (two lanes up) between them.
+  auto convert = [&](int t, int sb) __attribute__((always_inline)) {
+    bf16x8 f[kT];
+    split8<kT>(raw, f);
+    if (xa_lane) {
+      store_frag<kT>(xa_slot(sb), 32 * kC, img_off<8>(st_n, st_c), f);
+      float chain = 0.f;
+#pragma unroll
+      for (int q = 0; q < kNQ; ++q) {
+        float c = chain;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) c = fmaf(raw[e], raw[e], c);
+        // lane of chunk 2(q+1) + hh takes the value of chunk 2q + hh (row_shr:2 in the 8-lane group)
+        const float up = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, c), 0x112, 0xf, 0xf, false));
+        chain = (st_c >> 1) == q ? c : (q + 1 < kNQ && (st_c >> 1) == q + 1 ? up : chain);
+      }
+      // chunks 6 (hh = 0) and 7 (hh = 1) hold the two half sums; x2 = own half + other half
+      const float other = __shfl_xor(chain, 1);
+      if (st_c == 6) x2_slot(sb)[st_n] = chain + other;
+    } else {
+      store_frag<kT>(ga_slot(sb), 32 * 32, img_off<4>(st_n, st_c), f);
+      if constexpr (GD) {
+        if (st_c == 0) {
+          const int g = t * 32 + st_n;
+          const bool ok = t < ntiles && g < npix;
+          const int b = ok ? g / HW : 0;
+          ro_slot(sb)[st_n] = ok ? static_cast<unsigned>(((b * gd_ld + gd_p0) * HW + (g - b * HW)) * 4) : kOOB;
+        }
+      }
+    }
+  };
+
+  // Per-lane parts of the transposed-read addresses: lane 16G + 4qq + pp supplies row qq of
+  // its group's 4-row block, columns 4pp..4pp+3 of the group's 16 (G & 1 selects which 16).
+  const int G = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+  const int tr_c16 = 2 * (G & 1) + (pp >> 1);  // 16-B chunk within a 32-column tile
+  const int tr_sub = 4 * (pp & 1);             // element offset inside the chunk
+
+  // ---- owners: one prototype tile against one pixel tile --------------------------------------
+  f32x16 gp[2] = {zero16(), zero16()};  // sum_n g_s x  (rows p, cols: physical x columns)
+  f32x16 gw = zero16();                 // g_logits^T act (rows k, cols p)
+  float gsum = 0.f;                     // sum_n g_s, this half-wave's rows
+  const int p = (owner ? wave : 0) * 32 + j;
+  const bool pvalid = p < P;
+  const float p2 = owner ? reinterpret_cast<const float*>(img + io.p2)[p] : 0.f;
+  auto owner_tile = [&](int sb, bool stamp) __attribute__((always_inline)) {
+    const bf16* XA = xa_slot(sb);
+    const bf16* GA = ga_slot(sb);
+    float x2r[16], gdv[16];
+    load_rows16(x2_slot(sb) + 4 * h, x2r);
+    if constexpr (GD) {
+      float rof[16];
+      load_rows16(reinterpret_cast<const float*>(ro_slot(sb)) + 4 * h, rof);
+      const unsigned pcol = static_cast<unsigned>(p * HW * 4);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const unsigned ro = __float_as_uint(rof[r]);
+        gdv[r] = BufIO<float>::load(rgd, (ro != kOOB && pvalid) ? ro + pcol : kOOB, 0);
+      }
+    }
+    f32x16 acc;  // ||x||^2 + ||p||^2, then the (-2P) image does the rest
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = x2r[r] + p2;
+#pragma unroll
+    for (int q = 0; q < kNQ; ++q) {
+      bf16x8 xa[kT], pb[kT];
+      load_frag<kT>(XA, 32 * kC, img_off<8>(j, 2 * q + h), xa);
+      load_frag<kT>(Pimg, Pp * kC, img_off<8>(p, 2 * q + h), pb);
+      acc = mma_split<kT>(xa, pb, acc);
+    }
+    f32x16 gacc = zero16();  // both class k-steps run: W^T rows / GA columns past K are zero
+    SCHED_FENCE();
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 ga[kT], wb[kT];
+      load_frag<kT>(GA, 32 * 32, img_off<4>(j, 2 * s + h), ga);
+      load_frag<kT>(WTimg, Pp * 32, img_off<4>(p, 2 * s + h), wb);
+      gacc = mma_split<kT>(ga, wb, gacc);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float d = relu_f(acc[r]);
+      float a;
+      float gd = gacc[r] * act_grad_and_base<ACT>(d, eps, a);  // grad_unit is in the W^T image
+      if constexpr (GD) gd += gdv[r];
+      const float gs = d > 0.f ? gd : 0.f;  // relu backward
+      gsum += gs;
+      acc[r] = gs;
+      gacc[r] = a;  // act_unit is applied to g_W in the slab reduce
+    }
+    SCHED_FENCE();
+    if (stamp) STAMP(4);
+    bf16x8 gsf[2][kT], actf[2][kT];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      acc_operand<kT>(acc, s, gsf[s]);
+      acc_operand<kT>(gacc, s, actf[s]);
+    }
+    // g_s -> [p][n] image: fragment elements 0..3 are rows 16s + 4h + 0..3 (slot 4s + h),
+    // elements 4..7 rows 16s + 8 + 4h + 0..3 (slot 4s + 2 + h).
+    bf16* GS = gs_slot(sb);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int t = 0; t < kT; ++t) {
+        const s16x8 v = __builtin_bit_cast(s16x8, gsf[s][t]);
+        *reinterpret_cast<s16x4*>(GS + t * Pp * 32 + gs_off(p, 4 * s + h)) = __builtin_shufflevector(v, v, 0, 1, 2, 3);
+        *reinterpret_cast<s16x4*>(GS + t * Pp * 32 + gs_off(p, 4 * s + 2 + h)) =
+            __builtin_shufflevector(v, v, 4, 5, 6, 7);
+      }
+    SCHED_FENCE();
+    if (stamp) STAMP(5);
+    // g_P^T += g_s^T X: B = x[n][c] with k = n in the accumulator's order, from XA transposed.
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int r1 = 16 * s + 4 * h + qq, r2 = r1 + 8;
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        bf16x8 xt[kT];
+        const int c16 = 4 * ct + tr_c16;
+#pragma unroll
+        for (int t = 0; t < kT; ++t)
+          xt[t] = tr_frag(XA + t * 32 * kC + r1 * kC + ((c16 ^ swz<8>(r1)) << 3) + tr_sub,
+                          XA + t * 32 * kC + r2 * kC + ((c16 ^ swz<8>(r2)) << 3) + tr_sub);
+        gp[ct] = mma_split<kT>(gsf[s], xt, gp[ct]);
+      }
+      // g_W += g_logits^T act: A = g_logits[n][k] transposed (lane = class).
+      bf16x8 glt[kT];
+#pragma unroll
+      for (int t = 0; t < kT; ++t)
+        glt[t] = tr_frag(GA + t * 32 * 32 + r1 * 32 + ((tr_c16 ^ swz<4>(r1)) << 3) + tr_sub,
+                         GA + t * 32 * 32 + r2 * 32 + ((tr_c16 ^ swz<4>(r2)) << 3) + tr_sub);
+      gw = mma_split<kT>(glt, actf[s], gw);
+    }
+  };
+
+  // ---- x waves: g_x of one tile from the g_s image of slot sb ---------------------------------
+  // D[c][n] = sum_p (-2P)^T[c][p] g_s^T[p][n] (c = physical column 32 xw + row), and
+  // s[n] = sum_p g_s[n][p]; g_x = D + 2 x s. Register r of half h holds channel
+  // 32 xw + 16 (r >> 3) + 4 ((r >> 2) & 1) + (r & 3) + 8h (chan_of of its column).
+  // s[n]: the g_s fragments of k-steps 0 and 1 exchanged by v_permlane16_swap so that every
+  // lane holds pixel (lane & 15) (first) or 16 + (lane & 15) (second), then one
+  // v_mfma_f32_16x16x32_bf16 against ones per term and pixel half: 32 prototypes per MFMA at
+  // half the cycles of the 32x32x16 form.
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = static_cast<bf16>(1.f);
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  // The (-2P)^T fragments of this wave's channel tile are the same for every pixel tile: read
+  // once into registers (kMaxPp / 16 k-steps x T terms x 4 VGPRs = 96); per prototype tile only
+  // the g_s fragments come from LDS (8 transposed reads, one tile ahead).
+  constexpr int kMaxNpt = kMaxPp / 32;
+  bf16x8 pa[kMaxNpt][2][kT];
+  auto gs_frags = [&](const bf16* GS, int pt, bf16x8 (&b)[2][kT]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int r1 = 32 * pt + 16 * s + 8 * h + qq, r2 = r1 + 4;
+#pragma unroll
+      for (int t2 = 0; t2 < kT; ++t2)
+        b[s][t2] = tr_frag(GS + t2 * Pp * 32 + gs_off(r1, 4 * (G & 1) + pp), GS + t2 * Pp * 32 + gs_off(r2, 4 * (G & 1) + pp));
+    }
+  };
+  auto gx_tile = [&](int t, int sb, bool stamp) __attribute__((always_inline)) {
+    const bf16* GS = gs_slot(sb);
+    const int g = t * 32 + j;
+    unsigned pix = kOOB;
+    if (g < npix) {
+      const int b = g / HW;
+      pix = static_cast<unsigned>((b * kC + 32 * xw + 8 * h) * HW + (g - b * HW)) * sz;
+    }
+    // x (for the 2 x s term) and, for chunk c > 0, the earlier chunks' g_x: loads issued before
+    // the MFMA loop so their latency hides under it.
+    float xr[16], old[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const unsigned co = static_cast<unsigned>((16 * (r >> 3) + 4 * ((r >> 2) & 1) + (r & 3)) * HW) * sz;
+      xr[r] = BufIO<TX>::load(rx, pix, co);
+      old[r] = BufIO<TX>::load(rgx, accumulate ? pix : kOOB, co);
+    }
+    f32x16 acc = zero16();
+    f32x4 s_lo = {0.f, 0.f, 0.f, 0.f}, s_hi = {0.f, 0.f, 0.f, 0.f};
+    bf16x8 b0[2][kT], b1[2][kT];
+    auto step = [&](int pt, bf16x8 (&b)[2][kT]) __attribute__((always_inline)) {
+      acc = mma_split<kT>(pa[pt][0], b[0], acc);
+      acc = mma_split<kT>(pa[pt][1], b[1], acc);
+#pragma unroll
+      for (int t2 = 0; t2 < kT; ++t2) {
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 f0 = __builtin_bit_cast(u32x4, b[0][t2]), f1 = __builtin_bit_cast(u32x4, b[1][t2]);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const auto r = __builtin_amdgcn_permlane16_swap(f0[v], f1[v], false, false);
+          f0[v] = r[0];
+          f1[v] = r[1];
+        }
+        s_lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, __builtin_bit_cast(bf16x8, f0), s_lo, 0, 0, 0);
+        s_hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, __builtin_bit_cast(bf16x8, f1), s_hi, 0, 0, 0);
+      }
+    };
+    // Ping-pong over prototype tiles: tile pt + 1's reads (8, within the 15 LDS operations a
+    // wave keeps in flight) are issued, pinned by a scheduling barrier, before tile pt's MFMAs.
+    gs_frags(GS, 0, b0);
+#pragma unroll
+    for (int pt = 0; pt < kMaxNpt; pt += 2) {
+      if (pt < npt) {
+        if (pt + 1 < npt) gs_frags(GS, pt + 1, b1);
+        SCHED_FENCE();
+        step(pt, b0);
+        SCHED_FENCE();
+      }
+      if (pt + 1 < npt) {
+        if (pt + 2 < npt) gs_frags(GS, pt + 2, b0);
+        SCHED_FENCE();
+        step(pt + 1, b1);
+        SCHED_FENCE();
+      }
+    }
+    if (stamp) STAMP(5);
+    const float sn = j < 16 ? s_lo[0] : s_hi[0];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const unsigned co = static_cast<unsigned>((16 * (r >> 3) + 4 * ((r >> 2) & 1) + (r & 3)) * HW) * sz;
+      const float v = acc[r] + sn * (2.f * xr[r]);  // conv(x^2, ones) backward: sum_p g_s * 2x
+      BufIO<TX>::store(rgx, accumulate ? old[r] + v : v, pix, co);  // chunk c > 0 adds
+    }
+  };
+
+  // ---- prologue: operand images + tile 0 staged, tile 1 loading ------------------------------
+  STAMP(0);
+  STAMP_RT(7);
+  lds_copy(Pimg, img + io.p, io.p2 - io.p);  // (-2P) and W^T images
+  if (owner) {
+    stage_load(tile_of(0));
+    convert(tile_of(0), 0);
+    if (iters > 1) stage_load(tile_of(1));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's image DMA has landed
+  __syncthreads();
+  STAMP(1);
+
+  // ---- main loop: owners stage tile i+1 and work on tile i; x waves finish g_x of tile i-1.
+  // Two loops (the role is wave-uniform) with the same barrier count, so neither role's
+  // loop-carried registers are live in the other's loop.
+  if (owner) {
+    for (int i = 0; i <= iters; ++i) {
+      if (i == 2) STAMP(2);
+      if (i + 1 < iters) {
+        convert(tile_of(i + 1), (i + 1) & 1);
+        if (i + 2 < iters) stage_load(tile_of(i + 2));
+      }
+      if (i < iters && wave < npt) owner_tile(i & 1, i == 2);
+      if (i == 2) STAMP(3);
+      __syncthreads();
+    }
+  } else {
+    {
+      const int c16 = 4 * xw + tr_c16;
+#pragma unroll
+      for (int pt = 0; pt < kMaxNpt; ++pt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int r1 = (pt < npt ? 32 * pt : 0) + 16 * s + 8 * h + qq, r2 = r1 + 4;
+#pragma unroll
+          for (int t2 = 0; t2 < kT; ++t2)
+            pa[pt][s][t2] = tr_frag(Pimg + t2 * Pp * kC + r1 * kC + ((c16 ^ swz<8>(r1)) << 3) + tr_sub,
+                                    Pimg + t2 * Pp * kC + r2 * kC + ((c16 ^ swz<8>(r2)) << 3) + tr_sub);
+        }
+    }
+    for (int i = 0; i <= iters; ++i) {
+      if (i == 2) STAMP(2);
+      if (i >= 1) gx_tile(tile_of(i - 1), (i - 1) & 1, i == 2);
+      if (i == 2) STAMP(3);
+      __syncthreads();
+    }
+  }
+  STAMP(6);
+
+  // ---- slab: this workgroup's g_P (x -2: XA holds +x), g_W, sum_n g_s -------------------------
+  if (owner && wave < npt) {
+    const int E = Pp * kC + 32 * Pp + Pp;
+    float* my_slab = slab + static_cast<size_t>(blockIdx.x) * E;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        my_slab[static_cast<size_t>(wave * 32 + acc_row(r, h)) * kC + chan_of_col(32 * ct + j)] = -2.f * gp[ct][r];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) my_slab[static_cast<size_t>(Pp) * kC + acc_row(r, h) * Pp + wave * 32 + j] = gw[r];
+    gsum += __shfl_xor(gsum, 32);
+    if (h == 0) my_slab[static_cast<size_t>(Pp) * kC + 32 * Pp + wave * 32 + j] = gsum;
+  }
+}
+
+template <typename TX, int ACT, bool GD>
+int fused_t(const Geometry& g, const void* x, const unsigned char* img, float eps, const float* g_logits,
+            const float* g_dist, void* g_x, int accumulate, float* ws, int grid, hipStream_t stream) {
+  if (int st = ensure_lds<l2_bwd_fused_bf16_kernel<TX, ACT, GD>>()) return st;
+  const unsigned long long npix = static_cast<unsigned long long>(g.npix);
+  const unsigned xb = static_cast<unsigned>(npix * kC * sizeof(TX));
+  const unsigned glb = g_logits ? static_cast<unsigned>(npix * g.K * 4) : 0u;
+  const unsigned gdb = g_dist ? static_cast<unsigned>(npix * g.ldd * 4) : 0u;
+  KernelTimer timer("l2_bwd_fused_bf16_kernel", stream);
+  hipLaunchKernelGGL((l2_bwd_fused_bf16_kernel<TX, ACT, GD>), dim3(grid), dim3(kThreads),
+                     static_cast<size_t>(fused_lds(g.Pp).total), stream, static_cast<const TX*>(x), xb, g.HW, g.npix, img,
+                     g.P, g.Pp, g.K, eps, g_logits, glb, g_dist, gdb, g.ldd, g.p0, static_cast<TX*>(g_x), accumulate, ws);
+  return check_launch("l2_bwd_fused_bf16_kernel");
+}
+
+}  // namespace
+
+bool bf16_bwd_fused_fits(const Geometry& g, int terms) {
+  return terms == kT && g.C == kC && g.Pp <= kMaxPp && static_cast<size_t>(fused_lds(g.Pp).total) <= kMaxLds &&
+         bf16_sizes_ok(g);
+}
+
+int bf16_bwd_fused_grid(const Geometry& g) { return g.ntiles < 256 ? g.ntiles : 256; }
+
+int launch_bwd_fused_bf16(const Geometry& g, bool x_bf16, const void* x, const float* protos, const void* img,
+                          float eps, int act_kind, const float* g_logits, const float* g_dist, void* g_x,
+                          float* g_protos, float* g_w, float* ws, hipStream_t stream, int accumulate) {
+  const unsigned char* blk = static_cast<const unsigned char*>(img);
+  const int grid = bf16_bwd_fused_grid(g);
+  auto go = [&](auto tx, auto aa, auto gd) __attribute__((always_inline)) {
+    using TX = std::remove_pointer_t<decltype(tx)>;
+    return fused_t<TX, decltype(aa)::value, decltype(gd)::value>(g, x, blk, eps, g_logits, g_dist, g_x, accumulate, ws,
+                                                                 grid, stream);
+  };
+  using A0 = std::integral_constant<int, 0>;
+  using A1 = std::integral_constant<int, 1>;
+  using GT = std::true_type;
+  using GF = std::false_type;
+  float* f = nullptr;
+  uint16_t* b = nullptr;
+  int st;
+  if (act_kind == 0)
+    st = x_bf16 ? (g_dist ? go(b, A0(), GT()) : go(b, A0(), GF())) : (g_dist ? go(f, A0(), GT()) : go(f, A0(), GF()));
+  else
+    st = x_bf16 ? (g_dist ? go(b, A1(), GT()) : go(b, A1(), GF())) : (g_dist ? go(f, A1(), GT()) : go(f, A1(), GF()));
+  if (st) return st;
+  return launch_bwd_reduce_bf16(g, ws, grid, protos, act_kind, g_protos, g_logits ? g_w : nullptr, stream);
+}
+
+}  // namespace protoseg
+
+#ifdef PROTOSEG_STAMPS
+// Debug builds only: copy (and clear) the fused kernel's per-wave phase stamps.
+extern "C" int protoseg_debug_stamps_fused(void* dst, size_t bytes) {
+  using protoseg::g_stamps_fused;
+  const size_t n = bytes < sizeof(g_stamps_fused) ? bytes : sizeof(g_stamps_fused);
+  if (hipDeviceSynchronize() != hipSuccess) return 3;
+  if (dst && hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps_fused), n, 0, hipMemcpyDeviceToHost) != hipSuccess) return 3;
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamps_fused)) != hipSuccess) return 3;
+  return hipMemset(p, 0, sizeof(g_stamps_fused)) == hipSuccess ? 0 : 3;
+}
+#endif

@@ -37,6 +37,15 @@ int launch_fwd_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, co
 int launch_bwd_x_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const void* img, float eps,
                       int act_kind, const float* g_logits, const float* g_dist, void* g_x, hipStream_t stream,
                       int accumulate = 0);
+// One-kernel backward (l2_bwd_fused.hip): bf16x3 only, Pp <= 192 per launch; g_x (+= when
+// accumulate), and the g_P / g_W slab in ws, summed by launch_bwd_reduce_bf16.
+bool bf16_bwd_fused_fits(const Geometry& g, int terms);
+int launch_bwd_fused_bf16(const Geometry& g, bool x_bf16, const void* x, const float* protos, const void* img,
+                          float eps, int act_kind, const float* g_logits, const float* g_dist, void* g_x,
+                          float* g_protos, float* g_w, float* ws, hipStream_t stream, int accumulate = 0);
+// Fixed-order sum of `slabs` partial slabs in ws (+ 2p sum g_s) into g_protos / g_w.
+int launch_bwd_reduce_bf16(const Geometry& g, const float* ws, int slabs, const float* protos, int act_kind,
+                           float* g_protos, float* g_w, hipStream_t stream);
 int launch_bwd_pw_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const float* protos, const void* img,
                        float eps, int act_kind, const float* g_logits, const float* g_dist, float* g_protos,
                        float* g_w, float* ws, hipStream_t stream);

@@ -735,6 +735,32 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
   const int terms = terms_of(precision);
   const bool xb = x_dtype == PROTOSEG_BF16;
   float* ws = static_cast<float*>(workspace);
+  // Training backward (g_x and g_P / g_W) at bf16x3: one fused kernel per chunk of <= 192
+  // prototypes (l2_bwd_fused.hip); chunk c > 0 adds its x-gradient to g_x.
+  if (terms == 2 && C == 64 && g_x && (g_protos || g_w) && bf16_sizes_ok(geo)) {
+    const int nchunk = static_cast<int>(ceil_div(P, 192));
+    const int per = static_cast<int>(ceil_div(P, nchunk));
+    Geometry gc = geometry_of(B, C, H, W, per, K);
+    if (bf16_bwd_fused_fits(gc, terms)) {
+      KernelSpan span(nchunk > 1 ? "l2_bwd_fused_bf16_kernel" : "", "", s);
+      for (int c = 0; c < nchunk; ++c) {
+        const int p0 = c * per, pc = P - p0 < per ? P - p0 : per;
+        gc = geometry_of(B, C, H, W, pc, K);
+        gc.ldw = gc.ldd = P;
+        gc.p0 = p0;
+        ImageBlock img;
+        if (int st = img.build(gc, terms, protos + static_cast<size_t>(p0) * C, g_logits ? w_last + p0 : nullptr,
+                               act_kind, eps, s))
+          return st;
+        if (int st = launch_bwd_fused_bf16(gc, xb, x, protos + static_cast<size_t>(p0) * C, img.ptr, eps, act_kind,
+                                           g_logits, g_dist, g_x,
+                                           g_protos ? g_protos + static_cast<size_t>(p0) * C : nullptr,
+                                           g_w ? g_w + p0 : nullptr, ws, s, c > 0))
+          return st;
+      }
+      return PROTOSEG_OK;
+    }
+  }
   // P too large for the bf16 backward's LDS images (e.g. P = 361, 19 prototypes/class): run it
   // over prototype chunks of <= 192. g_P rows and g_W columns are per prototype; g_x is a sum
   // over prototypes, so chunk c > 0 adds to it; g_dist rows are read at (b * P + p0 + p).

@@ -62,6 +62,8 @@ def main():
                                            prec, P_(gl), null, null, P_(gp), P_(gw), P_(ws), ws_b, s()),
         "bwd_x": lambda: _lib.call("protoseg_l2_bwd", P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 0, prec,
                                    P_(gl), null, P_(gx), null, null, null, 0, s()),
+        "bwd_full": lambda: _lib.call("protoseg_l2_bwd", P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 0, prec,
+                                      P_(gl), null, P_(gx), P_(gp), P_(gw), P_(ws), ws_b, s()),
         "bwd_pw": lambda: _lib.call("protoseg_l2_bwd", P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 0, prec,
                                     P_(gl), null, null, P_(gp), P_(gw), P_(ws), ws_b, s()),
     }
