@@ -186,21 +186,19 @@ __device__ __forceinline__ void load_x_raw(rsrc_t rx, unsigned off, unsigned cs,
     for (int jj = 0; jj < 8; ++jj) raw[q * 8 + jj] = BufIO<TX>::load(rx, off, chan_base(q, jj) * cs);
 }
 
-// Split fragments + ||x||^2 (fma chain over the lane's half of the channels, then both halves).
+// Split fragments + ||x||^2 in the family's fixed order (x2_tree_halves).
 template <int T>
 __device__ __forceinline__ float x_frags(const float (&raw)[kNQ * 8], bf16x8 (&xb)[kNQ][T]) {
-  float x2 = 0.f;
+  float sq[kNQ];
 #pragma unroll
   for (int q = 0; q < kNQ; ++q) {
     float v[8];
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      v[jj] = raw[q * 8 + jj];
-      x2 = fmaf(v[jj], v[jj], x2);
-    }
+    for (int jj = 0; jj < 8; ++jj) v[jj] = raw[q * 8 + jj];
+    sq[q] = chunk_sq(v);
     split8<T>(v, xb[q]);
   }
-  return x2 + __shfl_xor(x2, 32);
+  return x2_tree_halves(sq);
 }
 
 // ||x||^2 + ||p||^2 - 2 P . X for prototype tile pt (layout A: rows p, cols the wave's 32
@@ -650,24 +648,22 @@ __global__ __launch_bounds__(MAXT) void l2_bwd_pw_bf16_kernel(
   };
 
   // Raw tile -> split images. Wave 0 of the stream: XA and ||x||^2 (lane = (pixel, half), the
-  // x_frags chain of the forward, so the distances match it bit for bit); the other waves (all
+  // family's fixed order, so the distances match the forward bit for bit); the other waves (all
   // of them when npt == 1): XB (x * -2, exact), GA, GT.
   auto convert = [&](int t) {
     if (w == 0) {
-      float s2 = 0.f;
+      float sq[kNQ];
 #pragma unroll
       for (int q = 0; q < kNQ; ++q) {
         float v[8];
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-          v[jj] = lds_val(Xs + pair_off<R::kPairX>(chan_of(q, h, jj), j));
-          s2 = fmaf(v[jj], v[jj], s2);
-        }
+        for (int jj = 0; jj < 8; ++jj) v[jj] = lds_val(Xs + pair_off<R::kPairX>(chan_of(q, h, jj), j));
+        sq[q] = chunk_sq(v);
         bf16x8 f[T];
         split8<T>(v, f);
         store_frag<T>(XA, 32 * kC, img_off<8>(j, 2 * q + h), f);
       }
-      const float x2 = s2 + __shfl_xor(s2, 32);
+      const float x2 = x2_tree_halves(sq);
       if (h == 0) x2s[j] = x2;
     }
     const int nthr = npt > 1 ? nt_stream - 64 : nt_stream;

@@ -99,5 +99,24 @@ __device__ __forceinline__ void dma(rsrc_t r, void* lds, unsigned voff, unsigned
                  : "memory");
 }
 
+// ||x||^2 of one pixel in the bf16 family's fixed order: s_{q,h} = fma chain over the 8
+// channels chan_of(q, h, 0..7) starting from 0, u_q = s_{q,0} + s_{q,1}, and
+// x2 = (u_0 + u_1) + (u_2 + u_3). Every kernel of the family that needs ||x||^2 (forward,
+// x-backward, pw-backward, fused backward) forms exactly this value, so all of them compute
+// bit-identical distances and the backward's relu mask is the forward's.
+__device__ __forceinline__ float chunk_sq(const float (&v)[8]) {
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s = fmaf(v[e], v[e], s);
+  return s;
+}
+// Lane layout with the channel half h on lane bit 5 (layout A / per-pixel rows): s[q] = s_{q,h}.
+__device__ __forceinline__ float x2_tree_halves(const float (&s)[4]) {
+  float u[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) u[q] = s[q] + __shfl_xor(s[q], 32);
+  return (u[0] + u[1]) + (u[2] + u[3]);
+}
+
 }  // namespace bf16l
 }  // namespace protoseg

@@ -32,6 +32,21 @@
 namespace protoseg {
 __device__ unsigned long long g_stamps_fused[1 << 17];
 }
+// 16 slots per wave (tools/stamps_fused.py); each stamp is fenced so the phases it brackets are
+// not reordered across it (debug builds only: production code has neither stamps nor fences).
+#define FSTAMP(slot)                                                                                 \
+  do {                                                                                               \
+    __builtin_amdgcn_sched_barrier(0);                                                               \
+    const unsigned _w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);                         \
+    if ((threadIdx.x & 63) == 0 && _w * 16 + (slot) < (1u << 17))                                    \
+      ::protoseg::g_stamps_fused[_w * 16 + (slot)] =                                                 \
+          (slot) == 14 ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();            \
+    __builtin_amdgcn_sched_barrier(0);                                                               \
+  } while (0)
+#else
+#define FSTAMP(slot) \
+  do {               \
+  } while (0)
 #endif
 #include "bf16_split.h"
 #include "l2_bf16_common.h"
@@ -50,10 +65,18 @@ constexpr int kXWaves = 2;                  // channel-tile waves (64 channels =
 constexpr int kThreads = (kOwners + kXWaves) * 64;
 constexpr int kMaxPp = kOwners * 32;        // prototypes per launch
 
+// Raw tile slot (LDS-DMA target, dwords): x as [32 pieces][2 rows c][32 n] with a 68-dword piece
+// stride (rows c and c + 4, read together by the ||x||^2 chains, fall in different banks; bf16 x
+// lands zero-extended in a dword), then g_logits as the tile's flat [32 n][K] run (K <= 32).
+constexpr int kRawPiece = 68;
+constexpr int kRawXDw = 32 * kRawPiece;
+constexpr int kRawSlot = (kRawXDw + 32 * 32) * 4;  // 12,800 B
+__device__ __forceinline__ constexpr int raw_x(int c, int n) { return (c >> 1) * kRawPiece + (c & 1) * 32 + n; }
+
 // LDS regions (bytes). The (-2P) and W^T images are adjacent, as in the operand-image block,
 // so one LDS-DMA copy fills both.
 struct FusedLds {
-  int pimg, wtimg, xa, ga, x2s, rowoff, gs, total;
+  int pimg, wtimg, xa, ga, x2s, rowoff, gs, raw, total;
 };
 __host__ __device__ inline FusedLds fused_lds(int Pp) {
   FusedLds o;
@@ -65,6 +88,14 @@ __host__ __device__ inline FusedLds fused_lds(int Pp) {
   o.rowoff = o.x2s + 2 * 32 * 4;        // [2 slots][32] u32: g_dist byte offset per pixel
   o.gs = o.rowoff + 2 * 32 * 4;         // [2 slots][T][Pp][32 n] bf16, 8-B slots swizzled
   o.total = o.gs + 2 * kT * Pp * 64;
+  // Raw tiles (LDS-DMA targets, 2 slots). The operand images are read into registers in the
+  // prologue, so their region is free afterwards and holds the raw slots when it is big enough.
+  if (o.xa - o.pimg >= 2 * kRawSlot) {
+    o.raw = o.pimg;
+  } else {
+    o.raw = o.total;
+    o.total += 2 * kRawSlot;
+  }
   return o;
 }
 
@@ -119,63 +150,64 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
   auto ro_slot = [&](int sb) __attribute__((always_inline)) { return reinterpret_cast<unsigned*>(smem_raw + L.rowoff) + sb * 32; };
   auto gs_slot = [&](int sb) __attribute__((always_inline)) { return reinterpret_cast<bf16*>(smem_raw + L.gs) + sb * kT * Pp * 32; };
 
-  // ---- owners: staging ---------------------------------------------------------------------
-  // Tile t's raw inputs are loaded into registers one iteration before they are converted into
-  // the split images (the compiler tracks the loads, so the wait is exactly the conversion's).
-  // One 8-value chunk per lane: owners 0..3 hold the XA chunks (pixel 8w + (lane >> 3), chunk
-  // lane & 7 = 2q + hh: channels chan_of(q, hh, 0..7)); owners 4, 5 the GA chunks (pixel
-  // 16 (w - 4) + (lane >> 2), classes 8 (lane & 3) .. + 7).
-  float raw[8];
-  const bool xa_lane = wave < 4;
-  const int st_n = xa_lane ? 8 * wave + (lane >> 3) : 16 * (wave - 4) + (lane >> 2);
-  const int st_c = xa_lane ? lane & 7 : lane & 3;
-  auto stage_load = [&](int t) __attribute__((always_inline)) {
-    const int g = t * 32 + st_n;
-    const bool ok = t < ntiles && g < npix;
-    if (xa_lane) {
-      unsigned off = kOOB;
-      if (ok) {
-        const int b = g / HW;
-        off = static_cast<unsigned>((b * kC + chan_of(st_c >> 1, st_c & 1, 0)) * HW + (g - b * HW)) * sz;
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e)  // chan_of(q, hh, e) - chan_of(q, hh, 0) = 8 (e >> 2) + (e & 3)
-        raw[e] = BufIO<TX>::load(rx, off, static_cast<unsigned>((8 * (e >> 2) + (e & 3)) * HW) * sz);
-    } else {
-      const unsigned off = ok ? static_cast<unsigned>((g * K + 8 * st_c) * 4) : kOOB;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) raw[e] = BufIO<float>::load(rg, 8 * st_c + e < K ? off : kOOB, static_cast<unsigned>(e * 4));
+  // ---- staging (all 8 waves) ------------------------------------------------------------------
+  // Tile t's raw x and g_logits land in raw slot rs by LDS-DMA (no registers, whole cache lines):
+  // x piece k (rows 2k, 2k + 1: lane = pixel) for k = 4 wave .. 4 wave + 3, and g_logits pieces
+  // m = wave, wave + 8, ... of the tile's contiguous 32 K floats. Out-of-range lanes land as 0.
+  using XS = std::conditional_t<sizeof(TX) == 4, float, uint32_t>;
+  auto raw_slot = [&](int rs) __attribute__((always_inline)) { return reinterpret_cast<XS*>(smem_raw + L.raw + rs * kRawSlot); };
+  auto stage_dma = [&](int t, int rs) __attribute__((always_inline)) {
+    XS* R = raw_slot(rs);
+    const int n = lane & 31, g = t * 32 + n;
+    unsigned off = kOOB;
+    if (t < ntiles && g < npix) {
+      const int b = g / HW;
+      off = static_cast<unsigned>((b * kC + (lane >> 5)) * HW + (g - b * HW)) * sz;
     }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int k = 4 * wave + m;
+      dma<TX>(rx, R + k * kRawPiece, off, static_cast<unsigned>(2 * k * HW) * sz);
+    }
+    const int lim = t < ntiles ? min(32, npix - t * 32) * K : 0;  // valid floats of the tile's run
+    float* RG = reinterpret_cast<float*>(R + kRawXDw);
+    for (int m = wave; m * 64 < 32 * K; m += 8)
+      dma<float>(rg, RG + m * 64, m * 64 + lane < lim ? static_cast<unsigned>(lane * 4) : kOOB,
+                 static_cast<unsigned>((t * 32 * K + m * 64) * 4));
   };
-  // Registers -> split images of slot sb. ||x||^2 follows the forward's x_frags chain exactly
-  // (per channel half hh: one fma chain over q = 0..3, e = 0..7; then + the other half): four
-  // rounds, the chain value moving from chunk 2q + hh to 2(q+1) + hh (two lanes up) between them.
-  auto convert = [&](int t, int sb) __attribute__((always_inline)) {
+  // Raw slot rs -> split images of slot sb, pixels 4 wave .. 4 wave + 3 per wave: lanes 0..31
+  // the 8 XA chunks of a pixel (lane = 8 (pixel) + chunk 2q + hh: channels chan_of(q, hh, 0..7)),
+  // lanes 32..47 its 4 GA chunks (classes 8 kc .. 8 kc + 7). ||x||^2 in the family's fixed order
+  // (chunk_sq per lane, then chunk pairs (q, 0)+(q, 1), q pairs, halves: three butterflies over
+  // the pixel's 8 lanes), so the distances match the forward's bit for bit.
+  auto convert = [&](int t, int rs, int sb) __attribute__((always_inline)) {
+    const XS* R = raw_slot(rs);
+    float v[8];
     bf16x8 f[kT];
-    split8<kT>(raw, f);
-    if (xa_lane) {
-      store_frag<kT>(xa_slot(sb), 32 * kC, img_off<8>(st_n, st_c), f);
-      float chain = 0.f;
+    if (lane < 32) {
+      const int n = 4 * wave + (lane >> 3), ch = lane & 7;
 #pragma unroll
-      for (int q = 0; q < kNQ; ++q) {
-        float c = chain;
+      for (int e = 0; e < 8; ++e) v[e] = lds_val(R + raw_x(chan_of(ch >> 1, ch & 1, e), n));
+      split8<kT>(v, f);
+      store_frag<kT>(xa_slot(sb), 32 * kC, img_off<8>(n, ch), f);
+      float s = chunk_sq(v);
+      s += __shfl_xor(s, 1);
+      s += __shfl_xor(s, 2);
+      s += __shfl_xor(s, 4);
+      if (ch == 0) x2_slot(sb)[n] = s;
+    } else if (lane < 48) {
+      const int n = 4 * wave + ((lane - 32) >> 2), kc = lane & 3;
+      const float* RG = reinterpret_cast<const float*>(R + kRawXDw);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) c = fmaf(raw[e], raw[e], c);
-        // lane of chunk 2(q+1) + hh takes the value of chunk 2q + hh (row_shr:2 in the 8-lane group)
-        const float up = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, c), 0x112, 0xf, 0xf, false));
-        chain = (st_c >> 1) == q ? c : (q + 1 < kNQ && (st_c >> 1) == q + 1 ? up : chain);
-      }
-      // chunks 6 (hh = 0) and 7 (hh = 1) hold the two half sums; x2 = own half + other half
-      const float other = __shfl_xor(chain, 1);
-      if (st_c == 6) x2_slot(sb)[st_n] = chain + other;
-    } else {
-      store_frag<kT>(ga_slot(sb), 32 * 32, img_off<4>(st_n, st_c), f);
+      for (int e = 0; e < 8; ++e) v[e] = 8 * kc + e < K ? RG[n * K + 8 * kc + e] : 0.f;
+      split8<kT>(v, f);
+      store_frag<kT>(ga_slot(sb), 32 * 32, img_off<4>(n, kc), f);
       if constexpr (GD) {
-        if (st_c == 0) {
-          const int g = t * 32 + st_n;
+        if (kc == 0) {
+          const int g = t * 32 + n;
           const bool ok = t < ntiles && g < npix;
           const int b = ok ? g / HW : 0;
-          ro_slot(sb)[st_n] = ok ? static_cast<unsigned>(((b * gd_ld + gd_p0) * HW + (g - b * HW)) * 4) : kOOB;
+          ro_slot(sb)[n] = ok ? static_cast<unsigned>(((b * gd_ld + gd_p0) * HW + (g - b * HW)) * 4) : kOOB;
         }
       }
     }
@@ -194,6 +226,8 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
   const int p = (owner ? wave : 0) * 32 + j;
   const bool pvalid = p < P;
   const float p2 = owner ? reinterpret_cast<const float*>(img + io.p2)[p] : 0.f;
+  // this wave's prototype-tile B fragments of S and g_act (registers, loaded in the prologue)
+  bf16x8 preg[kNQ][kT], wreg[2][kT];
   auto owner_tile = [&](int sb, bool stamp) __attribute__((always_inline)) {
     const bf16* XA = xa_slot(sb);
     const bf16* GA = ga_slot(sb);
@@ -214,20 +248,20 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
     for (int r = 0; r < 16; ++r) acc[r] = x2r[r] + p2;
 #pragma unroll
     for (int q = 0; q < kNQ; ++q) {
-      bf16x8 xa[kT], pb[kT];
+      bf16x8 xa[kT];
       load_frag<kT>(XA, 32 * kC, img_off<8>(j, 2 * q + h), xa);
-      load_frag<kT>(Pimg, Pp * kC, img_off<8>(p, 2 * q + h), pb);
-      acc = mma_split<kT>(xa, pb, acc);
+      acc = mma_split<kT>(xa, preg[q], acc);
     }
+    if (stamp) FSTAMP(7);
     f32x16 gacc = zero16();  // both class k-steps run: W^T rows / GA columns past K are zero
     SCHED_FENCE();
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      bf16x8 ga[kT], wb[kT];
+      bf16x8 ga[kT];
       load_frag<kT>(GA, 32 * 32, img_off<4>(j, 2 * s + h), ga);
-      load_frag<kT>(WTimg, Pp * 32, img_off<4>(p, 2 * s + h), wb);
-      gacc = mma_split<kT>(ga, wb, gacc);
+      gacc = mma_split<kT>(ga, wreg[s], gacc);
     }
+    if (stamp) FSTAMP(8);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float d = relu_f(acc[r]);
@@ -240,7 +274,7 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
       gacc[r] = a;  // act_unit is applied to g_W in the slab reduce
     }
     SCHED_FENCE();
-    if (stamp) STAMP(4);
+    if (stamp) FSTAMP(9);
     bf16x8 gsf[2][kT], actf[2][kT];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -260,7 +294,7 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
             __builtin_shufflevector(v, v, 4, 5, 6, 7);
       }
     SCHED_FENCE();
-    if (stamp) STAMP(5);
+    if (stamp) FSTAMP(10);
     // g_P^T += g_s^T X: B = x[n][c] with k = n in the accumulator's order, from XA transposed.
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -275,6 +309,7 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
                           XA + t * 32 * kC + r2 * kC + ((c16 ^ swz<8>(r2)) << 3) + tr_sub);
         gp[ct] = mma_split<kT>(gsf[s], xt, gp[ct]);
       }
+      if (stamp && s == 1) FSTAMP(11);
       // g_W += g_logits^T act: A = g_logits[n][k] transposed (lane = class).
       bf16x8 glt[kT];
 #pragma unroll
@@ -334,6 +369,7 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
     auto step = [&](int pt, bf16x8 (&b)[2][kT]) __attribute__((always_inline)) {
       acc = mma_split<kT>(pa[pt][0], b[0], acc);
       acc = mma_split<kT>(pa[pt][1], b[1], acc);
+#ifndef FUSED_NO_ONES
 #pragma unroll
       for (int t2 = 0; t2 < kT; ++t2) {
         typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -347,6 +383,7 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
         s_lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, __builtin_bit_cast(bf16x8, f0), s_lo, 0, 0, 0);
         s_hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, __builtin_bit_cast(bf16x8, f1), s_hi, 0, 0, 0);
       }
+#endif
     };
     // Ping-pong over prototype tiles: tile pt + 1's reads (8, within the 15 LDS operations a
     // wave keeps in flight) are issued, pinned by a scheduling barrier, before tile pt's MFMAs.
@@ -366,7 +403,7 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
         SCHED_FENCE();
       }
     }
-    if (stamp) STAMP(5);
+    if (stamp) FSTAMP(6);
     const float sn = j < 16 ? s_lo[0] : s_hi[0];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -376,32 +413,69 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
     }
   };
 
-  // ---- prologue: operand images + tile 0 staged, tile 1 loading ------------------------------
-  STAMP(0);
-  STAMP_RT(7);
+  // ---- prologue + main loop ------------------------------------------------------------------
+  // Operand images -> LDS -> registers (owners: their tile's S / g_act B fragments; x waves:
+  // their channel tile's (-2P)^T fragments); then the image region becomes the raw slots:
+  // tiles 0 and 1 land by DMA, tile 0 is converted.
+  FSTAMP(0);
+  FSTAMP(14);
   lds_copy(Pimg, img + io.p, io.p2 - io.p);  // (-2P) and W^T images
-  if (owner) {
-    stage_load(tile_of(0));
-    convert(tile_of(0), 0);
-    if (iters > 1) stage_load(tile_of(1));
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's image DMA has landed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  STAMP(1);
-
-  // ---- main loop: owners stage tile i+1 and work on tile i; x waves finish g_x of tile i-1.
-  // Two loops (the role is wave-uniform) with the same barrier count, so neither role's
-  // loop-carried registers are live in the other's loop.
+  // The rest of the prologue and the main loop are written once per role (the role is
+  // wave-uniform; both paths run the same barriers), so neither role's register-resident
+  // operands or loop-carried values are live in the other's code.
+  auto prologue_tail = [&]() __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // image reads done before the DMA reuses it
+    __syncthreads();
+    stage_dma(tile_of(0), 0);
+    if (iters > 1) stage_dma(tile_of(1), 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    convert(tile_of(0), 0, 0);
+    __syncthreads();
+    FSTAMP(1);
+  };
+  // Main loop: all waves convert tile i+1 (raw slot (i+1)&1, landed last iteration) and start
+  // tile i+2's DMA into raw slot i&1 (converted last iteration); then owners work on tile i and
+  // the x waves finish g_x of tile i-1.
   if (owner) {
-    for (int i = 0; i <= iters; ++i) {
-      if (i == 2) STAMP(2);
-      if (i + 1 < iters) {
-        convert(tile_of(i + 1), (i + 1) & 1);
-        if (i + 2 < iters) stage_load(tile_of(i + 2));
+#pragma unroll
+    for (int q = 0; q < kNQ; ++q) load_frag<kT>(Pimg, Pp * kC, img_off<8>(p, 2 * q + h), preg[q]);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) load_frag<kT>(WTimg, Pp * 32, img_off<4>(p, 2 * s2 + h), wreg[s2]);
+    prologue_tail();
+    // Unrolled by two so the image slot of every LDS access is a compile-time constant.
+    auto owner_iter = [&](int i, auto slot) __attribute__((always_inline)) {
+      constexpr int sb = decltype(slot)::value;
+      if (i == 2) FSTAMP(2);
+      // Owners 4, 5 share their SIMDs with owners 0, 1 (waves w and w + 4 pair up): they stage
+      // after their tile instead of before it, so the two waves of a SIMD are in different
+      // phases (one's MFMAs beside the other's conversion VALU / LDS traffic).
+#ifndef FUSED_NO_STAGGER
+      const bool late = wave >= 4;
+#else
+      const bool late = false;
+#endif
+      if (!late) {
+        if (i + 1 < iters) convert(tile_of(i + 1), sb ^ 1, sb ^ 1);
+        if (i == 2) FSTAMP(5);
+        if (i + 2 < iters) stage_dma(tile_of(i + 2), sb);
+        if (i == 2) FSTAMP(6);
       }
-      if (i < iters && wave < npt) owner_tile(i & 1, i == 2);
-      if (i == 2) STAMP(3);
+      if (i < iters && wave < npt) owner_tile(sb, i == 2);
+      if (late) {
+        if (i + 1 < iters) convert(tile_of(i + 1), sb ^ 1, sb ^ 1);
+        if (i + 2 < iters) stage_dma(tile_of(i + 2), sb);
+      }
+      if (i == 2) FSTAMP(3);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile i+2
       __syncthreads();
+      if (i == 2) FSTAMP(4);
+    };
+    for (int i = 0; i <= iters; i += 2) {
+      owner_iter(i, std::integral_constant<int, 0>());
+      if (i + 1 <= iters) owner_iter(i + 1, std::integral_constant<int, 1>());
     }
   } else {
     {
@@ -417,14 +491,28 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
                                     Pimg + t2 * Pp * kC + r2 * kC + ((c16 ^ swz<8>(r2)) << 3) + tr_sub);
         }
     }
+    prologue_tail();
     for (int i = 0; i <= iters; ++i) {
-      if (i == 2) STAMP(2);
-      if (i >= 1) gx_tile(tile_of(i - 1), (i - 1) & 1, i == 2);
-      if (i == 2) STAMP(3);
+      if (i == 2) FSTAMP(2);
+#ifndef FUSED_NO_XSTAGE
+      if (i + 1 < iters) convert(tile_of(i + 1), (i + 1) & 1, (i + 1) & 1);
+      if (i == 2) FSTAMP(5);
+      if (i + 2 < iters) stage_dma(tile_of(i + 2), i & 1);
+#endif
+      // g_x's x loads are issued after the DMA and waited for before its stores, so the DMA has
+      // landed by then (vector-memory operations retire in issue order); without g_x, wait here.
+      if (i >= 1) {
+        gx_tile(tile_of(i - 1), (i - 1) & 1, i == 2);
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      if (i == 2) FSTAMP(7);
+      if (i == 2) FSTAMP(3);
       __syncthreads();
+      if (i == 2) FSTAMP(4);
     }
   }
-  STAMP(6);
+  FSTAMP(13);
 
   // ---- slab: this workgroup's g_P (x -2: XA holds +x), g_W, sum_n g_s -------------------------
   if (owner && wave < npt) {

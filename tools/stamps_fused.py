@@ -1,10 +1,10 @@
 """Per-wave phase timing of l2_bwd_fused_bf16_kernel from a `make stamps` build.
 
 Run on the GPU box: PROTOSEG_HIP_LIB=<csrc>/build_stamps/libprotoseg_hip.so python3 tools/stamps_fused.py
-Slots: 0 start, 1 prologue done, 2 iteration 2 starts (after the barrier); owners: 4 S and g_act
-MFMAs done, 5 epilogue + g_s image done, 3 tile done; x waves: 3 tile i+1 converted, 4 tile i+2
-loads issued, 5 g_x MFMA loop of tile i-1 done; 6 loop done; 7 start (s_memrealtime).
-Cycles are shader clocks (s_memtime).
+16 slots per wave (FSTAMP in l2_bwd_fused.hip): 0 start, 1 prologue done, 2 iteration 2 starts,
+3 iteration 2 work done (before its barrier), 4 after that barrier, 13 loop done, 14 start
+(s_memrealtime); owners: 5 convert, 6 stage loads issued, 7 S, 8 g_act, 9 epilogue, 10 split +
+g_s image, 11 g_P (+ first g_W); x waves: 6 g_x MFMA loop, 7 stores issued. Shader clocks.
 """
 import ctypes
 import os
@@ -51,26 +51,36 @@ def main():
     bwd()
     buf = np.zeros((1 << 17,), dtype=np.uint64)
     assert lib.protoseg_debug_stamps_fused(buf.ctypes.data, buf.nbytes) == 0
-    st = buf.reshape(-1, 8).astype(np.int64)
+    st = buf.reshape(-1, 16).astype(np.int64)
     wave = np.arange(len(st)) % 8
     live = st[:, 0] != 0
     print(f"waves recorded: {live.sum()}")
+
+    def seg(s, a, b, name):
+        ok = (s[:, a] != 0) & (s[:, b] != 0)
+        if ok.any():
+            print(f"  {name:16s} {pct(s[ok, b] - s[ok, a])}")
+
     for role, sel in (("owner", live & (wave < 6)), ("x wave", live & (wave >= 6))):
         s = st[sel]
         print(f"-- {role} ({len(s)})")
-        print(f"  prologue       {pct(s[:, 1] - s[:, 0])}")
-        print(f"  loop total     {pct(s[:, 6] - s[:, 1])}")
-        ok = s[:, 2] != 0
-        s2 = s[ok]
+        seg(s, 0, 1, "prologue")
+        seg(s, 1, 13, "loop total")
+        seg(s, 2, 4, "iteration 2")
+        seg(s, 3, 4, "it2 barrier wait")
         if role == "owner":
-            print(f"  it2 stage+S+ga {pct(s2[:, 4] - s2[:, 2])}")
-            print(f"  it2 epilogue   {pct(s2[:, 5] - s2[:, 4])}")
-            print(f"  it2 g_P, g_W   {pct(s2[:, 3] - s2[:, 5])}")
-            print(f"  it2 tile       {pct(s2[:, 3] - s2[:, 2])}")
+            seg(s, 2, 5, "it2 convert")
+            seg(s, 5, 6, "it2 stage issue")
+            seg(s, 6, 7, "it2 S")
+            seg(s, 7, 8, "it2 g_act")
+            seg(s, 8, 9, "it2 epilogue")
+            seg(s, 9, 10, "it2 split + g_s")
+            seg(s, 10, 11, "it2 g_P+g_W(0)")
+            seg(s, 11, 3, "it2 g_W(1) end")
         else:
-            print(f"  it2 g_x MFMA   {pct(s2[:, 5] - s2[:, 2])}")
-            print(f"  it2 g_x total  {pct(s2[:, 3] - s2[:, 2])}")
-    rt = (st[live, 7] - st[live, 7].min()) * 10
+            seg(s, 2, 6, "it2 g_x MFMA")
+            seg(s, 6, 7, "it2 g_x stores")
+    rt = (st[live, 14] - st[live, 14].min()) * 10
     print(f"start (realtime) spread ns: p50 {np.percentile(rt, 50):.0f} max {rt.max():.0f}")
 
 
