@@ -4,6 +4,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "protoseg_host.h"
 
@@ -32,6 +33,10 @@ std::mutex g_timer_mu;
 std::string g_timer_kernel;
 std::string g_timer_last;  // full name of the last kernel the hook bracketed
 hipEvent_t g_timer_start = nullptr, g_timer_stop = nullptr;
+// Per-launch mode (protoseg_timing_events_n): launch i of the matching kernel records pair i;
+// spans are off, so a chunked call's launches are timed one by one, as rocprofv3 sees them.
+std::vector<hipEvent_t> g_starts, g_stops;
+int g_launches = 0;
 }  // namespace
 
 namespace {
@@ -49,7 +54,7 @@ thread_local bool t_span_active = false;
 // Exact kernel name, or a family prefix: "l2_fwd" matches l2_fwd_kernel and l2_fwd_bf16_kernel,
 // whichever family serves the call. Caller holds g_timer_mu.
 bool hook_matches(const char* kernel) {
-  if (!g_timer_start) return false;
+  if (!g_timer_start && g_starts.empty()) return false;
   const size_t n = g_timer_kernel.size();
   return g_timer_kernel == kernel || (std::strncmp(kernel, g_timer_kernel.c_str(), n) == 0 && kernel[n] == '_');
 }
@@ -57,7 +62,7 @@ bool hook_matches(const char* kernel) {
 
 KernelSpan::KernelSpan(const char* kernel_a, const char* kernel_b, hipStream_t s) {
   std::lock_guard<std::mutex> lock(g_timer_mu);
-  if (t_span_active || !(hook_matches(kernel_a) || hook_matches(kernel_b))) return;
+  if (t_span_active || !g_starts.empty() || !(hook_matches(kernel_a) || hook_matches(kernel_b))) return;
   if (record(g_timer_start, s) == hipSuccess) {
     t_span_active = true;
     stop_ = g_timer_stop;
@@ -74,6 +79,16 @@ KernelSpan::~KernelSpan() {
 KernelTimer::KernelTimer(const char* kernel, hipStream_t s) {
   std::lock_guard<std::mutex> lock(g_timer_mu);
   if (!hook_matches(kernel)) return;
+  if (!g_starts.empty()) {  // per-launch mode: the next free pair, silently none past the last
+    g_timer_last = kernel;
+    const size_t i = static_cast<size_t>(g_launches);
+    if (i < g_starts.size() && record(g_starts[i], s) == hipSuccess) {
+      ++g_launches;
+      stop_ = g_stops[i];
+      s_ = s;
+    }
+    return;
+  }
   if (t_span_active) {  // inside a matching span: name the kernel, leave the events to the span
     g_timer_last = kernel;
     return;
@@ -96,8 +111,38 @@ extern "C" const char* protoseg_timing_kernel(void) {
   return protoseg::g_timer_last.c_str();
 }
 
+extern "C" int protoseg_timing_events_n(const char* kernel, void* const* start_events, void* const* stop_events,
+                                        int n) {
+  std::lock_guard<std::mutex> lock(protoseg::g_timer_mu);
+  protoseg::g_starts.clear();
+  protoseg::g_stops.clear();
+  protoseg::g_launches = 0;
+  protoseg::g_timer_start = protoseg::g_timer_stop = nullptr;
+  if (!kernel || !start_events || !stop_events || n <= 0) {
+    protoseg::g_timer_kernel.clear();
+    return PROTOSEG_OK;
+  }
+  for (int i = 0; i < n; ++i) {
+    if (!start_events[i] || !stop_events[i]) return protoseg::fail(PROTOSEG_ERR_INVALID, "null timing event %d", i);
+    protoseg::g_starts.push_back(static_cast<hipEvent_t>(start_events[i]));
+    protoseg::g_stops.push_back(static_cast<hipEvent_t>(stop_events[i]));
+  }
+  protoseg::g_timer_kernel = kernel;
+  return PROTOSEG_OK;
+}
+
+extern "C" int protoseg_timing_launches(void) {
+  std::lock_guard<std::mutex> lock(protoseg::g_timer_mu);
+  const int n = protoseg::g_launches;
+  protoseg::g_launches = 0;
+  return n;
+}
+
 extern "C" int protoseg_timing_events(const char* kernel, void* start_event, void* stop_event) {
   std::lock_guard<std::mutex> lock(protoseg::g_timer_mu);
+  protoseg::g_starts.clear();
+  protoseg::g_stops.clear();
+  protoseg::g_launches = 0;
   if (!kernel || !start_event || !stop_event) {
     protoseg::g_timer_kernel.clear();
     protoseg::g_timer_start = protoseg::g_timer_stop = nullptr;

@@ -38,6 +38,8 @@ SIGNATURES = {
     "protoseg_last_error": (ctypes.c_char_p, []),
     "protoseg_timing_events": (_i, [ctypes.c_char_p, _vp, _vp]),
     "protoseg_timing_kernel": (ctypes.c_char_p, []),
+    "protoseg_timing_events_n": (_i, [ctypes.c_char_p, _vp, _vp, _i]),
+    "protoseg_timing_launches": (_i, []),
     "protoseg_l2_supported": (_i, [_i, _i, _i]),
     "protoseg_l2_fwd": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _i, _vp, _vp, _vp, _vp]),
     "protoseg_l2_bwd_workspace_size": (_sz, [_i, _i, _i, _i, _i, _i]),

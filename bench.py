@@ -153,24 +153,37 @@ class LayerStep:
             self.grad_flat[self.P * self.C:].copy_(self.g_w.view(-1))
             dist.all_reduce(self.grad_flat)
 
-    def kernel_names(self):
-        """Kernel families behind the fwd / bwd_x / bwd_pw calls. The library's timing hook
-        matches a family prefix (l2_fwd -> l2_fwd_bf16_kernel or l2_fwd_kernel, whichever the
-        shape and precision select) and reports the full name it bracketed; bwd_pw's call also
-        runs the slab-reduce kernel, outside the bracket."""
-        return ["l2_fwd", "l2_bwd_x", "l2_bwd_pw"]
+    @property
+    def fused(self):
+        """bf16x3 at C = 64: the training backward is one fused kernel per prototype chunk
+        (l2_bwd_fused.hip); other precisions run the two-kernel backward."""
+        return self.prec == _lib.PRECISIONS["bf16x3"] and self.C == 64
 
-    # algorithmic work per launch (unpadded P, K; SURVEY.md §8d)
+    def kernel_names(self):
+        """Kernel families behind the step's timed calls. The library's timing hook matches a
+        family prefix (l2_fwd -> l2_fwd_bf16_kernel or l2_fwd_kernel, whichever the shape and
+        precision select) and reports the full name it bracketed; the backward call also runs
+        the operand-image prep and slab-reduce kernels, outside the bracket (inside it when the
+        call runs over prototype chunks: then the bracket spans all chunks)."""
+        return ["l2_fwd", "l2_bwd_fused"] if self.fused else ["l2_fwd", "l2_bwd_x", "l2_bwd_pw"]
+
+    def timed_calls(self):
+        return [self.fwd, self.bwd] if self.fused else [self.fwd, self.bwd_x, self.bwd_pw]
+
+    # algorithmic work per call (unpadded P, K; SURVEY.md §8d); layer_report divides by launches
     def work(self):
         n = self.B * self.h * self.w
         xb = self.x.element_size()
         mm = 2.0 * n * self.P * self.C
         last = 2.0 * n * self.P * self.K
-        f, x, pw = self.kernel_names()
+        fwd = (mm + last + 2.0 * n * self.C, n * self.C * xb + n * self.P * 4 + n * self.K * 4)
+        if self.fused:  # S, g_act, g_x, g_P, g_W: 3 distance-sized + 2 class-sized products
+            return {"l2_fwd": fwd,
+                    "l2_bwd_fused": (3 * mm + 2 * last, n * self.C * xb + n * self.K * 4 + n * self.C * xb)}
         return {
-            f: (mm + last + 2.0 * n * self.C, n * self.C * xb + n * self.P * 4 + n * self.K * 4),
-            x: (2 * mm + last, n * self.C * xb + n * self.K * 4 + n * self.C * xb),
-            pw: (2 * mm + 2 * last, n * self.C * xb + n * self.K * 4),
+            "l2_fwd": fwd,
+            "l2_bwd_x": (2 * mm + last, n * self.C * xb + n * self.K * 4 + n * self.C * xb),
+            "l2_bwd_pw": (2 * mm + 2 * last, n * self.C * xb + n * self.K * 4),
         }
 
 
@@ -216,7 +229,7 @@ def time_layer(step: LayerStep, steps: int, warmup: int, world: int, use_graph: 
     alone (protoseg_timing_events) during eager calls on the same stream."""
     names = step.kernel_names()
     step_calls = [step.fwd, step.bwd]
-    calls = [step.fwd, step.bwd_x, step.bwd_pw]
+    calls = step.timed_calls()
     stream = torch.cuda.Stream(step.device)
     with torch.cuda.stream(stream):
         for _ in range(max(1, warmup)):
@@ -244,28 +257,39 @@ def time_layer(step: LayerStep, steps: int, warmup: int, world: int, use_graph: 
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
-        # per-kernel device time: the library records a start/stop event pair around the one
-        # named kernel (protoseg_timing_events) of an eager call on this stream, so the figure
-        # is the kernel alone, as rocprofv3 reports it (not the call's prep / reduce launches).
+        # per-kernel device time: the library records a start/stop event pair around each launch
+        # of the one named kernel (protoseg_timing_events_n) in an eager call on this stream, so
+        # the figure is the kernel alone, per dispatch, as rocprofv3 reports it (not the call's
+        # prep / reduce launches; a prototype-chunked call yields one pair per chunk).
         lib = _lib.load()
         per_kernel = {n: [] for n in names}
-        actual = {}
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        for ev in e:
-            ev.record(stream)  # creates the HIP events
+        actual, launches = {}, {}
+        npair = 8
+        e = [[torch.cuda.Event(enable_timing=True) for _ in range(npair)] for _ in range(2)]
+        for row in e:
+            for ev in row:
+                ev.record(stream)  # creates the HIP events
         torch.cuda.synchronize()
+        starts = (ctypes.c_void_p * npair)(*[ev.cuda_event for ev in e[0]])
+        stops = (ctypes.c_void_p * npair)(*[ev.cuda_event for ev in e[1]])
         for n, c in zip(names, calls):
-            lib.protoseg_timing_events(n.encode(), ctypes.c_void_p(e[0].cuda_event), ctypes.c_void_p(e[1].cuda_event))
+            lib.protoseg_timing_events_n(n.encode(), starts, stops, npair)
             try:
+                lib.protoseg_timing_launches()
                 for _ in range(steps):
                     c()
                     torch.cuda.synchronize()
-                    per_kernel[n].append(e[0].elapsed_time(e[1]) * 1e-3)
+                    k = lib.protoseg_timing_launches()
+                    if k < 1 or k > npair:
+                        raise RuntimeError(f"timing hook bracketed {k} launches of {n}*")
+                    launches[n] = k
+                    per_kernel[n] += [e[0][i].elapsed_time(e[1][i]) * 1e-3 for i in range(k)]
                 actual[n] = lib.protoseg_timing_kernel().decode()
                 if not actual[n].startswith(n + "_"):
                     raise RuntimeError(f"timing hook did not bracket a {n}* kernel (got {actual[n]!r})")
             finally:
-                lib.protoseg_timing_events(None, None, None)
+                lib.protoseg_timing_events_n(None, None, None, 0)
+    step.launches = launches
     return elapsed, {n: float(np.mean(v)) for n, v in per_kernel.items()}, actual
 
 
@@ -568,8 +592,10 @@ def time_bound_boxes(steps, warmup, device, H=1024, W=2048, h=129, w=257, P=190,
 def layer_report(step: LayerStep, per_kernel, actual, args):
     """Roofline of the step's dominant kernel (event-timed, algorithmic work per launch) and the
     per-kernel table."""
-    work = step.work()
-    dominant = max(per_kernel, key=per_kernel.get)
+    # per launch: a prototype-chunked call runs its kernel once per chunk (near-equal chunks)
+    launches = getattr(step, "launches", {})
+    work = {n: (f / launches.get(n, 1), b / launches.get(n, 1)) for n, (f, b) in step.work().items()}
+    dominant = max(per_kernel, key=lambda n: per_kernel[n] * launches.get(n, 1))
     flops, nbytes = work[dominant]
     prec = args.precision if "_bf16" in actual[dominant] else "f32"  # the family that ran
     roof = roofline_entry(flops, nbytes, per_kernel[dominant], prec)
@@ -580,8 +606,8 @@ def layer_report(step: LayerStep, per_kernel, actual, args):
     kernels = {}
     for n, s in per_kernel.items():
         f, b = work[n]
-        kernels[actual[n]] = {"ms": round(s * 1e3, 4), "tflops": round(f / s / 1e12, 2),
-                              "gbps": round(b / s / 1e9, 1)}
+        kernels[actual[n]] = {"ms": round(s * 1e3, 4), "launches_per_call": launches.get(n, 1),
+                              "tflops": round(f / s / 1e12, 2), "gbps": round(b / s / 1e9, 1)}
     return roof, kernels
 
 

@@ -69,6 +69,13 @@ int protoseg_timing_events(const char* kernel, void* start_event, void* stop_eve
  * l2_fwd_bf16_kernel); protoseg_timing_kernel() returns the full name of the last kernel the
  * hook bracketed ("" if none), i.e. which family served the call. */
 const char* protoseg_timing_kernel(void);
+/* Per-launch form: launch i (0 <= i < n) of the named kernel records start_events[i] /
+ * stop_events[i], so a call that runs the kernel several times (prototype chunks) is timed
+ * launch by launch, the durations rocprofv3 reports per dispatch (no span over the chunks'
+ * prep / reduce launches). protoseg_timing_launches() returns how many pairs were recorded
+ * since the hook was set or last queried, and resets that count. */
+int protoseg_timing_events_n(const char* kernel, void* const* start_events, void* const* stop_events, int n);
+int protoseg_timing_launches(void);
 
 /*
  * Prototype layer forward. Replaces model.py:203-221 (_l2_convolution), 231-237
