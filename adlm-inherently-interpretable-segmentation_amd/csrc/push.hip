@@ -5,16 +5,20 @@
 // image to the host and runs (a) a 2M-iteration Python loop mapping pixels to patch sets,
 // (b) a per-prototype gather + np.argmin. Here both stay on the device:
 //   patch_mask_kernel   label map -> uint32 class bitmask per patch (push.py:184-186, 214-223)
-//   push_argmin_kernel  fused distance + masked per-prototype min key (push.py:249-263)
+//   push_argmin_kernel  fused distance + masked per-prototype top-2 keys (push.py:249-263)
+//   push_top2_kernel    folds the pixel stripes' partial top-2
 //   push_merge_kernel   strict-'<' fold in image order + winner gather (push.py:265-281)
+#include <map>
+#include <mutex>
+
+#include "bf16_split.h"
+#include "l2_bf16_common.h"
 #include "protoseg_device.h"
 #include "protoseg_host.h"
 
 namespace protoseg {
 
 namespace {
-
-constexpr int kArgminWaves = 4;
 
 template <typename TL>
 __global__ __launch_bounds__(256) void patch_mask_kernel(const TL* __restrict__ label, int H, int W, int h, int w,
@@ -54,109 +58,248 @@ __global__ __launch_bounds__(256) void patch_mask_kernel(const TL* __restrict__ 
     mask[static_cast<size_t>(img) * h * w + static_cast<size_t>(pi) * w + q] = smask[q];
 }
 
-// Layout B tiles (pixel on the register rows, prototype on the lane): the per-prototype
-// minimum over pixels is an in-register min plus one half-wave exchange.
-// key = (float_bits(d) << 32) | patch — d >= 0 after relu, so the bit pattern orders like d
-// and ties resolve to the lowest patch index.
+// push_argmin_kernel: one workgroup per (pixel-block stripe, image, chunk of up to 8 prototype
+// tiles of 32). The image's pixels are walked in blocks of kPushBlk 32-pixel tiles; each block's
+// x ([C][128] of the NCHW map) is read from HBM ONCE, by LDS-DMA (buffer_load_dword ... lds,
+// no registers) into one of two LDS buffers, so block b + 1 streams in while block b is
+// computed. Wave w of the workgroup owns prototype tile w % nptc (its 32 prototypes' vectors in
+// registers) and the pixel tiles tt = w / nptc, w / nptc + split, ... of every block, so all
+// 4 SIMDs carry the same MFMA load (P = 190: 6 tiles x 2 = 12 waves).
+// Layout B (pixel on the accumulator rows, prototype on the lane): A = x from LDS, lane (j, h)
+// reads channels 32 ct + 16 h + r of pixel j (LDS rows of XS = 130 floats: the two half-waves
+// land 32 banks apart, conflict-free); B = the same channels of prototype j; the products run
+// on v_mfma_f32_32x32x2_f32, an exact f32 fma chain. ||x||^2 comes from the same A values
+// (fma chain per half, then the two halves added), so every prototype tile sees the same value.
+// Per lane, the smallest distance of its prototype over its rows with its patch, and the
+// runner-up distance, are kept; as keys float_bits(d) << 32 | patch (d >= 0 after relu, so the
+// bits order like d; equal distances resolve to the lower patch; the runner-up's patch bits are
+// all ones) the half-waves merge and each (stripe, part) writes a partial top-2 that
+// push_top2_kernel folds. The runner-up distance lets the host flag near-ties (SURVEY.md §7,
+// hard part 2).
+constexpr int kPushBlk = 4;                 // 32-pixel tiles per staged block
+constexpr int kPushBlkPix = kPushBlk * 32;  // 128 pixels
+constexpr int kPushXS = kPushBlkPix + 2;    // LDS row stride (floats): 16 * XS = 32 (mod 64) banks
+constexpr int kPushMaxTiles = 8;            // prototype tiles per chunk
+#ifndef PUSH_SPLIT
+#define PUSH_SPLIT 2
+#endif
+#ifndef PUSH_WG_TARGET
+#define PUSH_WG_TARGET 512
+#endif
+constexpr int kPushSplit = PUSH_SPLIT;      // waves per prototype tile (pixel tiles split)
+
+// LDS: 2 buffers of [C rows x XS] x + [128] patch class masks, then [waves][64] per-wave rows.
+__host__ __device__ inline int push_buf_floats(int C) { return C * kPushXS + kPushBlkPix; }
+__host__ __device__ inline size_t push_lds_bytes(int C, int waves) {
+  return static_cast<size_t>(2) * push_buf_floats(C) * 4 + static_cast<size_t>(waves) * 128 * 4;
+}
+
+// (b1, s1) and (b2, s2), each b <= s: the two smallest of the four.
+__device__ __forceinline__ void top2_merge(unsigned long long& b, unsigned long long& s, unsigned long long b2,
+                                           unsigned long long s2) {
+  const unsigned long long lo = b < b2 ? b : b2, hi = b < b2 ? b2 : b;
+  const unsigned long long sm = s < s2 ? s : s2;
+  b = lo;
+  s = hi < sm ? hi : sm;
+}
+
 template <int NC>
-__global__ __launch_bounds__(kArgminWaves * 64) void push_argmin_kernel(
-    const float* __restrict__ x, int HW, const float* __restrict__ protos, int P,
+__global__ __launch_bounds__(kPushMaxTiles * kPushSplit * 64) void push_argmin_kernel(
+    const float* __restrict__ x, int HW, const float* __restrict__ protos, int P, int pt0, int nptc,
     const int32_t* __restrict__ proto_class, const uint32_t* __restrict__ mask,
-    unsigned long long* __restrict__ keys) {
+    unsigned long long* __restrict__ part, int stripes) {
+  using namespace bf16l;
   constexpr int C = NC * 32;
-  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
-  const int pt = blockIdx.x;
-  const int img = blockIdx.z;
-  const int p = pt * 32 + j;
+  extern __shared__ __attribute__((aligned(16))) float push_smem[];
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = wave_id();
+  const int nw = blockDim.x >> 6;
+  const int ptl = wave % nptc, sub = wave / nptc;  // prototype tile in the chunk, pixel-tile part
+  const int stripe = blockIdx.x, img = blockIdx.y;
+  // this wave's epilogue rows, two tiles: [32] ||x||^2, [32] class masks (as float bits) each
+  float* xw = push_smem + 2 * push_buf_floats(C) + wave * 128;
+  const int p = (pt0 + static_cast<int>(blockIdx.z) * kPushMaxTiles + ptl) * 32 + j;
   const bool pvalid = p < P;
+  // this lane's B fragments: prototype p, channels 32 ct + 16 h .. + 15 (four 16-B loads per
+  // group; lanes past P read row P - 1 and are masked out below)
   float pv[NC][16];
+  const float4* prow = reinterpret_cast<const float4*>(protos + static_cast<size_t>(pvalid ? p : P - 1) * C + 16 * h);
 #pragma unroll
   for (int ct = 0; ct < NC; ++ct)
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
-      pv[ct][r] = pvalid ? protos[static_cast<size_t>(p) * C + ct * 32 + acc_row(r, h)] : 0.f;
-  float p2 = 0.f;
-  if (pvalid) {
-#pragma clang fp contract(off)
-    for (int c = 0; c < C; ++c) {
-      const float v = protos[static_cast<size_t>(p) * C + c];
-      p2 += v * v;
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = prow[ct * 8 + q];
+      pv[ct][4 * q] = v.x;
+      pv[ct][4 * q + 1] = v.y;
+      pv[ct][4 * q + 2] = v.z;
+      pv[ct][4 * q + 3] = v.w;
     }
-  }
+  // ||p||^2 from the same registers: an fma chain over this half's channels, then the two halves
+  // added (the sum is the same in both halves). Also consumes the loads before the loop, so the
+  // compiler's own vmcnt wait for them does not land at the first MFMA, where it would also wait
+  // for the LDS-DMA prefetch of the next block (inline asm the wait-count pass cannot see).
+  float p2 = 0.f;
+#pragma unroll
+  for (int ct = 0; ct < NC; ++ct)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) p2 = fmaf(pv[ct][r], pv[ct][r], p2);
+  p2 += __shfl_xor(p2, 32);
   const int cls = pvalid ? proto_class[p] : -1;
   const bool active = cls >= 0 && cls < 32;
-  // classes of this wave's 32 prototypes: a tile without any of them is skipped
   const uint32_t wave_classes = wave_or(active ? (1u << cls) : 0u);
-  const float* xi = x + static_cast<size_t>(img) * C * HW;
-  const uint32_t* mi = mask + static_cast<size_t>(img) * HW;
+  const rsrc_t rx = make_rsrc(x + static_cast<size_t>(img) * C * HW, static_cast<unsigned>(C * HW * 4));
+  const rsrc_t rm = make_rsrc(mask + static_cast<size_t>(img) * HW, static_cast<unsigned>(HW * 4));
 
-  unsigned long long best = ~0ull;
-  const int ntiles = (HW + 31) / 32;
-  for (int t = blockIdx.y * kArgminWaves + wave; t < ntiles; t += gridDim.y * kArgminWaves) {
-    const int n = t * 32 + j;
-    const bool valid = n < HW;
-    float xv[NC][16];
+  // block blk -> LDS buffer sb: row c = channel c, 128 pixels, then the 128 patch masks (2 DMA
+  // wave-instructions per row; pixels past the map land as 0), spread over the workgroup's waves
+  auto stage = [&](int blk, int sb) __attribute__((always_inline)) {
+    float* X = push_smem + sb * push_buf_floats(C);
+    const int n0 = blk * kPushBlkPix;
+    for (int i = wave; i < 2 * C + 2; i += nw) {
+      const int c = i >> 1, half = i & 1;
+      const int n = n0 + 64 * half + lane;
+      if (c < C)
+        dma<float>(rx, X + c * kPushXS + 64 * half, n < HW ? static_cast<unsigned>((c * HW + n) * 4) : kOOB, 0u);
+      else
+        dma<float>(rm, X + C * kPushXS + 64 * half, n < HW ? static_cast<unsigned>(n * 4) : kOOB, 0u);
+    }
+  };
+
+  // per lane: best distance and its patch, runner-up distance (candidates arrive in increasing
+  // patch order, so a strict '<' keeps the lowest patch among equal distances)
+  float bd = __builtin_inff(), sd = __builtin_inff();
+  uint32_t bi = 0xffffffffu;
+  const uint32_t clsbit = active ? (1u << cls) : 0u;
+  // one tile's A fragments from LDS -> distances accumulator + ||x||^2 (fma chain per half,
+  // halves added), staged with the tile's masks into this wave's rows for the epilogue
+  auto mfma_tile = [&](const float* X, int tt, f32x16& acc, float* rows) __attribute__((always_inline)) {
+    acc = zero16();
     float x2 = 0.f;
 #pragma unroll
     for (int ct = 0; ct < NC; ++ct)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float v = xi[static_cast<size_t>(ct * 32 + acc_row(r, h)) * HW + (valid ? n : 0)];
-        xv[ct][r] = valid ? v : 0.f;
-        x2 = fmaf(xv[ct][r], xv[ct][r], x2);
+        const float xa = X[(ct * 32 + 16 * h + r) * kPushXS + tt * 32 + j];
+        x2 = fmaf(xa, xa, x2);
+        acc = mfma32(xa, pv[ct][r], acc);
       }
     x2 += __shfl_xor(x2, 32);
-    const uint32_t mk0 = mi[valid ? n : 0];
-    const uint32_t mk = valid ? mk0 : 0u;
-    // skip tiles holding no patch of any class of this wave's prototypes
-    if ((wave_or(mk) & wave_classes) == 0u) continue;
-
-    f32x16 acc = zero16();
-#pragma unroll
-    for (int ct = 0; ct < NC; ++ct)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc = mfma32(xv[ct][r], pv[ct][r], acc);
+    if (h == 0) rows[j] = x2;
+  };
+  auto epilogue = [&](const f32x16& acc, const float* rows, int nbase) __attribute__((always_inline)) {
+    float x2r[16], mkr[16];
+    load_rows16(rows + 4 * h, x2r);
+    load_rows16(rows + 32 + 4 * h, mkr);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int nr = acc_row(r, h);
-      const float x2n = __shfl(x2, nr);
-      const uint32_t mkn = __shfl(mk, nr);
-      const float d = l2_distance(x2n, p2, acc[r]);
-      if (active && ((mkn >> cls) & 1u)) {
-        const unsigned long long key =
-            (static_cast<unsigned long long>(__float_as_uint(d)) << 32) | static_cast<uint32_t>(t * 32 + nr);
-        best = key < best ? key : best;
+      const float d = l2_distance(x2r[r], p2, acc[r]);
+      const float dm = (__float_as_uint(mkr[r]) & clsbit) ? d : __builtin_inff();  // outside the class: absent
+      const bool c = dm < bd;
+      sd = c ? bd : fminf(sd, dm);
+      bi = c ? static_cast<uint32_t>(nbase + acc_row(r, h)) : bi;
+      bd = c ? dm : bd;
+    }
+  };
+
+  const int nblk = (HW + kPushBlkPix - 1) / kPushBlkPix;
+  int sb = 0;
+  if (stripe < nblk) stage(stripe, 0);
+  for (int blk = stripe; blk < nblk; blk += stripes, sb ^= 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of block blk
+    __syncthreads();  // every wave's DMA of blk landed; block blk - stripes fully consumed
+#ifndef PUSH_NO_DMA
+    if (blk + stripes < nblk) stage(blk + stripes, sb ^ 1);
+#endif
+    if (wave_classes == 0u) continue;  // no prototype of this wave is pushed (wave-uniform)
+    const float* X = push_smem + sb * push_buf_floats(C);
+    const uint32_t* MK = reinterpret_cast<const uint32_t*>(X + C * kPushXS);
+    const int n0 = blk * kPushBlkPix;
+    // this wave's tiles in pairs: both tiles' MFMA chains are issued before the first tile's
+    // epilogue, so the epilogue's VALU work overlaps the second chain in the MFMA pipe
+#pragma unroll 1
+    for (int ta = sub; ta < kPushBlk; ta += 2 * kPushSplit) {
+      const int tb = ta + kPushSplit;
+      const uint32_t mka = MK[ta * 32 + j];
+      const uint32_t mkb = tb < kPushBlk ? MK[tb * 32 + j] : 0u;
+      // tiles holding no patch of any class of this wave's prototypes are skipped
+      const bool run_a = __ballot((mka & wave_classes) != 0u) != 0ull;
+      const bool run_b = __ballot((mkb & wave_classes) != 0u) != 0ull;
+      if (h == 0) {
+        xw[32 + j] = __uint_as_float(mka);
+        xw[96 + j] = __uint_as_float(mkb);
       }
+      f32x16 acc_a, acc_b;
+      if (run_a) mfma_tile(X, ta, acc_a, xw);
+      if (run_b) mfma_tile(X, tb, acc_b, xw + 64);
+      wave_lds_fence();
+#ifndef PUSH_NO_EPI
+      if (run_a) epilogue(acc_a, xw, n0 + ta * 32);
+      if (run_b) epilogue(acc_b, xw + 64, n0 + tb * 32);
+#endif
+      wave_lds_fence();  // the row reads are done before the next pair rewrites them
     }
   }
-  const unsigned long long other = shfl_xor_u64(best, 32);
-  best = other < best ? other : best;
-  if (h == 0 && pvalid && best != ~0ull) atomicMin(&keys[static_cast<size_t>(img) * P + p], best);
+  unsigned long long best = bd == __builtin_inff() ? ~0ull : (static_cast<unsigned long long>(__float_as_uint(bd)) << 32) | bi;
+  unsigned long long second = sd == __builtin_inff() ? ~0ull : (static_cast<unsigned long long>(__float_as_uint(sd)) << 32) | 0xffffffffu;
+  top2_merge(best, second, shfl_xor_u64(best, 32), shfl_xor_u64(second, 32));
+  if (h == 0 && pvalid) {
+    unsigned long long* o = part + ((static_cast<size_t>(img) * stripes * kPushSplit + stripe * kPushSplit + sub) * P + p) * 2;
+    o[0] = best;
+    o[1] = second;
+  }
+}
+
+// Folds the stripes' partial top-2 of each (image, prototype): img_keys = the minimum key,
+// img_second (optional) = the runner-up key (another patch), UINT64_MAX when absent.
+__global__ __launch_bounds__(256) void push_top2_kernel(const unsigned long long* __restrict__ part, int n_img,
+                                                        int stripes, int P, unsigned long long* __restrict__ keys,
+                                                        unsigned long long* __restrict__ second) {
+  const long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= static_cast<long long>(n_img) * P) return;
+  const int img = static_cast<int>(i / P), p = static_cast<int>(i - static_cast<long long>(img) * P);
+  unsigned long long b = ~0ull, s = ~0ull;
+  for (int st = 0; st < stripes; ++st) {
+    const unsigned long long* o = part + ((static_cast<size_t>(img) * stripes + st) * P + p) * 2;
+    top2_merge(b, s, o[0], o[1]);
+  }
+  keys[i] = b;
+  if (second) second[i] = s;
 }
 
 // One wave per prototype: fold the batch's keys in image order (strict '<', push.py:265),
-// then copy the winning feature vector (push.py:276-280).
-__global__ __launch_bounds__(256) void push_merge_kernel(const unsigned long long* __restrict__ keys, int n_img,
+// then copy the winning feature vector (push.py:276-280). With the runner-up keys, the
+// running second-smallest distance over every patch seen so far is kept too (near-tie flag).
+__global__ __launch_bounds__(256) void push_merge_kernel(const unsigned long long* __restrict__ keys,
+                                                         const unsigned long long* __restrict__ keys2, int n_img,
                                                          long long first_img, const float* __restrict__ x, int C,
                                                          int hw, int P, float* __restrict__ gdist,
-                                                         long long* __restrict__ gimg, int* __restrict__ gpatch,
-                                                         float* __restrict__ gfmap) {
+                                                         float* __restrict__ gsecond, long long* __restrict__ gimg,
+                                                         int* __restrict__ gpatch, float* __restrict__ gfmap) {
   const int p = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (p >= P) return;
   float best = gdist[p];
+  float sec = gsecond ? gsecond[p] : 0.f;
   int win = -1;
   uint32_t patch = 0;
   for (int img = 0; img < n_img; ++img) {
     const unsigned long long key = keys[static_cast<size_t>(img) * P + p];
     if (key == ~0ull) continue;  // no patch of the prototype's class (push.py:255-256)
     const float d = __uint_as_float(static_cast<uint32_t>(key >> 32));
+    if (gsecond) {
+      const unsigned long long k2 = keys2[static_cast<size_t>(img) * P + p];
+      const float d2 = k2 == ~0ull ? __builtin_inff() : __uint_as_float(static_cast<uint32_t>(k2 >> 32));
+      if (d < best)
+        sec = best < d2 ? best : d2;
+      else
+        sec = d < sec ? d : sec;
+    }
     if (d < best) {
       best = d;
       win = img;
       patch = static_cast<uint32_t>(key);
     }
   }
+  if (lane == 0 && gsecond) gsecond[p] = sec;
   if (win < 0) return;
   if (lane == 0) {
     gdist[p] = best;
@@ -205,50 +348,110 @@ extern "C" int protoseg_patch_class_mask(const void* label, int label_dtype, int
   return check_launch("patch_mask_kernel");
 }
 
+namespace {
+// Partial top-2 scratch ([n_img][stripes x split][P][2] u64): one grow-only block per (device, stream),
+// reused by later calls on that stream (kernels on one stream are ordered), so a call is only
+// kernel launches and can be captured in a HIP graph once the block exists.
+void* push_scratch(size_t need, hipStream_t s, int* status) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> blocks;
+  int dev = 0;
+  *status = PROTOSEG_OK;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    *status = check_launch("hipGetDevice");
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lock(mu);
+  auto& b = blocks[{dev, s}];
+  if (b.second < need) {
+    if (b.first && (hipStreamSynchronize(s) != hipSuccess || hipFree(b.first) != hipSuccess)) {
+      *status = check_launch("push scratch regrow");
+      return nullptr;
+    }
+    b = {nullptr, 0};
+    const size_t bytes = need < (1u << 20) ? (1u << 20) : need;
+    const hipError_t e = hipMalloc(&b.first, bytes);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      b = {nullptr, 0};
+      *status = fail(PROTOSEG_ERR_HIP, "hipMalloc (push scratch, %zu B): %s", bytes, hipGetErrorString(e));
+      return nullptr;
+    }
+    b.second = bytes;
+  }
+  return b.first;
+}
+}  // namespace
+
 extern "C" int protoseg_push_argmin(const float* x, int n_img, int C, int h, int w, const float* protos, int P,
                                     const int32_t* proto_class, const uint32_t* mask, uint64_t* img_keys,
-                                    protoseg_stream_t stream) {
+                                    uint64_t* img_second, protoseg_stream_t stream) {
   if (!x || !protos || !proto_class || !mask || !img_keys)
     return fail(PROTOSEG_ERR_INVALID, "null pointer argument");
   if (n_img <= 0 || h <= 0 || w <= 0 || P <= 0) return fail(PROTOSEG_ERR_INVALID, "bad shape");
   const int nc = nc_of_push(C);
   if (!nc) return fail(PROTOSEG_ERR_UNSUPPORTED, "C=%d", C);
   if (n_img > 65535) return fail(PROTOSEG_ERR_UNSUPPORTED, "n_img=%d per call", n_img);
+  if (reinterpret_cast<uintptr_t>(protos) % 16 != 0) return fail(PROTOSEG_ERR_INVALID, "protos must be 16-B aligned");
+  const long long HW = static_cast<long long>(h) * w;
+  if (HW >= (1LL << 31) / 2) return fail(PROTOSEG_ERR_UNSUPPORTED, "h*w=%lld", HW);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (hipMemsetAsync(img_keys, 0xff, static_cast<size_t>(n_img) * P * sizeof(uint64_t), s) != hipSuccess)
-    return check_launch("memset img_keys");
-  const int HW = h * w;
   const int npt = static_cast<int>(ceil_div(P, 32));
-  const long long ntiles = ceil_div(HW, 32);
-  long long splits = 1024 / (static_cast<long long>(npt) * n_img);
-  if (splits < 1) splits = 1;
-  const long long need = ceil_div(ntiles, kArgminWaves);
-  if (splits > need) splits = need;
-  const dim3 grid(npt, static_cast<unsigned>(splits), n_img);
-  auto* keys = reinterpret_cast<unsigned long long*>(img_keys);
-  if (nc == 1)
-    hipLaunchKernelGGL(push_argmin_kernel<1>, grid, dim3(kArgminWaves * 64), 0, s, x, HW, protos, P, proto_class,
-                       mask, keys);
-  else if (nc == 2)
-    hipLaunchKernelGGL(push_argmin_kernel<2>, grid, dim3(kArgminWaves * 64), 0, s, x, HW, protos, P, proto_class,
-                       mask, keys);
-  else
-    hipLaunchKernelGGL(push_argmin_kernel<4>, grid, dim3(kArgminWaves * 64), 0, s, x, HW, protos, P, proto_class,
-                       mask, keys);
-  return check_launch("push_argmin_kernel");
+  const int nchunk = static_cast<int>(ceil_div(npt, kPushMaxTiles));
+  // prototype chunks of 8 tiles; the last launch's chunk may be narrower (fewer waves)
+  const int full = npt / kPushMaxTiles, rem = npt - full * kPushMaxTiles;
+  const long long nblk = ceil_div(HW, kPushBlkPix);
+  // about 2 workgroups per CU over all images and chunks, at least one block per stripe
+  long long stripes = ceil_div(PUSH_WG_TARGET, static_cast<long long>(n_img) * nchunk);
+  if (stripes > nblk) stripes = nblk;
+  if (stripes < 1) stripes = 1;
+  const size_t need = static_cast<size_t>(n_img) * stripes * kPushSplit * P * 2 * sizeof(unsigned long long);
+  int st = PROTOSEG_OK;
+  auto* part = static_cast<unsigned long long*>(push_scratch(need, s, &st));
+  if (st) return st;
+  auto launch = [&](auto kern, int chunks, int pt0, int nptc) {
+    if (chunks <= 0) return;
+    const int waves = nptc * kPushSplit;
+    KernelTimer timer("push_argmin_kernel", s);
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(stripes), n_img, chunks), dim3(waves * 64),
+                       push_lds_bytes(C, waves), s, x, static_cast<int>(HW), protos, P, pt0, nptc, proto_class, mask,
+                       part, static_cast<int>(stripes));
+  };
+  if (nc == 1) {
+    launch(push_argmin_kernel<1>, full, 0, kPushMaxTiles);
+    launch(push_argmin_kernel<1>, rem ? 1 : 0, full * kPushMaxTiles, rem);
+  } else if (nc == 2) {
+    if (int e = ensure_lds<push_argmin_kernel<2>, 72 * 1024>()) return e;
+    launch(push_argmin_kernel<2>, full, 0, kPushMaxTiles);
+    launch(push_argmin_kernel<2>, rem ? 1 : 0, full * kPushMaxTiles, rem);
+  } else {
+    if (int e = ensure_lds<push_argmin_kernel<4>, 140 * 1024>()) return e;
+    launch(push_argmin_kernel<4>, full, 0, kPushMaxTiles);
+    launch(push_argmin_kernel<4>, rem ? 1 : 0, full * kPushMaxTiles, rem);
+  }
+  if (int e = check_launch("push_argmin_kernel")) return e;
+  const long long n = static_cast<long long>(n_img) * P;
+  hipLaunchKernelGGL(push_top2_kernel, dim3(static_cast<unsigned>(ceil_div(n, 256))), dim3(256), 0, s, part, n_img,
+                     static_cast<int>(stripes) * kPushSplit, P, reinterpret_cast<unsigned long long*>(img_keys),
+                     reinterpret_cast<unsigned long long*>(img_second));
+  return check_launch("push_top2_kernel");
 }
 
-extern "C" int protoseg_push_merge(const uint64_t* img_keys, int n_img, int64_t first_img, const float* x, int C,
-                                   int hw, int P, float* global_dist, int64_t* global_img, int32_t* global_patch,
+extern "C" int protoseg_push_merge(const uint64_t* img_keys, const uint64_t* img_second, int n_img,
+                                   int64_t first_img, const float* x, int C, int hw, int P, float* global_dist,
+                                   float* global_second, int64_t* global_img, int32_t* global_patch,
                                    float* global_fmap, protoseg_stream_t stream) {
   if (!img_keys || !x || !global_dist || !global_img || !global_patch || !global_fmap)
     return fail(PROTOSEG_ERR_INVALID, "null pointer argument");
+  if (!img_second != !global_second)
+    return fail(PROTOSEG_ERR_INVALID, "img_second and global_second are given together or not at all");
   if (n_img <= 0 || C <= 0 || hw <= 0 || P <= 0) return fail(PROTOSEG_ERR_INVALID, "bad shape");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int waves_per_block = 4;
   hipLaunchKernelGGL(push_merge_kernel, dim3(static_cast<unsigned>(ceil_div(P, waves_per_block))),
-                     dim3(waves_per_block * 64), 0, s, reinterpret_cast<const unsigned long long*>(img_keys), n_img,
-                     static_cast<long long>(first_img), x, C, hw, P, global_dist,
+                     dim3(waves_per_block * 64), 0, s, reinterpret_cast<const unsigned long long*>(img_keys),
+                     reinterpret_cast<const unsigned long long*>(img_second), n_img,
+                     static_cast<long long>(first_img), x, C, hw, P, global_dist, global_second,
                      reinterpret_cast<long long*>(global_img), global_patch, global_fmap);
   return check_launch("push_merge_kernel");
 }

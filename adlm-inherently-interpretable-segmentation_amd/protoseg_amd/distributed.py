@@ -2,9 +2,9 @@
 
 Two exchange steps exist on the hot path:
   * training: gradients are summed over ranks once per optimizer step (on the iter_size
-    accumulation boundary of module.py:235-243). ``GradientBuckets`` flattens the
-    parameters into a few large contiguous buckets (xGMI rings are per-link bound, so few
-    big collectives beat many small ones) and all-reduces each bucket asynchronously;
+    accumulation boundary of module.py:235-243), by ``GradientBuckets`` (a few large
+    asynchronous bucket all-reduces launched from backward's gradient hooks, used by
+    train.PatchClassificationStep and bench.py's multi-GPU step);
   * push: images are independent, so each rank scans a contiguous shard and one MIN
     all-reduce over packed 64-bit keys (distance bits << 32 | image index) reproduces the
     serial scan's "strictly smaller, earlier image wins" order exactly (push.py:101, 265);
@@ -64,6 +64,11 @@ def reduce_push_state(state, group=None) -> None:
     patch = torch.where(mine, state.patch.to(torch.int64) + 1, torch.zeros_like(img))
     dist.all_reduce(fmap, op=dist.ReduceOp.SUM, group=group)
     dist.all_reduce(patch, op=dist.ReduceOp.SUM, group=group)
+    if state.second is not None:
+        # global runner-up: the winning rank offers its own runner-up, every other rank its best
+        cand = torch.where(mine, state.second, torch.minimum(state.dist, state.second))
+        dist.all_reduce(cand, op=dist.ReduceOp.MIN, group=group)
+        state.second.copy_(cand)
     gimg = gkey & 0xFFFFFFFF
     state.dist.copy_((gkey >> 32).to(torch.int32).view(torch.float32))
     state.img.copy_(torch.where(gimg == INT32_MAX, torch.full_like(gimg, -1), gimg))
@@ -87,11 +92,19 @@ def reduce_bound_boxes(boxes, device="cpu", group=None):
 
 
 class GradientBuckets:
-    """Sums .grad of ``params`` over ranks with a few large asynchronous all-reduces.
+    """Sums (or averages) the .grad of ``params`` over ranks with a few large asynchronous
+    all-reduces — the exchange step of data-parallel training (train.PatchClassificationStep,
+    and bench.py's multi-GPU step).
 
-    Buckets are filled in reverse registration order (the order backward produces grads),
-    each up to ``bucket_mb`` MiB; ``allreduce()`` launches them all and ``wait()`` averages.
-    Used for the prototype-layer gradients in bench.py and for full models in train.py.
+    Buckets are filled in reverse registration order (the order backward produces grads), each
+    up to ``bucket_mb`` MiB; xGMI rings are per-link bound, so few large collectives beat many
+    small ones. ``arm()`` before the backward of the step that ends a gradient accumulation
+    (module.py:235-243: the optimizer steps every iter_size micro-steps) makes each bucket's
+    all-reduce start from the gradient hook of its last parameter, so the exchange overlaps the
+    rest of the backward; buckets are always launched in index order, so every rank issues the
+    same collective sequence. ``wait()`` launches whatever has not started (a parameter that got
+    no gradient contributes zeros and is left without one), waits, and writes the reduced
+    gradients back. Without ``arm()``, ``allreduce()`` + ``wait()`` do the same after backward.
     """
 
     def __init__(self, params: Iterable[torch.nn.Parameter], bucket_mb: float = 64.0, group=None,
@@ -111,32 +124,69 @@ class GradientBuckets:
             size += nbytes
         if cur:
             self.buckets.append(cur)
-        self._pending = []
+        self._bucket_of = {id(p): b for b, bucket in enumerate(self.buckets) for p in bucket}
+        self._hooks = []
+        self._armed = False
+        self._ready = [0] * len(self.buckets)
+        self._pending: List[Optional[tuple]] = [None] * len(self.buckets)
+        self._next = 0
+
+    def _world(self) -> int:
+        return world_info(self.group)[1]
+
+    def arm(self) -> None:
+        """Launch each bucket's all-reduce from backward's gradient hooks (next backward only)."""
+        if self._world() == 1:
+            return
+        if not self._hooks:
+            for p in self.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        self._ready = [0] * len(self.buckets)
+        self._armed = True
+
+    def _on_grad(self, p) -> None:
+        if not self._armed:
+            return
+        b = self._bucket_of[id(p)]
+        self._ready[b] += 1
+        while self._next < len(self.buckets) and self._ready[self._next] == len(self.buckets[self._next]):
+            self._launch(self._next)
+
+    def _launch(self, b: int) -> None:
+        bucket = self.buckets[b]
+        flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in bucket])
+        work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self._pending[b] = (flat, work, [p.grad is not None for p in bucket])
+        self._next = b + 1
 
     def allreduce(self) -> None:
-        rank, world = world_info(self.group)
-        if world == 1:
+        """Launch every bucket not yet launched (in index order)."""
+        if self._world() == 1:
             return
-        self._pending = []
-        for bucket in self.buckets:
-            grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in bucket]
-            flat = torch.cat([g.reshape(-1) for g in grads])
-            work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-            self._pending.append((bucket, flat, work))
+        while self._next < len(self.buckets):
+            self._launch(self._next)
 
     def wait(self) -> None:
-        _, world = world_info(self.group)
-        for bucket, flat, work in self._pending:
+        world = self._world()
+        if world == 1:
+            return
+        self.allreduce()
+        for b, bucket in enumerate(self.buckets):
+            flat, work, had = self._pending[b]
             work.wait()
             if self.average:
                 flat.div_(world)
             off = 0
-            for p in bucket:
+            for p, h in zip(bucket, had):
                 n = p.numel()
-                g = flat[off:off + n].view_as(p)
-                if p.grad is None:
-                    p.grad = g.clone()
-                else:
-                    p.grad.copy_(g)
+                if h:  # a parameter without a gradient on this rank stays without one
+                    p.grad.copy_(flat[off:off + n].view_as(p))
                 off += n
-        self._pending = []
+        self._pending = [None] * len(self.buckets)
+        self._next = 0
+        self._armed = False
+
+    def remove_hooks(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

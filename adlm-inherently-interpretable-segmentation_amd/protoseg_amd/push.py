@@ -66,20 +66,23 @@ def patch_class_mask(labels: Tensor, h: int, w: int, lut: Optional[Tensor] = Non
     return mask
 
 
-def push_argmin(x: Tensor, protos: Tensor, proto_class: Tensor, mask: Tensor) -> Tensor:
+def push_argmin(x: Tensor, protos: Tensor, proto_class: Tensor, mask: Tensor, with_second: bool = False):
     """Per image and prototype, the masked minimum key (float_bits(d) << 32 | patch) as int64
-    storage of uint64 [n, P]; -1 (all ones) when the image has no patch of the class."""
+    storage of uint64 [n, P]; -1 (all ones) when the image has no patch of the class. With
+    ``with_second`` also the runner-up of the same image (float_bits(d2) << 32 | 0xFFFFFFFF: the
+    second-smallest class-patch distance), as a pair."""
     dev = _lib.require_device(x, protos, proto_class, mask)
     x = x.float().contiguous()
     protos = protos.reshape(protos.shape[0], -1).float().contiguous()
     n, C, h, w = x.shape
     P = protos.shape[0]
     keys = torch.empty((n, P), device=dev, dtype=torch.int64)
+    second = torch.empty_like(keys) if with_second else None
     with torch.cuda.device(dev):
         _lib.call("protoseg_push_argmin", _lib.ptr(x), n, C, h, w, _lib.ptr(protos), P,
                   _lib.ptr(proto_class.to(torch.int32).contiguous()), _lib.ptr(mask.contiguous()), _lib.ptr(keys),
-                  _lib.stream_of(dev))
-    return keys
+                  _lib.ptr(second), _lib.stream_of(dev))
+    return (keys, second) if with_second else keys
 
 
 def decode_keys(keys: Tensor):
@@ -93,11 +96,14 @@ def decode_keys(keys: Tensor):
 
 @dataclass
 class PushState:
-    """Running global minimum (push.py:55-61): distance, image index, patch index, feature vector."""
+    """Running global minimum (push.py:55-61): distance, image index, patch index, feature
+    vector; plus the runner-up distance over every class patch seen (near-tie flags)."""
     dist: Tensor
     img: Tensor
     patch: Tensor
     fmap: Tensor
+    second: Optional[Tensor] = None
+    near_ties: Optional[np.ndarray] = None
     # per image index: (H_img, W_img, h, w) needed for the receptive-field boxes
     geometry: Dict[int, tuple] = field(default_factory=dict)
 
@@ -106,27 +112,46 @@ class PushState:
         return cls(dist=torch.full((P,), math.inf, device=device, dtype=torch.float32),
                    img=torch.full((P,), -1, device=device, dtype=torch.int64),
                    patch=torch.full((P,), -1, device=device, dtype=torch.int32),
-                   fmap=torch.zeros((P, C), device=device, dtype=torch.float32))
+                   fmap=torch.zeros((P, C), device=device, dtype=torch.float32),
+                   second=torch.full((P,), math.inf, device=device, dtype=torch.float32))
 
 
 def push_update(state: PushState, x: Tensor, labels: Tensor, protos: Tensor, proto_class: Tensor, first_img: int,
                 lut: Optional[Tensor] = None) -> None:
-    """One batch of images (dataset indices first_img ..): mask -> argmin -> strict-'<' merge."""
+    """One batch of images (dataset indices first_img ..): mask -> argmin -> strict-'<' merge.
+    This is push_prototypes' inner step (one call per batch of equal-geometry images)."""
     x = x.float().contiguous()
     n, C, h, w = x.shape
     if labels.dim() == 2:
         labels = labels.unsqueeze(0)
     mask = patch_class_mask(labels, h, w, lut)
-    keys = push_argmin(x, protos, proto_class, mask)
+    keys, second = push_argmin(x, protos, proto_class, mask, with_second=True)
     dev = x.device
     P = keys.shape[1]
+    if state.second is None:
+        state.second = torch.full((P,), math.inf, device=dev, dtype=torch.float32)
     with torch.cuda.device(dev):
-        _lib.call("protoseg_push_merge", _lib.ptr(keys), n, int(first_img), _lib.ptr(x), C, h * w, P,
-                  _lib.ptr(state.dist), _lib.ptr(state.img), _lib.ptr(state.patch), _lib.ptr(state.fmap),
-                  _lib.stream_of(dev))
+        _lib.call("protoseg_push_merge", _lib.ptr(keys), _lib.ptr(second), n, int(first_img), _lib.ptr(x), C, h * w,
+                  P, _lib.ptr(state.dist), _lib.ptr(state.second), _lib.ptr(state.img), _lib.ptr(state.patch),
+                  _lib.ptr(state.fmap), _lib.stream_of(dev))
     H, W = labels.shape[-2:]
     for i in range(n):
         state.geometry[first_img + i] = (int(H), int(W), int(h), int(w))
+
+
+def near_ties(state: PushState, protos: Tensor, rtol: float = 1e-5) -> np.ndarray:
+    """Prototypes whose winning patch beats the runner-up (any image, any class patch) by no
+    more than the f32 rounding band of the expanded distance, rtol * (||x||^2 + ||p||^2) with x
+    the winning feature vector: there the reference's own rounding (or its Python-set order
+    for exact ties inside an image, push.py:214-230) may pick the other patch (SURVEY.md §7,
+    hard part 2). ``protos`` are the prototype vectors the push measured against."""
+    if state.second is None:
+        raise ValueError("push state has no runner-up distances")
+    p = protos.detach().reshape(protos.shape[0], -1).float().to(state.fmap.device)
+    band = rtol * ((state.fmap * state.fmap).sum(1) + (p * p).sum(1))
+    found = state.img >= 0
+    tie = found & torch.isfinite(state.second) & (state.second - state.dist <= band)
+    return np.nonzero(tie.cpu().numpy())[0]
 
 
 _ACT_KINDS = {"log": _lib.ACT_LOG, "linear": _lib.ACT_LINEAR, "identity": _lib.ACT_IDENTITY}
@@ -329,7 +354,7 @@ def push_prototypes(dataset, prototype_network_parallel, prototype_layer_stride=
     rank, world = world_info(process_group)
     lo, hi = shard_bounds(len(dataset.img_ids), rank, world)
 
-    def load(push_iter):
+    def load_raw(push_iter):
         img_id = dataset.img_ids[push_iter]
         with open(dataset.get_img_path(img_id), "rb") as f:
             img = Image.open(f).convert("RGB")
@@ -341,17 +366,42 @@ def push_prototypes(dataset, prototype_network_parallel, prototype_layer_stride=
         labels = torch.as_tensor(np.ascontiguousarray(gt_ann)).to(device)
         if labels.dtype not in (torch.int64, torch.int32, torch.uint8):
             labels = labels.to(torch.int64)
-        img_tensor = to_normalized_tensor(img, mean, std).unsqueeze(0).to(device)
+        return to_normalized_tensor(img, mean, std).unsqueeze(0).to(device), labels
+
+    def load(push_iter):
+        img_tensor, labels = load_raw(push_iter)
         return ppnet.conv_features(img_tensor), labels
 
     log("Updating prototypes...")
+    per = max(1, int(images_per_batch))
     with torch.no_grad():
+        # Runs of up to images_per_batch consecutive images of one geometry go through the
+        # backbone as one batch and through mask -> argmin -> merge as ONE push_update call;
+        # the merge folds them in image order, so the result is the serial scan's.
+        run: List[tuple] = []
+
+        def flush():
+            if run:
+                imgs = torch.cat([r[0] for r in run], 0)
+                labels = torch.stack([r[1] for r in run], 0)
+                push_update(state, ppnet.conv_features(imgs), labels, ppnet.prototype_vectors, proto_class_t,
+                            run[0][2], lut)
+                run.clear()
+
         for push_iter in range(lo, hi):
-            conv_features, labels = load(push_iter)
-            push_update(state, conv_features, labels, ppnet.prototype_vectors, proto_class_t, push_iter, lut)
+            img_tensor, labels = load_raw(push_iter)
+            if run and (len(run) == per or run[0][0].shape != img_tensor.shape or run[0][1].shape != labels.shape
+                        or run[0][1].dtype != labels.dtype):
+                flush()
+            run.append((img_tensor, labels, push_iter))
+        flush()
 
     if world > 1:
         reduce_push_state(state, process_group)
+    state.near_ties = near_ties(state, ppnet.prototype_vectors)
+    if len(state.near_ties):
+        log(f"\t{len(state.near_ties)} prototype(s) won by a margin within f32 rounding of the runner-up patch: "
+            f"{state.near_ties.tolist()[:20]}")
 
     with_class = bool(save_prototype_class_identity)
     proto_rf_boxes = rf_boxes(state, proto_class, with_class)

@@ -3,9 +3,12 @@
 
 Workload (BASELINE.json metric: 513x513, 19 prototypes/class; configs[1] cityscapes_no_kld_imnet
 otherwise): 513x513 crops -> 65x65 feature maps, C=64, P=361 (19 classes x 19), K=19; the
-P=190 (10/class, the gin files' count) step is a side line with its own roofline. One "step" = the prototype layer's forward
-(distances + logits, one fused kernel) and backward (g_x, g_prototypes, g_last_layer) over a
-batch of B images per GPU, plus the data-parallel gradient all-reduce (RCCL) when N>1.
+P=190 (10/class, the gin files' count) step is a side line with its own roofline. One "step" = the
+prototype layer's forward (distances + logits, one fused kernel), backward (g_x, g_prototypes,
+g_last_layer; one fused kernel per prototype chunk), the data-parallel gradient exchange when
+N>1 (protoseg_amd.distributed.GradientBuckets: bucketed RCCL all-reduce, the exchange of
+train.PatchClassificationStep) and the Adam update of P and W (module.py:391), over a batch of B
+images per GPU.
 Synthetic data (seed 20220227): X = sigmoid(N(0, 2^2)), prototypes U[0,1),
 last layer from the class identity; inputs resident in HBM before timing starts.
 
@@ -83,8 +86,15 @@ class LayerStep:
         self.ws = torch.empty(self.ws_bytes, device=device, dtype=torch.uint8)
         self.xdt = _lib.F32 if x_dtype == torch.float32 else _lib.BF16
         self.device = device
-        self.grad_flat = torch.empty(P * C + K * P, **f32)
         self.prec = _lib.PRECISIONS[precision]
+        # The trained parameters (sharing storage with the kernels' buffers; the backward writes
+        # their .grad in place) and the reference's optimizer (module.py:391: Adam; lr of the
+        # prototype vectors, gin joint_optimizer_lr_prototype_vectors). capturable: the update
+        # runs inside the step's HIP graph.
+        self.params = [torch.nn.Parameter(self.protos), torch.nn.Parameter(self.w_last)]
+        self.params[0].grad, self.params[1].grad = self.g_p, self.g_w
+        self.opt = torch.optim.Adam(self.params, lr=2.5e-4, capturable=True, fused=True)
+        self.buckets = None
 
     def _stream(self):
         return _lib.stream_of(self.device)
@@ -147,11 +157,18 @@ class LayerStep:
                   _lib.ptr(self.g_dist), _lib.ptr(self.g_x), _lib.ptr(self.g_p), _lib.ptr(self.g_w),
                   _lib.ptr(self.ws), self.ws_bytes, self._stream())
 
-    def allreduce(self, world):
+    def opt_step(self):
+        self.opt.step()
+
+    def exchange(self, world):
+        """Data-parallel gradient exchange: the training step's GradientBuckets (bucketed RCCL
+        all-reduce, averaged), the same class train.PatchClassificationStep uses."""
         if world > 1:
-            self.grad_flat[: self.P * self.C].copy_(self.g_p.view(-1))
-            self.grad_flat[self.P * self.C:].copy_(self.g_w.view(-1))
-            dist.all_reduce(self.grad_flat)
+            if self.buckets is None:
+                from protoseg_amd.distributed import GradientBuckets
+                self.buckets = GradientBuckets(self.params, average=True)
+            self.buckets.allreduce()
+            self.buckets.wait()
 
     @property
     def fused(self):
@@ -220,31 +237,35 @@ def capture(fn, stream):
 
 
 def time_layer(step: LayerStep, steps: int, warmup: int, world: int, use_graph: bool):
-    """Times `steps` training steps of the prototype layer (fwd + bwd [+ all-reduce]).
+    """Times `steps` training steps of the prototype layer: forward, backward (g_x, g_P, g_W),
+    [N > 1: the bucketed gradient all-reduce], Adam update of P and W.
 
-    A step is the forward call and one backward call (g_x, g_P, g_W), as the autograd op
-    issues them. With use_graph the step's C-ABI calls are captured once into a HIP graph and
-    each step is one replay (no host launch gaps); the all-reduce stays outside the graph.
-    Per-kernel device times come from HIP events the library records around the named kernel
-    alone (protoseg_timing_events) during eager calls on the same stream."""
+    A step is the forward call and one backward call, as the autograd op issues them, then the
+    optimizer. With use_graph the C-ABI calls and the (capturable) Adam update are captured into
+    HIP graphs and replayed (no host launch gaps); at N > 1 the all-reduce runs between the
+    backward graph and the optimizer graph. Per-kernel device times come from HIP events the
+    library records around each launch of the named kernel during eager calls on the same stream."""
     names = step.kernel_names()
-    step_calls = [step.fwd, step.bwd]
     calls = step.timed_calls()
     stream = torch.cuda.Stream(step.device)
     with torch.cuda.stream(stream):
         for _ in range(max(1, warmup)):
-            for c in step_calls + calls:
+            for c in [step.fwd, step.bwd] + calls:
                 c()
-            step.allreduce(world)
+            step.exchange(world)
+            step.opt_step()
         torch.cuda.synchronize()
-        if use_graph:
-            g_step = capture(lambda: [c() for c in step_calls], stream)
+        if use_graph and world == 1:
+            g_step = capture(lambda: [step.fwd(), step.bwd(), step.opt_step()], stream)
             run_step = g_step.replay
-            for _ in range(warmup):
-                run_step()
-                step.allreduce(world)
+        elif use_graph:
+            g_grad = capture(lambda: [step.fwd(), step.bwd()], stream)
+            g_opt = capture(step.opt_step, stream)
+            run_step = lambda: (g_grad.replay(), step.exchange(world), g_opt.replay())  # noqa: E731
         else:
-            run_step = lambda: [c() for c in step_calls]  # noqa: E731
+            run_step = lambda: (step.fwd(), step.bwd(), step.exchange(world), step.opt_step())  # noqa: E731
+        for _ in range(warmup):
+            run_step()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -252,7 +273,6 @@ def time_layer(step: LayerStep, steps: int, warmup: int, world: int, use_graph: 
         t0 = time.perf_counter()
         for _ in range(steps):
             run_step()
-            step.allreduce(world)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -297,7 +317,7 @@ def time_kld_step(step: LayerStep, steps: int, warmup: int):
     """BASELINE configs[2] step on one GPU: forward, KLD loss (module.py:167-208) forward and
     backward, layer backward with g_logits and the KLD g_dist, as one HIP graph per step.
     Returns ms per step and the per-launch event times of the two KLD calls."""
-    calls = [step.fwd, step.kld_fwd, step.kld_bwd, step.bwd_gd]
+    calls = [step.fwd, step.kld_fwd, step.kld_bwd, step.bwd_gd, step.opt_step]
     stream = torch.cuda.Stream(step.device)
     with torch.cuda.stream(stream):
         for _ in range(max(1, warmup)):
@@ -328,7 +348,8 @@ def time_kld_step(step: LayerStep, steps: int, warmup: int):
     loss = float(step.kld_loss)
     n = step.B * step.h * step.w
     kb = float(np.mean(ms_b)) * 1e-3
-    return {"workload": "cityscapes_kld_imnet step on 1 GPU: fwd + KLD fwd/bwd (loss_weight_kld 0.25) + bwd with g_dist",
+    return {"workload": "cityscapes_kld_imnet step on 1 GPU: fwd + KLD fwd/bwd (loss_weight_kld 0.25) + bwd with g_dist "
+                        "+ Adam update",
             "ms_per_step": round(elapsed / steps * 1e3, 4), "img_per_s": round(step.B * steps / elapsed, 1),
             "kld_forward_ms": round(float(np.mean(ms_f)), 4), "kld_backward_ms": round(kb * 1e3, 4),
             "kld_backward_gbps": round(n * step.P * 4 / kb / 1e9, 1), "loss": round(loss, 6)}
@@ -393,42 +414,65 @@ def make_push_inputs(n_img, C, H, W, h, w, P, K, device, seed):
     return x, protos, labels, pc
 
 
+def kernel_launch_times(name, fn, reps, npair=8):
+    """Per-launch device seconds of the kernel `name` over `reps` eager calls of fn(), from the
+    library's per-launch event hook (protoseg_timing_events_n). Returns (mean s per launch,
+    launches per call)."""
+    lib = _lib.load()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(npair)] for _ in range(2)]
+    for row in ev:
+        for e in row:
+            e.record()
+    torch.cuda.synchronize()
+    starts = (ctypes.c_void_p * npair)(*[e.cuda_event for e in ev[0]])
+    stops = (ctypes.c_void_p * npair)(*[e.cuda_event for e in ev[1]])
+    times, per_call = [], 0
+    lib.protoseg_timing_events_n(name.encode(), starts, stops, npair)
+    try:
+        lib.protoseg_timing_launches()
+        for _ in range(reps):
+            fn()
+            torch.cuda.synchronize()
+            k = lib.protoseg_timing_launches()
+            if k < 1 or k > npair:
+                raise RuntimeError(f"timing hook bracketed {k} launches of {name}")
+            per_call = k
+            times += [ev[0][i].elapsed_time(ev[1][i]) * 1e-3 for i in range(k)]
+    finally:
+        lib.protoseg_timing_events_n(None, None, None, 0)
+    return float(np.mean(times)), per_call
+
+
 def time_push(n_img, steps, warmup, device, C=64, H=1024, W=2048, h=129, w=257, P=190, K=19):
+    """The shipped push driver's inner step (push.push_update, one call per batch of n_img
+    equal-geometry images, as push_prototypes issues it with images_per_batch = n_img):
+    patch mask -> top-2 argmin -> strict-'<' merge. Wall time per image over `steps` calls;
+    the argmin kernel's per-launch device time from the library's event hook."""
     from protoseg_amd import push as dpush
     x, protos, labels, pc = make_push_inputs(n_img, C, H, W, h, w, P, K, device, SEED)
     state = dpush.PushState.create(P, C, device)
-    keys = torch.empty((n_img, P), device=device, dtype=torch.int64)
-    mask = torch.empty((n_img, h * w), device=device, dtype=torch.int32)
-    stream = _lib.stream_of(device)
 
-    def run(ev=None):
-        _lib.call("protoseg_patch_class_mask", _lib.ptr(labels), _lib.U8, n_img, H, W, h, w, ctypes.c_void_p(None), 0,
-                  _lib.ptr(mask), stream)
-        if ev is not None:
-            ev[0].record()
-        _lib.call("protoseg_push_argmin", _lib.ptr(x), n_img, C, h, w, _lib.ptr(protos), P, _lib.ptr(pc),
-                  _lib.ptr(mask), _lib.ptr(keys), stream)
-        if ev is not None:
-            ev[1].record()
-        _lib.call("protoseg_push_merge", _lib.ptr(keys), n_img, 0, _lib.ptr(x), C, h * w, P, _lib.ptr(state.dist),
-                  _lib.ptr(state.img), _lib.ptr(state.patch), _lib.ptr(state.fmap), stream)
+    def run():
+        dpush.push_update(state, x, labels, protos, pc, 0)
 
     for _ in range(warmup):
         run()
     torch.cuda.synchronize()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps)]
     t0 = time.perf_counter()
-    for s in range(steps):
-        run(evs[s])
+    for _ in range(steps):
+        run()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    argmin_s = float(np.mean([e[0].elapsed_time(e[1]) for e in evs])) * 1e-3
+    argmin_s, launches = kernel_launch_times("push_argmin_kernel", run, steps)
+    argmin_call = argmin_s * launches
     flops = 2.0 * n_img * h * w * P * C
-    nbytes = n_img * (C * h * w * 4 + H * W * 1)
+    nbytes = n_img * (C * h * w * 4 + h * w * 4)  # x read once + the u32 patch mask
     return {"ms_per_img": round(elapsed / (steps * n_img) * 1e3, 4), "images_per_call": n_img,
-            "workload": f"push mask+argmin+merge, labels {H}x{W} u8, map {C}x{h}x{w} f32, P={P}, K={K}",
-            "argmin_kernel_ms_per_img": round(argmin_s / n_img * 1e3, 4),
-            "roofline": roofline_entry(flops, nbytes, argmin_s, "f32") | {"kernel": "push_argmin_kernel"}}
+            "workload": f"push_prototypes inner step (push_update: mask+top-2 argmin+merge), labels {H}x{W} u8, "
+                        f"map {C}x{h}x{w} f32, P={P}, K={K}",
+            "argmin_kernel_ms_per_img": round(argmin_call / n_img * 1e3, 4), "argmin_launches_per_call": launches,
+            "roofline": roofline_entry(flops / launches, nbytes / launches, argmin_s, "f32") |
+            {"kernel": "push_argmin_kernel"}}
 
 
 def cpu_push_baseline(budget_s, C=64, H=1024, W=2048, h=129, w=257, P=190, K=19):
@@ -698,7 +742,8 @@ def main():
             "vs_baseline": None,
             "dtype": f"{args.x_dtype} in; {args.precision} products, f32 accumulate",
             "data": "synthetic (seeded; SURVEY.md §8d shapes), inputs resident in HBM",
-            "config": {"workload": f"prototype layer fwd+bwd (+RCCL grad all-reduce when N>1), 513x513 crop -> "
+            "config": {"workload": f"prototype layer training step: fwd + bwd (+ bucketed RCCL grad all-reduce when N>1) + "
+                                   f"Adam update, 513x513 crop -> "
                                    f"{args.fmap}x{args.fmap} map, {args.protos // max(1, args.classes)} prototypes/class "
                                    f"(P={args.protos}, the metric's config), cityscapes_*_imnet.gin otherwise",
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
@@ -712,7 +757,7 @@ def main():
             out[f"protos_{side.P}"] = {
                 "prototypes": side.P, "img_per_s": round(args.batch * args.steps / e_side, 1),
                 "ms_per_step": round(e_side / args.steps * 1e3, 4),
-                "workload": "cityscapes_no_kld_imnet.gin prototype layer fwd+bwd (10 prototypes/class)",
+                "workload": "cityscapes_no_kld_imnet.gin prototype layer training step (10 prototypes/class)",
                 "roofline": roof_s, "kernels": kernels_s}
         if kld is not None:
             out["kld_step"] = kld

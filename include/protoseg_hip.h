@@ -145,19 +145,27 @@ int protoseg_patch_class_mask(const void* label, int label_dtype, int n_img, int
  * Push, step 2: for every image and prototype, the masked argmin of the distance over the
  * patches of the prototype's class. Replaces segmentation/push.py:193 + 209-263 (distances
  * for the whole image, D2H copy, per-prototype gather of class patches and np.argmin).
- * Distances are computed in-kernel with the same arithmetic as protoseg_l2_fwd.
+ * Distances are computed in-kernel (f32 MFMA, an exact f32 fma chain) with the reference's
+ * rounding order for relu(||x||^2 + (||p||^2 - 2 x.p)), model.py:217-219.
  *
- *   x           [n_img, C, h, w] f32
+ *   x           [n_img, C, h, w] f32, C in {32, 64, 128}
  *   proto_class [P] int32: argmax(prototype_class_identity[p]) (push.py:251); <0 = never pushed
  *   mask        [n_img, h*w] uint32 from protoseg_patch_class_mask
  *   img_keys    [n_img, P] uint64 out: (float_bits(d_min) << 32) | patch_index, or
  *               UINT64_MAX when the image holds no patch of the prototype's class.
+ *   img_second  [n_img, P] uint64 out or NULL: the runner-up of the same image, as
+ *               (float_bits(d_second) << 32) | 0xFFFFFFFF: the second-smallest distance over the
+ *               class patches (another patch; equal to d_min on an exact tie), UINT64_MAX if
+ *               the image holds fewer than two class patches.
  * Ties inside one image resolve to the lowest patch index (the reference's order is the
- * iteration order of a Python set, push.py:214-230).
+ * iteration order of a Python set, push.py:214-230); img_second lets the caller flag the
+ * prototypes whose winner is within rounding of another patch.
+ * Scratch for the per-stripe partials is allocated once per (device, stream) and reused.
  */
 int protoseg_push_argmin(const float* x, int n_img, int C, int h, int w,
                          const float* protos, int P, const int32_t* proto_class,
-                         const uint32_t* mask, uint64_t* img_keys, protoseg_stream_t stream);
+                         const uint32_t* mask, uint64_t* img_keys, uint64_t* img_second,
+                         protoseg_stream_t stream);
 
 /*
  * Push, step 3: fold a batch of per-image keys into the running global minimum in image
@@ -165,15 +173,18 @@ int protoseg_push_argmin(const float* x, int n_img, int C, int h, int w,
  * winning feature vector (push.py:276-280).
  *
  *   img_keys      [n_img, P] from protoseg_push_argmin on the same x
+ *   img_second    [n_img, P] its runner-up keys, or NULL (then global_second must be NULL)
  *   first_img     dataset index of image 0 of this batch
  *   global_dist   [P] f32 in/out (init +inf)
+ *   global_second [P] f32 in/out or NULL (init +inf): the second-smallest distance over every
+ *                 class patch seen so far (any image), for near-tie flags
  *   global_img    [P] int64 in/out (init -1)
  *   global_patch  [P] int32 in/out (init -1)
  *   global_fmap   [P, C] f32 in/out
  */
-int protoseg_push_merge(const uint64_t* img_keys, int n_img, int64_t first_img,
+int protoseg_push_merge(const uint64_t* img_keys, const uint64_t* img_second, int n_img, int64_t first_img,
                         const float* x, int C, int hw, int P,
-                        float* global_dist, int64_t* global_img, int32_t* global_patch,
+                        float* global_dist, float* global_second, int64_t* global_img, int32_t* global_patch,
                         float* global_fmap, protoseg_stream_t stream);
 
 /*

@@ -62,7 +62,7 @@ def test_argument_validation_returns_status_without_gpu():
     assert st == _lib.ERR_UNSUPPORTED and b"precision" in lib.protoseg_last_error()
     st = lib.protoseg_patch_class_mask(null, 2, 1, 4, 4, 2, 2, null, 0, null, null)
     assert st == _lib.ERR_INVALID
-    st = lib.protoseg_push_argmin(dummy, 1, 48, 2, 2, dummy, 3, dummy, dummy, dummy, null)
+    st = lib.protoseg_push_argmin(dummy, 1, 48, 2, 2, dummy, 3, dummy, dummy, dummy, null, null)
     assert st == _lib.ERR_UNSUPPORTED
     with pytest.raises(_lib.ProtosegError, match="status 1"):
-        _lib.call("protoseg_push_merge", null, 1, 0, null, 64, 4, 3, null, null, null, null, null)
+        _lib.call("protoseg_push_merge", null, null, 1, 0, null, 64, 4, 3, null, null, null, null, null, null)

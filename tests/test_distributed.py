@@ -20,18 +20,21 @@ def _free_port():
 
 
 def _serial_truth(per_image):
-    """Strict '<' in image order over (dist, patch, fmap) per image and prototype."""
+    """Strict '<' in image order over (dist, patch, fmap) per image and prototype; runner-up =
+    the second smallest of every image's (best, runner-up) distances."""
     n_img, P = len(per_image), per_image[0][0].shape[0]
     best = [math.inf] * P
     img = [-1] * P
     patch = [-1] * P
     fmap = [None] * P
     for i in range(n_img):
-        d, q, f = per_image[i]
+        d, q, f, _ = per_image[i]
         for j in range(P):
             if float(d[j]) < best[j]:
                 best[j], img[j], patch[j], fmap[j] = float(d[j]), i, int(q[j]), f[j]
-    return best, img, patch, fmap
+    second = [sorted([float(im[0][j]) for im in per_image] + [float(im[3][j]) for im in per_image])[1]
+              for j in range(P)]
+    return best, img, patch, fmap, second
 
 
 def _make_images(n_img, P, C):
@@ -42,7 +45,8 @@ def _make_images(n_img, P, C):
         d[torch.rand(P, generator=gen) < 0.2] = math.inf            # class absent in this image
         q = torch.randint(0, 500, (P,), generator=gen, dtype=torch.int32)
         f = torch.rand(P, C, generator=gen)
-        out.append((d, q, f))
+        d2 = d + torch.randint(0, 3, (P,), generator=gen).float() / 8  # the image's runner-up
+        out.append((d, q, f, d2))
     return out
 
 
@@ -54,8 +58,9 @@ def _worker(rank, world, port, n_img, P, C, result_q):
         lo, hi = shard_bounds(n_img, rank, world)
         st = PushState.create(P, C, "cpu")
         for i in range(lo, hi):  # host emulation of the device merge for this rank's shard
-            d, q, f = images[i]
+            d, q, f, d2 = images[i]
             better = d < st.dist
+            st.second = torch.where(better, torch.minimum(st.dist, d2), torch.minimum(st.second, d))
             st.dist = torch.where(better, d, st.dist)
             st.img = torch.where(better, torch.full_like(st.img, i), st.img)
             st.patch = torch.where(better, q, st.patch)
@@ -76,7 +81,8 @@ def _worker(rank, world, port, n_img, P, C, result_q):
             if lo <= int(st.img[j]) < hi:
                 boxes[j] = torch.tensor([int(st.img[j]), j, j + 3, 2 * j, 2 * j + 5, j % 4])
         merged = reduce_bound_boxes(boxes.numpy())
-        result_q.put((rank, st.dist, st.img, st.patch, st.fmap, len(st.geometry), grads, len(gb.buckets), merged))
+        result_q.put((rank, st.dist, st.img, st.patch, st.fmap, len(st.geometry), grads, len(gb.buckets), merged,
+                      st.second))
     finally:
         dist.destroy_process_group()
 
@@ -94,8 +100,9 @@ def test_sharded_push_reduction_equals_serial_scan(n_img):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    best, img, patch, fmap = _serial_truth(_make_images(n_img, P, C))
-    for rank, d, im, pa, fm, ngeo, grads, nbuckets, boxes in results:
+    best, img, patch, fmap, second = _serial_truth(_make_images(n_img, P, C))
+    for rank, d, im, pa, fm, ngeo, grads, nbuckets, boxes, sec in results:
+        assert sec.tolist() == second  # the sharded runner-up equals the serial one
         assert ngeo == n_img
         for j in range(P):  # every rank holds the union of the per-shard bound boxes
             exp = [-1] * 6 if img[j] < 0 else [img[j], j, j + 3, 2 * j, 2 * j + 5, j % 4]

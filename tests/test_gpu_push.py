@@ -168,3 +168,86 @@ def test_push_full_resolution_properties(device):
         tol = 2e-6 * norm[member, j].max() + 1e-5 * (1 + best)
         assert exact[q, j] <= best + 2 * tol
         assert abs(float(d[j]) - exact[q, j]) <= tol
+
+
+@pytest.mark.parametrize("C,P,n_img,h,w", [(64, 190, 3, 33, 47), (128, 300, 2, 20, 31), (32, 520, 1, 65, 65),
+                                           (64, 19, 4, 7, 9)])
+def test_push_top2_keys_vs_brute_force(device, C, P, n_img, h, w):
+    """Per image: the best key and the runner-up distance (another class patch) against a float64
+    brute force of the masked distances; prototype chunks of 8 tiles (P > 256), C = 32 / 128,
+    maps smaller than one 128-pixel block."""
+    push = _push()
+    K = 19
+    gen = torch.Generator().manual_seed(C + P)
+    x = torch.sigmoid(2 * torch.randn(n_img, C, h, w, generator=gen))
+    protos = torch.rand(P, C, generator=gen)
+    pc = torch.argmax(po.class_identity(P, K), dim=1).to(torch.int32)
+    pc[::7] = -1  # never pushed
+    rng = np.random.default_rng(P)
+    labels = rng.integers(0, K + 1, size=(n_img, 4 * h, 4 * w)).astype(np.int64)
+    mask = push.patch_class_mask(torch.from_numpy(labels).to(device), h, w)
+    keys, second = push.push_argmin(x.to(device), protos.to(device), pc.to(device), mask, with_second=True)
+    m = mask.cpu().numpy().view(np.uint32)
+    for i in range(n_img):
+        d1, q1, f1 = push.decode_keys(keys[i].cpu())
+        d2, q2, f2 = push.decode_keys(second[i].cpu())
+        xd = x[i].double().reshape(C, -1).t()
+        exact = (torch.cdist(xd, protos.double()) ** 2).numpy()
+        norm = (xd ** 2).sum(1).numpy()[:, None] + (protos.double() ** 2).sum(1).numpy()[None, :]
+        for j in range(P):
+            member = ((m[i] >> max(int(pc[j]), 0)) & 1).astype(bool) if pc[j] >= 0 else np.zeros(h * w, bool)
+            n_member = int(member.sum())
+            assert bool(f1[j]) == (n_member >= 1) and bool(f2[j]) == (n_member >= 2), (i, j)
+            if n_member == 0:
+                continue
+            tol = 2e-6 * norm[member, j].max() + 1e-5
+            srt = np.sort(exact[member, j])
+            assert member[int(q1[j])] and abs(float(d1[j]) - exact[int(q1[j]), j]) <= tol
+            assert exact[int(q1[j]), j] <= srt[0] + 2 * tol
+            if n_member >= 2:  # runner-up distance (its patch bits are all ones)
+                assert int(q2[j]) == 0xFFFFFFFF
+                assert abs(float(d2[j]) - srt[1]) <= 2 * tol
+                assert float(d2[j]) >= float(d1[j])
+
+
+def test_near_tie_flag_fires_on_constructed_ties(device):
+    """Exact ties built into the data: (a) a winning patch's feature vector copied to another
+    patch of the same class in the same image, (b) a second image identical to the first
+    (cross-image tie: strict '<' keeps image 0). near_ties flags exactly the tied prototypes."""
+    push = _push()
+    C, h, w, P, K = 64, 12, 14, 38, 19
+    gen = torch.Generator().manual_seed(5)
+    x = torch.sigmoid(2 * torch.randn(1, C, h, w, generator=gen))
+    protos = torch.rand(P, C, generator=gen)
+    pc = torch.argmax(po.class_identity(P, K), dim=1).to(torch.int32)
+    labels = torch.from_numpy(np.repeat(np.repeat(np.random.default_rng(9).integers(1, K + 1, size=(h, w)), 4, 0),
+                                        4, 1).astype(np.int64))
+    lab = labels.to(device)
+    st = push.PushState.create(P, C, device)
+    push.push_update(st, x.to(device), lab, protos.to(device), pc.to(device), 0)
+    base_flags = push.near_ties(st, protos)
+    # (a) duplicate prototype 3's winning patch at another patch of its class
+    j = 3
+    q = int(st.patch[j])
+    small = labels.reshape(h, 4, w, 4)[:, 0, :, 0].reshape(-1)
+    same = [int(t) for t in np.nonzero(small.numpy() == small[q].item())[0] if t != q]
+    assert same, "test setup: the class of the winning patch has another patch"
+    x2 = x.clone()
+    x2.view(1, C, -1)[0, :, same[0]] = x.view(1, C, -1)[0, :, q]
+    st2 = push.PushState.create(P, C, device)
+    push.push_update(st2, x2.to(device), lab, protos.to(device), pc.to(device), 0)
+    flags = push.near_ties(st2, protos)
+    assert j in flags
+    assert int(st2.patch[j]) == min(q, same[0])  # exact tie inside an image -> lower patch index
+    assert float(st2.second[j]) == float(st2.dist[j])
+    # (b) the same image twice: every found prototype ties across images, image 0 wins
+    st3 = push.PushState.create(P, C, device)
+    push.push_update(st3, torch.cat([x, x]).to(device), torch.stack([lab, lab]), protos.to(device), pc.to(device), 0)
+    found = np.nonzero(st3.img.cpu().numpy() >= 0)[0]
+    assert len(found) > 0 and set(found) <= set(push.near_ties(st3, protos))
+    assert (st3.img.cpu().numpy()[found] == 0).all()
+    # flags of the untouched scan are only genuine near-ties: the gap is within the band
+    band = 1e-5 * ((st.fmap.cpu() ** 2).sum(1) + (protos ** 2).sum(1))
+    gap = (st.second - st.dist).cpu()
+    for k in range(P):
+        assert (k in base_flags) == bool(st.img[k] >= 0 and gap[k] <= band[k])
