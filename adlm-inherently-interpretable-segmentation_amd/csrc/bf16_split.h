@@ -198,6 +198,13 @@ __device__ __forceinline__ float act_grad_and_base(float d, float eps, float& ac
 // never binds). fmaxf(x, 0), or med3 with +inf (folded back to fmaxnum), also emits a NaN-quieting
 // v_max_f32 x, x: IEEE mode cannot prove that an MFMA result is not a signalling NaN.
 __device__ __forceinline__ float relu_f(float x) { return __builtin_amdgcn_fmed3f(x, 0.f, 3.402823466e38f); }
+// The deeplab_simple add-on (model.py:124-128: nn.Sigmoid) applied on the layer's x load when
+// the caller passes the pre-activation (PROTOSEG_X_SIGMOID): 1 / (1 + 2^(-x log2 e)) as one
+// v_exp_f32 + v_rcp_f32. Forward and backward form it with this one sequence, so the backward's
+// recomputed distances (and relu mask) are the forward's bit for bit. Within 2 ulp of torch.
+__device__ __forceinline__ float sigmoid_f(float v) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(v * -1.44269504088896341f));
+}
 __host__ __device__ inline float act_unit(int act_kind) { return act_kind == 0 ? kLn2 : 1.f; }
 __host__ __device__ inline float act_grad_unit(int act_kind, float eps) { return act_kind == 0 ? eps - 1.f : -1.f; }
 

@@ -242,7 +242,7 @@ __global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
     const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const unsigned char* __restrict__ img, int P, int Pp,
     int K, float eps, float* __restrict__ dist, unsigned d_bytes,
     float* __restrict__ act_out, unsigned a_bytes, float* __restrict__ logits, unsigned l_bytes, int ld, int p0,
-    int accumulate) {
+    int accumulate, int xsig) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   STAMP(0);
   STAMP_RT(7);
@@ -278,7 +278,15 @@ __global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
   // tile's logits accumulator over those prototype tiles.
   auto run_tile = [&](int t, const float (&raw)[kNQ * 8], int pt0, int dpt) {
     bf16x8 xb[kNQ][T];
-    const float x2 = x_frags<T>(raw, xb);
+    float xv[kNQ * 8];
+    if (xsig) {  // wave-uniform: sigmoid of the pre-activation (model.py:124-128) on the load
+#pragma unroll
+      for (int i = 0; i < kNQ * 8; ++i) xv[i] = sigmoid_f(raw[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < kNQ * 8; ++i) xv[i] = raw[i];
+    }
+    const float x2 = x_frags<T>(xv, xb);
     const int g = t * 32 + j;
     const bool valid = g < npix;
     const int b = valid ? g / HW : 0;
@@ -925,7 +933,7 @@ int fwd_t(const Geometry& g, const Bytes& nb, const void* x, const unsigned char
   KernelTimer timer("l2_fwd_bf16_kernel", stream);
   hipLaunchKernelGGL((l2_fwd_bf16_kernel<TX, T, ACT, ACTS, LOGITS>), dim3(want < cap ? want : cap), dim3(kWavesF * 64), lds,
                      stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, img, g.P, g.Pp, g.K, eps, dist, nb.d, act,
-                     nb.a, logits, nb.l, g.ldd, g.p0, accumulate);
+                     nb.a, logits, nb.l, g.ldd, g.p0, accumulate, g.xsig);
   return check_launch("l2_fwd_bf16_kernel");
 }
 

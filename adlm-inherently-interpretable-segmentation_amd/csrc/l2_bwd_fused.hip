@@ -128,7 +128,7 @@ template <typename TX, int ACT, bool GD>
 __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
     const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const unsigned char* __restrict__ img, int P, int Pp,
     int K, float eps, const float* __restrict__ g_logits, unsigned gl_bytes, const float* __restrict__ g_dist,
-    unsigned gd_bytes, int gd_ld, int gd_p0, TX* __restrict__ g_x, int accumulate, float* __restrict__ slab) {
+    unsigned gd_bytes, int gd_ld, int gd_p0, TX* __restrict__ g_x, int accumulate, float* __restrict__ slab, int xsig) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const FusedLds L = fused_lds(Pp);
   const ImgOffsets io = img_offsets(Pp, kT);
@@ -188,6 +188,11 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
       const int n = 4 * wave + (lane >> 3), ch = lane & 7;
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = lds_val(R + raw_x(chan_of(ch >> 1, ch & 1, e), n));
+      if (xsig) {  // wave-uniform; pixels past the map stay 0 (their g_s is 0 anyway)
+        const bool ok = t < ntiles && t * 32 + n < npix;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = ok ? sigmoid_f(v[e]) : 0.f;
+      }
       split8<kT>(v, f);
       store_frag<kT>(xa_slot(sb), 32 * kC, img_off<8>(n, ch), f);
       float s = chunk_sq(v);
@@ -408,7 +413,13 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const unsigned co = static_cast<unsigned>((16 * (r >> 3) + 4 * ((r >> 2) & 1) + (r & 3)) * HW) * sz;
-      const float v = acc[r] + sn * (2.f * xr[r]);  // conv(x^2, ones) backward: sum_p g_s * 2x
+      float v;
+      if (xsig) {  // through the sigmoid: g_pre = g_x s (1 - s)
+        const float s = sigmoid_f(xr[r]);
+        v = (acc[r] + sn * (2.f * s)) * (s * (1.f - s));
+      } else {
+        v = acc[r] + sn * (2.f * xr[r]);  // conv(x^2, ones) backward: sum_p g_s * 2x
+      }
       BufIO<TX>::store(rgx, accumulate ? old[r] + v : v, pix, co);  // chunk c > 0 adds
     }
   };
@@ -541,7 +552,8 @@ int fused_t(const Geometry& g, const void* x, const unsigned char* img, float ep
   KernelTimer timer("l2_bwd_fused_bf16_kernel", stream);
   hipLaunchKernelGGL((l2_bwd_fused_bf16_kernel<TX, ACT, GD>), dim3(grid), dim3(kThreads),
                      static_cast<size_t>(fused_lds(g.Pp).total), stream, static_cast<const TX*>(x), xb, g.HW, g.npix, img,
-                     g.P, g.Pp, g.K, eps, g_logits, glb, g_dist, gdb, g.ldd, g.p0, static_cast<TX*>(g_x), accumulate, ws);
+                     g.P, g.Pp, g.K, eps, g_logits, glb, g_dist, gdb, g.ldd, g.p0, static_cast<TX*>(g_x), accumulate, ws,
+                     g.xsig);
   return check_launch("l2_bwd_fused_bf16_kernel");
 }
 

@@ -12,6 +12,7 @@ struct Geometry {
   int npix, ntiles;  // B*H*W pixels, 32-pixel tiles
   int ldw = 0;       // row stride of w_last / g_w (= P, or the full P for a prototype chunk)
   int ldd = 0, p0 = 0;  // g_dist: prototypes per image (= P, or the full P) and the chunk's first
+  int xsig = 0;         // x is the add-on's pre-activation: sigmoid on load (bf16 fwd + fused bwd)
 };
 
 // bf16 split family (C = 64). `terms` = 2 (3 products) or 3 (6 products).

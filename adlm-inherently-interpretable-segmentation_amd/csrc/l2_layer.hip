@@ -647,11 +647,44 @@ extern "C" int protoseg_l2_supported(int C, int P, int K) {
   return C == 64 && P <= kMaxChunkedP ? 1 : 0;  // bf16 precisions only, over prototype chunks
 }
 
+extern "C" int protoseg_l2_max_protos(int C, int precision) {
+  if (nc_of(C) == 0 || precision < PROTOSEG_PREC_BF16X3 || precision > PROTOSEG_PREC_F32) return 0;
+  if (C == 64 && terms_of(precision)) return kMaxChunkedP;
+  int p = 0;
+  while (f32_family_fits(C, p + 32)) p += 32;
+  return p;
+}
+
+// PROTOSEG_X_SIGMOID in act_kind: x is the add-on's pre-activation and the kernels apply the
+// sigmoid on load (model.py:124-128). Served by the bf16 forward and the fused backward only.
+bool x_sigmoid_path(int B, int C, int H, int W, int P, int K, int precision) {
+  if (precision != PROTOSEG_PREC_BF16X3 || C != 64 || P <= 0 || P > kMaxChunkedP || K < 0 || K > 32) return false;
+  if (B <= 0 || H <= 0 || W <= 0 || static_cast<long long>(B) * H * W >= (1LL << 31)) return false;
+  return bf16_sizes_ok(geometry_of(B, C, H, W, P, K));
+}
+
+int split_x_sigmoid(int& act_kind, int B, int C, int H, int W, int P, int K, int precision) {
+  const int xsig = (act_kind & PROTOSEG_X_SIGMOID) ? 1 : 0;
+  act_kind &= ~PROTOSEG_X_SIGMOID;
+  if (xsig && !x_sigmoid_path(B, C, H, W, P, K, precision))
+    return -fail(PROTOSEG_ERR_UNSUPPORTED,
+                 "PROTOSEG_X_SIGMOID needs precision BF16X3, C = 64 and the bf16 size bounds "
+                 "(protoseg_l2_x_sigmoid_supported)");
+  return xsig;
+}
+
+extern "C" int protoseg_l2_x_sigmoid_supported(int B, int C, int H, int W, int P, int K, int precision) {
+  return x_sigmoid_path(B, C, H, W, P, K, precision) ? 1 : 0;
+}
+
 extern "C" int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P,
                                const float* w_last, int K, float eps, int act_kind, int precision, float* dist_out,
                                float* act_out, float* logits_out, protoseg_stream_t stream) {
+  const int xsig = split_x_sigmoid(act_kind, B, C, H, W, P, K, precision);
+  if (xsig < 0) return -xsig;
   Geometry geo;
   if (int st = validate(x, x_dtype, B, C, H, W, protos, P, K, act_kind, precision, &geo)) return st;
+  geo.xsig = xsig;
   if (logits_out && (!w_last || K <= 0)) return fail(PROTOSEG_ERR_INVALID, "logits_out needs w_last and K > 0");
   if (!dist_out && !act_out && !logits_out) return PROTOSEG_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -680,6 +713,7 @@ extern "C" int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, 
         gc = geometry_of(B, C, H, W, pc, K);
         gc.ldw = gc.ldd = P;
         gc.p0 = p0;
+        gc.xsig = xsig;
         ImageBlock img;
         if (int st = img.build(gc, terms, protos + static_cast<size_t>(p0) * C, logits_out ? w_last + p0 : nullptr,
                                act_kind, eps, s))
@@ -714,11 +748,13 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
                                const float* w_last, int K, float eps, int act_kind, int precision,
                                const float* g_logits, const float* g_dist, void* g_x, float* g_protos, float* g_w,
                                void* workspace, size_t workspace_bytes, protoseg_stream_t stream) {
+  const int xsig = split_x_sigmoid(act_kind, B, C, H, W, P, K, precision);
+  if (xsig < 0) return -xsig;
   Geometry geo;
   if (int st = validate(x, x_dtype, B, C, H, W, protos, P, K, act_kind, precision, &geo)) return st;
   if (g_logits && (!w_last || K <= 0)) return fail(PROTOSEG_ERR_INVALID, "g_logits needs w_last and K > 0");
   if (g_w && !g_logits) return fail(PROTOSEG_ERR_INVALID, "g_w needs g_logits");
-  if (g_protos || g_w) {
+  if (g_protos || g_w || xsig) {  // the fused kernel (every X_SIGMOID backward) writes its slab
     const size_t need = protoseg_l2_bwd_workspace_size(B, C, H, W, P, K);
     if (!workspace || workspace_bytes < need)
       return fail(PROTOSEG_ERR_INVALID, "workspace %zu B < %zu B", workspace_bytes, need);
@@ -737,7 +773,7 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
   float* ws = static_cast<float*>(workspace);
   // Training backward (g_x and g_P / g_W) at bf16x3: one fused kernel per chunk of <= 192
   // prototypes (l2_bwd_fused.hip); chunk c > 0 adds its x-gradient to g_x.
-  if (terms == 2 && C == 64 && g_x && (g_protos || g_w) && bf16_sizes_ok(geo)) {
+  if (terms == 2 && C == 64 && bf16_sizes_ok(geo) && (xsig || (g_x && (g_protos || g_w)))) {
     const int nchunk = static_cast<int>(ceil_div(P, 192));
     const int per = static_cast<int>(ceil_div(P, nchunk));
     Geometry gc = geometry_of(B, C, H, W, per, K);
@@ -748,6 +784,7 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
         gc = geometry_of(B, C, H, W, pc, K);
         gc.ldw = gc.ldd = P;
         gc.p0 = p0;
+        gc.xsig = xsig;
         ImageBlock img;
         if (int st = img.build(gc, terms, protos + static_cast<size_t>(p0) * C, g_logits ? w_last + p0 : nullptr,
                                act_kind, eps, s))
@@ -761,6 +798,7 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
       return PROTOSEG_OK;
     }
   }
+  if (xsig) return fail(PROTOSEG_ERR_UNSUPPORTED, "PROTOSEG_X_SIGMOID: no fused backward for this shape");
   // P too large for the bf16 backward's LDS images (e.g. P = 361, 19 prototypes/class): run it
   // over prototype chunks of <= 192. g_P rows and g_W columns are per prototype; g_x is a sum
   // over prototypes, so chunk c > 0 adds to it; g_dist rows are read at (b * P + p0 + p).

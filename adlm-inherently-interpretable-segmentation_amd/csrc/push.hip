@@ -94,10 +94,11 @@ __host__ __device__ inline size_t push_lds_bytes(int C, int waves) {
   return static_cast<size_t>(2) * push_buf_floats(C) * 4 + static_cast<size_t>(waves) * 128 * 4;
 }
 
-// (b1, s1) and (b2, s2), each b <= s: the two smallest of the four.
+// (b1, s1) and (b2, s2), each b <= s: the two smallest of the four. A best key that becomes the
+// runner-up drops its patch (bits all ones), like every runner-up key: only its distance counts.
 __device__ __forceinline__ void top2_merge(unsigned long long& b, unsigned long long& s, unsigned long long b2,
                                            unsigned long long s2) {
-  const unsigned long long lo = b < b2 ? b : b2, hi = b < b2 ? b2 : b;
+  const unsigned long long lo = b < b2 ? b : b2, hi = (b < b2 ? b2 : b) | 0xffffffffull;
   const unsigned long long sm = s < s2 ? s : s2;
   b = lo;
   s = hi < sm ? hi : sm;

@@ -26,6 +26,7 @@ OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_HIP = 0, 1, 2, 3
 F32, BF16, I64, I32, U8 = 0, 1, 2, 3, 4
 # enum protoseg_act
 ACT_LOG, ACT_LINEAR, ACT_IDENTITY = 0, 1, 2
+X_SIGMOID = 0x100  # OR-ed into the layer's act_kind: sigmoid of the pre-activation on load
 # enum protoseg_precision
 PREC_BF16X3, PREC_BF16X6, PREC_F32 = 0, 1, 2
 PRECISIONS = {"bf16x3": PREC_BF16X3, "bf16x6": PREC_BF16X6, "f32": PREC_F32}
@@ -41,6 +42,8 @@ SIGNATURES = {
     "protoseg_timing_events_n": (_i, [ctypes.c_char_p, _vp, _vp, _i]),
     "protoseg_timing_launches": (_i, []),
     "protoseg_l2_supported": (_i, [_i, _i, _i]),
+    "protoseg_l2_max_protos": (_i, [_i, _i]),
+    "protoseg_l2_x_sigmoid_supported": (_i, [_i, _i, _i, _i, _i, _i, _i]),
     "protoseg_l2_fwd": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _i, _vp, _vp, _vp, _vp]),
     "protoseg_l2_bwd_workspace_size": (_sz, [_i, _i, _i, _i, _i, _i]),
     "protoseg_l2_bwd": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp,

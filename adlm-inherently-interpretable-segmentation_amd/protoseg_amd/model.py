@@ -145,7 +145,24 @@ class PPNet(nn.Module):
             return -distances
         return self.prototype_activation_function(distances)
 
+    def _sigmoid_free_add_on(self):
+        """The add-on layers minus their final nn.Sigmoid (model.py:124-128 and the bottleneck /
+        regular add-ons all end in one) when forward() can hand the pre-activation to the layer
+        kernels, which apply the sigmoid on load (sigmoid(X) never materialised); else None."""
+        if not getattr(self, "fuse_add_on_sigmoid", True) or not getattr(self, "patch_classification", False):
+            return None
+        layers = list(self.add_on_layers)
+        if not layers or not isinstance(layers[-1], nn.Sigmoid) or self._kernel_activation() is None:
+            return None
+        return nn.Sequential(*layers[:-1])
+
     def forward(self, x, **kwargs):
+        head = self._sigmoid_free_add_on()
+        if head is not None:  # conv_features() without its sigmoid, fused into the layer's load
+            feats = self.features(x)
+            if isinstance(feats, list):
+                return [self.forward_from_conv_features(head(f), x_sigmoid=True, **kwargs) for f in feats]
+            return self.forward_from_conv_features(head(feats), x_sigmoid=True, **kwargs)
         conv_features = self.conv_features(x)
         if isinstance(conv_features, list):
             return [self.forward_from_conv_features(c, **kwargs) for c in conv_features]
@@ -159,12 +176,16 @@ class PPNet(nn.Module):
         logits, distances = self.forward_from_conv_features(conv_features, **kwargs)
         return logits, distances, conv_features
 
-    def forward_from_conv_features(self, conv_features, return_activations=False, return_distances=False):
+    def forward_from_conv_features(self, conv_features, return_activations=False, return_distances=False,
+                                   x_sigmoid=False):
         """model.py:259-299. Patch classification: one fused kernel gives distances (NCHW) and
-        logits (NHWC) — the permute / activation / Linear / reshape of model.py:271-278 included."""
+        logits (NHWC) — the permute / activation / Linear / reshape of model.py:271-278 included.
+        x_sigmoid=True: ``conv_features`` is the add-on's pre-activation (see forward())."""
         if isinstance(conv_features, list):
-            return [self.forward_from_conv_features(c) for c in conv_features]
+            return [self.forward_from_conv_features(c, x_sigmoid=x_sigmoid) for c in conv_features]
         act_name = self._kernel_activation()
+        if x_sigmoid and not (getattr(self, "patch_classification", False) and act_name is not None):
+            conv_features, x_sigmoid = torch.sigmoid(conv_features), False
         if getattr(self, "patch_classification", False):
             if act_name is None:  # a user-supplied activation: distances on the kernel, the rest in torch
                 distances = self._l2_convolution(conv_features)
@@ -175,7 +196,7 @@ class PPNet(nn.Module):
             distances, logits, acts = ops.prototype_layer(
                 conv_features, self.prototype_vectors, self.last_layer.weight, self.epsilon, act_name,
                 with_dist=not return_activations, with_logits=True, with_act=return_activations,
-                precision=getattr(self, "precision", None))
+                precision=getattr(self, "precision", None), x_sigmoid=x_sigmoid)
             return (logits, acts) if return_activations else (logits, distances)
 
         # ProtoPNet global min pooling (model.py:284-299); distances from the kernel

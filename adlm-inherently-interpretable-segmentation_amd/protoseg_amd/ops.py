@@ -44,6 +44,17 @@ def supported(C: int, P: int, K: int) -> bool:
     return bool(_lib.load().protoseg_l2_supported(C, P, K))
 
 
+def x_sigmoid_supported(x: Tensor, P: int, K: int, precision: Optional[str] = None) -> bool:
+    """Whether the kernels can apply the add-on's sigmoid on load for this call."""
+    B, C, H, W = x.shape
+    return bool(_lib.load().protoseg_l2_x_sigmoid_supported(B, C, H, W, P, K, precision_code(precision)))
+
+
+def max_protos(C: int, precision: Optional[str] = None) -> int:
+    """Largest P one layer call serves at (C, precision) (protoseg_l2_max_protos)."""
+    return int(_lib.load().protoseg_l2_max_protos(C, precision_code(precision)))
+
+
 @torch.library.custom_op("protoseg::l2_forward", mutates_args=(), device_types="cuda")
 def l2_forward(x: Tensor, protos: Tensor, w_last: Tensor, eps: float, act_kind: int, precision: int,
                with_dist: bool, with_logits: bool, with_act: bool) -> Tuple[Tensor, Tensor, Tensor]:
@@ -79,7 +90,8 @@ def _(x, protos, w_last, eps, act_kind, precision, with_dist, with_logits, with_
 def l2_backward(x: Tensor, protos: Tensor, w_last: Tensor, g_logits: Optional[Tensor], g_dist: Optional[Tensor],
                 eps: float, act_kind: int, precision: int, need_x: bool, need_protos: bool,
                 need_w: bool) -> Tuple[Tensor, Tensor, Tensor]:
-    """Backward of l2_forward with respect to (x, protos, w_last); unrequested grads are empty."""
+    """Backward of l2_forward with respect to (x, protos, w_last); unrequested grads are empty.
+    With X_SIGMOID in act_kind, g_x is the gradient w.r.t. the pre-activation."""
     dev = _lib.require_device(x, protos, w_last, g_logits, g_dist)
     x = x.contiguous()
     protos = protos.contiguous()
@@ -95,7 +107,8 @@ def l2_backward(x: Tensor, protos: Tensor, w_last: Tensor, g_logits: Optional[Te
     if need_w is False and g_logits is None and need_protos is False and need_x is False:
         return g_x, g_p, g_w
     lib = _lib.load()
-    ws_bytes = lib.protoseg_l2_bwd_workspace_size(B, C, H, W, P, K) if (need_protos or need_w) else 0
+    fused_sig = bool(act_kind & _lib.X_SIGMOID)
+    ws_bytes = lib.protoseg_l2_bwd_workspace_size(B, C, H, W, P, K) if (need_protos or need_w or fused_sig) else 0
     ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8) if ws_bytes else None
     with torch.cuda.device(dev):
         _lib.call("protoseg_l2_bwd", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P, _lib.ptr(w_last), K,
@@ -132,7 +145,7 @@ def _act_grad_as_dist_grad(x, protos, w_last, g_act, eps, act_kind, precision):
     B, _, H, W = x.shape
     P = protos.shape[0]
     ga = g_act.reshape(B, H, W, P).permute(0, 3, 1, 2).float()
-    if act_kind == _lib.ACT_LINEAR:
+    if act_kind & ~_lib.X_SIGMOID == _lib.ACT_LINEAR:
         return -ga
     d = l2_forward(x, protos, w_last, eps, act_kind, precision, True, False, False)[0]
     return ga * ((eps - 1.0) / ((d + 1.0) * (d + eps)))
@@ -157,12 +170,19 @@ torch.library.register_autograd("protoseg::l2_forward", _backward, setup_context
 
 def prototype_layer(x: Tensor, prototype_vectors: Tensor, last_layer_weight: Tensor, eps: float = 1e-4,
                     activation: str = "log", with_dist: bool = True, with_logits: bool = True,
-                    with_act: bool = False, precision: Optional[str] = None) -> Tuple[Tensor, Tensor, Tensor]:
+                    with_act: bool = False, precision: Optional[str] = None,
+                    x_sigmoid: bool = False) -> Tuple[Tensor, Tensor, Tensor]:
     """Distances, logits and activations of the PPNet prototype layer (1x1 prototypes).
 
     x: [B, C, H, W] add-on-layer output (float32, bfloat16, or float16 widened to f32); prototype_vectors: [P, C, 1, 1]
     or [P, C]; last_layer_weight: [K, P]. Returns (distances [B,P,H,W], logits [B,H,W,K],
     activations [B*H*W, P]) with unrequested outputs empty.
+
+    x_sigmoid=True: x is the add-on layers' pre-activation and the layer input is sigmoid(x)
+    (model.py:124-128's final nn.Sigmoid). The kernels apply it on load where
+    protoseg_l2_x_sigmoid_supported says so (bf16x3, C = 64), so sigmoid(x) is never written to
+    HBM and autograd returns the pre-activation's gradient; other shapes / precisions take
+    torch.sigmoid first.
     """
     if activation not in ACT_KINDS:
         raise _lib.ProtosegError(f"activation {activation!r} has no HIP kernel ('log' or 'linear')")
@@ -175,7 +195,13 @@ def prototype_layer(x: Tensor, prototype_vectors: Tensor, last_layer_weight: Ten
         # fp16 feature maps (BASELINE config 5, DenseNet-161 fp16): widened exactly to f32 at the
         # boundary; the layer computes as for f32 input and autograd narrows g_x back to fp16.
         x = x.float()
-    return torch.ops.protoseg.l2_forward(x, protos, last_layer_weight, float(eps), ACT_KINDS[activation],
+    act_kind = ACT_KINDS[activation]
+    if x_sigmoid:
+        if x.is_cuda and x_sigmoid_supported(x, protos.shape[0], last_layer_weight.shape[0], precision):
+            act_kind |= _lib.X_SIGMOID
+        else:
+            x = torch.sigmoid(x)
+    return torch.ops.protoseg.l2_forward(x, protos, last_layer_weight, float(eps), act_kind,
                                          precision_code(precision), with_dist, with_logits, with_act)
 
 

@@ -210,11 +210,18 @@ def batch_bound_boxes(items, protos: Tensor, proto_class: np.ndarray, rf_boxes_a
     """Bound boxes (push.py:309-343) of every pushed prototype in one act_upsample + one
     bound_boxes launch per image geometry. ``items`` yields (proto_ids, x [1, C, h, w],
     labels [H, W]) per winning image. Returns {prototype id: (start_h, end_h, start_w, end_w)}."""
-    from .ops import l2_distances
+    from .ops import l2_distances, max_protos
     groups: Dict[tuple, dict] = {}
     for ids, x, labels in items:
         idt = torch.as_tensor(np.asarray(ids, dtype=np.int64), device=x.device)
-        dist = l2_distances(x.float(), protos.detach()[idt], eps, precision="f32")[0]  # [m_i, h, w]
+        # f32 distances (the push's own arithmetic); more winners on one image than one f32
+        # call holds (P > 384 at C = 64, e.g. 30 prototypes/class) go in slices
+        step = max_protos(x.shape[1], "f32")
+        if step <= 0:
+            raise _lib.ProtosegError(f"no f32 layer kernel for C={x.shape[1]}")
+        pv = protos.detach()
+        dist = torch.cat([l2_distances(x.float(), pv[idt[s:s + step]], eps, precision="f32")[0]
+                          for s in range(0, len(idt), step)], 0)  # [m_i, h, w]
         key = (tuple(dist.shape[1:]), tuple(labels.shape[-2:]), labels.dtype)
         g = groups.setdefault(key, {"ids": [], "dist": [], "labels": [], "li": []})
         g["li"].extend([len(g["labels"])] * len(ids))

@@ -47,6 +47,12 @@ enum protoseg_dtype {
  * IDENTITY (protoseg_act_upsample only): the input already holds activations, e.g. from the
  * caller's prototype_activation_function_in_numpy (push.py:317-318). */
 enum protoseg_act { PROTOSEG_ACT_LOG = 0, PROTOSEG_ACT_LINEAR = 1, PROTOSEG_ACT_IDENTITY = 2 };
+/* Flag OR-ed into protoseg_l2_fwd / _bwd's act_kind: x is the add-on layers' pre-activation and
+ * the kernels apply the add-on's final nn.Sigmoid on load (model.py:124-128, 164-175), so
+ * sigmoid(x) is never materialised; the backward returns the gradient w.r.t. the pre-activation
+ * (g_x * s (1 - s)). Served where protoseg_l2_x_sigmoid_supported() says so (BF16X3, C = 64),
+ * PROTOSEG_ERR_UNSUPPORTED elsewhere. A backward with this flag always needs the workspace. */
+enum { PROTOSEG_X_SIGMOID = 0x100 };
 
 /* Arithmetic of the x.p / W.act / gradient products (always f32 accumulation):
  *  BF16X3  operands split in 2 bf16 terms, 3 bf16 MFMAs per product (|rel err| ~ 1e-5 on d)
@@ -124,6 +130,15 @@ int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, int W,
 
 /* 1 if (C, P, K) is inside the compiled kernel family, else 0. */
 int protoseg_l2_supported(int C, int P, int K);
+
+/* Largest P one protoseg_l2_fwd / _bwd call serves at (C, precision): 4096 for the bf16
+ * precisions at C = 64 (prototype chunks), otherwise the f32 family's LDS bound (C = 64: 384);
+ * 0 when C is outside the family or precision is unknown. Callers holding more prototypes
+ * (push's bound-box distances at F32) slice them into calls of at most this many. */
+int protoseg_l2_max_protos(int C, int precision);
+
+/* 1 if protoseg_l2_fwd / _bwd accept PROTOSEG_X_SIGMOID for this shape and precision, else 0. */
+int protoseg_l2_x_sigmoid_supported(int B, int C, int H, int W, int P, int K, int precision);
 
 /*
  * Push, step 1: label map -> per-patch class bitmask. Replaces segmentation/push.py:184-186

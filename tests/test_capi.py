@@ -38,6 +38,21 @@ def test_version_and_supported_shapes():
     assert lib.protoseg_l2_supported(64, 570, 19) == 1    # 30 prototypes/class: bf16 prototype chunks
     assert lib.protoseg_l2_supported(64, 5000, 19) == 0   # beyond the chunked bound
     assert lib.protoseg_l2_supported(128, 1000, 19) == 0  # C = 128 has no chunked family
+    assert lib.protoseg_l2_max_protos(64, _lib.PREC_BF16X3) == 4096
+    assert lib.protoseg_l2_max_protos(64, _lib.PREC_BF16X6) == 4096
+    assert lib.protoseg_l2_max_protos(64, _lib.PREC_F32) == 384   # the f32 family's LDS bound
+    assert 0 < lib.protoseg_l2_max_protos(128, _lib.PREC_BF16X3) < 384
+    assert lib.protoseg_l2_max_protos(48, _lib.PREC_F32) == 0
+    assert lib.protoseg_l2_max_protos(64, 9) == 0
+    for C in (32, 64, 128):
+        m = lib.protoseg_l2_max_protos(C, _lib.PREC_F32)
+        assert lib.protoseg_l2_supported(C, m, 19) == 1
+    # on-load sigmoid of the add-on pre-activation: bf16x3 at C = 64, any P <= 4096
+    assert lib.protoseg_l2_x_sigmoid_supported(32, 64, 65, 65, 361, 19, _lib.PREC_BF16X3) == 1
+    assert lib.protoseg_l2_x_sigmoid_supported(32, 64, 65, 65, 190, 19, _lib.PREC_BF16X6) == 0
+    assert lib.protoseg_l2_x_sigmoid_supported(32, 64, 65, 65, 190, 19, _lib.PREC_F32) == 0
+    assert lib.protoseg_l2_x_sigmoid_supported(2, 128, 9, 9, 38, 19, _lib.PREC_BF16X3) == 0
+    assert lib.protoseg_l2_x_sigmoid_supported(4096, 64, 256, 256, 190, 19, _lib.PREC_BF16X3) == 0  # > 2^31 B
 
 
 def test_workspace_size_is_host_only_and_aligned():
@@ -60,6 +75,9 @@ def test_argument_validation_returns_status_without_gpu():
     assert st == _lib.ERR_UNSUPPORTED
     st = lib.protoseg_l2_fwd(dummy, 0, 1, 64, 2, 2, dummy, 19, dummy, 19, 1e-4, 0, 9, null, null, null, null)
     assert st == _lib.ERR_UNSUPPORTED and b"precision" in lib.protoseg_last_error()
+    st = lib.protoseg_l2_fwd(dummy, 0, 1, 64, 2, 2, dummy, 19, dummy, 19, 1e-4, _lib.X_SIGMOID, _lib.PREC_F32,
+                             null, null, null, null)
+    assert st == _lib.ERR_UNSUPPORTED and b"X_SIGMOID" in lib.protoseg_last_error()
     st = lib.protoseg_patch_class_mask(null, 2, 1, 4, 4, 2, 2, null, 0, null, null)
     assert st == _lib.ERR_INVALID
     st = lib.protoseg_push_argmin(dummy, 1, 48, 2, 2, dummy, 3, dummy, dummy, dummy, null, null)

@@ -141,6 +141,26 @@ def test_bound_boxes_full_resolution_end_to_end(device):
         assert tuple(box[j]) == box_ref, (j, box[j], box_ref)
 
 
+def test_batch_bound_boxes_more_winners_than_one_f32_call(device):
+    """P = 570 (30 prototypes/class): 450 prototypes win on one image, more than one f32 layer
+    call holds (384 at C = 64); the sliced distance calls give the boxes of per-slice calls."""
+    push = _push()
+    rng = np.random.default_rng(570)
+    C, h, w, H, W, P = 64, 9, 17, 72, 136, 570
+    x = torch.from_numpy(rng.random((1, C, h, w)).astype(np.float32)).to(device)
+    protos = torch.from_numpy(rng.random((P, C)).astype(np.float32)).to(device)
+    y = torch.from_numpy(_labels(rng, H, W)[0]).to(device)
+    pc = np.arange(P) // 30
+    ids = np.arange(450) * 570 // 450
+    rfb = np.zeros((P, 6), np.int64)
+    rfb[:, 1:5] = [bo.rf_box(int(j) % h, int(j) % w, H, W, h, w) for j in range(P)]
+    whole = push.batch_bound_boxes([(ids, x, y)], protos, pc, rfb)
+    parts = {}
+    for s in range(0, len(ids), 150):
+        parts.update(push.batch_bound_boxes([(ids[s:s + 150], x, y)], protos, pc, rfb))
+    assert len(whole) == len(ids) and whole == parts
+
+
 def test_push_prototypes_writes_bound_boxes(device, tmp_path):
     """push_prototypes end to end: proto_bound_boxes (push.py:338-343) from each prototype's
     winning image equal the oracle chain on that image's distances."""

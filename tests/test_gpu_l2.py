@@ -407,3 +407,101 @@ def test_fp16_features_widen_exactly(device):
     assert_scaled_close(logits.detach(), ref_logits, 1e-4, "logits")
     assert xd.grad.dtype == torch.float16
     assert_scaled_close(xd.grad.float(), ref_gx, 2e-3, "g_x(fp16)")
+
+
+def _pre_activation(B, C, h, w, seed, dtype=torch.float32):
+    """The deeplab_simple add-on's input (§8d: X = sigmoid(N(0, 2^2)), so pre = N(0, 2^2))."""
+    return (2.0 * torch.randn(B, C, h, w, generator=torch.Generator().manual_seed(seed))).to(dtype)
+
+
+@pytest.mark.parametrize("P,xdtype,with_gdist", [(38, torch.float32, False), (190, torch.float32, True),
+                                                 (190, torch.bfloat16, False), (361, torch.float32, True),
+                                                 (570, torch.float32, False)])
+def test_x_sigmoid_fused_on_load_vs_oracle(device, P, xdtype, with_gdist):
+    """PROTOSEG_X_SIGMOID (model.py:124-128's nn.Sigmoid applied on the layer's x load): forward
+    and backward equal the oracle on sigmoid(pre); g_x is the pre-activation's gradient
+    g_x * s (1 - s). P = 361 / 570 run the prototype chunks (g_x accumulated across chunks)."""
+    ops = _ops()
+    B, C, h, w, K = 2, 64, 23, 29, 19
+    pre = _pre_activation(B, C, h, w, seed=P, dtype=xdtype)
+    _, protos, w_last = po.synthetic_inputs(B, C, h, w, P, K, seed=P + 1)
+    gen = torch.Generator().manual_seed(P + 2)
+    w_last = w_last + 0.05 * torch.randn(w_last.shape, generator=gen)
+    g_logits = torch.randn(B, h, w, K, generator=gen)
+    g_dist = 0.05 * torch.randn(B, P, h, w, generator=gen) if with_gdist else None
+    assert ops.x_sigmoid_supported(pre.to(device), P, K, "bf16x3")
+    prd = pre.to(device).requires_grad_(True)
+    pd = protos.to(device).requires_grad_(True)
+    wd = w_last.to(device).requires_grad_(True)
+    dist, logits, _ = ops.prototype_layer(prd, pd, wd, 1e-4, "log", precision="bf16x3", x_sigmoid=True)
+    outs, grads = [logits], [g_logits.to(device)]
+    if with_gdist:
+        outs.append(dist)
+        grads.append(g_dist.to(device))
+    torch.autograd.backward(outs, grads)
+    s = torch.sigmoid(pre.float())
+    ref_logits, ref_dist, ref_gx, ref_gp, ref_gw = po.forward_backward(s, protos, w_last, g_logits, g_dist)
+    assert_dist_close(dist.detach(), ref_dist, s, protos)
+    assert_scaled_close(logits.detach(), ref_logits, 1e-4, "logits")
+    rtol = 1e-4 if xdtype == torch.float32 else 1e-2  # bf16 g_x output
+    assert prd.grad.dtype == xdtype
+    assert_scaled_close(prd.grad.float(), ref_gx * s * (1 - s), rtol, "g_pre")
+    assert_scaled_close(pd.grad, ref_gp, 1e-4, "g_protos")
+    assert_scaled_close(wd.grad, ref_gw, 1e-4, "g_w")
+
+
+def test_x_sigmoid_other_precisions_take_torch_sigmoid(device):
+    """bf16x6 / f32 have no on-load sigmoid: prototype_layer applies torch.sigmoid first (same
+    result), and the C ABI refuses the flag for them (fails loudly, no silent misuse)."""
+    from protoseg_amd import _lib
+    ops = _ops()
+    pre = _pre_activation(1, 64, 9, 11, seed=3)
+    _, protos, w_last = po.synthetic_inputs(1, 64, 9, 11, 38, 19, seed=4)
+    for precision in ("bf16x6", "f32"):
+        assert not ops.x_sigmoid_supported(pre, 38, 19, precision)
+        d, lg, _ = ops.prototype_layer(pre.to(device), protos.to(device), w_last.to(device), precision=precision,
+                                       x_sigmoid=True)
+        ref_logits, ref_dist = po.forward_from_conv_features(torch.sigmoid(pre), protos[:, :, None, None], w_last)
+        assert_dist_close(d, ref_dist, torch.sigmoid(pre), protos)
+        assert_scaled_close(lg, ref_logits, 1e-4, "logits")
+        with pytest.raises(_lib.ProtosegError, match="X_SIGMOID"):
+            ops.l2_forward(pre.to(device), protos.to(device), w_last.to(device), 1e-4, _lib.X_SIGMOID,
+                           ops.PRECISIONS[precision], True, True, False)
+
+
+def test_ppnet_forward_image_fuses_add_on_sigmoid(device):
+    """PPNet.forward(image) (model.py:239-246): the add-on's sigmoid runs inside the layer kernels
+    (the backbone output goes in as the pre-activation); logits / distances and every gradient
+    (prototypes, last layer, backbone through g_pre) equal the oracle on sigmoid(features(image))."""
+    from protoseg_amd.model import PPNet
+    from protoseg_amd.deeplab import deeplabv2_resnet101_features
+    torch.manual_seed(0)
+    feats = deeplabv2_resnet101_features(n_blocks=(1, 1, 1, 1), scales=[])
+    net = PPNet(feats, 513, (190, 64, 1, 1), None, 19, add_on_layers_type="deeplab_simple",
+                patch_classification=True).to(device)
+    net.eval()
+    assert net._sigmoid_free_add_on() is not None
+    image = torch.randn(2, 3, 65, 65, generator=torch.Generator().manual_seed(8)).to(device)
+    logits, dist = net(image)
+    (logits.square().sum() + 0.1 * dist.sum()).backward()
+    g_head = [p.grad.detach().clone() for p in net.features.parameters() if p.grad is not None]
+    assert g_head, "backbone gets a gradient through the fused sigmoid"
+    with torch.no_grad():
+        pre = net.features(image).float().cpu()
+    s = torch.sigmoid(pre)
+    protos = net.prototype_vectors.detach().cpu()
+    wl = net.last_layer.weight.detach().cpu()
+    ref_logits, ref_dist = po.forward_from_conv_features(s, protos, wl)
+    assert_dist_close(dist.detach(), ref_dist, s, protos.reshape(190, 64))
+    assert_scaled_close(logits.detach(), ref_logits, 1e-4, "logits")
+    _, _, _, ref_gp, ref_gw = po.forward_backward(s, protos, wl, 2 * ref_logits, torch.full_like(ref_dist, 0.1))
+    assert_scaled_close(net.prototype_vectors.grad.reshape(190, 64), ref_gp, 1e-4, "g_protos")
+    assert_scaled_close(net.last_layer.weight.grad, ref_gw, 1e-4, "g_w")
+    # the unfused path (sigmoid materialised by nn.Sigmoid) gives the same backbone gradient
+    net.zero_grad()
+    net.fuse_add_on_sigmoid = False
+    l2, d2 = net(image)
+    (l2.square().sum() + 0.1 * d2.sum()).backward()
+    g_ref = [p.grad for p in net.features.parameters() if p.grad is not None]
+    for a, b in zip(g_head, g_ref):
+        assert_scaled_close(a, b, 1e-3, "backbone grad")
