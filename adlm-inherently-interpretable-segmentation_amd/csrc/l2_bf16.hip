@@ -138,12 +138,20 @@ __device__ float proto_norm2_64(const float* __restrict__ protos, int p, bool va
 }
 
 
-// blockIdx.y selects the image, so the five loops (each a few load round trips) run concurrently.
+// blockIdx.y selects the image, so the five loops (each a few load round trips) run concurrently;
+// blockIdx.z the prototype chunk (rows z*per .. of `P` in all; chunk z's images at z*chunk_bytes),
+// so a chunked call builds every chunk's images in one launch.
 template <int T>
-__global__ __launch_bounds__(256) void l2_prep_bf16_kernel(const float* __restrict__ protos, int P, int Pp,
+__global__ __launch_bounds__(256) void l2_prep_bf16_kernel(const float* __restrict__ protos, int P, int per,
                                                            const float* __restrict__ w_last, int K, int ldw,
-                                                           float w_scale,
-                                                           float wt_scale, unsigned char* __restrict__ block) {
+                                                           float w_scale, float wt_scale,
+                                                           unsigned char* __restrict__ block, unsigned chunk_bytes) {
+  const int p0 = static_cast<int>(blockIdx.z) * per;
+  protos += static_cast<size_t>(p0) * kC;
+  if (w_last) w_last += p0;
+  block += static_cast<size_t>(blockIdx.z) * chunk_bytes;
+  P = P - p0 < per ? P - p0 : per;
+  const int Pp = (P + 31) & ~31;
   const ImgOffsets o = img_offsets(Pp, T);
   const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
   switch (blockIdx.y) {
@@ -835,12 +843,20 @@ __global__ __launch_bounds__(MAXT) void l2_bwd_pw_bf16_kernel(
 
 // Slab sum: 64 elements x 4 slab groups per workgroup, groups combined in fixed order; each
 // thread keeps 8 independent loads in flight.
+// blockIdx.y = prototype chunk: its slabs start at y * chunk_elems, its prototypes at y * per.
 __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __restrict__ slab, int S, int P,
-                                                                  int Pp, int K, int ldw, const float* __restrict__ protos,
+                                                                  int per, int K, int ldw, const float* __restrict__ protos,
                                                                   float w_unit, float* __restrict__ g_protos,
-                                                                  float* __restrict__ g_w) {
+                                                                  float* __restrict__ g_w, size_t chunk_elems) {
   __shared__ float part[4][64];
   __shared__ float gpart[4][64];
+  const int p0 = static_cast<int>(blockIdx.y) * per;
+  slab += blockIdx.y * chunk_elems;
+  protos += static_cast<size_t>(p0) * kC;
+  if (g_protos) g_protos += static_cast<size_t>(p0) * kC;
+  if (g_w) g_w += p0;
+  P = P - p0 < per ? P - p0 : per;
+  const int Pp = (P + 31) & ~31;
   const int E = Pp * kC + 32 * Pp + Pp;
   const int e = blockIdx.x * 64 + (threadIdx.x & 63);
   const int grp = threadIdx.x >> 6;
@@ -1040,27 +1056,42 @@ size_t bf16_image_bytes(const Geometry& g, int terms) {
   return static_cast<size_t>(img_offsets(g.Pp, terms).total);
 }
 
-int launch_prep_bf16(const Geometry& g, int terms, const float* protos, const float* w_last, int act_kind, float eps,
-                     void* img, hipStream_t stream) {
-  const int items = g.Pp * 8;  // the largest image loop (P rows x 8 chunks)
-  const dim3 grid(static_cast<unsigned>(ceil_div(items, 256)), 5);
+int launch_prep_bf16_chunks(const Geometry& g, int per, int nchunk, int terms, const float* protos,
+                            const float* w_last, int act_kind, float eps, void* img, hipStream_t stream) {
+  const int Pp = static_cast<int>(ceil_div(per, 32) * 32);
+  const int items = Pp * 8;  // the largest image loop (P rows x 8 chunks)
+  const dim3 grid(static_cast<unsigned>(ceil_div(items, 256)), 5, static_cast<unsigned>(nchunk));
   unsigned char* blk = static_cast<unsigned char*>(img);
+  const unsigned cb = static_cast<unsigned>(img_offsets(Pp, terms).total);
   const float ws = act_unit(act_kind), wts = act_grad_unit(act_kind, eps);
   if (terms == 2)
-    hipLaunchKernelGGL(l2_prep_bf16_kernel<2>, grid, dim3(256), 0, stream, protos, g.P, g.Pp, w_last, g.K, g.ldw, ws,
-                       wts, blk);
+    hipLaunchKernelGGL(l2_prep_bf16_kernel<2>, grid, dim3(256), 0, stream, protos, g.P, per, w_last, g.K, g.ldw, ws,
+                       wts, blk, cb);
   else
-    hipLaunchKernelGGL(l2_prep_bf16_kernel<3>, grid, dim3(256), 0, stream, protos, g.P, g.Pp, w_last, g.K, g.ldw, ws,
-                       wts, blk);
+    hipLaunchKernelGGL(l2_prep_bf16_kernel<3>, grid, dim3(256), 0, stream, protos, g.P, per, w_last, g.K, g.ldw, ws,
+                       wts, blk, cb);
   return check_launch("l2_prep_bf16_kernel");
+}
+
+int launch_prep_bf16(const Geometry& g, int terms, const float* protos, const float* w_last, int act_kind, float eps,
+                     void* img, hipStream_t stream) {
+  return launch_prep_bf16_chunks(g, g.P, 1, terms, protos, w_last, act_kind, eps, img, stream);
+}
+
+int launch_bwd_reduce_bf16_chunks(const Geometry& g, int per, int nchunk, const float* ws, int slabs,
+                                  size_t chunk_elems, const float* protos, int act_kind, float* g_protos, float* g_w,
+                                  hipStream_t stream) {
+  const int Pp = static_cast<int>(ceil_div(per, 32) * 32);
+  const int elems = Pp * kC + 32 * Pp;
+  hipLaunchKernelGGL(l2_bwd_reduce_bf16_kernel, dim3(static_cast<unsigned>(ceil_div(elems, 64)), nchunk), dim3(256),
+                     0, stream, ws, slabs, g.P, per, g.K, g.ldw, protos, act_unit(act_kind), g_protos, g_w,
+                     chunk_elems);
+  return check_launch("l2_bwd_reduce_bf16_kernel");
 }
 
 int launch_bwd_reduce_bf16(const Geometry& g, const float* ws, int slabs, const float* protos, int act_kind,
                            float* g_protos, float* g_w, hipStream_t stream) {
-  const int elems = g.Pp * kC + 32 * g.Pp;
-  hipLaunchKernelGGL(l2_bwd_reduce_bf16_kernel, dim3(static_cast<unsigned>(ceil_div(elems, 64))), dim3(256), 0,
-                     stream, ws, slabs, g.P, g.Pp, g.K, g.ldw, protos, act_unit(act_kind), g_protos, g_w);
-  return check_launch("l2_bwd_reduce_bf16_kernel");
+  return launch_bwd_reduce_bf16_chunks(g, g.P, 1, ws, slabs, 0, protos, act_kind, g_protos, g_w, stream);
 }
 
 int launch_fwd_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const void* img, float eps, int act_kind,

@@ -124,11 +124,13 @@ __device__ __forceinline__ int gs_off(int row, int slot) { return row * 32 + ((s
 // Channel of physical column u of a CPR-8 image row (chunk u>>3 holds chan_of(q, h, 0..7)).
 __device__ __forceinline__ constexpr int chan_of_col(int u) { return chan_of(u >> 4, (u >> 3) & 1, u & 7); }
 
-template <typename TX, int ACT, bool GD>
+// XSIG: x is the add-on's pre-activation (PROTOSEG_X_SIGMOID): a template parameter, so the
+// plain instantiations carry no trace of it (registers, scheduling).
+template <typename TX, int ACT, bool GD, bool XSIG>
 __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
     const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const unsigned char* __restrict__ img, int P, int Pp,
     int K, float eps, const float* __restrict__ g_logits, unsigned gl_bytes, const float* __restrict__ g_dist,
-    unsigned gd_bytes, int gd_ld, int gd_p0, TX* __restrict__ g_x, int accumulate, float* __restrict__ slab, int xsig) {
+    unsigned gd_bytes, int gd_ld, int gd_p0, TX* __restrict__ g_x, int accumulate, float* __restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const FusedLds L = fused_lds(Pp);
   const ImgOffsets io = img_offsets(Pp, kT);
@@ -188,7 +190,7 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
       const int n = 4 * wave + (lane >> 3), ch = lane & 7;
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = lds_val(R + raw_x(chan_of(ch >> 1, ch & 1, e), n));
-      if (xsig) {  // wave-uniform; pixels past the map stay 0 (their g_s is 0 anyway)
+      if constexpr (XSIG) {  // pixels past the map stay 0 (their g_s is 0 anyway)
         const bool ok = t < ntiles && t * 32 + n < npix;
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = ok ? sigmoid_f(v[e]) : 0.f;
@@ -369,11 +371,18 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
       old[r] = BufIO<TX>::load(rgx, accumulate ? pix : kOOB, co);
     }
     f32x16 acc = zero16();
+#ifdef FUSED_XACC2
+    f32x16 acc1 = zero16();  // second chain: k-step 1 of every prototype tile
+#endif
     f32x4 s_lo = {0.f, 0.f, 0.f, 0.f}, s_hi = {0.f, 0.f, 0.f, 0.f};
     bf16x8 b0[2][kT], b1[2][kT];
     auto step = [&](int pt, bf16x8 (&b)[2][kT]) __attribute__((always_inline)) {
       acc = mma_split<kT>(pa[pt][0], b[0], acc);
+#ifdef FUSED_XACC2
+      acc1 = mma_split<kT>(pa[pt][1], b[1], acc1);
+#else
       acc = mma_split<kT>(pa[pt][1], b[1], acc);
+#endif
 #ifndef FUSED_NO_ONES
 #pragma unroll
       for (int t2 = 0; t2 < kT; ++t2) {
@@ -409,12 +418,16 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
       }
     }
     if (stamp) FSTAMP(6);
+#ifdef FUSED_XACC2
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] += acc1[r];
+#endif
     const float sn = j < 16 ? s_lo[0] : s_hi[0];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const unsigned co = static_cast<unsigned>((16 * (r >> 3) + 4 * ((r >> 2) & 1) + (r & 3)) * HW) * sz;
       float v;
-      if (xsig) {  // through the sigmoid: g_pre = g_x s (1 - s)
+      if constexpr (XSIG) {  // through the sigmoid: g_pre = g_x s (1 - s)
         const float s = sigmoid_f(xr[r]);
         v = (acc[r] + sn * (2.f * s)) * (s * (1.f - s));
       } else {
@@ -503,6 +516,9 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
         }
     }
     prologue_tail();
+#ifdef FUSED_XPRIO
+    __builtin_amdgcn_s_setprio(FUSED_XPRIO);  // the x waves are the loop's critical path
+#endif
     for (int i = 0; i <= iters; ++i) {
       if (i == 2) FSTAMP(2);
 #ifndef FUSED_NO_XSTAGE
@@ -541,19 +557,18 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
   }
 }
 
-template <typename TX, int ACT, bool GD>
+template <typename TX, int ACT, bool GD, bool XSIG>
 int fused_t(const Geometry& g, const void* x, const unsigned char* img, float eps, const float* g_logits,
             const float* g_dist, void* g_x, int accumulate, float* ws, int grid, hipStream_t stream) {
-  if (int st = ensure_lds<l2_bwd_fused_bf16_kernel<TX, ACT, GD>>()) return st;
+  if (int st = ensure_lds<l2_bwd_fused_bf16_kernel<TX, ACT, GD, XSIG>>()) return st;
   const unsigned long long npix = static_cast<unsigned long long>(g.npix);
   const unsigned xb = static_cast<unsigned>(npix * kC * sizeof(TX));
   const unsigned glb = g_logits ? static_cast<unsigned>(npix * g.K * 4) : 0u;
   const unsigned gdb = g_dist ? static_cast<unsigned>(npix * g.ldd * 4) : 0u;
   KernelTimer timer("l2_bwd_fused_bf16_kernel", stream);
-  hipLaunchKernelGGL((l2_bwd_fused_bf16_kernel<TX, ACT, GD>), dim3(grid), dim3(kThreads),
+  hipLaunchKernelGGL((l2_bwd_fused_bf16_kernel<TX, ACT, GD, XSIG>), dim3(grid), dim3(kThreads),
                      static_cast<size_t>(fused_lds(g.Pp).total), stream, static_cast<const TX*>(x), xb, g.HW, g.npix, img,
-                     g.P, g.Pp, g.K, eps, g_logits, glb, g_dist, gdb, g.ldd, g.p0, static_cast<TX*>(g_x), accumulate, ws,
-                     g.xsig);
+                     g.P, g.Pp, g.K, eps, g_logits, glb, g_dist, gdb, g.ldd, g.p0, static_cast<TX*>(g_x), accumulate, ws);
   return check_launch("l2_bwd_fused_bf16_kernel");
 }
 
@@ -568,13 +583,15 @@ int bf16_bwd_fused_grid(const Geometry& g) { return g.ntiles < 256 ? g.ntiles : 
 
 int launch_bwd_fused_bf16(const Geometry& g, bool x_bf16, const void* x, const float* protos, const void* img,
                           float eps, int act_kind, const float* g_logits, const float* g_dist, void* g_x,
-                          float* g_protos, float* g_w, float* ws, hipStream_t stream, int accumulate) {
+                          float* g_protos, float* g_w, float* ws, hipStream_t stream, int accumulate, int reduce) {
   const unsigned char* blk = static_cast<const unsigned char*>(img);
   const int grid = bf16_bwd_fused_grid(g);
   auto go = [&](auto tx, auto aa, auto gd) __attribute__((always_inline)) {
     using TX = std::remove_pointer_t<decltype(tx)>;
-    return fused_t<TX, decltype(aa)::value, decltype(gd)::value>(g, x, blk, eps, g_logits, g_dist, g_x, accumulate, ws,
-                                                                 grid, stream);
+    constexpr int kA = decltype(aa)::value;
+    constexpr bool kG = decltype(gd)::value;
+    if (g.xsig) return fused_t<TX, kA, kG, true>(g, x, blk, eps, g_logits, g_dist, g_x, accumulate, ws, grid, stream);
+    return fused_t<TX, kA, kG, false>(g, x, blk, eps, g_logits, g_dist, g_x, accumulate, ws, grid, stream);
   };
   using A0 = std::integral_constant<int, 0>;
   using A1 = std::integral_constant<int, 1>;
@@ -587,7 +604,7 @@ int launch_bwd_fused_bf16(const Geometry& g, bool x_bf16, const void* x, const f
     st = x_bf16 ? (g_dist ? go(b, A0(), GT()) : go(b, A0(), GF())) : (g_dist ? go(f, A0(), GT()) : go(f, A0(), GF()));
   else
     st = x_bf16 ? (g_dist ? go(b, A1(), GT()) : go(b, A1(), GF())) : (g_dist ? go(f, A1(), GT()) : go(f, A1(), GF()));
-  if (st) return st;
+  if (st || !reduce) return st;
   return launch_bwd_reduce_bf16(g, ws, grid, protos, act_kind, g_protos, g_logits ? g_w : nullptr, stream);
 }
 

@@ -29,6 +29,10 @@ size_t bf16_image_bytes(const Geometry& g, int terms);
 // act_kind / eps select the constant factors folded into the W and W^T images (bf16_split.h).
 int launch_prep_bf16(const Geometry& g, int terms, const float* protos, const float* w_last, int act_kind, float eps,
                      void* img, hipStream_t stream);
+// The images of nchunk prototype chunks of `per` rows (g.P rows in all, W columns at stride
+// g.ldw) in one launch; chunk c's images at c * bf16_image_bytes(Pp(per)).
+int launch_prep_bf16_chunks(const Geometry& g, int per, int nchunk, int terms, const float* protos,
+                            const float* w_last, int act_kind, float eps, void* img, hipStream_t stream);
 
 // accumulate != 0: logits += this call's (prototype chunks of one forward).
 int launch_fwd_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const void* img, float eps, int act_kind,
@@ -41,12 +45,20 @@ int launch_bwd_x_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, 
 // One-kernel backward (l2_bwd_fused.hip): bf16x3 only, Pp <= 192 per launch; g_x (+= when
 // accumulate), and the g_P / g_W slab in ws, summed by launch_bwd_reduce_bf16.
 bool bf16_bwd_fused_fits(const Geometry& g, int terms);
+// reduce = 0: the slab is left in ws for launch_bwd_reduce_bf16_chunks (one reduce per call).
 int launch_bwd_fused_bf16(const Geometry& g, bool x_bf16, const void* x, const float* protos, const void* img,
                           float eps, int act_kind, const float* g_logits, const float* g_dist, void* g_x,
-                          float* g_protos, float* g_w, float* ws, hipStream_t stream, int accumulate = 0);
+                          float* g_protos, float* g_w, float* ws, hipStream_t stream, int accumulate = 0,
+                          int reduce = 1);
+int bf16_bwd_fused_grid(const Geometry& g);
 // Fixed-order sum of `slabs` partial slabs in ws (+ 2p sum g_s) into g_protos / g_w.
 int launch_bwd_reduce_bf16(const Geometry& g, const float* ws, int slabs, const float* protos, int act_kind,
                            float* g_protos, float* g_w, hipStream_t stream);
+// nchunk chunks of `per` prototypes (g.P in all, g_w columns at stride g.ldw); chunk c's slabs
+// at ws + c * chunk_elems.
+int launch_bwd_reduce_bf16_chunks(const Geometry& g, int per, int nchunk, const float* ws, int slabs,
+                                  size_t chunk_elems, const float* protos, int act_kind, float* g_protos, float* g_w,
+                                  hipStream_t stream);
 int launch_bwd_pw_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const float* protos, const void* img,
                        float eps, int act_kind, const float* g_logits, const float* g_dist, float* g_protos,
                        float* g_w, float* ws, hipStream_t stream);

@@ -604,18 +604,21 @@ constexpr size_t kImageBlockMin = 512 * 1024;
 
 struct ImageBlock {
   void* ptr = nullptr;
+  // per > 0: the images of ceil(g.P / per) prototype chunks of `per` rows, one prep launch.
   int build(const Geometry& g, int terms, const float* protos, const float* w_last, int act_kind, float eps,
-            hipStream_t s) {
+            hipStream_t s, int per = 0) {
     static std::mutex mu;
     static std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> blocks;
-    const size_t need = bf16_image_bytes(g, terms);
+    const int nchunk = per > 0 ? static_cast<int>(ceil_div(g.P, per)) : 1;
+    const size_t need = per > 0 ? nchunk * bf16_image_bytes(geometry_of(1, g.C, 1, 1, per, g.K), terms)
+                                : bf16_image_bytes(g, terms);
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return check_launch("hipGetDevice");
     {
       std::lock_guard<std::mutex> lock(mu);
       auto& b = blocks[{dev, s}];
       if (b.second < need) {
-        if (b.first) {  // never for supported shapes (kImageBlockMin covers Pp <= 384, T = 3)
+        if (b.first) {  // once per stream at most (kImageBlockMin covers one launch's images; chunked calls may grow it)
           if (hipStreamSynchronize(s) != hipSuccess || hipFree(b.first) != hipSuccess)
             return check_launch("image block regrow");
           b = {nullptr, 0};
@@ -631,6 +634,7 @@ struct ImageBlock {
       }
       ptr = b.first;
     }
+    if (per > 0) return launch_prep_bf16_chunks(g, per, nchunk, terms, protos, w_last, act_kind, eps, ptr, s);
     return launch_prep_bf16(g, terms, protos, w_last, act_kind, eps, ptr, s);
   }
 };
@@ -741,6 +745,13 @@ extern "C" size_t protoseg_l2_bwd_workspace_size(int B, int C, int H, int W, int
   size_t need = f32_pw_workspace(g);
   const size_t b16 = bf16_bwd_pw_workspace(g);
   if (C == 64 && b16 > need) need = b16;
+  if (C == 64) {  // fused backward: one slab per workgroup and prototype chunk (fused_chunks)
+    const int nchunk = static_cast<int>(ceil_div(P, 192)), per = static_cast<int>(ceil_div(P, nchunk));
+    const Geometry gc = geometry_of(B, C, H, W, per, K);
+    const size_t fused = static_cast<size_t>(nchunk) * bf16_bwd_fused_grid(gc) *
+                         (static_cast<size_t>(gc.Pp) * C + 32 * gc.Pp + gc.Pp) * sizeof(float);
+    if (fused > need) need = fused;
+  }
   return ((need + 255) / 256) * 256;
 }
 
@@ -778,24 +789,28 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
     const int per = static_cast<int>(ceil_div(P, nchunk));
     Geometry gc = geometry_of(B, C, H, W, per, K);
     if (bf16_bwd_fused_fits(gc, terms)) {
+      // One prep launch for every chunk's images, the chunks' fused kernels (each its own slab
+      // region; chunk c > 0 adds its g_x), one reduce launch over all chunks' slabs.
       KernelSpan span(nchunk > 1 ? "l2_bwd_fused_bf16_kernel" : "", "", s);
+      const size_t cb = bf16_image_bytes(gc, terms);
+      const int grid = bf16_bwd_fused_grid(gc);
+      const size_t chunk_elems = static_cast<size_t>(grid) * (static_cast<size_t>(gc.Pp) * C + 32 * gc.Pp + gc.Pp);
+      Geometry gall = geometry_of(B, C, H, W, P, K);
+      ImageBlock img;
+      if (int st = img.build(gall, terms, protos, g_logits ? w_last : nullptr, act_kind, eps, s, per)) return st;
       for (int c = 0; c < nchunk; ++c) {
         const int p0 = c * per, pc = P - p0 < per ? P - p0 : per;
         gc = geometry_of(B, C, H, W, pc, K);
         gc.ldw = gc.ldd = P;
         gc.p0 = p0;
         gc.xsig = xsig;
-        ImageBlock img;
-        if (int st = img.build(gc, terms, protos + static_cast<size_t>(p0) * C, g_logits ? w_last + p0 : nullptr,
-                               act_kind, eps, s))
-          return st;
-        if (int st = launch_bwd_fused_bf16(gc, xb, x, protos + static_cast<size_t>(p0) * C, img.ptr, eps, act_kind,
-                                           g_logits, g_dist, g_x,
-                                           g_protos ? g_protos + static_cast<size_t>(p0) * C : nullptr,
-                                           g_w ? g_w + p0 : nullptr, ws, s, c > 0))
+        if (int st = launch_bwd_fused_bf16(gc, xb, x, protos + static_cast<size_t>(p0) * C,
+                                           static_cast<unsigned char*>(img.ptr) + c * cb, eps, act_kind, g_logits,
+                                           g_dist, g_x, nullptr, nullptr, ws + c * chunk_elems, s, c > 0, 0))
           return st;
       }
-      return PROTOSEG_OK;
+      return launch_bwd_reduce_bf16_chunks(gall, per, nchunk, ws, grid, chunk_elems, protos, act_kind, g_protos,
+                                           g_logits ? g_w : nullptr, s);
     }
   }
   if (xsig) return fail(PROTOSEG_ERR_UNSUPPORTED, "PROTOSEG_X_SIGMOID: no fused backward for this shape");

@@ -1,0 +1,92 @@
+"""Interleaved A/B of library variants in ONE process (cdna_hip_programming.md §5.4 rule 24):
+each build_var/*/libprotoseg_hip.so is loaded side by side with the main library (RTLD_LOCAL),
+and every rep times each library's call back to back, so clock / thermal drift hits all
+variants alike. usage: python tools/ab_libs.py --protos 361 --call bwd_full [--reps 40]"""
+import argparse
+import ctypes
+import glob
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "adlm-inherently-interpretable-segmentation_amd"))
+
+import torch  # noqa: E402
+
+from protoseg_amd import _lib  # noqa: E402
+
+CSRC = os.path.join(ROOT, "adlm-inherently-interpretable-segmentation_amd", "csrc")
+
+
+def load(path):
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+    for name, (res, args) in _lib.SIGNATURES.items():
+        fn = getattr(lib, name, None)
+        if fn is not None:
+            fn.restype, fn.argtypes = res, args
+    return lib
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--protos", type=int, default=361)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--fmap", type=int, default=65)
+    ap.add_argument("--reps", type=int, default=40)
+    ap.add_argument("--call", default="bwd_full", choices=["bwd_full", "bwd_full_xsig", "fwd", "fwd_xsig"])
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    B, C, h, w, P, K = args.batch, 64, args.fmap, args.fmap, args.protos, 19
+    gen = torch.Generator().manual_seed(0)
+    x = torch.sigmoid(2 * torch.randn(B, C, h, w, generator=gen)).to(dev)
+    protos = torch.rand(P, C, generator=gen).to(dev)
+    wl = (torch.rand(K, P, generator=gen) - 0.5).to(dev)
+    gl = torch.randn(B, h, w, K, generator=gen).to(dev)
+    dist = torch.empty(B, P, h, w, device=dev)
+    logits = torch.empty(B, h, w, K, device=dev)
+    gx, gp, gw = torch.empty_like(x), torch.empty(P, C, device=dev), torch.empty(K, P, device=dev)
+    libs = {"main": load(os.path.join(CSRC, "libprotoseg_hip.so"))}
+    for d in sorted(glob.glob(os.path.join(CSRC, "build_var", "*", "libprotoseg_hip.so"))):
+        libs[os.path.basename(os.path.dirname(d))] = load(d)
+    ws_b = libs["main"].protoseg_l2_bwd_workspace_size(B, C, h, w, P, K)
+    ws = torch.empty(ws_b, device=dev, dtype=torch.uint8)
+    P_, s = _lib.ptr, _lib.stream_of(dev)
+    act = _lib.X_SIGMOID if args.call.endswith("xsig") else 0
+    prec = _lib.PRECISIONS["bf16x3"]
+
+    def call(lib):
+        if args.call.startswith("bwd"):
+            st = lib.protoseg_l2_bwd(P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, act, prec, P_(gl), None,
+                                     P_(gx), P_(gp), P_(gw), P_(ws), ws_b, s)
+        else:
+            st = lib.protoseg_l2_fwd(P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, act, prec, P_(dist), None,
+                                     P_(logits), s)
+        assert st == 0, lib.protoseg_last_error()
+
+    ref = None
+    for name, lib in libs.items():  # warm-up + the variants agree with main
+        call(lib)
+        torch.cuda.synchronize()
+        out = (gx if args.call.startswith("bwd") else logits).clone()
+        if ref is None:
+            ref = out
+        else:
+            err = (out - ref).abs().max().item() / (ref.abs().max().item() + 1e-30)
+            print(f"{name}: rel diff vs main {err:.2e}")
+    times = {k: [] for k in libs}
+    for _ in range(args.reps):
+        for name, lib in libs.items():
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            call(lib)
+            b.record()
+            times[name].append((a, b))
+    torch.cuda.synchronize()
+    print(f"== {args.call} P={P} B={B} fmap={args.fmap}")
+    for k, evs in times.items():
+        ms = sorted(a.elapsed_time(b) for a, b in evs)
+        print(f"{k:14s} median {ms[len(ms) // 2] * 1e3:8.1f} us  min {ms[0] * 1e3:8.1f} us")
+
+
+if __name__ == "__main__":
+    main()

@@ -54,6 +54,11 @@ def main():
                                              prec, null, null, P_(logits), s()),
         "fwd_dist_only": lambda: _lib.call("protoseg_l2_fwd", P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 0,
                                            prec, P_(dist), null, null, s()),
+        "fwd_xsig": lambda: _lib.call("protoseg_l2_fwd", P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4,
+                                      _lib.X_SIGMOID, prec, P_(dist), null, P_(logits), s()),
+        "bwd_full_xsig": lambda: _lib.call("protoseg_l2_bwd", P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4,
+                                           _lib.X_SIGMOID, prec, P_(gl), null, P_(gx), P_(gp), P_(gw), P_(ws), ws_b,
+                                           s()),
         "fwd_linear": lambda: _lib.call("protoseg_l2_fwd", P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 1,
                                         prec, P_(dist), null, P_(logits), s()),
         "bwd_x_linear": lambda: _lib.call("protoseg_l2_bwd", P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 1,
