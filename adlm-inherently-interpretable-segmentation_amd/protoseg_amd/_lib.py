@@ -42,6 +42,7 @@ SIGNATURES = {
     "protoseg_timing_events_n": (_i, [ctypes.c_char_p, _vp, _vp, _i]),
     "protoseg_timing_launches": (_i, []),
     "protoseg_l2_supported": (_i, [_i, _i, _i]),
+    "protoseg_adam_step": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _f, _f, _f, _vp]),
     "protoseg_l2_max_protos": (_i, [_i, _i]),
     "protoseg_l2_x_sigmoid_supported": (_i, [_i, _i, _i, _i, _i, _i, _i]),
     "protoseg_l2_fwd": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _i, _vp, _vp, _vp, _vp]),

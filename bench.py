@@ -89,11 +89,13 @@ class LayerStep:
         self.prec = _lib.PRECISIONS[precision]
         # The trained parameters (sharing storage with the kernels' buffers; the backward writes
         # their .grad in place) and the reference's optimizer (module.py:391: Adam; lr of the
-        # prototype vectors, gin joint_optimizer_lr_prototype_vectors). capturable: the update
-        # runs inside the step's HIP graph.
+        # prototype vectors, gin joint_optimizer_lr_prototype_vectors) on the HIP kernel
+        # (protoseg_amd.optim.Adam: one launch for both tensors, step count on the device, so the
+        # update runs inside the step's HIP graph).
+        from protoseg_amd.optim import Adam
         self.params = [torch.nn.Parameter(self.protos), torch.nn.Parameter(self.w_last)]
         self.params[0].grad, self.params[1].grad = self.g_p, self.g_w
-        self.opt = torch.optim.Adam(self.params, lr=2.5e-4, capturable=True, fused=True)
+        self.opt = Adam(self.params, lr=2.5e-4)
         self.buckets = None
 
     def _stream(self):

@@ -350,6 +350,21 @@ int protoseg_bound_boxes(const float* up, int m, int H, int W, const void* label
                          const int32_t* rf_box, float percentile, int margin, float* threshold, int32_t* box,
                          protoseg_stream_t stream);
 
+/*
+ * Optimizer step of the training step: torch.optim.Adam as the reference configures it
+ * (segmentation/module.py:391: amsgrad off, L2 weight decay per group) over n_tensors (<= 8) f32
+ * tensors in one launch, with torch's fused-Adam arithmetic:
+ *   g = grad + weight_decay * p;  m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g^2;
+ *   p -= lr / (1 - b1^t) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
+ *   params[k], grads[k], exp_avg[k], exp_avg_sq[k]: device f32 [numel[k]] (host pointer arrays)
+ *   state: device int32[2] = {step count t of the previous call, 0}; the call uses t + 1 and
+ *          stores it, so a HIP graph holding the call replays as successive steps.
+ */
+int protoseg_adam_step(int n_tensors, float* const* params, const float* const* grads,
+                       float* const* exp_avg, float* const* exp_avg_sq, const int64_t* numel,
+                       int32_t* state, float lr, float beta1, float beta2, float eps, float weight_decay,
+                       protoseg_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -78,6 +78,8 @@ def test_argument_validation_returns_status_without_gpu():
     st = lib.protoseg_l2_fwd(dummy, 0, 1, 64, 2, 2, dummy, 19, dummy, 19, 1e-4, _lib.X_SIGMOID, _lib.PREC_F32,
                              null, null, null, null)
     assert st == _lib.ERR_UNSUPPORTED and b"X_SIGMOID" in lib.protoseg_last_error()
+    st = lib.protoseg_adam_step(0, null, null, null, null, null, null, 1e-3, 0.9, 0.999, 1e-8, 0.0, null)
+    assert st == _lib.ERR_INVALID
     st = lib.protoseg_patch_class_mask(null, 2, 1, 4, 4, 2, 2, null, 0, null, null)
     assert st == _lib.ERR_INVALID
     st = lib.protoseg_push_argmin(dummy, 1, 48, 2, 2, dummy, 3, dummy, dummy, dummy, null, null)

@@ -6,7 +6,7 @@ NAME=$1; FLAGS=$2
 CSRC=$(dirname "$0")/../adlm-inherently-interpretable-segmentation_amd/csrc
 OUT=$CSRC/build_var/$NAME
 mkdir -p "$OUT"
-for s in capi l2_layer l2_bf16 l2_bwd_fused push kld eval knn bbox; do
+for s in capi l2_layer l2_bf16 l2_bwd_fused push kld eval knn bbox adam; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function $FLAGS -I$CSRC/../../include -I$CSRC -c $CSRC/$s.hip -o $OUT/$s.o &
 done
 wait
