@@ -2,7 +2,6 @@
 bucketed gradient all-reduce averages exactly."""
 import math
 import os
-import socket
 
 import pytest
 import torch
@@ -14,9 +13,12 @@ from protoseg_amd.push import PushState
 
 
 def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    """A fresh rendezvous file for init_method='file://' (name kept from the TCP version)."""
+    import tempfile
+    fd, path = tempfile.mkstemp(prefix="protoseg_gloo_")
+    os.close(fd)
+    os.unlink(path)
+    return path
 
 
 def _serial_truth(per_image):
@@ -51,8 +53,9 @@ def _make_images(n_img, P, C):
 
 
 def _worker(rank, world, port, n_img, P, C, result_q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # file rendezvous (no TCP port to race for) and gloo's pair sockets on loopback
+    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+    dist.init_process_group("gloo", init_method=f"file://{port}", rank=rank, world_size=world)
     try:
         images = _make_images(n_img, P, C)
         lo, hi = shard_bounds(n_img, rank, world)

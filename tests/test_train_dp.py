@@ -4,7 +4,6 @@ gradients after an iter_size = 2 accumulation and parameters after the optimizer
 void pixels, the KLD term and the L1 penalty on. The prototype layer here is the oracle's torch
 restatement (model.py:203-283) so the test runs without a GPU; the step logic is the product's."""
 import os
-import socket
 
 import torch
 import torch.distributed as dist
@@ -82,8 +81,9 @@ def _run(world, rank, micro_steps, result_q=None):
 
 
 def _worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # file rendezvous (no TCP port to race for) and gloo's pair sockets on loopback
+    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+    dist.init_process_group("gloo", init_method=f"file://{port}", rank=rank, world_size=world)
     try:
         _run(world, rank, 2, q)
     finally:
@@ -91,9 +91,10 @@ def _worker(rank, world, port, q):
 
 
 def test_dp_step_equals_single_process_on_concatenated_batch():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    import tempfile
+    fd, port = tempfile.mkstemp(prefix="protoseg_gloo_")  # file rendezvous (no TCP port race)
+    os.close(fd)
+    os.unlink(port)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
