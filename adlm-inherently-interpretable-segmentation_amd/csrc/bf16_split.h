@@ -162,12 +162,14 @@ template <> struct BufIO<uint16_t> {
 //   act' = grad_unit * grad_base(d): log: (eps-1) * 1/((d+1)(d+eps))   ((eps-1) is in W^T)
 //                                    linear: -1 * 1                   (-1 is in W^T)
 // v_rcp_f32 + v_log_f32 replace the IEEE division and the denormal-safe logf: the ratio
-// (d+1)/(d+eps) lies in (1, 1e4], where v_log_f32 is accurate to ~1 ulp.
+// (d+1)/(d+eps) lies in (1, 1e4], where v_log_f32 is accurate to ~1 ulp. The forward forms the
+// ratio as 1 + (1-eps)/(d+eps) (one add, one rcp, one fma: a VALU op fewer per element than
+// (d+1) * rcp(d+eps); same absolute rounding, one ulp of the ratio).
 constexpr float kLn2 = 0.6931471805599453f;
 template <int ACT>
 __device__ __forceinline__ float act_base(float d, float eps) {
   if constexpr (ACT == 0) {
-    return __builtin_amdgcn_logf((d + 1.f) * __builtin_amdgcn_rcpf(d + eps));
+    return __builtin_amdgcn_logf(fmaf(1.f - eps, __builtin_amdgcn_rcpf(d + eps), 1.f));
   } else {
     return -d;
   }

@@ -216,8 +216,13 @@ __device__ __forceinline__ f32x16 s_tile(const bf16* Pimg, int Pp, int pt, const
                                          const float (&p2r)[16]) {
   const int j = threadIdx.x & 31, h = (threadIdx.x & 63) >> 5;
   f32x16 acc;
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = x2 + p2r[r];
+  for (int r = 0; r < 16; r += 2) {  // v_pk_add_f32: two rows per VALU op
+    const f32x2 v = f32x2{x2, x2} + f32x2{p2r[r], p2r[r + 1]};
+    acc[r] = v.x;
+    acc[r + 1] = v.y;
+  }
 #pragma unroll
   for (int q = 0; q < kNQ; ++q) {
     bf16x8 pa[T];
@@ -335,13 +340,13 @@ __global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
       }
     };
     const int npt_full = P / 32;  // tiles whose 32 rows are all below P
+    // Full tiles in a loop of their own and the (at most one) partial tile after it: with both
+    // bodies in one loop the logits accumulator lives in different registers on the two paths,
+    // and every iteration ended in 16 v_mov (after an s_nop for the last MFMA) to merge them.
+    int pt = pt0;
 #pragma unroll 1
-    for (int pt = pt0; pt < npt; pt += dpt) {
-      if (pt < npt_full)
-        proto_tile(pt, std::true_type());
-      else
-        proto_tile(pt, std::false_type());
-    }
+    for (; pt < npt_full; pt += dpt) proto_tile(pt, std::true_type());
+    if (pt < npt) proto_tile(pt, std::false_type());
     return lacc;
   };
   auto store_logits = [&](int t, const f32x16& lacc) {

@@ -94,6 +94,8 @@ def test_backward_matches_golden(device, name, precision):
     (1, 128, 6, 7, 64, 32),       # C = 128, K = 32 (max)
     (2, 64, 65, 65, 190, 19),     # cityscapes crop, 10 prototypes/class
     (1, 64, 65, 65, 361, 19),     # 19 prototypes/class
+    (2, 64, 41, 41, 210, 21),     # pascal_*.gin: 21 classes x 10, 321x321 window -> 41x41
+    (2, 64, 21, 21, 50, 5),       # cells.gin: 5 classes x 10, MSC scale 0.5 of the 321 window
 ])
 @pytest.mark.parametrize("activation", ["log", "linear"])
 @pytest.mark.parametrize("precision", PRECISIONS)
