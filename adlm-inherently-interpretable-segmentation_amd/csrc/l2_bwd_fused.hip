@@ -125,8 +125,11 @@ __device__ __forceinline__ int gs_off(int row, int slot) { return row * 32 + ((s
 __device__ __forceinline__ constexpr int chan_of_col(int u) { return chan_of(u >> 4, (u >> 3) & 1, u & 7); }
 
 // XSIG: x is the add-on's pre-activation (PROTOSEG_X_SIGMOID): a template parameter, so the
-// plain instantiations carry no trace of it (registers, scheduling).
-template <typename TX, int ACT, bool GD, bool XSIG>
+// plain instantiations carry no trace of it (registers, scheduling). NPT: prototype tiles of
+// the launch when known at compile time (6: Pp = 192, every chunk at P = 190 / 361 / 570), else
+// 0 (read from Pp): with it the x waves' g_x loop is one straight-line block instead of a
+// branch per prototype tile (each branch a scheduling boundary with its own s_waitcnt).
+template <typename TX, int ACT, bool GD, bool XSIG, int NPT>
 __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
     const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const unsigned char* __restrict__ img, int P, int Pp,
     int K, float eps, const float* __restrict__ g_logits, unsigned gl_bytes, const float* __restrict__ g_dist,
@@ -138,7 +141,7 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
   bf16* WTimg = reinterpret_cast<bf16*>(smem_raw + L.wtimg);
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = wave_id();
   const int ntiles = (npix + 31) / 32;
-  const int npt = Pp / 32;
+  const int npt = NPT ? NPT : Pp / 32;
   const int iters = (ntiles - static_cast<int>(blockIdx.x) + static_cast<int>(gridDim.x) - 1) / static_cast<int>(gridDim.x);
   const bool owner = wave < kOwners;
   const int xw = wave - kOwners;  // x wave index (channel tile), valid when !owner
@@ -557,16 +560,16 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
   }
 }
 
-template <typename TX, int ACT, bool GD, bool XSIG>
+template <typename TX, int ACT, bool GD, bool XSIG, int NPT>
 int fused_t(const Geometry& g, const void* x, const unsigned char* img, float eps, const float* g_logits,
             const float* g_dist, void* g_x, int accumulate, float* ws, int grid, hipStream_t stream) {
-  if (int st = ensure_lds<l2_bwd_fused_bf16_kernel<TX, ACT, GD, XSIG>>()) return st;
+  if (int st = ensure_lds<l2_bwd_fused_bf16_kernel<TX, ACT, GD, XSIG, NPT>>()) return st;
   const unsigned long long npix = static_cast<unsigned long long>(g.npix);
   const unsigned xb = static_cast<unsigned>(npix * kC * sizeof(TX));
   const unsigned glb = g_logits ? static_cast<unsigned>(npix * g.K * 4) : 0u;
   const unsigned gdb = g_dist ? static_cast<unsigned>(npix * g.ldd * 4) : 0u;
   KernelTimer timer("l2_bwd_fused_bf16_kernel", stream);
-  hipLaunchKernelGGL((l2_bwd_fused_bf16_kernel<TX, ACT, GD, XSIG>), dim3(grid), dim3(kThreads),
+  hipLaunchKernelGGL((l2_bwd_fused_bf16_kernel<TX, ACT, GD, XSIG, NPT>), dim3(grid), dim3(kThreads),
                      static_cast<size_t>(fused_lds(g.Pp).total), stream, static_cast<const TX*>(x), xb, g.HW, g.npix, img,
                      g.P, g.Pp, g.K, eps, g_logits, glb, g_dist, gdb, g.ldd, g.p0, static_cast<TX*>(g_x), accumulate, ws);
   return check_launch("l2_bwd_fused_bf16_kernel");
@@ -590,8 +593,12 @@ int launch_bwd_fused_bf16(const Geometry& g, bool x_bf16, const void* x, const f
     using TX = std::remove_pointer_t<decltype(tx)>;
     constexpr int kA = decltype(aa)::value;
     constexpr bool kG = decltype(gd)::value;
-    if (g.xsig) return fused_t<TX, kA, kG, true>(g, x, blk, eps, g_logits, g_dist, g_x, accumulate, ws, grid, stream);
-    return fused_t<TX, kA, kG, false>(g, x, blk, eps, g_logits, g_dist, g_x, accumulate, ws, grid, stream);
+    const bool six = g.Pp == 6 * 32;
+    if (g.xsig)
+      return six ? fused_t<TX, kA, kG, true, 6>(g, x, blk, eps, g_logits, g_dist, g_x, accumulate, ws, grid, stream)
+                 : fused_t<TX, kA, kG, true, 0>(g, x, blk, eps, g_logits, g_dist, g_x, accumulate, ws, grid, stream);
+    return six ? fused_t<TX, kA, kG, false, 6>(g, x, blk, eps, g_logits, g_dist, g_x, accumulate, ws, grid, stream)
+               : fused_t<TX, kA, kG, false, 0>(g, x, blk, eps, g_logits, g_dist, g_x, accumulate, ws, grid, stream);
   };
   using A0 = std::integral_constant<int, 0>;
   using A1 = std::integral_constant<int, 1>;
