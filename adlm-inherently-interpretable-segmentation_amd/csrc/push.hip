@@ -84,7 +84,7 @@ constexpr int kPushMaxTiles = 8;            // prototype tiles per chunk
 #define PUSH_SPLIT 2
 #endif
 #ifndef PUSH_WG_TARGET
-#define PUSH_WG_TARGET 512
+#define PUSH_WG_TARGET 256
 #endif
 constexpr int kPushSplit = PUSH_SPLIT;      // waves per prototype tile (pixel tiles split)
 
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(kPushMaxTiles * kPushSplit * 64) void push_argmin_k
   const int stripe = blockIdx.x, img = blockIdx.y;
   // this wave's epilogue rows, two tiles: [32] ||x||^2, [32] class masks (as float bits) each
   float* xw = push_smem + 2 * push_buf_floats(C) + wave * 128;
-  const int p = (pt0 + static_cast<int>(blockIdx.z) * kPushMaxTiles + ptl) * 32 + j;
+  const int p = (pt0 + static_cast<int>(blockIdx.z) * nptc + ptl) * 32 + j;  // chunk z of nptc tiles
   const bool pvalid = p < P;
   // this lane's B fragments: prototype p, channels 32 ct + 16 h .. + 15 (four 16-B loads per
   // group; lanes past P read row P - 1 and are masked out below)
@@ -398,12 +398,17 @@ extern "C" int protoseg_push_argmin(const float* x, int n_img, int C, int h, int
   if (HW >= (1LL << 31) / 2) return fail(PROTOSEG_ERR_UNSUPPORTED, "h*w=%lld", HW);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int npt = static_cast<int>(ceil_div(P, 32));
-  const int nchunk = static_cast<int>(ceil_div(npt, kPushMaxTiles));
-  // prototype chunks of 8 tiles; the last launch's chunk may be narrower (fewer waves)
-  const int full = npt / kPushMaxTiles, rem = npt - full * kPushMaxTiles;
+  // prototype chunks of equal width (P = 361: 6 + 6 tiles, not 8 + 4, so both launches keep 3
+  // waves per SIMD): `per` tiles in `full` chunks, then the remainder chunk
+  const int per = static_cast<int>(ceil_div(npt, ceil_div(npt, kPushMaxTiles)));
+  const int full = npt / per, rem = npt - full * per;
   const long long nblk = ceil_div(HW, kPushBlkPix);
-  // about 2 workgroups per CU over all images and chunks, at least one block per stripe
-  long long stripes = ceil_div(PUSH_WG_TARGET, static_cast<long long>(n_img) * nchunk);
+  // One generation of workgroups per launch (one per CU: 12 waves at ~120 VGPRs fill a CU's
+  // wave slots), each walking many 128-pixel blocks, so the prologue (prototype vectors, ||p||^2,
+  // first DMA) and the tail are paid once: 2 generations of half-length workgroups measured
+  // 22 % slower (P = 190, 8 images: 148 -> 115 us). Each prototype-chunk launch gets its own
+  // generation (stripes do not shrink with the chunk count).
+  long long stripes = ceil_div(PUSH_WG_TARGET, static_cast<long long>(n_img));
   if (stripes > nblk) stripes = nblk;
   if (stripes < 1) stripes = 1;
   const size_t need = static_cast<size_t>(n_img) * stripes * kPushSplit * P * 2 * sizeof(unsigned long long);
@@ -419,16 +424,16 @@ extern "C" int protoseg_push_argmin(const float* x, int n_img, int C, int h, int
                        part, static_cast<int>(stripes));
   };
   if (nc == 1) {
-    launch(push_argmin_kernel<1>, full, 0, kPushMaxTiles);
-    launch(push_argmin_kernel<1>, rem ? 1 : 0, full * kPushMaxTiles, rem);
+    launch(push_argmin_kernel<1>, full, 0, per);
+    launch(push_argmin_kernel<1>, rem ? 1 : 0, full * per, rem);
   } else if (nc == 2) {
     if (int e = ensure_lds<push_argmin_kernel<2>, 72 * 1024>()) return e;
-    launch(push_argmin_kernel<2>, full, 0, kPushMaxTiles);
-    launch(push_argmin_kernel<2>, rem ? 1 : 0, full * kPushMaxTiles, rem);
+    launch(push_argmin_kernel<2>, full, 0, per);
+    launch(push_argmin_kernel<2>, rem ? 1 : 0, full * per, rem);
   } else {
     if (int e = ensure_lds<push_argmin_kernel<4>, 140 * 1024>()) return e;
-    launch(push_argmin_kernel<4>, full, 0, kPushMaxTiles);
-    launch(push_argmin_kernel<4>, rem ? 1 : 0, full * kPushMaxTiles, rem);
+    launch(push_argmin_kernel<4>, full, 0, per);
+    launch(push_argmin_kernel<4>, rem ? 1 : 0, full * per, rem);
   }
   if (int e = check_launch("push_argmin_kernel")) return e;
   const long long n = static_cast<long long>(n_img) * P;

@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--fmap", type=int, default=65)
     ap.add_argument("--reps", type=int, default=40)
-    ap.add_argument("--call", default="bwd_full", choices=["bwd_full", "bwd_full_xsig", "fwd", "fwd_xsig"])
+    ap.add_argument("--call", default="bwd_full", choices=["bwd_full", "bwd_full_xsig", "fwd", "fwd_xsig", "push"])
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     B, C, h, w, P, K = args.batch, 64, args.fmap, args.fmap, args.protos, 19
@@ -54,8 +54,22 @@ def main():
     act = _lib.X_SIGMOID if args.call.endswith("xsig") else 0
     prec = _lib.PRECISIONS["bf16x3"]
 
+    if args.call == "push":  # push argmin over 8 Cityscapes-sized maps (bench.py's push leg)
+        n_img, ph, pw = 8, 129, 257
+        xp = torch.sigmoid(2 * torch.randn(n_img, C, ph, pw, generator=gen)).to(dev)
+        lab = torch.randint(0, K + 1, (n_img, 1024, 2048), generator=gen, dtype=torch.uint8).to(dev)
+        mask = torch.empty((n_img, ph * pw), device=dev, dtype=torch.int32)
+        pcls = torch.clamp(torch.arange(P) // max(1, P // K), max=K - 1).to(torch.int32).to(dev)
+        keys = torch.empty((n_img, P), device=dev, dtype=torch.int64)
+        second = torch.empty_like(keys)
+        st = libs["main"].protoseg_patch_class_mask(P_(lab), _lib.U8, n_img, 1024, 2048, ph, pw, None, 0, P_(mask), s)
+        assert st == 0
+
     def call(lib):
-        if args.call.startswith("bwd"):
+        if args.call == "push":
+            st = lib.protoseg_push_argmin(P_(xp), n_img, C, ph, pw, P_(protos), P, P_(pcls), P_(mask), P_(keys),
+                                          P_(second), s)
+        elif args.call.startswith("bwd"):
             st = lib.protoseg_l2_bwd(P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, act, prec, P_(gl), None,
                                      P_(gx), P_(gp), P_(gw), P_(ws), ws_b, s)
         else:
@@ -67,7 +81,7 @@ def main():
     for name, lib in libs.items():  # warm-up + the variants agree with main
         call(lib)
         torch.cuda.synchronize()
-        out = (gx if args.call.startswith("bwd") else logits).clone()
+        out = (keys.float() if args.call == "push" else gx if args.call.startswith("bwd") else logits).clone()
         if ref is None:
             ref = out
         else:
