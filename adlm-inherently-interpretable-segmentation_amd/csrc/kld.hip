@@ -4,9 +4,10 @@
 // masked_select, a log_softmax and two kl_div per pair and host syncs per class (module.py:170,
 // 174). Here the same quantities come from these launches:
 //   kld_lists_kernel     prototype -> class buckets (ascending prototype ids), module.py:173
-//   kld_partial_kernel   one workgroup per (class c, image b, pixel range s): over the range's
-//                        class pixels, the local max m_i and sum_n exp(z_i - m_i) of each class
-//                        prototype (z = distance), and T_ij = sum_n exp(z_i - m_i) (z_i - z_j)
+//   kld_partial_kernel   one workgroup per (class c, image b, pixel range s), one pass over the
+//                        range's class pixels (running max): the local max m_i and
+//                        sum_n exp(z_i - m_i) of each class prototype (z = distance), and
+//                        T_ij = sum_n exp(z_i - m_i) (z_i - z_j)
 //   kld_merge_kernel     per (c, b): L_i = log-sum-exp over the ranges (module.py:183) and
 //                        KL(p_i || p_j) = sum_s exp(m_i^s - L_i) T_ij^s - (L_i - L_j), which is
 //                        sum_n p_i (lp_i - lp_j) regrouped (module.py:190-198)
@@ -104,47 +105,42 @@ constexpr int kKldListMaxP = 1 << 20;
 __global__ __launch_bounds__(64) void kld_lists_kernel(const int32_t* __restrict__ proto_class, int P, int K,
                                                        int max_per_class, int* __restrict__ off,
                                                        int* __restrict__ idx, int* __restrict__ stat) {
-  __shared__ int s_count[kKldMaxClasses + 1], s_next[kKldMaxClasses + 1];
+  // Bucket c's running count and write position live in lane c's registers (no LDS, no
+  // barriers): ballots give each chunk's members, a broadcast of lane c gives their base.
   const int lane = threadIdx.x;
-  if (lane <= K) s_count[lane] = 0;
-  __syncthreads();
+  int cnt = 0;
   for (int p0 = 0; p0 < P; p0 += 64) {
     const int p = p0 + lane;
     const int bk = p < P ? bucket_of(proto_class[p], K) : -1;
     for (int c = 0; c <= K; ++c) {
       const unsigned long long m = __ballot(bk == c);
-      if (lane == 0) s_count[c] += __popcll(m);
+      if (lane == c) cnt += __popcll(m);
     }
   }
-  __syncthreads();
-  int cnt = lane <= K ? s_count[lane] : 0;
   int incl = cnt;
 #pragma unroll
   for (int sft = 1; sft < 64; sft <<= 1) {
     const int v = __shfl_up(incl, sft);
     if (lane >= sft) incl += v;
   }
-  if (lane <= K) {
-    off[lane] = incl - cnt;
-    s_next[lane] = incl - cnt;
-  }
+  if (lane <= K) off[lane] = incl - cnt;
   if (lane == K) off[K + 1] = incl;
   const bool over = lane < K && cnt > max_per_class;
   const unsigned long long any_over = __ballot(over);
-  __syncthreads();
+  int next = incl - cnt;  // lane c: next free slot of bucket c
   for (int p0 = 0; p0 < P; p0 += 64) {
     const int p = p0 + lane;
     const int bk = p < P ? bucket_of(proto_class[p], K) : -1;
     for (int c = 0; c <= K; ++c) {
       const unsigned long long m = __ballot(bk == c);
+      if (m == 0ull) continue;  // uniform
+      const int base = __shfl(next, c);
       if (bk == c) {
         const int below = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
                                                     __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0));
-        idx[s_next[c] + below] = p;
+        idx[base + below] = p;
       }
-      __syncthreads();
-      if (lane == 0) s_next[c] += __popcll(m);
-      __syncthreads();
+      if (lane == c) next += __popcll(m);
     }
   }
   if (lane == 0) {
@@ -166,6 +162,11 @@ __device__ __forceinline__ void lse_merge(float& m, float& s, float mo, float so
 }
 
 // One workgroup per (class c, image b, pixel range s). LDS (dynamic): [mpc][257] e | [mpc][257] z.
+// ONE pass over the range (online log-sum-exp): per 256-pixel chunk the class pixels' distances
+// are compacted into LDS, the chunk's max per prototype updates the running max m_i, the
+// accumulators S_i = sum e_i and T_ij = sum e_i (z_i - z_j) (e_i = exp(z_i - m_i)) are rescaled
+// by exp(m_old - m_new), and the chunk is added. The range partial (m_i, S_i, T_ij, count) is the
+// one a separate max pass would give, up to rounding.
 template <typename TL>
 __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* __restrict__ dist, int P, int HW,
                                                                   const TL* __restrict__ label, int K, int mpc,
@@ -173,8 +174,8 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
                                                                   const int* __restrict__ idx, float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) float kld_smem[];
   __shared__ int s_proto[kKldMaxPerClass];
-  __shared__ float s_red[4][kKldMaxPerClass];
   __shared__ float s_m[kKldMaxPerClass];
+  __shared__ float s_scale[kKldMaxPerClass];
   __shared__ int s_cnt[4];
   const int c = blockIdx.x, b = blockIdx.y, rs = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -186,44 +187,15 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
     if (tid == 0) out[2 * kKldMaxPerClass] = 0.f;
     return;
   }
-  if (tid < npc) s_proto[tid] = idx[o0 + tid];
+  if (tid < npc) {
+    s_proto[tid] = idx[o0 + tid];
+    s_m[tid] = -INFINITY;
+  }
   __syncthreads();
   const TL* lab = label + static_cast<size_t>(b) * HW;
   const float* db = dist + static_cast<size_t>(b) * P * HW;
   const int n0 = rs * kKldRange, n1 = min(HW, n0 + kKldRange);
 
-  // ---- local max per prototype and pixel count over the range's class pixels
-  float m[kKldMaxPerClass];
-#pragma unroll
-  for (int i = 0; i < kKldMaxPerClass; ++i) m[i] = -INFINITY;
-  int cnt = 0;
-  for (int n = n0 + tid; n < n1; n += kKldThreads) {
-    if (label_at(lab, n) != c) continue;
-    ++cnt;
-#pragma unroll
-    for (int i = 0; i < kKldMaxPerClass; ++i)
-      if (i < npc) m[i] = fmaxf(m[i], db[static_cast<size_t>(s_proto[i]) * HW + n]);
-  }
-#pragma unroll
-  for (int i = 0; i < kKldMaxPerClass; ++i) {
-    if (i < npc) {
-      float mi = m[i];
-#pragma unroll
-      for (int sh = 32; sh >= 1; sh >>= 1) mi = fmaxf(mi, __shfl_xor(mi, sh));
-      if (lane == 0) s_red[wave][i] = mi;
-    }
-  }
-#pragma unroll
-  for (int sh = 32; sh >= 1; sh >>= 1) cnt += __shfl_xor(cnt, sh);
-  if (lane == 0) s_cnt[wave] = cnt;
-  __syncthreads();
-  const int total = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
-  if (tid < npc) s_m[tid] = fmaxf(fmaxf(s_red[0][tid], s_red[1][tid]), fmaxf(s_red[2][tid], s_red[3][tid]));
-  if (tid == 0) out[2 * kKldMaxPerClass] = static_cast<float>(total);
-  if (total == 0) return;  // uniform
-  __syncthreads();
-
-  // ---- S_i = sum e_i and T_ij = sum e_i (z_i - z_j), e_i = exp(z_i - m_i), from staged chunks
   float* se = kld_smem;                          // [npc][257]
   float* sz = kld_smem + npc * kKldLdsStride;    // [npc][257]
   const int E = npc * npc;
@@ -231,6 +203,7 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
   G = G < 1 ? 1 : (G > 16 ? 16 : G);
   const int ntask = E * G;  // <= 1024
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  int total = 0;
   for (int base = n0; base < n1; base += kKldThreads) {
     // the chunk's class pixels, compacted in pixel order (wave ballots + prefix)
     const int n = base + tid;
@@ -245,14 +218,36 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
       __syncthreads();
       continue;
     }
+    total += kq;
     if (in) {
       int pos = below;
       for (int w = 0; w < wave; ++w) pos += s_cnt[w];
-      for (int i = 0; i < npc; ++i) {
-        const float z = db[static_cast<size_t>(s_proto[i]) * HW + n];
-        se[i * kKldLdsStride + pos] = expf(z - s_m[i]);
-        sz[i * kKldLdsStride + pos] = z;
+      for (int i = 0; i < npc; ++i) sz[i * kKldLdsStride + pos] = db[static_cast<size_t>(s_proto[i]) * HW + n];
+    }
+    __syncthreads();
+    {  // chunk max per prototype (8 threads per row) -> running max and the rescale factor
+      const int i = tid >> 3, l8 = tid & 7;
+      float mx = -INFINITY;
+      if (i < npc)
+        for (int q = l8; q < kq; q += 8) mx = fmaxf(mx, sz[i * kKldLdsStride + q]);
+      mx = fmaxf(mx, __shfl_xor(mx, 1));
+      mx = fmaxf(mx, __shfl_xor(mx, 2));
+      mx = fmaxf(mx, __shfl_xor(mx, 4));
+      if (i < npc && l8 == 0) {
+        const float mo = s_m[i], mn = fmaxf(mo, mx);
+        s_scale[i] = expf(mo - mn);  // mo = -inf (first chunk with pixels): 0, nothing to rescale
+        s_m[i] = mn;
       }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int task = tid + k * kKldThreads;
+      if (task < ntask) acc[k] *= s_scale[(task / G) / npc];
+    }
+    for (int t = tid; t < npc * kq; t += kKldThreads) {
+      const int i = t / kq, q = t - i * kq;
+      se[i * kKldLdsStride + q] = expf(sz[i * kKldLdsStride + q] - s_m[i]);
     }
     __syncthreads();
 #pragma unroll
@@ -275,6 +270,8 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
     }
     __syncthreads();
   }
+  if (tid == 0) out[2 * kKldMaxPerClass] = static_cast<float>(total);
+  if (total == 0) return;  // uniform
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int task = tid + k * kKldThreads;

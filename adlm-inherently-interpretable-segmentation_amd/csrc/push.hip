@@ -258,10 +258,20 @@ __global__ __launch_bounds__(256) void push_top2_kernel(const unsigned long long
   if (i >= static_cast<long long>(n_img) * P) return;
   const int img = static_cast<int>(i / P), p = static_cast<int>(i - static_cast<long long>(img) * P);
   unsigned long long b = ~0ull, s = ~0ull;
-  for (int st = 0; st < stripes; ++st) {
-    const unsigned long long* o = part + ((static_cast<size_t>(img) * stripes + st) * P + p) * 2;
-    top2_merge(b, s, o[0], o[1]);
+  const unsigned long long* o = part + (static_cast<size_t>(img) * stripes * P + p) * 2;
+  const size_t step = static_cast<size_t>(P) * 2;
+  int st = 0;
+  for (; st + 8 <= stripes; st += 8) {  // 8 independent loads in flight, then the fold in order
+    unsigned long long kb[8], ks[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      kb[u] = o[(st + u) * step];
+      ks[u] = o[(st + u) * step + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) top2_merge(b, s, kb[u], ks[u]);
   }
+  for (; st < stripes; ++st) top2_merge(b, s, o[st * step], o[st * step + 1]);
   keys[i] = b;
   if (second) second[i] = s;
 }
