@@ -32,17 +32,27 @@ __global__ __launch_bounds__(256) void patch_mask_kernel(const TL* __restrict__ 
   const double pw = static_cast<double>(W) / static_cast<double>(w);
   for (int q = threadIdx.x; q < w; q += blockDim.x) smask[q] = 0u;
   __syncthreads();
-  // Rows of this patch row: push.py:217 patch_i = int(pixel_i / patch_height).
+  // Rows of this patch row: push.py:217 patch_i = int(pixel_i / patch_height). int(i / ph) is
+  // non-decreasing in i, so they are the contiguous run [r0, r1) found once (f64 divisions per
+  // candidate row, not per row and column).
   int i0 = static_cast<int>(floor(pi * ph)) - 2;
   int i1 = static_cast<int>(ceil((pi + 1) * ph)) + 2;
   i0 = i0 < 0 ? 0 : i0;
   i1 = i1 > H ? H : i1;
+  int r0 = i1, r1 = i1;
+  for (int i = i0; i < i1; ++i) {
+    const int q = static_cast<int>(static_cast<double>(i) / ph);
+    if (q == pi && r0 == i1) r0 = i;
+    if (q > pi) {
+      r1 = i;
+      break;
+    }
+  }
   const TL* L = label + static_cast<size_t>(img) * H * W;
   for (int col = threadIdx.x; col < W; col += blockDim.x) {
     const int pj = static_cast<int>(static_cast<double>(col) / pw);  // push.py:219
     uint32_t bits = 0u;
-    for (int i = i0; i < i1; ++i) {
-      if (static_cast<int>(static_cast<double>(i) / ph) != pi) continue;
+    for (int i = r0; i < r1; ++i) {
       const long long raw = static_cast<long long>(L[static_cast<size_t>(i) * W + col]);
       long long c = raw;
       if (lut) {

@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--fmap", type=int, default=65)
     ap.add_argument("--reps", type=int, default=40)
-    ap.add_argument("--call", default="bwd_full", choices=["bwd_full", "bwd_full_xsig", "fwd", "fwd_xsig", "push", "kld"])
+    ap.add_argument("--call", default="bwd_full", choices=["bwd_full", "bwd_full_xsig", "fwd", "fwd_xsig", "push", "mask", "kld"])
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     B, C, h, w, P, K = args.batch, 64, args.fmap, args.fmap, args.protos, 19
@@ -54,7 +54,7 @@ def main():
     act = _lib.X_SIGMOID if args.call.endswith("xsig") else 0
     prec = _lib.PRECISIONS["bf16x3"]
 
-    if args.call == "push":  # push argmin over 8 Cityscapes-sized maps (bench.py's push leg)
+    if args.call in ("push", "mask"):  # push argmin over 8 Cityscapes-sized maps (bench.py's push leg)
         n_img, ph, pw = 8, 129, 257
         xp = torch.sigmoid(2 * torch.randn(n_img, C, ph, pw, generator=gen)).to(dev)
         lab = torch.randint(0, K + 1, (n_img, 1024, 2048), generator=gen, dtype=torch.uint8).to(dev)
@@ -78,7 +78,9 @@ def main():
         assert st == 0
 
     def call(lib):
-        if args.call == "kld":
+        if args.call == "mask":
+            st = lib.protoseg_patch_class_mask(P_(lab), _lib.U8, n_img, 1024, 2048, ph, pw, None, 0, P_(mask), s)
+        elif args.call == "kld":
             st = lib.protoseg_kld_forward(P_(dist), B, P, h * w, P_(tgt), _lib.I64, P_(pcls), K, mpc, P_(kloss), None,
                                           P_(kws), kws_b, s)
         elif args.call == "push":
@@ -96,7 +98,7 @@ def main():
     for name, lib in libs.items():  # warm-up + the variants agree with main
         call(lib)
         torch.cuda.synchronize()
-        out = (kloss.reshape(1) if args.call == "kld" else keys.float() if args.call == "push" else
+        out = (mask.float() if args.call == "mask" else kloss.reshape(1) if args.call == "kld" else keys.float() if args.call == "push" else
                gx if args.call.startswith("bwd") else logits).clone()
         if ref is None:
             ref = out
