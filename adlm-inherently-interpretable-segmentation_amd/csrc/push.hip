@@ -49,19 +49,46 @@ __global__ __launch_bounds__(256) void patch_mask_kernel(const TL* __restrict__ 
     }
   }
   const TL* L = label + static_cast<size_t>(img) * H * W;
-  for (int col = threadIdx.x; col < W; col += blockDim.x) {
-    const int pj = static_cast<int>(static_cast<double>(col) / pw);  // push.py:219
-    uint32_t bits = 0u;
-    for (int i = r0; i < r1; ++i) {
-      const long long raw = static_cast<long long>(L[static_cast<size_t>(i) * W + col]);
-      long long c = raw;
-      if (lut) {
-        if (raw < 0 || raw >= lut_size) continue;
-        c = lut[raw];
-      }
-      if (c > 0 && c <= 32) bits |= 1u << (c - 1);  // push.py:222-223: class c -> key c-1
+  // 4 consecutive columns per thread (one 4-byte load per row for u8 labels); columns of one
+  // patch are OR-ed in registers, so LDS atomics go once per (thread, patch), not per column
+  const bool vec4 = sizeof(TL) == 1 && (W & 3) == 0 && (reinterpret_cast<uintptr_t>(label) & 3) == 0;
+  auto cls_bit = [&](long long raw) -> uint32_t {
+    long long c = raw;
+    if (lut) {
+      if (raw < 0 || raw >= lut_size) return 0u;
+      c = lut[raw];
     }
-    if (bits && pj < w) atomicOr(&smask[pj], bits);
+    return (c > 0 && c <= 32) ? 1u << (c - 1) : 0u;  // push.py:222-223: class c -> key c-1
+  };
+  for (int c0 = 4 * static_cast<int>(threadIdx.x); c0 < W; c0 += 4 * static_cast<int>(blockDim.x)) {
+    uint32_t b4[4] = {0u, 0u, 0u, 0u};
+    const int nc = W - c0 < 4 ? W - c0 : 4;
+    for (int i = r0; i < r1; ++i) {
+      const TL* row = L + static_cast<size_t>(i) * W + c0;
+      if (vec4) {
+        const uint32_t q = *reinterpret_cast<const uint32_t*>(row);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) b4[k] |= cls_bit(static_cast<long long>((q >> (8 * k)) & 0xffu));
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (k < nc) b4[k] |= cls_bit(static_cast<long long>(row[k]));
+      }
+    }
+    int cur = -1;
+    uint32_t acc = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k >= nc) break;
+      const int pj = static_cast<int>(static_cast<double>(c0 + k) / pw);  // push.py:219
+      if (pj != cur) {
+        if (acc && cur >= 0 && cur < w) atomicOr(&smask[cur], acc);
+        cur = pj;
+        acc = 0u;
+      }
+      acc |= b4[k];
+    }
+    if (acc && cur >= 0 && cur < w) atomicOr(&smask[cur], acc);
   }
   __syncthreads();
   for (int q = threadIdx.x; q < w; q += blockDim.x)
