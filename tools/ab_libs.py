@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--fmap", type=int, default=65)
     ap.add_argument("--reps", type=int, default=40)
-    ap.add_argument("--call", default="bwd_full", choices=["bwd_full", "bwd_full_xsig", "fwd", "fwd_xsig", "push", "mask", "kld"])
+    ap.add_argument("--call", default="bwd_full", choices=["bwd_full", "bwd_full_xsig", "fwd", "fwd_xsig", "push", "mask", "kld", "kldb"])
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     B, C, h, w, P, K = args.batch, 64, args.fmap, args.fmap, args.protos, 19
@@ -65,7 +65,7 @@ def main():
         st = libs["main"].protoseg_patch_class_mask(P_(lab), _lib.U8, n_img, 1024, 2048, ph, pw, None, 0, P_(mask), s)
         assert st == 0
 
-    if args.call == "kld":  # KLD forward on the layer's distances (bench.py setup_kld: 8x8 label blocks)
+    if args.call in ("kld", "kldb"):  # KLD forward (kldb: + backward) on the layer's distances (bench.py setup_kld: 8x8 label blocks)
         blocks = torch.randint(0, K + 1, (B, (h + 7) // 8, (w + 7) // 8), generator=gen)
         tgt = blocks.repeat_interleave(8, 1).repeat_interleave(8, 2)[:, :h, :w].reshape(B, -1).contiguous().to(dev)
         pcls = torch.clamp(torch.arange(P) // (P // K), max=K - 1).to(torch.int32).to(dev)
@@ -73,6 +73,8 @@ def main():
         kws_b = libs["main"].protoseg_kld_workspace_size(B, P, h * w, K)
         kws = torch.empty(kws_b, device=dev, dtype=torch.uint8)
         kloss = torch.empty((), device=dev)
+        kg = torch.full((), 0.25, device=dev)
+        gdist = torch.empty_like(dist)
         st = libs["main"].protoseg_l2_fwd(P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 0,
                                           _lib.PRECISIONS["bf16x3"], P_(dist), None, P_(logits), s)
         assert st == 0
@@ -80,9 +82,12 @@ def main():
     def call(lib):
         if args.call == "mask":
             st = lib.protoseg_patch_class_mask(P_(lab), _lib.U8, n_img, 1024, 2048, ph, pw, None, 0, P_(mask), s)
-        elif args.call == "kld":
+        elif args.call in ("kld", "kldb"):
             st = lib.protoseg_kld_forward(P_(dist), B, P, h * w, P_(tgt), _lib.I64, P_(pcls), K, mpc, P_(kloss), None,
                                           P_(kws), kws_b, s)
+            if args.call == "kldb" and st == 0:
+                st = lib.protoseg_kld_backward(P_(dist), B, P, h * w, P_(tgt), _lib.I64, P_(pcls), K, mpc, P_(kg),
+                                               P_(kws), kws_b, P_(gdist), s)
         elif args.call == "push":
             st = lib.protoseg_push_argmin(P_(xp), n_img, C, ph, pw, P_(protos), P, P_(pcls), P_(mask), P_(keys),
                                           P_(second), s)
@@ -98,7 +103,8 @@ def main():
     for name, lib in libs.items():  # warm-up + the variants agree with main
         call(lib)
         torch.cuda.synchronize()
-        out = (mask.float() if args.call == "mask" else kloss.reshape(1) if args.call == "kld" else keys.float() if args.call == "push" else
+        out = (gdist if args.call == "kldb" else mask.float() if args.call == "mask" else
+               kloss.reshape(1) if args.call == "kld" else keys.float() if args.call == "push" else
                gx if args.call.startswith("bwd") else logits).clone()
         if ref is None:
             ref = out
