@@ -102,7 +102,10 @@ template <typename TX, int NC>
 __global__ __launch_bounds__(kFwdWaves * 64) void l2_fwd_kernel(
     const TX* __restrict__ x, int HW, int npix, const float* __restrict__ protos, int P, int Pp,
     const float* __restrict__ w_last, int K, float eps, int act_kind, float* __restrict__ dist,
-    float* __restrict__ act_out, float* __restrict__ logits) {
+    float* __restrict__ act_out, float* __restrict__ logits, int ld, int p0, int ldw, int accumulate) {
+  // Prototype chunk p0 .. p0 + P of ld in all (ld = P, p0 = 0 for a whole call): distance rows at
+  // b * ld + p0 + p, activation columns at g * ld + p0 + p, W columns at stride ldw (w_last
+  // points at column p0), logits added to the earlier chunks' when accumulate != 0.
   constexpr int C = NC * 32;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Pt = smem;                      // [Pp/32][C][33]
@@ -112,7 +115,7 @@ __global__ __launch_bounds__(kFwdWaves * 64) void l2_fwd_kernel(
   if (do_logits) {
     for (int idx = threadIdx.x; idx < Pp * 32; idx += blockDim.x) {
       const int p = idx >> 5, k = idx & 31;
-      Wl[idx] = (p < P && k < K) ? w_last[static_cast<size_t>(k) * P + p] : 0.f;
+      Wl[idx] = (p < P && k < K) ? w_last[static_cast<size_t>(k) * ldw + p] : 0.f;
     }
   }
   stage_prototypes<NC>(Pt, p2s, protos, P, Pp);
@@ -133,7 +136,7 @@ __global__ __launch_bounds__(kFwdWaves * 64) void l2_fwd_kernel(
 #pragma unroll 1
     for (int pt = 0; pt < npt; ++pt) {
       // row p = pt*32 + 4h + row_of(r) of D[b] (clamped to a valid row for padded lanes)
-      float* dpt = dist ? dist + (static_cast<size_t>(b) * P + pt * 32 + 4 * h) * HW + n : nullptr;
+      float* dpt = dist ? dist + (static_cast<size_t>(b) * ld + p0 + pt * 32 + 4 * h) * HW + n : nullptr;
       f32x16 acc = zero16();
       const float* Pa = Pt + pt * C * kLdt + j;
 #pragma unroll
@@ -147,7 +150,7 @@ __global__ __launch_bounds__(kFwdWaves * 64) void l2_fwd_kernel(
         const bool st = valid && p < P;
         if (dpt && st) dpt[static_cast<size_t>(row_of(r)) * HW] = d;
         const float a = activation(d, eps, act_kind);
-        if (act_out && st) act_out[static_cast<size_t>(g) * P + p] = a;
+        if (act_out && st) act_out[static_cast<size_t>(g) * ld + p0 + p] = a;
         acc[r] = a;
       }
       if (do_logits) {
@@ -160,7 +163,10 @@ __global__ __launch_bounds__(kFwdWaves * 64) void l2_fwd_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int k = acc_row(r, h);
-        if (k < K) logits[static_cast<size_t>(g) * K + k] = lacc[r];
+        if (k < K) {
+          float* lp = logits + static_cast<size_t>(g) * K + k;
+          *lp = accumulate ? *lp + lacc[r] : lacc[r];
+        }
       }
     }
   }
@@ -170,7 +176,8 @@ template <typename TX, int NC>
 __global__ __launch_bounds__(kFwdWaves * 64) void l2_bwd_x_kernel(
     const TX* __restrict__ x, int HW, int npix, const float* __restrict__ protos, int P, int Pp,
     const float* __restrict__ w_last, int K, float eps, int act_kind, const float* __restrict__ g_logits,
-    const float* __restrict__ g_dist, TX* __restrict__ g_x) {
+    const float* __restrict__ g_dist, TX* __restrict__ g_x, int ld, int p0, int ldw, int accumulate) {
+  // chunk conventions as l2_fwd_kernel; g_x of chunk c > 0 is added (a sum over prototypes)
   constexpr int C = NC * 32;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Pt = smem;                      // [Pp/32][C][33]
@@ -179,7 +186,7 @@ __global__ __launch_bounds__(kFwdWaves * 64) void l2_bwd_x_kernel(
   if (g_logits) {
     for (int idx = threadIdx.x; idx < Pp * 32; idx += blockDim.x) {
       const int pt = idx >> 10, k = (idx >> 5) & 31, p = pt * 32 + (idx & 31);
-      Wt[idx] = (p < P && k < K) ? w_last[static_cast<size_t>(k) * P + p] : 0.f;
+      Wt[idx] = (p < P && k < K) ? w_last[static_cast<size_t>(k) * ldw + p] : 0.f;
     }
   }
   stage_prototypes<NC>(Pt, p2s, protos, P, Pp);
@@ -218,7 +225,7 @@ __global__ __launch_bounds__(kFwdWaves * 64) void l2_bwd_x_kernel(
       for (int ct = 0; ct < NC; ++ct)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc = mfma32(Pa[(ct * 32 + acc_row(r, h)) * kLdt], xv[ct][r], acc);
-      const float* gdpt = g_dist ? g_dist + (static_cast<size_t>(b) * P + pt * 32 + 4 * h) * HW + n : nullptr;
+      const float* gdpt = g_dist ? g_dist + (static_cast<size_t>(b) * ld + p0 + pt * 32 + 4 * h) * HW + n : nullptr;
       f32x16 gacc = zero16();
       if (g_logits) {
         const float* Wa = Wt + pt * 1024 + j;
@@ -256,7 +263,9 @@ __global__ __launch_bounds__(kFwdWaves * 64) void l2_bwd_x_kernel(
         for (int r = 0; r < 16; ++r) {
           // channel c = 32ct + acc_row(r, h). conv(x^2, ones) backward then pow backward:
           // gsum * (2x); plus the xp branch accumulated in gx.
-          XIO<TX>::store(gxh, static_cast<size_t>(ct * 32 + row_of(r)) * HW, gx[ct][r] + gsum * (2.f * xv[ct][r]));
+          const size_t o = static_cast<size_t>(ct * 32 + row_of(r)) * HW;
+          const float v = gx[ct][r] + gsum * (2.f * xv[ct][r]);
+          XIO<TX>::store(gxh, o, accumulate ? XIO<TX>::load(gxh, o) + v : v);
         }
     }
   }
@@ -502,24 +511,26 @@ int pw_splits(long long ntiles, int Pp) {
 
 template <typename TX, int NC>
 int launch_fwd(const Geometry& geo, const void* x, const float* protos, const float* w_last, float eps,
-               int act_kind, float* dist, float* act, float* logits, hipStream_t stream) {
+               int act_kind, float* dist, float* act, float* logits, hipStream_t stream, int accumulate = 0) {
   if (int st = ensure_lds<l2_fwd_kernel<TX, NC>>()) return st;
   const size_t lds = layer_lds_bytes(geo.C, geo.Pp);
   KernelTimer timer("l2_fwd_kernel", stream);
   hipLaunchKernelGGL((l2_fwd_kernel<TX, NC>), dim3(layer_grid(geo)), dim3(kFwdWaves * 64), lds, stream,
                      static_cast<const TX*>(x), geo.HW, geo.npix, protos, geo.P, geo.Pp, w_last, geo.K, eps,
-                     act_kind, dist, act, logits);
+                     act_kind, dist, act, logits, geo.ldd, geo.p0, geo.ldw, accumulate);
   return check_launch("l2_fwd_kernel");
 }
 
 template <typename TX, int NC>
 int launch_bwd_x(const Geometry& geo, const void* x, const float* protos, const float* w_last, float eps,
-                 int act_kind, const float* g_logits, const float* g_dist, void* g_x, hipStream_t stream) {
+                 int act_kind, const float* g_logits, const float* g_dist, void* g_x, hipStream_t stream,
+                 int accumulate = 0) {
   if (int st = ensure_lds<l2_bwd_x_kernel<TX, NC>>()) return st;
   KernelTimer timer("l2_bwd_x_kernel", stream);
   hipLaunchKernelGGL((l2_bwd_x_kernel<TX, NC>), dim3(layer_grid(geo)), dim3(kFwdWaves * 64),
                      layer_lds_bytes(geo.C, geo.Pp), stream, static_cast<const TX*>(x), geo.HW, geo.npix, protos,
-                     geo.P, geo.Pp, w_last, geo.K, eps, act_kind, g_logits, g_dist, static_cast<TX*>(g_x));
+                     geo.P, geo.Pp, w_last, geo.K, eps, act_kind, g_logits, g_dist, static_cast<TX*>(g_x), geo.ldd,
+                     geo.p0, geo.ldw, accumulate);
   return check_launch("l2_bwd_x_kernel");
 }
 
@@ -645,18 +656,21 @@ constexpr int kMaxChunkedP = 4096;
 
 bool f32_family_fits(int C, int Pp) { return layer_lds_bytes(C, Pp) <= kMaxLds; }
 
+// Largest P one f32-family launch stages (its LDS holds every prototype of the launch).
+int f32_launch_protos(int C) {
+  int p = 0;
+  while (f32_family_fits(C, p + 32)) p += 32;
+  return p;
+}
+
 extern "C" int protoseg_l2_supported(int C, int P, int K) {
   if (nc_of(C) == 0 || P <= 0 || K < 0 || K > 32) return 0;
-  if (f32_family_fits(C, padded_protos(P))) return 1;
-  return C == 64 && P <= kMaxChunkedP ? 1 : 0;  // bf16 precisions only, over prototype chunks
+  return P <= kMaxChunkedP ? 1 : 0;  // beyond one launch's LDS: prototype chunks (both families)
 }
 
 extern "C" int protoseg_l2_max_protos(int C, int precision) {
   if (nc_of(C) == 0 || precision < PROTOSEG_PREC_BF16X3 || precision > PROTOSEG_PREC_F32) return 0;
-  if (C == 64 && terms_of(precision)) return kMaxChunkedP;
-  int p = 0;
-  while (f32_family_fits(C, p + 32)) p += 32;
-  return p;
+  return kMaxChunkedP;
 }
 
 // PROTOSEG_X_SIGMOID in act_kind: x is the add-on's pre-activation and the kernels apply the
@@ -729,13 +743,28 @@ extern "C" int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, 
       return PROTOSEG_OK;
     }
   }
-  if (!f32_family_fits(C, geo.Pp))
-    return fail(PROTOSEG_ERR_UNSUPPORTED, "C=%d P=%d: served by the bf16 precisions only (prototype chunks)", C, P);
-  return dispatch(x_dtype, C, [&](auto tx, auto nc) {
-    using TX = std::remove_pointer_t<decltype(tx)>;
-    return launch_fwd<TX, decltype(nc)::value>(geo, x, protos, w_last, eps, act_kind, dist_out, act_out,
-                                               logits_out, s);
-  });
+  // f32 family: prototype chunks of at most one launch's LDS (C = 64: 384 rows); distance and
+  // activation rows at (b * P + p0 + p), logits summed over the chunks
+  const int fmax = f32_launch_protos(C);
+  const int nchunk = static_cast<int>(ceil_div(P, fmax)), per = static_cast<int>(ceil_div(P, nchunk));
+  KernelSpan span(nchunk > 1 ? "l2_fwd_kernel" : "", "", s);
+  for (int c = 0; c < nchunk; ++c) {
+    const int p0 = c * per, pc = P - p0 < per ? P - p0 : per;
+    Geometry gc = geo;
+    if (nchunk > 1) {
+      gc = geometry_of(B, C, H, W, pc, K);
+      gc.ldw = gc.ldd = P;
+      gc.p0 = p0;
+    }
+    const int st = dispatch(x_dtype, C, [&](auto tx, auto nc) {
+      using TX = std::remove_pointer_t<decltype(tx)>;
+      return launch_fwd<TX, decltype(nc)::value>(gc, x, protos + static_cast<size_t>(p0) * C,
+                                                 w_last ? w_last + p0 : nullptr, eps, act_kind, dist_out, act_out,
+                                                 logits_out, s, c > 0);
+    });
+    if (st) return st;
+  }
+  return PROTOSEG_OK;
 }
 
 extern "C" size_t protoseg_l2_bwd_workspace_size(int B, int C, int H, int W, int P, int K) {
@@ -848,8 +877,6 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
       return PROTOSEG_OK;
     }
   }
-  if (!f32_family_fits(C, geo.Pp))
-    return fail(PROTOSEG_ERR_UNSUPPORTED, "C=%d P=%d: served by the bf16 precisions only (prototype chunks)", C, P);
   const bool bf16_x = g_x && terms && bf16_bwd_x_fits(geo, terms);
   const bool bf16_pw = (g_protos || g_w) && terms && bf16_bwd_pw_fits(geo, terms);
   ImageBlock img;
@@ -859,11 +886,27 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
     int st;
     if (bf16_x)
       st = launch_bwd_x_bf16(geo, xb, terms, x, img.ptr, eps, act_kind, g_logits, g_dist, g_x, s);
-    else
-      st = dispatch(x_dtype, C, [&](auto tx, auto nc) {
-        using TX = std::remove_pointer_t<decltype(tx)>;
-        return launch_bwd_x<TX, decltype(nc)::value>(geo, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_x, s);
-      });
+    else {  // f32 family: prototype chunks of one launch's LDS, chunk c > 0 adds to g_x
+      const int fmax = f32_launch_protos(C);
+      const int nchunk = static_cast<int>(ceil_div(P, fmax)), per = static_cast<int>(ceil_div(P, nchunk));
+      KernelSpan span(nchunk > 1 ? "l2_bwd_x_kernel" : "", "", s);
+      st = PROTOSEG_OK;
+      for (int c = 0; c < nchunk && !st; ++c) {
+        const int p0 = c * per, pc = P - p0 < per ? P - p0 : per;
+        Geometry gc = geo;
+        if (nchunk > 1) {
+          gc = geometry_of(B, C, H, W, pc, K);
+          gc.ldw = gc.ldd = P;
+          gc.p0 = p0;
+        }
+        st = dispatch(x_dtype, C, [&](auto tx, auto nc) {
+          using TX = std::remove_pointer_t<decltype(tx)>;
+          return launch_bwd_x<TX, decltype(nc)::value>(gc, x, protos + static_cast<size_t>(p0) * C,
+                                                       g_logits ? w_last + p0 : w_last, eps, act_kind, g_logits,
+                                                       g_dist, g_x, s, c > 0);
+        });
+      }
+    }
     if (st) return st;
   }
   if (g_protos || g_w) {

@@ -95,11 +95,11 @@ int protoseg_timing_launches(void);
  *   dist_out   [B, P, H, W]   f32 or NULL   distances (model.py:219, NCHW)
  *   act_out    [B*H*W, P]     f32 or NULL   prototype activations (model.py:273)
  *   logits_out [B, H, W, K]   f32 or NULL   logits NHWC (model.py:278)
- * Supported (protoseg_l2_supported() is authoritative): K <= 32 and
- *   - C = 64, BF16X3 / BF16X6: any P <= 4096; prototypes beyond one launch's LDS images run as
- *     prototype chunks inside the call (forward chunks of <= 384 rows at BF16X3, fewer at BF16X6);
- *   - C in {32, 64, 128}, F32 (and the bf16 requests the bf16 family cannot serve, C != 64):
- *     P padded to 32 must fit the f32 family's LDS (C = 64: P <= 384), no chunking;
+ * Supported (protoseg_l2_supported() is authoritative): K <= 32, P <= 4096 and
+ *   - C = 64, BF16X3 / BF16X6: prototypes beyond one launch's LDS images run as prototype chunks
+ *     inside the call (forward chunks of <= 384 rows at BF16X3, fewer at BF16X6);
+ *   - C in {32, 64, 128}, F32 (and the bf16 requests the bf16 family cannot serve, C != 64): the
+ *     f32 family, over prototype chunks of what one launch's LDS holds (C = 64: 384, C = 128: 224);
  *   - every tensor addressed by the kernels (B*H*W*max(P, C)*4 bytes) below 2^31 bytes.
  */
 int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, int W,
@@ -131,10 +131,10 @@ int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, int W,
 /* 1 if (C, P, K) is inside the compiled kernel family, else 0. */
 int protoseg_l2_supported(int C, int P, int K);
 
-/* Largest P one protoseg_l2_fwd / _bwd call serves at (C, precision): 4096 for the bf16
- * precisions at C = 64 (prototype chunks), otherwise the f32 family's LDS bound (C = 64: 384);
- * 0 when C is outside the family or precision is unknown. Callers holding more prototypes
- * (push's bound-box distances at F32) slice them into calls of at most this many. */
+/* Largest P one protoseg_l2_fwd / _bwd call serves at (C, precision): 4096 (prototype chunks
+ * inside the call, both families); 0 when C is outside the family or precision is unknown.
+ * Callers holding more prototypes (push's bound-box distances) slice them into calls of at most
+ * this many. */
 int protoseg_l2_max_protos(int C, int precision);
 
 /* 1 if protoseg_l2_fwd / _bwd accept PROTOSEG_X_SIGMOID for this shape and precision, else 0. */

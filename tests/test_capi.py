@@ -37,11 +37,11 @@ def test_version_and_supported_shapes():
     assert lib.protoseg_l2_supported(64, 190, 33) == 0    # more than 32 classes
     assert lib.protoseg_l2_supported(64, 570, 19) == 1    # 30 prototypes/class: bf16 prototype chunks
     assert lib.protoseg_l2_supported(64, 5000, 19) == 0   # beyond the chunked bound
-    assert lib.protoseg_l2_supported(128, 1000, 19) == 0  # C = 128 has no chunked family
+    assert lib.protoseg_l2_supported(128, 1000, 19) == 1  # f32 family over prototype chunks
     assert lib.protoseg_l2_max_protos(64, _lib.PREC_BF16X3) == 4096
     assert lib.protoseg_l2_max_protos(64, _lib.PREC_BF16X6) == 4096
-    assert lib.protoseg_l2_max_protos(64, _lib.PREC_F32) == 384   # the f32 family's LDS bound
-    assert 0 < lib.protoseg_l2_max_protos(128, _lib.PREC_BF16X3) < 384
+    assert lib.protoseg_l2_max_protos(64, _lib.PREC_F32) == 4096  # f32 family chunks too
+    assert lib.protoseg_l2_max_protos(128, _lib.PREC_BF16X3) == 4096
     assert lib.protoseg_l2_max_protos(48, _lib.PREC_F32) == 0
     assert lib.protoseg_l2_max_protos(64, 9) == 0
     for C in (32, 64, 128):

@@ -362,7 +362,7 @@ def test_prototype_chunked_backward_with_g_dist(device, precision, with_logits):
 
 
 @pytest.mark.parametrize("activation", ["log", "linear"])
-@pytest.mark.parametrize("precision", ["bf16x3", "bf16x6"])
+@pytest.mark.parametrize("precision", PRECISIONS)
 def test_prototype_chunked_forward_backward_p570(device, precision, activation):
     """30 prototypes/class (P = 570, the DenseNet config's prototype count): the forward runs in
     two prototype chunks (distance / activation rows at b * P + p0 + p, logits summed), the
@@ -387,11 +387,25 @@ def test_prototype_chunked_forward_backward_p570(device, precision, activation):
     assert_scaled_close(gw, ref_gw, 1e-4, "g_w")
 
 
-def test_p570_f32_precision_fails_loudly(device):
-    """The f32 family cannot hold 570 prototypes: the call reports it instead of computing."""
-    x, protos, w_last = po.synthetic_inputs(1, 64, 4, 4, 570, 19, seed=1)
-    with pytest.raises(RuntimeError):
-        run_layer(x, protos, w_last, device=device, precision="f32")
+@pytest.mark.parametrize("C,P,K", [(128, 400, 19), (32, 1200, 5)])
+def test_f32_family_prototype_chunks_other_widths(device, C, P, K):
+    """The f32 family (any C of the family) over prototype chunks: C = 128 stages at most 224
+    prototypes per launch, C = 32 a few hundred; forward and backward against the oracle."""
+    B, h, w = 1, 7, 9
+    x, protos, w_last = po.synthetic_inputs(B, C, h, w, P, K, seed=C + P)
+    gen = torch.Generator().manual_seed(P)
+    g_logits = torch.randn(B, h, w, K, generator=gen)
+    g_dist = torch.randn(B, P, h, w, generator=gen) * 0.1
+    dist, logits, _ = run_layer(x, protos, w_last, device=device, precision="f32")
+    ref_logits, ref_dist, ref_gx, ref_gp, ref_gw = po.forward_backward(x, protos, w_last, g_logits, g_dist)
+    assert_dist_close(dist, ref_dist, x, protos)
+    assert_scaled_close(logits, ref_logits, 1e-4, "logits")
+    ops = _ops()
+    gx, gp, gw = ops.l2_backward(x.to(device), protos.to(device), w_last.to(device), g_logits.to(device),
+                                 g_dist.to(device), 1e-4, 0, prec("f32"), True, True, True)
+    assert_scaled_close(gx, ref_gx, 1e-4, "g_x")
+    assert_scaled_close(gp, ref_gp, 1e-4, "g_protos")
+    assert_scaled_close(gw, ref_gw, 1e-4, "g_w")
 
 
 def test_fp16_features_widen_exactly(device):
