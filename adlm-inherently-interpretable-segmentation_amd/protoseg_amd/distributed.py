@@ -69,15 +69,25 @@ def reduce_push_state(state, group=None) -> None:
         cand = torch.where(mine, state.second, torch.minimum(state.dist, state.second))
         dist.all_reduce(cand, op=dist.ReduceOp.MIN, group=group)
         state.second.copy_(cand)
+    # geometry (H, W, h, w) of each prototype's winning image, for its rf box (push.py:288-307):
+    # the owner rank's row of a [P, 4] tensor, summed over ranks (a plain collective, no pickles)
+    mine_rows = torch.nonzero(mine).flatten().tolist()
+    own_img = state.img.cpu()
+    geo = torch.zeros((mine.shape[0], 4), dtype=torch.int64)
+    for j in mine_rows:
+        geo[j] = torch.tensor(state.geometry[int(own_img[j])], dtype=torch.int64)
+    geo = geo.to(mine.device)
+    dist.all_reduce(geo, op=dist.ReduceOp.SUM, group=group)
     gimg = gkey & 0xFFFFFFFF
     state.dist.copy_((gkey >> 32).to(torch.int32).view(torch.float32))
     state.img.copy_(torch.where(gimg == INT32_MAX, torch.full_like(gimg, -1), gimg))
     state.patch.copy_((patch - 1).to(torch.int32))
     state.fmap.copy_(fmap)
-    gathered: List[dict] = [None] * dist.get_world_size(group)  # type: ignore[list-item]
-    dist.all_gather_object(gathered, state.geometry, group=group)
-    for g in gathered:
-        state.geometry.update(g)
+    won = state.img.cpu().tolist()
+    geo_h = geo.cpu().tolist()
+    for j, im in enumerate(won):
+        if im >= 0:
+            state.geometry[int(im)] = tuple(int(v) for v in geo_h[j])
 
 
 def reduce_bound_boxes(boxes, device="cpu", group=None):

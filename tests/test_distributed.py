@@ -84,7 +84,9 @@ def _worker(rank, world, port, n_img, P, C, result_q):
             if lo <= int(st.img[j]) < hi:
                 boxes[j] = torch.tensor([int(st.img[j]), j, j + 3, 2 * j, 2 * j + 5, j % 4])
         merged = reduce_bound_boxes(boxes.numpy())
-        result_q.put((rank, st.dist, st.img, st.patch, st.fmap, len(st.geometry), grads, len(gb.buckets), merged,
+        # every prototype's winning image has its geometry on every rank (rf boxes)
+        geo_ok = all(st.geometry.get(int(i)) == (8, 8, 2, 2) for i in st.img.tolist() if i >= 0)
+        result_q.put((rank, st.dist, st.img, st.patch, st.fmap, geo_ok, grads, len(gb.buckets), merged,
                       st.second))
     finally:
         dist.destroy_process_group()
@@ -106,7 +108,7 @@ def test_sharded_push_reduction_equals_serial_scan(n_img):
     best, img, patch, fmap, second = _serial_truth(_make_images(n_img, P, C))
     for rank, d, im, pa, fm, ngeo, grads, nbuckets, boxes, sec in results:
         assert sec.tolist() == second  # the sharded runner-up equals the serial one
-        assert ngeo == n_img
+        assert ngeo  # winners' geometry reached every rank
         for j in range(P):  # every rank holds the union of the per-shard bound boxes
             exp = [-1] * 6 if img[j] < 0 else [img[j], j, j + 3, 2 * j, 2 * j + 5, j % 4]
             assert list(boxes[j]) == exp
