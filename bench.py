@@ -357,6 +357,58 @@ def time_kld_step(step: LayerStep, steps: int, warmup: int):
             "kld_backward_gbps": round(n * step.P * 4 / kb / 1e9, 1), "loss": round(loss, 6)}
 
 
+def time_sigmoid_step(step: LayerStep, steps: int, warmup: int):
+    """The add-on's nn.Sigmoid (model.py:124-128) in the training step at the headline shape:
+    (a) fused into the layer kernels' x load (PROTOSEG_X_SIGMOID: the step's input is the
+    pre-activation, the backward returns its gradient), against (b) the unfused step: sigmoid
+    forward, the layer step on sigmoid(X), sigmoid backward (torch's elementwise kernels).
+    Both as one HIP graph per step with the Adam update; returns ms per step of each."""
+    gen = torch.Generator(device="cpu").manual_seed(7)
+    pre = (2.0 * torch.randn(step.x.shape, generator=gen)).to(step.device, step.x.dtype)
+    g_pre = torch.empty_like(pre)
+    sig = torch.empty_like(pre)
+    null = ctypes.c_void_p(None)
+    act_f = _lib.ACT_LOG | _lib.X_SIGMOID
+
+    def common(x, act, gx):
+        _lib.call("protoseg_l2_fwd", _lib.ptr(x), step.xdt, step.B, step.C, step.h, step.w, _lib.ptr(step.protos),
+                  step.P, _lib.ptr(step.w_last), step.K, 1e-4, act, step.prec, _lib.ptr(step.dist), null,
+                  _lib.ptr(step.logits), step._stream())
+        _lib.call("protoseg_l2_bwd", _lib.ptr(x), step.xdt, step.B, step.C, step.h, step.w, _lib.ptr(step.protos),
+                  step.P, _lib.ptr(step.w_last), step.K, 1e-4, act, step.prec, _lib.ptr(step.g_logits), null,
+                  _lib.ptr(gx), _lib.ptr(step.g_p), _lib.ptr(step.g_w), _lib.ptr(step.ws), step.ws_bytes,
+                  step._stream())
+        step.opt_step()
+
+    def fused():
+        common(pre, act_f, g_pre)
+
+    def unfused():
+        torch.sigmoid(pre, out=sig)
+        common(sig, _lib.ACT_LOG, step.g_x)
+        torch.ops.aten.sigmoid_backward(step.g_x, sig, grad_input=g_pre)
+
+    out = {}
+    stream = torch.cuda.Stream(step.device)
+    with torch.cuda.stream(stream):
+        for name, fn in (("fused_on_load", fused), ("separate_sigmoid", unfused)):
+            for _ in range(max(1, warmup)):
+                fn()
+            torch.cuda.synchronize()
+            g = capture(fn, stream)
+            for _ in range(warmup):
+                g.replay()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                g.replay()
+            torch.cuda.synchronize()
+            out[name + "_ms"] = round((time.perf_counter() - t0) / steps * 1e3, 4)
+    out["workload"] = (f"layer training step incl. the add-on sigmoid, P={step.P}: fused into the x load "
+                       f"(PROTOSEG_X_SIGMOID) vs sigmoid fwd/bwd as separate HBM passes")
+    return out
+
+
 def host_cores():
     """CPUs this process may run on (the cpuset / affinity mask; os.cpu_count() is the whole
     machine) and the cgroup CPU quota in cores if one is set (None otherwise)."""
@@ -716,6 +768,10 @@ def main():
         kld = time_kld_step(kstep, max(5, args.steps // 4), 3)
         kld["prototypes"] = kstep.P
 
+    sigmoid = None
+    if world == 1 and args.precision == "bf16x3" and args.channels == 64:
+        sigmoid = time_sigmoid_step(step, max(5, args.steps // 2), 3)
+
     push = None
     if not args.no_push:
         push = time_push(args.push_images, args.push_steps, 1, device)
@@ -761,6 +817,8 @@ def main():
                 "ms_per_step": round(e_side / args.steps * 1e3, 4),
                 "workload": "cityscapes_no_kld_imnet.gin prototype layer training step (10 prototypes/class)",
                 "roofline": roof_s, "kernels": kernels_s}
+        if sigmoid is not None:
+            out["add_on_sigmoid"] = sigmoid
         if kld is not None:
             out["kld_step"] = kld
         if push is not None:
