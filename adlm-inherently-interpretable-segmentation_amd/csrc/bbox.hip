@@ -10,10 +10,15 @@
 //      margin (push.py:328-329, helpers.py:48-82).
 // Here: act_kernel (1), cubic_upsample_kernel (2: one thread per output pixel, OpenCV's
 // separable H-then-V INTER_CUBIC with A = -0.75, half-pixel centres, replicated border, every
-// product and sum rounded separately as the scalar OpenCV code writes them), and
-// bound_box_kernel (3-5: one 1024-thread workgroup per prototype map — an LDS radix select of
-// the two order statistics numpy's 'linear' percentile interpolates between, in numpy's f32
-// arithmetic, then the greedy walk with every row/column probe a workgroup-wide OR).
+// product and sum rounded separately as the scalar OpenCV code writes them), a radix select of
+// the two order statistics numpy's 'linear' percentile interpolates between (3: three passes of
+// select_hist_kernel, each map split over ~2048 / m workgroups, select_step_kernel between them),
+// and bound_box_kernel (3-5: one 1024-thread workgroup per prototype map — the threshold in
+// numpy's f32 arithmetic, then the greedy walk with every row/column probe a workgroup-wide OR).
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "protoseg_device.h"
 #include "protoseg_host.h"
 
@@ -146,99 +151,165 @@ __device__ __forceinline__ float fkey_inv(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
-struct Select {
-  uint32_t key;    // key of the element of the requested rank
-  uint32_t below;  // elements with a smaller key
-  uint32_t equal;  // elements with this key
-};
+// The percentile's order statistic is selected by a three-pass radix select over 11 + 11 + 10
+// key bits, split across many workgroups per map: pass p histograms, in LDS, the key bits
+// (sh, width) of a chunk's elements whose higher bits match the prefix found so far, and adds
+// the non-zero bins into the map's global histogram; a one-workgroup-per-map select then picks
+// the bin holding the wanted rank, extends the prefix and clears the histogram for the next
+// pass. The last pass also takes the smallest key above the 22-bit prefix block (the next order
+// statistic when no larger key shares the prefix), so no extra pass over the map is needed.
+constexpr int kHistThreads = 256;
+constexpr int kSelTarget = 2048;           // histogram workgroups per launch (all maps)
+constexpr int kSelMinChunk = 1 << 15;      // elements per histogram workgroup, at least
+constexpr int kPassShift[3] = {21, 10, 0};
+constexpr int kPassWidth[3] = {11, 11, 10};
 
-// Histogram of the keys matching (prefix, pmask), bin = (key >> sh) & bm. Four float4 loads
-// in flight per thread per iteration; the scalar tail covers n % 4 and unaligned maps.
-__device__ void key_histogram(const float* __restrict__ a, size_t n, uint32_t prefix, uint32_t pmask, int sh,
-                              uint32_t bm, uint32_t* hist) {
+// Per-map select state in the scratch block: {prefix, pmask, rank, below, min_above}.
+constexpr int kSelState = 8;
+
+// numpy 'linear' percentile on f32 (push.py:322): q / 100 in f32, virtual index (n - 1) * q in
+// f32, the two neighbouring ranks and the lerp weight.
+__device__ __forceinline__ void percentile_ranks(size_t n, float percentile, uint32_t& lo, uint32_t& hi, float& g) {
+  const float qq = percentile / 100.0f;
+  const float vidx = fmul(static_cast<float>(n - 1), qq);
+  if (vidx >= static_cast<float>(n - 1)) {
+    lo = hi = static_cast<uint32_t>(n - 1);
+  } else {
+    const float fl = floorf(vidx < 0.f ? 0.f : vidx);
+    lo = static_cast<uint32_t>(fl);
+    hi = lo + 1u;
+  }
+  g = vidx < 0.f ? 0.f : fsub(vidx, floorf(vidx));
+}
+
+// grid (m), 256 threads: clear the map's histogram, seed its select state.
+__global__ __launch_bounds__(256) void select_init_kernel(size_t n, float percentile, uint32_t* __restrict__ hist,
+                                                          uint32_t* __restrict__ state) {
+  uint32_t* h = hist + static_cast<size_t>(blockIdx.x) * kHistBins;
+  for (int i = threadIdx.x; i < kHistBins; i += 256) h[i] = 0u;
+  if (threadIdx.x == 0) {
+    uint32_t lo, hi;
+    float g;
+    percentile_ranks(n, percentile, lo, hi, g);
+    uint32_t* st = state + static_cast<size_t>(blockIdx.x) * kSelState;
+    st[0] = 0u;           // prefix
+    st[1] = 0u;           // pmask
+    st[2] = lo;           // rank still to find inside the prefix
+    st[3] = 0u;           // elements below the prefix
+    st[4] = 0xffffffffu;  // smallest key above the final 22-bit prefix block (pass 3)
+  }
+}
+
+// grid (chunks, m), 256 threads: pass `pass` histogram of one chunk of map blockIdx.y.
+__global__ __launch_bounds__(kHistThreads) void select_hist_kernel(const float* __restrict__ up, size_t n,
+                                                                   size_t chunk, int pass,
+                                                                   uint32_t* __restrict__ hist,
+                                                                   uint32_t* __restrict__ state) {
+  __shared__ uint32_t h[kHistBins];
+  __shared__ uint32_t s_min[kHistThreads / 64];
   const int t = threadIdx.x;
-  const bool aligned = (reinterpret_cast<uintptr_t>(a) & 15u) == 0;
-  size_t n4 = aligned ? n / 4 : 0;
-  const float4* a4 = reinterpret_cast<const float4*>(a);
+  const int map = blockIdx.y;
+  const uint32_t* st = state + static_cast<size_t>(map) * kSelState;
+  const uint32_t prefix = st[0], pmask = st[1];
+  const int sh = kPassShift[pass];
+  const uint32_t bm = (1u << kPassWidth[pass]) - 1u;
+  const uint32_t above = prefix | 0x3ffu;  // pass 3: keys beyond the 22-bit prefix block
+  for (int i = t; i < kHistBins; i += kHistThreads) h[i] = 0u;
+  __syncthreads();
+  const size_t c0 = static_cast<size_t>(blockIdx.x) * chunk;
+  const size_t c1 = c0 + chunk < n ? c0 + chunk : n;
+  const float* a = up + static_cast<size_t>(map) * n + c0;
+  const size_t len = c1 > c0 ? c1 - c0 : 0;
+  uint32_t mn = 0xffffffffu;
   auto put = [&](float f) {
     const uint32_t k = fkey(f);
-    if ((k & pmask) == prefix) atomicAdd(&hist[(k >> sh) & bm], 1u);
+    if ((k & pmask) == prefix) atomicAdd(&h[(k >> sh) & bm], 1u);
+    if (pass == 2 && k > above) mn = k < mn ? k : mn;
   };
+  const bool aligned = (reinterpret_cast<uintptr_t>(a) & 15u) == 0;
+  const size_t n4 = aligned ? len / 4 : 0;
+  const float4* a4 = reinterpret_cast<const float4*>(a);
   size_t i = t;
-  for (; i + 3 * kBoxThreads < n4; i += 4 * kBoxThreads) {
+  for (; i + 3 * kHistThreads < n4; i += 4 * kHistThreads) {  // four float4 loads in flight
     float4 v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = a4[i + u * kBoxThreads];
+    for (int u = 0; u < 4; ++u) v[u] = a4[i + u * kHistThreads];
 #pragma unroll
     for (int u = 0; u < 4; ++u) { put(v[u].x); put(v[u].y); put(v[u].z); put(v[u].w); }
   }
-  for (; i < n4; i += kBoxThreads) {
+  for (; i < n4; i += kHistThreads) {
     const float4 v = a4[i];
     put(v.x); put(v.y); put(v.z); put(v.w);
   }
-  for (size_t j = n4 * 4 + t; j < n; j += kBoxThreads) put(a[j]);
+  for (size_t j = n4 * 4 + t; j < len; j += kHistThreads) put(a[j]);
+  if (pass == 2) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const uint32_t v = __shfl_xor(mn, o);
+      mn = v < mn ? v : mn;
+    }
+    if ((t & 63) == 0) s_min[t >> 6] = mn;
+  }
+  __syncthreads();
+  uint32_t* gh = hist + static_cast<size_t>(map) * kHistBins;
+  for (int b = t; b <= static_cast<int>(bm); b += kHistThreads)
+    if (h[b]) atomicAdd(&gh[b], h[b]);
+  if (pass == 2 && t == 0) {
+    uint32_t m = s_min[0];
+    for (int w = 1; w < kHistThreads / 64; ++w) m = s_min[w] < m ? s_min[w] : m;
+    if (m != 0xffffffffu) atomicMin(&state[static_cast<size_t>(map) * kSelState + 4], m);
+  }
 }
 
-// Key of the element of rank `rank` (0-based, ascending) of a[0..n): three LDS histogram passes
-// over 11 + 11 + 10 key bits; bins scanned by the whole workgroup (2 bins per thread).
-__device__ Select block_select(const float* __restrict__ a, size_t n, uint32_t rank, uint32_t* hist,
-                               uint32_t* scan, uint32_t* bcast) {
+// Whole-workgroup (1024 threads, 2 bins each) search of a map's global histogram for the bin
+// holding `rank`: returns (bin, elements in lower bins, elements in the bin).
+struct BinPick {
+  uint32_t bin, excl, count;
+};
+__device__ BinPick pick_bin(const uint32_t* __restrict__ gh, uint32_t rank, uint32_t* scan, uint32_t* bcast) {
   const int t = threadIdx.x;
-  uint32_t prefix = 0, pmask = 0, below = 0, equal = 0;
-  const int shifts[3] = {21, 10, 0};
-  const int widths[3] = {11, 11, 10};
-  for (int pass = 0; pass < 3; ++pass) {
-    const int sh = shifts[pass];
-    const uint32_t bm = (1u << widths[pass]) - 1u;
-    for (int i = t; i < kHistBins; i += kBoxThreads) hist[i] = 0u;
+  const uint32_t h0 = gh[2 * t], h1 = gh[2 * t + 1];
+  const uint32_t s = h0 + h1;
+  scan[t] = s;
+  __syncthreads();
+  for (int off = 1; off < kBoxThreads; off <<= 1) {
+    const uint32_t v = t >= off ? scan[t - off] : 0u;
     __syncthreads();
-    key_histogram(a, n, prefix, pmask, sh, bm, hist);
-    __syncthreads();
-    const uint32_t h0 = hist[2 * t], h1 = hist[2 * t + 1];
-    const uint32_t s = h0 + h1;
-    scan[t] = s;
-    __syncthreads();
-    for (int off = 1; off < kBoxThreads; off <<= 1) {
-      const uint32_t v = t >= off ? scan[t - off] : 0u;
-      __syncthreads();
-      scan[t] += v;
-      __syncthreads();
-    }
-    const uint32_t incl = scan[t], excl = incl - s;
-    if (excl <= rank && rank < incl) {
-      const uint32_t r = rank - excl;
-      if (r < h0) {
-        bcast[0] = 2u * t; bcast[1] = excl; bcast[2] = h0;
-      } else {
-        bcast[0] = 2u * t + 1u; bcast[1] = excl + h0; bcast[2] = h1;
-      }
-    }
-    __syncthreads();
-    const uint32_t b = bcast[0];
-    below += bcast[1];
-    rank -= bcast[1];
-    equal = bcast[2];
-    prefix |= b << sh;
-    pmask |= bm << sh;
+    scan[t] += v;
     __syncthreads();
   }
-  return {prefix, below, equal};
+  const uint32_t incl = scan[t], excl = incl - s;
+  if (excl <= rank && rank < incl) {
+    const uint32_t r = rank - excl;
+    if (r < h0) {
+      bcast[0] = 2u * t; bcast[1] = excl; bcast[2] = h0;
+    } else {
+      bcast[0] = 2u * t + 1u; bcast[1] = excl + h0; bcast[2] = h1;
+    }
+  }
+  __syncthreads();
+  const BinPick p{bcast[0], bcast[1], bcast[2]};
+  __syncthreads();
+  return p;
 }
 
-// Smallest key strictly above `key` (the next order statistic when `key` is unique).
-__device__ uint32_t block_min_above(const float* __restrict__ a, size_t n, uint32_t key, uint32_t* bcast) {
-  uint32_t m = 0xffffffffu;
-  for (size_t i = threadIdx.x; i < n; i += kBoxThreads) {
-    const uint32_t k = fkey(a[i]);
-    if (k > key && k < m) m = k;
+// grid (m), 1024 threads: after pass `pass` (0 or 1), extend the prefix and clear the histogram.
+__global__ __launch_bounds__(kBoxThreads) void select_step_kernel(int pass, uint32_t* __restrict__ hist,
+                                                                  uint32_t* __restrict__ state) {
+  __shared__ uint32_t scan[kBoxThreads];
+  __shared__ uint32_t bcast[4];
+  uint32_t* gh = hist + static_cast<size_t>(blockIdx.x) * kHistBins;
+  uint32_t* st = state + static_cast<size_t>(blockIdx.x) * kSelState;
+  const BinPick p = pick_bin(gh, st[2], scan, bcast);  // all reads of gh are behind pick_bin's barriers
+  gh[2 * threadIdx.x] = 0u;
+  gh[2 * threadIdx.x + 1] = 0u;
+  if (threadIdx.x == 0) {
+    const int sh = kPassShift[pass];
+    st[0] |= p.bin << sh;
+    st[1] |= ((1u << kPassWidth[pass]) - 1u) << sh;
+    st[2] -= p.excl;
+    st[3] += p.excl;
   }
-  if (threadIdx.x == 0) bcast[3] = 0xffffffffu;
-  __syncthreads();
-  atomicMin(&bcast[3], m);
-  __syncthreads();
-  const uint32_t r = bcast[3];
-  __syncthreads();
-  return r;
 }
 
 template <typename TL>
@@ -249,18 +320,18 @@ __device__ __forceinline__ long long label_value(const TL* L, size_t i, const in
   return lut[raw];
 }
 
-// grid (m), 1024 threads. rf [m, 4] = (start_h, end_h, start_w, end_w) of push.py:288-294;
-// box [m, 4] = (start_h, end_h + 1, start_w, end_w + 1) of helpers.py:82; -1 rows for maps whose
-// label index or rf box is out of range.
+// grid (m), 1024 threads, after the three select passes. rf [m, 4] = (start_h, end_h, start_w,
+// end_w) of push.py:288-294; box [m, 4] = (start_h, end_h + 1, start_w, end_w + 1) of
+// helpers.py:82; -1 rows for maps whose label index or rf box is out of range.
 template <typename TL>
 __global__ __launch_bounds__(kBoxThreads) void bound_box_kernel(
     const float* __restrict__ up, int H, int W, const TL* __restrict__ label, int n_label, const int32_t* label_index,
     const int32_t* __restrict__ lut, int lut_size, const int32_t* __restrict__ target_class,
-    const int32_t* __restrict__ rf, float percentile, int margin, float* __restrict__ thr_out,
-    int32_t* __restrict__ box_out) {
-  __shared__ uint32_t hist[kHistBins];
+    const int32_t* __restrict__ rf, float percentile, int margin, const uint32_t* __restrict__ hist,
+    const uint32_t* __restrict__ state, float* __restrict__ thr_out, int32_t* __restrict__ box_out) {
   __shared__ uint32_t scan[kBoxThreads];
   __shared__ uint32_t bcast[4];
+  __shared__ uint32_t s_next;
   const int map = blockIdx.x;
   const size_t n = static_cast<size_t>(H) * W;
   const float* U = up + static_cast<size_t>(map) * n;
@@ -275,21 +346,29 @@ __global__ __launch_bounds__(kBoxThreads) void bound_box_kernel(
   // push.py:322 np.percentile(upsampled, q): numpy 'linear' on f32 — q / 100 in f32,
   // virtual index (n - 1) * q in f32, lerp between the two neighbouring order statistics with
   // numpy's _lerp (a + (b - a) * g, or b - (b - a) * (1 - g) when g >= 0.5), all f32.
-  const float qq = percentile / 100.0f;
-  const float vidx = fmul(static_cast<float>(n - 1), qq);
   uint32_t lo, hi;
-  if (vidx >= static_cast<float>(n - 1)) {
-    lo = hi = static_cast<uint32_t>(n - 1);
-  } else {
-    const float fl = floorf(vidx < 0.f ? 0.f : vidx);
-    lo = static_cast<uint32_t>(fl);
-    hi = lo + 1u;
+  float g;
+  percentile_ranks(n, percentile, lo, hi, g);
+  // The last pass's bin: the full key of rank lo, the elements below it and equal to it.
+  const uint32_t* gh = hist + static_cast<size_t>(map) * kHistBins;
+  const uint32_t* st = state + static_cast<size_t>(map) * kSelState;
+  const uint32_t prefix = st[0], rank = st[2], below0 = st[3], min_above = st[4];
+  if (threadIdx.x == 0) s_next = 0xffffffffu;
+  const BinPick p = pick_bin(gh, rank, scan, bcast);
+  const uint32_t key = prefix | p.bin;
+  uint32_t key_hi = key;
+  if (hi != lo && hi >= below0 + p.excl + p.count) {
+    // the next order statistic: the next non-empty bin of the same 22-bit prefix, else the
+    // smallest key above the prefix block
+    const uint32_t b0 = 2u * threadIdx.x, b1 = b0 + 1u;
+    uint32_t nb = 0xffffffffu;
+    if (b1 > p.bin && gh[b1]) nb = b1;
+    if (b0 > p.bin && gh[b0]) nb = b0;
+    if (nb != 0xffffffffu) atomicMin(&s_next, nb);
+    __syncthreads();
+    key_hi = s_next != 0xffffffffu ? (prefix | s_next) : min_above;
   }
-  const float g = vidx < 0.f ? 0.f : fsub(vidx, floorf(vidx));
-  const Select s = block_select(U, n, lo, hist, scan, bcast);
-  uint32_t key_hi = s.key;
-  if (hi != lo && hi >= s.below + s.equal) key_hi = block_min_above(U, n, s.key, bcast);
-  const float A = fkey_inv(s.key), B = fkey_inv(key_hi);
+  const float A = fkey_inv(key), B = fkey_inv(key_hi);
   const float diff = fsub(B, A);
   const float thr = g >= 0.5f ? fsub(B, fmul(diff, fsub(1.0f, g))) : fadd(A, fmul(diff, g));
 
@@ -334,6 +413,39 @@ __global__ __launch_bounds__(kBoxThreads) void bound_box_kernel(
     box_out[4 * map + 2] = sw;
     box_out[4 * map + 3] = ew + 1;
   }
+}
+
+// Select histograms and state ([m][2048] u32 | [m][8] u32): one grow-only block per (device,
+// stream), reused by later calls on that stream (kernels on one stream are ordered), so a call is
+// only kernel launches and can be captured in a HIP graph once the block exists.
+void* select_scratch(size_t need, hipStream_t s, int* status) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> blocks;
+  int dev = 0;
+  *status = PROTOSEG_OK;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    *status = check_launch("hipGetDevice");
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lock(mu);
+  auto& b = blocks[{dev, s}];
+  if (b.second < need) {
+    if (b.first && (hipStreamSynchronize(s) != hipSuccess || hipFree(b.first) != hipSuccess)) {
+      *status = check_launch("bound-box scratch regrow");
+      return nullptr;
+    }
+    b = {nullptr, 0};
+    const size_t bytes = need < (1u << 20) ? (1u << 20) : need;
+    const hipError_t e = hipMalloc(&b.first, bytes);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      b = {nullptr, 0};
+      *status = fail(PROTOSEG_ERR_HIP, "hipMalloc (bound-box scratch, %zu B): %s", bytes, hipGetErrorString(e));
+      return nullptr;
+    }
+    b.second = bytes;
+  }
+  return b.first;
 }
 
 }  // namespace
@@ -381,24 +493,49 @@ extern "C" int protoseg_bound_boxes(const float* up, int m, int H, int W, const 
   if (margin < 0) return fail(PROTOSEG_ERR_INVALID, "margin must be >= 0");
   if (lut && lut_size <= 0) return fail(PROTOSEG_ERR_INVALID, "lut_size must be > 0");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (label_dtype != PROTOSEG_I64 && label_dtype != PROTOSEG_I32 && label_dtype != PROTOSEG_U8)
+    return fail(PROTOSEG_ERR_UNSUPPORTED, "label_dtype %d", label_dtype);
+  if (m > 65535) return fail(PROTOSEG_ERR_UNSUPPORTED, "m=%d maps per call", m);
+  const size_t n = static_cast<size_t>(H) * W;
+  const size_t hist_bytes = static_cast<size_t>(m) * kHistBins * sizeof(uint32_t);
+  int st = PROTOSEG_OK;
+  void* scratch = select_scratch(hist_bytes + static_cast<size_t>(m) * kSelState * sizeof(uint32_t), s, &st);
+  if (!scratch) return st;
+  uint32_t* hist = static_cast<uint32_t*>(scratch);
+  uint32_t* state = hist + static_cast<size_t>(m) * kHistBins;
+  // chunks per map: about kSelTarget histogram workgroups in all, each >= kSelMinChunk elements
+  size_t chunks = ceil_div(static_cast<size_t>(kSelTarget), static_cast<size_t>(m));
+  const size_t max_chunks = ceil_div(n, static_cast<size_t>(kSelMinChunk));
+  chunks = chunks > max_chunks ? max_chunks : chunks;
+  chunks = chunks < 1 ? 1 : chunks;
+  const size_t chunk = ceil_div(ceil_div(n, chunks), static_cast<size_t>(4)) * 4;  // float4-aligned chunk starts
+  chunks = ceil_div(n, chunk);
+  hipLaunchKernelGGL(select_init_kernel, dim3(m), dim3(256), 0, s, n, percentile, hist, state);
+  if (int e = check_launch("select_init_kernel")) return e;
+  for (int pass = 0; pass < 3; ++pass) {
+    hipLaunchKernelGGL(select_hist_kernel, dim3(static_cast<unsigned>(chunks), m), dim3(kHistThreads), 0, s, up, n,
+                       chunk, pass, hist, state);
+    if (int e = check_launch("select_hist_kernel")) return e;
+    if (pass == 2) break;
+    hipLaunchKernelGGL(select_step_kernel, dim3(m), dim3(kBoxThreads), 0, s, pass, hist, state);
+    if (int e = check_launch("select_step_kernel")) return e;
+  }
   switch (label_dtype) {
     case PROTOSEG_I64:
       hipLaunchKernelGGL(bound_box_kernel<int64_t>, dim3(m), dim3(kBoxThreads), 0, s, up, H, W,
                          static_cast<const int64_t*>(label), n_label, label_index, lut, lut_size, target_class, rf_box,
-                         percentile, margin, threshold, box);
+                         percentile, margin, hist, state, threshold, box);
       break;
     case PROTOSEG_I32:
       hipLaunchKernelGGL(bound_box_kernel<int32_t>, dim3(m), dim3(kBoxThreads), 0, s, up, H, W,
                          static_cast<const int32_t*>(label), n_label, label_index, lut, lut_size, target_class, rf_box,
-                         percentile, margin, threshold, box);
-      break;
-    case PROTOSEG_U8:
-      hipLaunchKernelGGL(bound_box_kernel<uint8_t>, dim3(m), dim3(kBoxThreads), 0, s, up, H, W,
-                         static_cast<const uint8_t*>(label), n_label, label_index, lut, lut_size, target_class, rf_box,
-                         percentile, margin, threshold, box);
+                         percentile, margin, hist, state, threshold, box);
       break;
     default:
-      return fail(PROTOSEG_ERR_UNSUPPORTED, "label_dtype %d", label_dtype);
+      hipLaunchKernelGGL(bound_box_kernel<uint8_t>, dim3(m), dim3(kBoxThreads), 0, s, up, H, W,
+                         static_cast<const uint8_t*>(label), n_label, label_index, lut, lut_size, target_class, rf_box,
+                         percentile, margin, hist, state, threshold, box);
+      break;
   }
   return check_launch("bound_box_kernel");
 }
