@@ -152,19 +152,24 @@ __device__ __forceinline__ float fkey_inv(uint32_t k) {
 }
 
 // The percentile's order statistic is selected by a three-pass radix select over 11 + 11 + 10
-// key bits, split across many workgroups per map: pass p histograms, in LDS, the key bits
-// (sh, width) of a chunk's elements whose higher bits match the prefix found so far, and adds
-// the non-zero bins into the map's global histogram; a one-workgroup-per-map select then picks
-// the bin holding the wanted rank, extends the prefix and clears the histogram for the next
-// pass. The last pass also takes the smallest key above the 22-bit prefix block (the next order
-// statistic when no larger key shares the prefix), so no extra pass over the map is needed.
+// key bits, split across many workgroups per map: pass p histograms, in LDS (one sub-histogram
+// per wave, so equal keys of different waves do not serialise on one LDS bin), the key bits
+// (sh, width) of a chunk's elements whose higher bits match the prefix found so far, and adds the
+// non-zero bins into the map's global histogram; a one-workgroup-per-map select then picks the
+// bin holding the wanted rank, extends the prefix and clears the histogram for the next pass.
+// Pass 2 also copies the elements of the chosen 11-bit bin into a per-map candidate list when
+// they fit (`cap` per map), so pass 3 reads only those instead of the whole map. The smallest
+// key above the final 22-bit prefix block (the next order statistic when no larger key shares
+// the prefix) is taken on the way: above the 11-bit block in pass 2, inside it in pass 3.
 constexpr int kHistThreads = 256;
+constexpr int kHistWaves = kHistThreads / 64;
 constexpr int kSelTarget = 2048;           // histogram workgroups per launch (all maps)
 constexpr int kSelMinChunk = 1 << 15;      // elements per histogram workgroup, at least
 constexpr int kPassShift[3] = {21, 10, 0};
 constexpr int kPassWidth[3] = {11, 11, 10};
 
-// Per-map select state in the scratch block: {prefix, pmask, rank, below, min_above}.
+// Per-map select state in the scratch block: {prefix, pmask, rank, below, min_above, -,
+// candidates written, candidate list in use}.
 constexpr int kSelState = 8;
 
 // numpy 'linear' percentile on f32 (push.py:322): q / 100 in f32, virtual index (n - 1) * q in
@@ -187,77 +192,149 @@ __global__ __launch_bounds__(256) void select_init_kernel(size_t n, float percen
                                                           uint32_t* __restrict__ state) {
   uint32_t* h = hist + static_cast<size_t>(blockIdx.x) * kHistBins;
   for (int i = threadIdx.x; i < kHistBins; i += 256) h[i] = 0u;
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < kSelState) {
     uint32_t lo, hi;
     float g;
     percentile_ranks(n, percentile, lo, hi, g);
-    uint32_t* st = state + static_cast<size_t>(blockIdx.x) * kSelState;
-    st[0] = 0u;           // prefix
-    st[1] = 0u;           // pmask
-    st[2] = lo;           // rank still to find inside the prefix
-    st[3] = 0u;           // elements below the prefix
-    st[4] = 0xffffffffu;  // smallest key above the final 22-bit prefix block (pass 3)
+    // prefix, pmask, rank still to find inside the prefix, elements below the prefix, smallest
+    // key above the final prefix block, -, candidates written, candidate list in use
+    const uint32_t init[kSelState] = {0u, 0u, lo, 0u, 0xffffffffu, 0u, 0u, 0u};
+    state[static_cast<size_t>(blockIdx.x) * kSelState + threadIdx.x] = init[threadIdx.x];
   }
 }
 
-// grid (chunks, m), 256 threads: pass `pass` histogram of one chunk of map blockIdx.y.
+// grid (chunks, m), 256 threads: pass PASS histogram of one chunk of map blockIdx.y (of its
+// candidate list in pass 3 when pass 2 filled one).
+template <int PASS>
 __global__ __launch_bounds__(kHistThreads) void select_hist_kernel(const float* __restrict__ up, size_t n,
-                                                                   size_t chunk, int pass,
-                                                                   uint32_t* __restrict__ hist,
+                                                                   size_t chunk, float* __restrict__ cand,
+                                                                   size_t cap, uint32_t* __restrict__ hist,
+                                                                   uint32_t* __restrict__ chunk_hist,
                                                                    uint32_t* __restrict__ state) {
-  __shared__ uint32_t h[kHistBins];
-  __shared__ uint32_t s_min[kHistThreads / 64];
-  const int t = threadIdx.x;
+  // one sub-histogram per wave in pass 1 (every element lands in it); passes 2 and 3 add only
+  // the few elements inside the prefix and keep the small footprint (more workgroups per CU)
+  constexpr int kSub = PASS == 0 ? kHistWaves : 1;
+  __shared__ uint32_t h[kSub][kHistBins];
+  __shared__ uint32_t s_min[kHistWaves];
+  __shared__ uint32_t s_fill;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int map = blockIdx.y;
-  const uint32_t* st = state + static_cast<size_t>(map) * kSelState;
+  uint32_t* st = state + static_cast<size_t>(map) * kSelState;
   const uint32_t prefix = st[0], pmask = st[1];
-  const int sh = kPassShift[pass];
-  const uint32_t bm = (1u << kPassWidth[pass]) - 1u;
-  const uint32_t above = prefix | 0x3ffu;  // pass 3: keys beyond the 22-bit prefix block
-  for (int i = t; i < kHistBins; i += kHistThreads) h[i] = 0u;
-  __syncthreads();
+  const bool use_cand = PASS == 2 && st[7] != 0u;
+  const bool fill_cand = PASS == 1 && st[7] != 0u;
+  const float* src = use_cand ? cand + static_cast<size_t>(map) * cap : up + static_cast<size_t>(map) * n;
+  const size_t total = use_cand ? st[6] : n;
   const size_t c0 = static_cast<size_t>(blockIdx.x) * chunk;
-  const size_t c1 = c0 + chunk < n ? c0 + chunk : n;
-  const float* a = up + static_cast<size_t>(map) * n + c0;
-  const size_t len = c1 > c0 ? c1 - c0 : 0;
+  if (c0 >= total) return;  // uniform (pass 3 on a short candidate list)
+  const size_t len = (c0 + chunk < total ? c0 + chunk : total) - c0;
+  const float* a = src + c0;
+  float* cdst = cand + static_cast<size_t>(map) * cap;
+  constexpr int sh = kPassShift[PASS];
+  constexpr uint32_t bm = (1u << kPassWidth[PASS]) - 1u;
+  // keys above the current prefix block: above the 11-bit block (pass 2), the 22-bit one (pass 3)
+  const uint32_t above = prefix | (PASS == 1 ? 0x1fffffu : 0x3ffu);
+  for (int i = t; i < kSub * kHistBins; i += kHistThreads) (&h[0][0])[i] = 0u;
+  uint32_t* crow = chunk_hist + (static_cast<size_t>(map) * gridDim.x) * kHistBins;  // pass 1's per-chunk rows
+  if (fill_cand && t == 0) {
+    // this chunk's slots in the candidate list: after the earlier chunks' elements of the bin
+    // (pass 1's per-chunk histogram rows)
+    const uint32_t b0 = prefix >> 21;
+    uint32_t base = 0u;
+    for (unsigned c = 0; c < blockIdx.x; ++c) base += crow[static_cast<size_t>(c) * kHistBins + b0];
+    s_fill = base;
+  }
+  __syncthreads();
   uint32_t mn = 0xffffffffu;
-  auto put = [&](float f) {
-    const uint32_t k = fkey(f);
-    if ((k & pmask) == prefix) atomicAdd(&h[(k >> sh) & bm], 1u);
-    if (pass == 2 && k > above) mn = k < mn ? k : mn;
+  uint32_t* hw = h[PASS == 0 ? wave : 0];
+  // Up to 16 values of this lane (bit u of `valid`): histogram, running min, candidate copy.
+  // Called with wave-uniform control flow (the copy's wave scan needs every lane).
+  auto process = [&](const float* v, int nv, uint32_t valid) {
+    uint32_t match = 0u;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (u >= nv) break;
+      const uint32_t k = fkey(v[u]);
+      const bool ok = (valid >> u) & 1u;
+      if (ok && (k & pmask) == prefix) {
+        atomicAdd(&hw[(k >> sh) & bm], 1u);
+        match |= 1u << u;
+      }
+      if (PASS > 0 && ok && k > above) mn = k < mn ? k : mn;
+    }
+    if (PASS == 1 && fill_cand) {
+      // wave-wide slots, value-major: value u's matches of all lanes are one contiguous run
+      // (ballot + mbcnt), so every store instruction writes consecutive addresses
+      unsigned long long bal[16];
+      uint32_t wtot = 0u;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        if (u >= nv) break;
+        bal[u] = __ballot((match >> u) & 1u);
+        wtot += __popcll(bal[u]);
+      }
+      if (wtot) {  // uniform
+        uint32_t base = 0u;
+        if (lane == 0) base = atomicAdd(&s_fill, wtot);
+        base = __shfl(base, 0);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          if (u >= nv) break;
+          if ((match >> u) & 1u) {
+            const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(bal[u] >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bal[u]), 0u));
+            if (pos < cap) cdst[pos] = v[u];
+          }
+          base += __popcll(bal[u]);
+        }
+      }
+    }
   };
   const bool aligned = (reinterpret_cast<uintptr_t>(a) & 15u) == 0;
   const size_t n4 = aligned ? len / 4 : 0;
   const float4* a4 = reinterpret_cast<const float4*>(a);
-  size_t i = t;
-  for (; i + 3 * kHistThreads < n4; i += 4 * kHistThreads) {  // four float4 loads in flight
-    float4 v[4];
+  size_t i0 = 0;
+  for (; i0 + 4 * kHistThreads <= n4; i0 += 4 * kHistThreads) {  // four float4 loads in flight
+    float v[16];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = a4[i + u * kHistThreads];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) { put(v[u].x); put(v[u].y); put(v[u].z); put(v[u].w); }
+    for (int u = 0; u < 4; ++u) {
+      const float4 q = a4[i0 + u * kHistThreads + t];
+      v[4 * u] = q.x; v[4 * u + 1] = q.y; v[4 * u + 2] = q.z; v[4 * u + 3] = q.w;
+    }
+    process(v, 16, 0xffffu);
   }
-  for (; i < n4; i += kHistThreads) {
-    const float4 v = a4[i];
-    put(v.x); put(v.y); put(v.z); put(v.w);
+  for (; i0 < n4; i0 += kHistThreads) {
+    const bool ok = i0 + t < n4;
+    const float4 q = ok ? a4[i0 + t] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float v[4] = {q.x, q.y, q.z, q.w};
+    process(v, 4, ok ? 0xfu : 0u);
   }
-  for (size_t j = n4 * 4 + t; j < len; j += kHistThreads) put(a[j]);
-  if (pass == 2) {
+  for (size_t j0 = n4 * 4; j0 < len; j0 += kHistThreads) {
+    const bool ok = j0 + t < len;
+    const float v[1] = {ok ? a[j0 + t] : 0.f};
+    process(v, 1, ok ? 1u : 0u);
+  }
+  if (PASS > 0) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
-      const uint32_t v = __shfl_xor(mn, o);
-      mn = v < mn ? v : mn;
+      const uint32_t y = __shfl_xor(mn, o);
+      mn = y < mn ? y : mn;
     }
-    if ((t & 63) == 0) s_min[t >> 6] = mn;
+    if (lane == 0) s_min[wave] = mn;
   }
   __syncthreads();
   uint32_t* gh = hist + static_cast<size_t>(map) * kHistBins;
-  for (int b = t; b <= static_cast<int>(bm); b += kHistThreads)
-    if (h[b]) atomicAdd(&gh[b], h[b]);
-  if (pass == 2 && t == 0) {
+  for (int b = t; b <= static_cast<int>(bm); b += kHistThreads) {
+    uint32_t c = 0u;
+#pragma unroll
+    for (int w = 0; w < kSub; ++w) c += h[w][b];
+    if (c) atomicAdd(&gh[b], c);
+    if (PASS == 0) crow[static_cast<size_t>(blockIdx.x) * kHistBins + b] = c;
+  }
+  if (PASS > 0 && t == 0) {
     uint32_t m = s_min[0];
-    for (int w = 1; w < kHistThreads / 64; ++w) m = s_min[w] < m ? s_min[w] : m;
-    if (m != 0xffffffffu) atomicMin(&state[static_cast<size_t>(map) * kSelState + 4], m);
+    for (int w = 1; w < kHistWaves; ++w) m = s_min[w] < m ? s_min[w] : m;
+    if (m != 0xffffffffu) atomicMin(&st[4], m);
   }
 }
 
@@ -293,8 +370,9 @@ __device__ BinPick pick_bin(const uint32_t* __restrict__ gh, uint32_t rank, uint
   return p;
 }
 
-// grid (m), 1024 threads: after pass `pass` (0 or 1), extend the prefix and clear the histogram.
-__global__ __launch_bounds__(kBoxThreads) void select_step_kernel(int pass, uint32_t* __restrict__ hist,
+// grid (m), 1024 threads: after pass `pass` (0 or 1), extend the prefix and clear the histogram;
+// after pass 1, turn the candidate list on when the chosen bin's elements fit in it.
+__global__ __launch_bounds__(kBoxThreads) void select_step_kernel(int pass, size_t cap, uint32_t* __restrict__ hist,
                                                                   uint32_t* __restrict__ state) {
   __shared__ uint32_t scan[kBoxThreads];
   __shared__ uint32_t bcast[4];
@@ -309,6 +387,10 @@ __global__ __launch_bounds__(kBoxThreads) void select_step_kernel(int pass, uint
     st[1] |= ((1u << kPassWidth[pass]) - 1u) << sh;
     st[2] -= p.excl;
     st[3] += p.excl;
+    if (pass == 0) {  // pass 2 copies the bin's elements out when they fit
+      st[6] = p.count;
+      st[7] = p.count <= cap ? 1u : 0u;
+    }
   }
 }
 
@@ -498,11 +580,10 @@ extern "C" int protoseg_bound_boxes(const float* up, int m, int H, int W, const 
   if (m > 65535) return fail(PROTOSEG_ERR_UNSUPPORTED, "m=%d maps per call", m);
   const size_t n = static_cast<size_t>(H) * W;
   const size_t hist_bytes = static_cast<size_t>(m) * kHistBins * sizeof(uint32_t);
+  const size_t state_bytes = static_cast<size_t>(m) * kSelState * sizeof(uint32_t);
+  // candidate list: up to 1/8 of each map (the chosen 11-bit bin is a quarter-octave of values)
+  const size_t cap = ceil_div(ceil_div(n, static_cast<size_t>(8)), static_cast<size_t>(4)) * 4;  // 16-B aligned lists
   int st = PROTOSEG_OK;
-  void* scratch = select_scratch(hist_bytes + static_cast<size_t>(m) * kSelState * sizeof(uint32_t), s, &st);
-  if (!scratch) return st;
-  uint32_t* hist = static_cast<uint32_t*>(scratch);
-  uint32_t* state = hist + static_cast<size_t>(m) * kHistBins;
   // chunks per map: about kSelTarget histogram workgroups in all, each >= kSelMinChunk elements
   size_t chunks = ceil_div(static_cast<size_t>(kSelTarget), static_cast<size_t>(m));
   const size_t max_chunks = ceil_div(n, static_cast<size_t>(kSelMinChunk));
@@ -510,16 +591,27 @@ extern "C" int protoseg_bound_boxes(const float* up, int m, int H, int W, const 
   chunks = chunks < 1 ? 1 : chunks;
   const size_t chunk = ceil_div(ceil_div(n, chunks), static_cast<size_t>(4)) * 4;  // float4-aligned chunk starts
   chunks = ceil_div(n, chunk);
+  const size_t cand_bytes = static_cast<size_t>(m) * cap * sizeof(float);
+  const size_t rows_bytes = static_cast<size_t>(m) * chunks * kHistBins * sizeof(uint32_t);
+  void* scratch = select_scratch(hist_bytes + state_bytes + cand_bytes + rows_bytes, s, &st);
+  if (!scratch) return st;
+  uint32_t* hist = static_cast<uint32_t*>(scratch);
+  uint32_t* state = hist + static_cast<size_t>(m) * kHistBins;
+  float* cand = reinterpret_cast<float*>(state + static_cast<size_t>(m) * kSelState);
+  uint32_t* rows = reinterpret_cast<uint32_t*>(cand + static_cast<size_t>(m) * cap);
+  const dim3 hgrid(static_cast<unsigned>(chunks), m);
   hipLaunchKernelGGL(select_init_kernel, dim3(m), dim3(256), 0, s, n, percentile, hist, state);
   if (int e = check_launch("select_init_kernel")) return e;
-  for (int pass = 0; pass < 3; ++pass) {
-    hipLaunchKernelGGL(select_hist_kernel, dim3(static_cast<unsigned>(chunks), m), dim3(kHistThreads), 0, s, up, n,
-                       chunk, pass, hist, state);
-    if (int e = check_launch("select_hist_kernel")) return e;
-    if (pass == 2) break;
-    hipLaunchKernelGGL(select_step_kernel, dim3(m), dim3(kBoxThreads), 0, s, pass, hist, state);
-    if (int e = check_launch("select_step_kernel")) return e;
-  }
+  hipLaunchKernelGGL(select_hist_kernel<0>, hgrid, dim3(kHistThreads), 0, s, up, n, chunk, cand, cap, hist, rows, state);
+  if (int e = check_launch("select_hist_kernel<0>")) return e;
+  hipLaunchKernelGGL(select_step_kernel, dim3(m), dim3(kBoxThreads), 0, s, 0, cap, hist, state);
+  if (int e = check_launch("select_step_kernel")) return e;
+  hipLaunchKernelGGL(select_hist_kernel<1>, hgrid, dim3(kHistThreads), 0, s, up, n, chunk, cand, cap, hist, rows, state);
+  if (int e = check_launch("select_hist_kernel<1>")) return e;
+  hipLaunchKernelGGL(select_step_kernel, dim3(m), dim3(kBoxThreads), 0, s, 1, cap, hist, state);
+  if (int e = check_launch("select_step_kernel")) return e;
+  hipLaunchKernelGGL(select_hist_kernel<2>, hgrid, dim3(kHistThreads), 0, s, up, n, chunk, cand, cap, hist, rows, state);
+  if (int e = check_launch("select_hist_kernel<2>")) return e;
   switch (label_dtype) {
     case PROTOSEG_I64:
       hipLaunchKernelGGL(bound_box_kernel<int64_t>, dim3(m), dim3(kBoxThreads), 0, s, up, H, W,
