@@ -163,7 +163,7 @@ __device__ __forceinline__ float fkey_inv(uint32_t k) {
 // the prefix) is taken on the way: above the 11-bit block in pass 2, inside it in pass 3.
 constexpr int kHistThreads = 256;
 constexpr int kHistWaves = kHistThreads / 64;
-constexpr int kSelTarget = 2048;           // histogram workgroups per launch (all maps)
+constexpr int kSelTarget = 4096;           // histogram workgroups per launch (all maps)
 constexpr int kSelMinChunk = 1 << 15;      // elements per histogram workgroup, at least
 constexpr int kPassShift[3] = {21, 10, 0};
 constexpr int kPassWidth[3] = {11, 11, 10};
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(kHistThreads) void select_hist_kernel(const float* 
                                                                    uint32_t* __restrict__ state) {
   // one sub-histogram per wave in pass 1 (every element lands in it); passes 2 and 3 add only
   // the few elements inside the prefix and keep the small footprint (more workgroups per CU)
-  constexpr int kSub = PASS == 0 ? kHistWaves : 1;
+  constexpr int kSub = PASS == 0 ? 2 : 1;
   __shared__ uint32_t h[kSub][kHistBins];
   __shared__ uint32_t s_min[kHistWaves];
   __shared__ uint32_t s_fill;
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(kHistThreads) void select_hist_kernel(const float* 
   }
   __syncthreads();
   uint32_t mn = 0xffffffffu;
-  uint32_t* hw = h[PASS == 0 ? wave : 0];
+  uint32_t* hw = h[PASS == 0 ? (wave & 1) : 0];
   // Up to 16 values of this lane (bit u of `valid`): histogram, running min, candidate copy.
   // Called with wave-uniform control flow (the copy's wave scan needs every lane).
   auto process = [&](const float* v, int nv, uint32_t valid) {
@@ -294,14 +294,15 @@ __global__ __launch_bounds__(kHistThreads) void select_hist_kernel(const float* 
   const size_t n4 = aligned ? len / 4 : 0;
   const float4* a4 = reinterpret_cast<const float4*>(a);
   size_t i0 = 0;
-  for (; i0 + 4 * kHistThreads <= n4; i0 += 4 * kHistThreads) {  // four float4 loads in flight
-    float v[16];
+  for (; i0 + 8 * kHistThreads <= n4; i0 += 8 * kHistThreads) {  // eight float4 loads in flight
+    float v[32];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 8; ++u) {
       const float4 q = a4[i0 + u * kHistThreads + t];
       v[4 * u] = q.x; v[4 * u + 1] = q.y; v[4 * u + 2] = q.z; v[4 * u + 3] = q.w;
     }
     process(v, 16, 0xffffu);
+    process(v + 16, 16, 0xffffu);
   }
   for (; i0 < n4; i0 += kHistThreads) {
     const bool ok = i0 + t < n4;
