@@ -142,6 +142,69 @@ __global__ __launch_bounds__(kUpThreads) void cubic_upsample_kernel(const float*
   }
 }
 
+// The same resize with four adjacent output columns per thread (W % 4 == 0): 1024 columns per
+// workgroup, the horizontal values of a source row stored and read as float4, and float4 row
+// stores. Every output value is the same operation sequence as cubic_upsample_kernel's.
+constexpr int kUp4Cols = 4 * kUpThreads;
+constexpr int kUp4MaxSrcRows = 16;
+
+__global__ __launch_bounds__(kUpThreads) void cubic_upsample4_kernel(const float* __restrict__ act, int h, int w,
+                                                                     int H, int W, int rows, double scale_y,
+                                                                     double scale_x, float* __restrict__ up) {
+  __shared__ float4 hr[kUp4MaxSrcRows][kUpThreads];
+  __shared__ float ycoef[kUpMaxRows][4];
+  __shared__ int yrow[kUpMaxRows][4];
+  const int t = threadIdx.x;
+  const int dx0 = blockIdx.x * kUp4Cols + 4 * t;
+  const int dy0 = blockIdx.y * rows;
+  const int dy1 = dy0 + rows < H ? dy0 + rows : H;
+  const int map = blockIdx.z;
+  int i0[4], i1[4];
+  float c_unused[4];
+  cubic_taps(dy0, scale_y, h, i0, c_unused);
+  cubic_taps(dy1 - 1, scale_y, h, i1, c_unused);
+  const int r0 = i0[0], r1 = i1[3];
+  if (t < dy1 - dy0) {
+    int yi[4];
+    float b[4];
+    cubic_taps(dy0 + t, scale_y, h, yi, b);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      ycoef[t][k] = b[k];
+      yrow[t][k] = yi[k] - r0;
+    }
+  }
+  const float* S = act + static_cast<size_t>(map) * h * w;
+  if (dx0 < W) {  // W % 4 == 0: the thread's four columns are all inside the row
+    int xi[4][4];
+    float a[4][4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cubic_taps(dx0 + e, scale_x, w, xi[e], a[e]);
+    for (int r = r0; r <= r1; ++r) {
+      const float* R = S + static_cast<size_t>(r) * w;
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        o[e] = fadd(fadd(fadd(fmul(R[xi[e][0]], a[e][0]), fmul(R[xi[e][1]], a[e][1])), fmul(R[xi[e][2]], a[e][2])),
+                    fmul(R[xi[e][3]], a[e][3]));
+      hr[r - r0][t] = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+  __syncthreads();
+  if (dx0 >= W) return;
+  float4* out = reinterpret_cast<float4*>(up + (static_cast<size_t>(map) * H + dy0) * W + dx0);
+  for (int j = 0; j < dy1 - dy0; ++j) {
+    const float4 s0 = hr[yrow[j][0]][t], s1 = hr[yrow[j][1]][t], s2 = hr[yrow[j][2]][t], s3 = hr[yrow[j][3]][t];
+    const float b0 = ycoef[j][0], b1 = ycoef[j][1], b2 = ycoef[j][2], b3 = ycoef[j][3];
+    float4 v;
+    v.x = fadd(fadd(fadd(fmul(s0.x, b0), fmul(s1.x, b1)), fmul(s2.x, b2)), fmul(s3.x, b3));
+    v.y = fadd(fadd(fadd(fmul(s0.y, b0), fmul(s1.y, b1)), fmul(s2.y, b2)), fmul(s3.y, b3));
+    v.z = fadd(fadd(fadd(fmul(s0.z, b0), fmul(s1.z, b1)), fmul(s2.z, b2)), fmul(s3.z, b3));
+    v.w = fadd(fadd(fadd(fmul(s0.w, b0), fmul(s1.w, b1)), fmul(s2.w, b2)), fmul(s3.w, b3));
+    out[static_cast<size_t>(j) * (W / 4)] = v;
+  }
+}
+
 // Order-preserving f32 <-> u32 (NaN sorts last, as np.sort puts it).
 __device__ __forceinline__ uint32_t fkey(float f) {
   const uint32_t b = __float_as_uint(f);
@@ -557,6 +620,15 @@ extern "C" int protoseg_act_upsample(const float* dist, int m, int h, int w, int
   // Output rows per tile: the source rows they touch (<= rows * h / H + 5) must fit the LDS window.
   long long rows = (static_cast<long long>(kUpMaxSrcRows - 6) * H) / h;
   rows = rows < 1 ? 1 : rows > kUpMaxRows ? kUpMaxRows : rows;
+  if (W % 4 == 0 && (reinterpret_cast<uintptr_t>(up) & 15u) == 0) {
+    // the float4 path: the source rows of a tile (<= rows4 * h / H + 5) fit its 16-row window
+    long long rows4 = (static_cast<long long>(kUp4MaxSrcRows - 6) * H) / h;
+    rows4 = rows4 < 1 ? 1 : rows4 > kUpMaxRows ? kUpMaxRows : rows4;
+    const dim3 grid4(static_cast<unsigned>(ceil_div(W, kUp4Cols)), static_cast<unsigned>(ceil_div(H, rows4)), m);
+    hipLaunchKernelGGL(cubic_upsample4_kernel, grid4, dim3(kUpThreads), 0, s, act, h, w, H, W, static_cast<int>(rows4),
+                       scale_y, scale_x, up);
+    return check_launch("cubic_upsample4_kernel");
+  }
   const dim3 grid(static_cast<unsigned>(ceil_div(W, kUpThreads)), static_cast<unsigned>(ceil_div(H, rows)), m);
   hipLaunchKernelGGL(cubic_upsample_kernel, grid, dim3(kUpThreads), 0, s, act, h, w, H, W, static_cast<int>(rows),
                      scale_y, scale_x, up);

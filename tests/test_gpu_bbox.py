@@ -32,7 +32,8 @@ def _labels(rng, H, W, n=1):
 
 
 @pytest.mark.parametrize("kind", ["log", "linear"])
-@pytest.mark.parametrize("h,w,H,W", [(9, 17, 64, 128), (7, 11, 57, 93), (65, 65, 513, 513)])
+@pytest.mark.parametrize("h,w,H,W", [(9, 17, 64, 128), (7, 11, 57, 93), (65, 65, 513, 513), (33, 70, 300, 1100),
+                                     (40, 30, 20, 12)])
 def test_act_upsample_vs_oracle(device, kind, h, w, H, W):
     push = _push()
     rng = np.random.default_rng(h * W)
