@@ -648,9 +648,10 @@ def time_eval(n_img, steps, warmup, device, H=1024, W=2048, h=129, w=257, P=190,
 
 def time_bound_boxes(steps, warmup, device, H=1024, W=2048, h=129, w=257, P=190, K=19):
     """Push post-step, high-activation bound boxes of all P prototypes (push.py:309-343) in one
-    act_upsample + bound_boxes pair. The dominant cost is cubic_upsample_kernel, an HBM-write
-    stream: algorithmic bytes = P * H * W * 4 (upsampled maps written once) + the P low-res
-    activation maps read."""
+    act_upsample + bound_boxes pair. The roofline line is the upsample, an HBM-write stream
+    (cubic_upsample4_kernel at W % 4 == 0): algorithmic bytes = P * H * W * 4 (upsampled maps
+    written once) + the P low-res activation maps read. bound_boxes_ms is the percentile select
+    (two full reads of the maps) and the greedy walk."""
     from protoseg_amd import push as dpush
     gen = torch.Generator().manual_seed(SEED + 7)
     dmaps = (torch.rand(P, h, w, generator=gen) * 6).to(device)
@@ -684,7 +685,7 @@ def time_bound_boxes(steps, warmup, device, H=1024, W=2048, h=129, w=257, P=190,
     return {"ms_per_push": round(wall * 1e3, 4), "prototypes": P,
             "workload": f"bound boxes: {P} maps {h}x{w} -> {H}x{W} cubic, 95th percentile, greedy crop",
             "act_upsample_ms": round(kern * 1e3, 4), "bound_boxes_ms": round((wall - kern) * 1e3, 4),
-            "roofline": roofline_entry(0.0, nbytes, kern) | {"kernel": "act_kernel + cubic_upsample_kernel"}}
+            "roofline": roofline_entry(0.0, nbytes, kern) | {"kernel": "act_kernel + cubic_upsample4_kernel"}}
 
 
 def layer_report(step: LayerStep, per_kernel, actual, args):
