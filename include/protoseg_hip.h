@@ -344,6 +344,10 @@ int protoseg_act_upsample(const float* dist, int m, int h, int w, int H, int W, 
  *   threshold [m] f32 out;  box [m, 4] int32 out = (start_h, end_h, start_w, end_w) as
  *         proto_bound_boxes[j, 1:5] (push.py:338-342); -1 (threshold NaN) when label_index or
  *         rf_box is out of range
+ * m <= 65535. Scratch (per-map histograms and select state, a candidate list of up to 1/8 of
+ * each map, per-chunk histogram rows: a little over m * H * W / 2 bytes) is a grow-only device block
+ * per (device, stream), allocated on the first call that needs it; later calls on the stream
+ * are kernel launches only (capturable in a HIP graph).
  */
 int protoseg_bound_boxes(const float* up, int m, int H, int W, const void* label, int label_dtype, int n_label,
                          const int32_t* label_index, const int32_t* lut, int lut_size, const int32_t* target_class,
