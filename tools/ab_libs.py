@@ -70,7 +70,7 @@ def main():
         tgt = blocks.repeat_interleave(8, 1).repeat_interleave(8, 2)[:, :h, :w].reshape(B, -1).contiguous().to(dev)
         pcls = torch.clamp(torch.arange(P) // (P // K), max=K - 1).to(torch.int32).to(dev)
         mpc = int(torch.bincount(pcls.cpu().long()).max())
-        kws_b = libs["main"].protoseg_kld_workspace_size(B, P, h * w, K)
+        kws_b = max(lb.protoseg_kld_workspace_size(B, P, h * w, K) for lb in libs.values())
         kws = torch.empty(kws_b, device=dev, dtype=torch.uint8)
         kloss = torch.empty((), device=dev)
         kg = torch.full((), 0.25, device=dev)
