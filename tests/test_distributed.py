@@ -88,6 +88,7 @@ def _worker(rank, world, port, n_img, P, C, result_q):
         geo_ok = all(st.geometry.get(int(i)) == (8, 8, 2, 2) for i in st.img.tolist() if i >= 0)
         result_q.put((rank, st.dist, st.img, st.patch, st.fmap, geo_ok, grads, len(gb.buckets), merged,
                       st.second))
+        dist.barrier()  # neither rank tears gloo down while the other is still in a collective
     finally:
         dist.destroy_process_group()
 
