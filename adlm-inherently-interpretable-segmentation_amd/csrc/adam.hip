@@ -6,10 +6,12 @@
 //   m  = b1 m + (1 - b1) g                  v = b2 v + (1 - b2) g g
 //   p -= (lr / (1 - b1^t)) m / (sqrt(v) / sqrt(1 - b2^t) + eps)
 //
-// the arithmetic of torch's fused Adam (f32, bias corrections from the step count t). The step
-// count lives on the device (state[0]), so the update can be captured in a HIP graph and replayed:
-// every workgroup reads t = state[0] + 1 at its start; the last workgroup to finish (ticket in
-// state[1], a vector atomic) stores t and resets the ticket, after every workgroup has read it.
+// the arithmetic of torch's fused Adam (f32, bias corrections from the step count t). Each tensor
+// has its own step count on the device (state[k][0]; torch keeps state[p]['step'] per parameter),
+// so the update can be captured in a HIP graph and replayed: every workgroup of tensor k reads
+// t = state[k][0] + 1 at its start; the last of tensor k's workgroups to finish (ticket in
+// state[k][1], a vector atomic) stores t and resets the ticket, after all of them have read it.
+// A tensor with no elements gets one workgroup, which only advances its count.
 #include "protoseg_host.h"
 
 namespace protoseg {
@@ -25,12 +27,13 @@ struct AdamTensors {
   const float* g[kAdamMaxTensors];
   float* m[kAdamMaxTensors];
   float* v[kAdamMaxTensors];
+  int* st[kAdamMaxTensors];
   long long n[kAdamMaxTensors];
   long long first_block[kAdamMaxTensors + 1];  // prefix sum of the tensors' workgroup counts
   int count;
 };
 
-__global__ __launch_bounds__(kAdamBlock) void adam_kernel(AdamTensors ts, int* __restrict__ state, float lr,
+__global__ __launch_bounds__(kAdamBlock) void adam_kernel(AdamTensors ts, float lr,
                                                           float beta1, float beta2, float eps, float wd) {
   __shared__ int last, t_sh;
   __shared__ float corr[2];
@@ -42,6 +45,8 @@ __global__ __launch_bounds__(kAdamBlock) void adam_kernel(AdamTensors ts, int* _
   const float* __restrict__ g = ts.g[k];
   float* __restrict__ m = ts.m[k];
   float* __restrict__ v = ts.v[k];
+  int* __restrict__ state = ts.st[k];
+  const int nblk = static_cast<int>(ts.first_block[k + 1] - ts.first_block[k]);
   // the element loads go out with the step-count load (one memory round trip, not two)
   float gi[kAdamPerThread], pi[kAdamPerThread], mi[kAdamPerThread], vi[kAdamPerThread];
 #pragma unroll
@@ -83,7 +88,7 @@ __global__ __launch_bounds__(kAdamBlock) void adam_kernel(AdamTensors ts, int* _
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence();
-    last = atomicAdd(state + 1, 1) == static_cast<int>(gridDim.x) - 1;
+    last = atomicAdd(state + 1, 1) == nblk - 1;
   }
   __syncthreads();
   if (last && threadIdx.x == 0) {
@@ -100,7 +105,7 @@ using namespace protoseg;
 
 extern "C" int protoseg_adam_step(int n_tensors, float* const* params, const float* const* grads,
                                   float* const* exp_avg, float* const* exp_avg_sq, const int64_t* numel,
-                                  int32_t* state, float lr, float beta1, float beta2, float eps, float weight_decay,
+                                  int32_t* const* state, float lr, float beta1, float beta2, float eps, float weight_decay,
                                   protoseg_stream_t stream) {
   if (n_tensors <= 0 || n_tensors > kAdamMaxTensors)
     return fail(PROTOSEG_ERR_INVALID, "n_tensors %d (1..%d)", n_tensors, kAdamMaxTensors);
@@ -112,20 +117,21 @@ extern "C" int protoseg_adam_step(int n_tensors, float* const* params, const flo
   ts.count = n_tensors;
   long long blocks = 0;
   for (int k = 0; k < n_tensors; ++k) {
-    if (numel[k] < 0 || (numel[k] > 0 && (!params[k] || !grads[k] || !exp_avg[k] || !exp_avg_sq[k])))
+    if (numel[k] < 0 || !state[k] || (numel[k] > 0 && (!params[k] || !grads[k] || !exp_avg[k] || !exp_avg_sq[k])))
       return fail(PROTOSEG_ERR_INVALID, "tensor %d: null pointer or negative numel", k);
+    ts.st[k] = state[k];
     ts.p[k] = params[k];
     ts.g[k] = grads[k];
     ts.m[k] = exp_avg[k];
     ts.v[k] = exp_avg_sq[k];
     ts.n[k] = numel[k];
     ts.first_block[k] = blocks;
-    blocks += ceil_div(numel[k], kAdamBlock * kAdamPerThread);
+    const long long nb = ceil_div(numel[k], kAdamBlock * kAdamPerThread);
+    blocks += nb > 0 ? nb : 1;  // numel 0: one workgroup that advances the step count
   }
   ts.first_block[n_tensors] = blocks;
-  if (blocks == 0) return PROTOSEG_OK;
   if (blocks >= (1LL << 31)) return fail(PROTOSEG_ERR_UNSUPPORTED, "too many elements");
   hipLaunchKernelGGL(adam_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kAdamBlock), 0,
-                     reinterpret_cast<hipStream_t>(stream), ts, state, lr, beta1, beta2, eps, weight_decay);
+                     reinterpret_cast<hipStream_t>(stream), ts, lr, beta1, beta2, eps, weight_decay);
   return check_launch("adam_kernel");
 }

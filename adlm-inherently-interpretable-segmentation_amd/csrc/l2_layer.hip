@@ -743,6 +743,9 @@ extern "C" int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, 
       return PROTOSEG_OK;
     }
   }
+  // the f32 family has no sigmoid-on-load: refuse here, as the backward does, rather than
+  // return distances of the pre-activation
+  if (xsig) return fail(PROTOSEG_ERR_UNSUPPORTED, "PROTOSEG_X_SIGMOID: no bf16 kernel serves this shape");
   // f32 family: prototype chunks of at most one launch's LDS (C = 64: 384 rows); distance and
   // activation rows at (b * P + p0 + p), logits summed over the chunks
   const int fmax = f32_launch_protos(C);

@@ -10,6 +10,7 @@
 //   push_merge_kernel   strict-'<' fold in image order + winner gather (push.py:265-281)
 #include <map>
 #include <mutex>
+#include <vector>
 
 #include "bf16_split.h"
 #include "l2_bf16_common.h"
@@ -358,6 +359,62 @@ __global__ __launch_bounds__(256) void push_merge_kernel(const unsigned long lon
     gfmap[static_cast<size_t>(p) * C + c] = x[(static_cast<size_t>(win) * C + c) * hw + patch];
 }
 
+// push_dist_kernel: the distances of m (gathered) prototypes at every pixel of one image in
+// push_argmin_kernel's arithmetic, operation for operation: the same layout-B MFMA chain
+// (A = x channel 32 ct + 16 h + r of pixel j, B = the same channel of prototype j, in the same
+// order), the same fma chains for ||x||^2 and ||p||^2 with the halves added, l2_distance. So two
+// patches tie here exactly when they tie in the argmin kernel. One wave per (32-pixel tile,
+// 32-prototype tile); x is read straight from HBM (a host-side tie resolution, not a hot path).
+template <int NC>
+__global__ __launch_bounds__(64) void push_dist_kernel(const float* __restrict__ x, int HW,
+                                                       const float* __restrict__ protos, int m,
+                                                       float* __restrict__ out) {
+  constexpr int C = NC * 32;
+  __shared__ float xs[32];
+  const int lane = threadIdx.x, j = lane & 31, h = lane >> 5;
+  const int n0 = blockIdx.x * 32;
+  const int p = blockIdx.y * 32 + j;
+  const bool pvalid = p < m;
+  float pv[NC][16];
+  const float4* prow = reinterpret_cast<const float4*>(protos + static_cast<size_t>(pvalid ? p : m - 1) * C + 16 * h);
+#pragma unroll
+  for (int ct = 0; ct < NC; ++ct)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = prow[ct * 8 + q];
+      pv[ct][4 * q] = v.x;
+      pv[ct][4 * q + 1] = v.y;
+      pv[ct][4 * q + 2] = v.z;
+      pv[ct][4 * q + 3] = v.w;
+    }
+  float p2 = 0.f;
+#pragma unroll
+  for (int ct = 0; ct < NC; ++ct)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) p2 = fmaf(pv[ct][r], pv[ct][r], p2);
+  p2 += __shfl_xor(p2, 32);
+  const int n = n0 + j;
+  f32x16 acc = zero16();
+  float x2 = 0.f;
+#pragma unroll
+  for (int ct = 0; ct < NC; ++ct)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float xa = n < HW ? x[static_cast<size_t>(ct * 32 + 16 * h + r) * HW + n] : 0.f;
+      x2 = fmaf(xa, xa, x2);
+      acc = mfma32(xa, pv[ct][r], acc);
+    }
+  x2 += __shfl_xor(x2, 32);
+  if (h == 0) xs[j] = x2;
+  __syncthreads();
+  if (!pvalid) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = acc_row(r, h);
+    if (n0 + row < HW) out[static_cast<size_t>(p) * HW + n0 + row] = l2_distance(xs[row], p2, acc[r]);
+  }
+}
+
 int nc_of_push(int C) { return C == 32 ? 1 : C == 64 ? 2 : C == 128 ? 4 : 0; }
 
 }  // namespace
@@ -399,10 +456,13 @@ extern "C" int protoseg_patch_class_mask(const void* label, int label_dtype, int
 namespace {
 // Partial top-2 scratch ([n_img][stripes x split][P][2] u64): one grow-only block per (device, stream),
 // reused by later calls on that stream (kernels on one stream are ordered), so a call is only
-// kernel launches and can be captured in a HIP graph once the block exists.
+// kernel launches and can be captured in a HIP graph once the block exists. A call that needs
+// more takes a NEW block and retires the old one without freeing it: a graph that captured an
+// earlier call still points there, and replaying it must not write into freed memory.
 void* push_scratch(size_t need, hipStream_t s, int* status) {
   static std::mutex mu;
   static std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> blocks;
+  static std::vector<void*> retired;  // kept until the process exits
   int dev = 0;
   *status = PROTOSEG_OK;
   if (hipGetDevice(&dev) != hipSuccess) {
@@ -412,10 +472,7 @@ void* push_scratch(size_t need, hipStream_t s, int* status) {
   std::lock_guard<std::mutex> lock(mu);
   auto& b = blocks[{dev, s}];
   if (b.second < need) {
-    if (b.first && (hipStreamSynchronize(s) != hipSuccess || hipFree(b.first) != hipSuccess)) {
-      *status = check_launch("push scratch regrow");
-      return nullptr;
-    }
+    if (b.first) retired.push_back(b.first);
     b = {nullptr, 0};
     const size_t bytes = need < (1u << 20) ? (1u << 20) : need;
     const hipError_t e = hipMalloc(&b.first, bytes);
@@ -488,6 +545,27 @@ extern "C" int protoseg_push_argmin(const float* x, int n_img, int C, int h, int
                      static_cast<int>(stripes) * kPushSplit, P, reinterpret_cast<unsigned long long*>(img_keys),
                      reinterpret_cast<unsigned long long*>(img_second));
   return check_launch("push_top2_kernel");
+}
+
+extern "C" int protoseg_push_distances(const float* x, int C, int h, int w, const float* protos, int m, float* dist,
+                                       protoseg_stream_t stream) {
+  if (!x || !protos || !dist) return fail(PROTOSEG_ERR_INVALID, "null pointer argument");
+  if (h <= 0 || w <= 0 || m <= 0) return fail(PROTOSEG_ERR_INVALID, "bad shape h=%d w=%d m=%d", h, w, m);
+  const int nc = nc_of_push(C);
+  if (!nc) return fail(PROTOSEG_ERR_UNSUPPORTED, "C=%d", C);
+  if (reinterpret_cast<uintptr_t>(protos) % 16 != 0) return fail(PROTOSEG_ERR_INVALID, "protos must be 16-B aligned");
+  const long long HW = static_cast<long long>(h) * w;
+  if (HW * C >= (1LL << 31) || HW * m >= (1LL << 31)) return fail(PROTOSEG_ERR_UNSUPPORTED, "h*w=%lld too large", HW);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid(static_cast<unsigned>(ceil_div(HW, 32)), static_cast<unsigned>(ceil_div(m, 32)));
+  const int n = static_cast<int>(HW);
+  if (nc == 1)
+    hipLaunchKernelGGL(push_dist_kernel<1>, grid, dim3(64), 0, s, x, n, protos, m, dist);
+  else if (nc == 2)
+    hipLaunchKernelGGL(push_dist_kernel<2>, grid, dim3(64), 0, s, x, n, protos, m, dist);
+  else
+    hipLaunchKernelGGL(push_dist_kernel<4>, grid, dim3(64), 0, s, x, n, protos, m, dist);
+  return check_launch("push_dist_kernel");
 }
 
 extern "C" int protoseg_push_merge(const uint64_t* img_keys, const uint64_t* img_second, int n_img,

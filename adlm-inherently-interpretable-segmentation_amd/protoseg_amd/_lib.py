@@ -51,6 +51,7 @@ SIGNATURES = {
                              _sz, _vp]),
     "protoseg_patch_class_mask": (_i, [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp]),
     "protoseg_push_argmin": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
+    "protoseg_push_distances": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _vp]),
     "protoseg_push_merge": (_i, [_vp, _vp, _i, _i64, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     "protoseg_kld_workspace_size": (_sz, [_i, _i, _i, _i]),
     "protoseg_kld_forward": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _vp, _sz, _vp]),

@@ -112,9 +112,11 @@ class GradientBuckets:
     (module.py:235-243: the optimizer steps every iter_size micro-steps) makes each bucket's
     all-reduce start from the gradient hook of its last parameter, so the exchange overlaps the
     rest of the backward; buckets are always launched in index order, so every rank issues the
-    same collective sequence. ``wait()`` launches whatever has not started (a parameter that got
-    no gradient contributes zeros and is left without one), waits, and writes the reduced
-    gradients back. Without ``arm()``, ``allreduce()`` + ``wait()`` do the same after backward.
+    same collective sequence. ``wait()`` launches whatever has not started, waits, and writes
+    the reduced gradients back: a parameter that got no gradient on a rank contributes zeros
+    there, and it gets the reduced gradient on every rank when any rank had one (a had-gradient
+    flag per parameter is summed with the bucket), so no replica skips an update the others
+    make. Without ``arm()``, ``allreduce()`` + ``wait()`` do the same after backward.
     """
 
     def __init__(self, params: Iterable[torch.nn.Parameter], bucket_mb: float = 64.0, group=None,
@@ -164,9 +166,15 @@ class GradientBuckets:
 
     def _launch(self, b: int) -> None:
         bucket = self.buckets[b]
-        flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in bucket])
+        # one had-gradient flag per parameter travels at the end of the bucket: after the SUM a
+        # parameter gets the reduced gradient on EVERY rank as soon as any rank had one, so the
+        # replicas' optimizers skip (or update) the same parameters
+        flags = [1.0 if p.grad is not None else 0.0 for p in bucket]
+        ref = bucket[0]
+        flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in bucket]
+                         + [torch.tensor(flags, dtype=ref.dtype, device=ref.device)])
         work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-        self._pending[b] = (flat, work, [p.grad is not None for p in bucket])
+        self._pending[b] = (flat, work)
         self._next = b + 1
 
     def allreduce(self) -> None:
@@ -182,16 +190,21 @@ class GradientBuckets:
             return
         self.allreduce()
         for b, bucket in enumerate(self.buckets):
-            flat, work, had = self._pending[b]
+            flat, work = self._pending[b]
             work.wait()
+            had = flat[-len(bucket):].tolist()
             if self.average:
                 flat.div_(world)
             off = 0
             for p, h in zip(bucket, had):
                 n = p.numel()
-                if h:  # a parameter without a gradient on this rank stays without one
-                    p.grad.copy_(flat[off:off + n].view_as(p))
-                off += n
+                if h > 0:  # some rank had a gradient: every rank takes the reduced one
+                    red = flat[off:off + n].view_as(p)
+                    if p.grad is None:
+                        p.grad = red.clone()
+                    else:
+                        p.grad.copy_(red)
+                off += n  # no rank had one: left without a gradient everywhere
         self._pending = [None] * len(self.buckets)
         self._next = 0
         self._armed = False

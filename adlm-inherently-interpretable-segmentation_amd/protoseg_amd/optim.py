@@ -3,14 +3,17 @@
 Reference: segmentation/module.py:391 builds ``torch.optim.Adam(optimizer_specs)`` (per-group
 ``lr`` / ``weight_decay``, default betas and eps, amsgrad off). This class takes the same
 ``params`` / param groups and hyper-parameters and runs each group's update for all its tensors
-in one launch (up to 8 tensors per launch), with the step count on the device so a HIP graph
-holding ``step()`` replays as successive steps. f32 tensors on the GPU only (fails loudly
+in one launch (up to 8 tensors per launch). As in torch, every parameter has its own step count
+(``state[p]['step']``): it lives on the device ({count, ticket} int32 per parameter) so a HIP
+graph holding ``step()`` replays as successive steps, and ``state_dict()`` /
+``load_state_dict()`` carry it as torch's float ``step`` scalar, so checkpoints move between this
+class and ``torch.optim.Adam`` in both directions. f32 tensors on the GPU only (fails loudly
 otherwise).
 """
 from __future__ import annotations
 
 import ctypes
-from typing import Iterable
+from typing import Dict, Iterable
 
 import torch
 
@@ -25,14 +28,18 @@ class Adam(torch.optim.Optimizer):
         if lr < 0 or eps < 0 or weight_decay < 0 or not (0 <= betas[0] < 1 and 0 <= betas[1] < 1):
             raise ValueError("invalid Adam hyper-parameters")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
-        self._state_dev = {}
+        self._steps: Dict[torch.Tensor, torch.Tensor] = {}
 
-    def _group_state(self, gi: int, device) -> torch.Tensor:
-        st = self._state_dev.get(gi)
-        if st is None:
-            st = torch.zeros(2, dtype=torch.int32, device=device)  # {step count, ticket}
-            self._state_dev[gi] = st
-        return st
+    def _counter(self, p: torch.Tensor) -> torch.Tensor:
+        """Device {step count, ticket} of parameter p, seeded from state[p]['step'] (a loaded
+        checkpoint) the first time it is needed."""
+        ctr = self._steps.get(p)
+        if ctr is None:
+            t = self.state[p].get("step", 0)
+            t = int(t.item()) if isinstance(t, torch.Tensor) else int(t)
+            ctr = torch.tensor([t, 0], dtype=torch.int32, device=p.device)
+            self._steps[p] = ctr
+        return ctr
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -40,7 +47,7 @@ class Adam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        for gi, group in enumerate(self.param_groups):
+        for group in self.param_groups:
             ps = [p for p in group["params"] if p.grad is not None]
             if not ps:
                 continue
@@ -50,13 +57,11 @@ class Adam(torch.optim.Optimizer):
                         or not p.grad.is_contiguous():
                     raise _lib.ProtosegError("protoseg Adam: contiguous float32 parameters and gradients only")
                 st = self.state[p]
-                if not st:
+                if "exp_avg" not in st:
                     st["exp_avg"] = torch.zeros_like(p)
                     st["exp_avg_sq"] = torch.zeros_like(p)
-            dev_state = self._group_state(gi, ps[0].device)
+                    st.setdefault("step", torch.tensor(0.0))
             b1, b2 = group["betas"]
-            # Tensors of one group share the step count: one launch per <= 8 tensors, the step
-            # count advanced by the first launch only (later launches of the group read it back).
             for s0 in range(0, len(ps), _MAX_PER_LAUNCH):
                 chunk = ps[s0:s0 + _MAX_PER_LAUNCH]
                 n = len(chunk)
@@ -64,21 +69,21 @@ class Adam(torch.optim.Optimizer):
                         (chunk, [p.grad for p in chunk], [self.state[p]["exp_avg"] for p in chunk],
                          [self.state[p]["exp_avg_sq"] for p in chunk])]
                 keep.append((ctypes.c_int64 * n)(*[p.numel() for p in chunk]))
+                keep.append((ctypes.c_void_p * n)(*[self._counter(p).data_ptr() for p in chunk]))
                 addr = [ctypes.cast(a, ctypes.c_void_p) for a in keep]
-                st_t = dev_state if s0 == 0 else self._replay_state(gi, dev_state)
                 with torch.cuda.device(chunk[0].device):
-                    _lib.call("protoseg_adam_step", n, *addr, _lib.ptr(st_t), float(group["lr"]), float(b1),
+                    _lib.call("protoseg_adam_step", n, *addr[:5], addr[5], float(group["lr"]), float(b1),
                               float(b2), float(group["eps"]), float(group["weight_decay"]),
                               _lib.stream_of(chunk[0].device))
         return loss
 
-    def _replay_state(self, gi: int, advanced: torch.Tensor) -> torch.Tensor:
-        """For a group's 2nd+ launch: {t - 1, 0}, so it uses the same step t as the first."""
-        key = ("r", gi)
-        st = self._state_dev.get(key)
-        if st is None:
-            st = torch.zeros(2, dtype=torch.int32, device=advanced.device)
-            self._state_dev[key] = st
-        st[0].copy_(advanced[0] - 1)
-        st[1].zero_()
-        return st
+    def state_dict(self):
+        """torch's layout: state[p] = {'step': float scalar, 'exp_avg', 'exp_avg_sq'} (the step
+        copied from the device counter; this synchronises with it)."""
+        for p, ctr in self._steps.items():
+            self.state[p]["step"] = torch.tensor(float(ctr[0].item()))
+        return super().state_dict()
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._steps = {}  # re-seeded from the loaded state[p]['step'] at the next step()

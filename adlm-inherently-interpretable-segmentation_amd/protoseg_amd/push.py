@@ -16,8 +16,10 @@ Semantics kept from the reference:
   * high-activation bound boxes push.py:309-343 + helpers.py:48-82 (bbox.hip), computed once
     per prototype on its final winning image — the reference recomputes them on every image
     that improves the prototype and keeps the last, i.e. the same image.
-Ties between patches of ONE image resolve to the lowest patch index; the reference's order
-there is the iteration order of a Python set (push.py:214, 230). See DESIGN.md.
+  * exact ties between patches of ONE image resolve in the reference's order: the kernel
+    takes the lowest patch index and flags the tie (runner-up distance == minimum); the host
+    then redoes np.argmin over the class patches in the list(set) order of push.py:214-230
+    for those prototypes only (``resolve_exact_ties``).
 
 Out of scope (host-side visualisation, needs cv2/matplotlib): the PNG outputs of
 push.py:344-481.
@@ -139,12 +141,109 @@ def push_update(state: PushState, x: Tensor, labels: Tensor, protos: Tensor, pro
         state.geometry[first_img + i] = (int(H), int(W), int(h), int(w))
 
 
+def push_distances(x: Tensor, protos: Tensor) -> Tensor:
+    """Distances [m, h*w] of ``protos`` [m, C] at every patch of ONE image x [1, C, h, w] (or
+    [C, h, w]) in push_argmin's arithmetic, operation for operation: a tie here is exactly a
+    tie that kernel saw."""
+    dev = _lib.require_device(x, protos)
+    x = x.float().contiguous()
+    if x.dim() == 4:
+        if x.shape[0] != 1:
+            raise ValueError("push_distances takes one image")
+        x = x[0]
+    C, h, w = x.shape
+    protos = protos.reshape(protos.shape[0], -1).float().contiguous()
+    m = protos.shape[0]
+    out = torch.empty((m, h * w), device=dev, dtype=torch.float32)
+    with torch.cuda.device(dev):
+        _lib.call("protoseg_push_distances", _lib.ptr(x), C, h, w, _lib.ptr(protos), m, _lib.ptr(out),
+                  _lib.stream_of(dev))
+    return out
+
+
+def reference_patch_order(labels: np.ndarray, cls: int, h: int, w: int) -> List[tuple]:
+    """``list(class_to_patch_index_dict[cls])`` of push.py:214-230: the patches of class ``cls``
+    (label value cls + 1) in the iteration order of the Python set the reference builds. A set's
+    order depends only on the sequence of first insertions, which is the row-major order of each
+    patch's first pixel of the class (push.py:216-223 walk the pixels row by row), so the set is
+    rebuilt here from that sequence: CPython's int-tuple hash is unseeded, and the reference's
+    Python (3.9, env.yml:17) shares the tuple hash and set growth rule of this interpreter."""
+    H, W = labels.shape
+    patch_height, patch_width = H / h, W / w  # float64, push.py:201-202
+    pix = np.flatnonzero(labels.reshape(-1) == cls + 1)
+    if pix.size == 0:
+        return []
+    pi = (pix // W / patch_height).astype(np.int64)  # int(pixel_i / patch_height), push.py:217
+    pj = (pix % W / patch_width).astype(np.int64)    # int(pixel_j / patch_width), push.py:219
+    q = pi * w + pj
+    uniq, first = np.unique(q, return_index=True)
+    s = set()
+    for patch in uniq[np.argsort(first, kind="stable")].tolist():
+        s.add((patch // w, patch % w))
+    return list(s)
+
+
+def exact_tie_candidates(state: PushState) -> np.ndarray:
+    """Prototypes whose winning distance equals the runner-up's exactly (the runner-up of the
+    winning image, or an equal distance in a later image): only these can hold an exact tie
+    inside their winning image, where the kernel's lowest-patch pick may differ from the
+    reference's set order."""
+    if state.second is None:
+        return np.zeros(0, dtype=np.int64)
+    tie = (state.img >= 0) & (state.second == state.dist)
+    return np.nonzero(tie.cpu().numpy())[0]
+
+
+def resolve_exact_ties(state: PushState, load: Callable, protos: Tensor, proto_class, lut: Optional[Tensor] = None,
+                       candidates=None, log: Callable = print) -> List[int]:
+    """push.py:249-263 in the reference's own order for the prototypes whose winning image holds
+    several class patches at exactly the minimum distance: np.argmin over the class's patches in
+    list(set) order picks the first of them (the kernel picked the lowest patch index).
+    ``load(img_index)`` returns (x [1, C, h, w], labels [H, W]) of that image as the scan saw
+    them. Updates state.patch / state.fmap in place; returns the prototypes that moved."""
+    cand = exact_tie_candidates(state) if candidates is None else np.asarray(candidates, dtype=np.int64)
+    if cand.size == 0:
+        return []
+    img = state.img.cpu().numpy()
+    dist = state.dist.cpu().numpy()
+    patch = state.patch.cpu().numpy()
+    pcls = np.asarray(proto_class.cpu() if isinstance(proto_class, Tensor) else proto_class).astype(np.int64)
+    lut_np = lut.cpu().numpy() if lut is not None else None
+    pv = protos.detach().reshape(protos.shape[0], -1).float()
+    moved = []
+    for im in np.unique(img[cand]):
+        ids = cand[img[cand] == im]
+        x, labels = load(int(im))
+        x = x.float()
+        _, C, h, w = x.shape
+        lab = labels.reshape(labels.shape[-2:]).cpu().numpy().astype(np.int64)
+        if lut_np is not None:  # the scan's table (dataset.convert_targets); ids outside it: no class
+            ok = (lab >= 0) & (lab < lut_np.size)
+            lab = np.where(ok, lut_np[np.clip(lab, 0, lut_np.size - 1)], -1)
+        d = push_distances(x, pv[torch.as_tensor(ids, device=pv.device)]).cpu().numpy()
+        for k, j in enumerate(ids.tolist()):
+            order = reference_patch_order(lab, int(pcls[j]), h, w)
+            if not order:
+                continue
+            all_dist = d[k, [pi * w + pj for pi, pj in order]]
+            q = int(np.argmin(all_dist))
+            if all_dist[q] != dist[j]:
+                log(f"\tprototype {j}: distances of image {im} not reproduced (tie left to the kernel)")
+                continue
+            pi, pj = order[q]
+            if pi * w + pj != patch[j]:
+                state.patch[j] = pi * w + pj
+                state.fmap[j] = x[0, :, pi, pj].to(state.fmap.device)
+                moved.append(j)
+    return moved
+
+
 def near_ties(state: PushState, protos: Tensor, rtol: float = 1e-5) -> np.ndarray:
     """Prototypes whose winning patch beats the runner-up (any image, any class patch) by no
     more than the f32 rounding band of the expanded distance, rtol * (||x||^2 + ||p||^2) with x
-    the winning feature vector: there the reference's own rounding (or its Python-set order
-    for exact ties inside an image, push.py:214-230) may pick the other patch (SURVEY.md §7,
-    hard part 2). ``protos`` are the prototype vectors the push measured against."""
+    the winning feature vector: there the reference's own rounding may pick the other patch
+    (hard part 2); exact ties are resolved in the reference's order by
+    ``resolve_exact_ties``. ``protos`` are the prototype vectors the push measured against."""
     if state.second is None:
         raise ValueError("push state has no runner-up distances")
     p = protos.detach().reshape(protos.shape[0], -1).float().to(state.fmap.device)
@@ -403,6 +502,12 @@ def push_prototypes(dataset, prototype_network_parallel, prototype_layer_stride=
             run.append((img_tensor, labels, push_iter))
         flush()
 
+    # exact ties inside a winning image, in the reference's set order (this rank's winners,
+    # before the shards merge: the owner's patch travels with its key)
+    with torch.no_grad():
+        moved = resolve_exact_ties(state, load, ppnet.prototype_vectors, proto_class_t, lut, log=log)
+    if moved:
+        log(f"\t{len(moved)} exact tie(s) resolved in the reference's patch order: {moved[:20]}")
     if world > 1:
         reduce_push_state(state, process_group)
     state.near_ties = near_ties(state, ppnet.prototype_vectors)

@@ -172,15 +172,32 @@ int protoseg_patch_class_mask(const void* label, int label_dtype, int n_img, int
  *               (float_bits(d_second) << 32) | 0xFFFFFFFF: the second-smallest distance over the
  *               class patches (another patch; equal to d_min on an exact tie), UINT64_MAX if
  *               the image holds fewer than two class patches.
- * Ties inside one image resolve to the lowest patch index (the reference's order is the
- * iteration order of a Python set, push.py:214-230); img_second lets the caller flag the
- * prototypes whose winner is within rounding of another patch.
- * Scratch for the per-stripe partials is allocated once per (device, stream) and reused.
+ * Ties inside one image resolve to the lowest patch index here; the reference's order is the
+ * iteration order of a Python set (push.py:214-230, 259-262), which the host restores for the
+ * prototypes whose winning image holds an exact tie (img_second's distance == img_keys',
+ * then protoseg_push_distances; protoseg_amd.push.resolve_exact_ties).
+ * Scratch for the per-stripe partials is allocated once per (device, stream) and grows only by
+ * a new block: blocks are never freed while the library is loaded, so a HIP graph that captured
+ * an earlier call keeps valid pointers (an enlarged call must be captured again).
  */
 int protoseg_push_argmin(const float* x, int n_img, int C, int h, int w,
                          const float* protos, int P, const int32_t* proto_class,
                          const uint32_t* mask, uint64_t* img_keys, uint64_t* img_second,
                          protoseg_stream_t stream);
+
+/*
+ * Push, exact-tie resolution: distances of m prototypes at every patch of ONE image in
+ * protoseg_push_argmin's arithmetic, operation for operation, so equal values here are exactly
+ * the ties that kernel saw. The host then picks, among the class patches at the minimum, the
+ * first in the reference's list(set) order (push.py:214-230 insertion order, np.argmin at
+ * 259-262). Replaces the reference's proto_dist_[patch_i, patch_j, j] gather (push.py:259-260)
+ * for those prototypes only.
+ *   x      [C, h, w] f32 (one image), C in {32, 64, 128}
+ *   protos [m, C] f32, 16-B aligned (the gathered prototypes)
+ *   dist   [m, h*w] f32 out
+ */
+int protoseg_push_distances(const float* x, int C, int h, int w, const float* protos, int m, float* dist,
+                            protoseg_stream_t stream);
 
 /*
  * Push, step 3: fold a batch of per-image keys into the running global minimum in image
@@ -361,12 +378,14 @@ int protoseg_bound_boxes(const float* up, int m, int H, int W, const void* label
  *   g = grad + weight_decay * p;  m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g^2;
  *   p -= lr / (1 - b1^t) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
  *   params[k], grads[k], exp_avg[k], exp_avg_sq[k]: device f32 [numel[k]] (host pointer arrays)
- *   state: device int32[2] = {step count t of the previous call, 0}; the call uses t + 1 and
- *          stores it, so a HIP graph holding the call replays as successive steps.
+ *   state[k]: device int32[2] per tensor = {its step count t of the previous call, 0}: tensor k
+ *          uses t + 1 and stores it (torch keeps one step per parameter, state[p]['step']), so a
+ *          HIP graph holding the call replays as successive steps; a tensor with numel 0 still
+ *          advances its count.
  */
 int protoseg_adam_step(int n_tensors, float* const* params, const float* const* grads,
                        float* const* exp_avg, float* const* exp_avg_sq, const int64_t* numel,
-                       int32_t* state, float lr, float beta1, float beta2, float eps, float weight_decay,
+                       int32_t* const* state, float lr, float beta1, float beta2, float eps, float weight_decay,
                        protoseg_stream_t stream);
 
 #ifdef __cplusplus

@@ -70,6 +70,48 @@ def push_case(n_img, C, H, W, h, w, P, K, seed):
                 duplicate_idx=np.asarray(duplicate_idx, dtype=np.int64))
 
 
+def push_ties_case(n_img, C, H, W, h, w, P, K, n_vec, seed):
+    """push.py:184-281 where exact ties inside an image are the rule: every patch of an image
+    carries one of ``n_vec`` feature vectors, so each prototype's class minimum is shared by
+    many patches and np.argmin over the list(set) order of push.py:214-230 picks the winner.
+    Images 0 and 2 share their vector table (equal minima across images: strict '<' keeps image
+    0); the labels differ, so the set orders differ."""
+    rng = np.random.default_rng(seed)
+    gen = torch.Generator().manual_seed(seed)
+    tables = torch.sigmoid(2.0 * torch.randn(2, C, n_vec, generator=gen))
+    xs = []
+    for i in range(n_img):
+        pick = torch.from_numpy(rng.integers(0, n_vec, size=h * w))
+        xs.append(tables[i % 2][:, pick].reshape(C, h, w))
+    x = torch.stack(xs)
+    protos = torch.rand(P, C, generator=gen)
+    proto_class = torch.argmax(po.class_identity(P, K), dim=1).numpy().astype(np.int32)
+    # class regions in blocks of 3 pixels: not aligned with the 8x8 patches, so patches hold
+    # several classes and each class's set is built in an order that is not the patch order
+    y = rng.integers(0, K + 1, size=(n_img, H // 3 + 1, W // 3 + 1))
+    labels = np.repeat(np.repeat(y, 3, axis=1), 3, axis=2)[:, :H, :W].astype(np.int64)
+    state = pu.PushOracleState(P, C)
+    dists, masks = [], []
+    for i in range(n_img):
+        d = po.l2_convolution(x[i:i + 1], protos[:, :, None, None], torch.ones(P, C, 1, 1))[0]
+        # equal feature vectors must give equal distances in the oracle's arithmetic
+        flat = d.reshape(P, -1).numpy()
+        vec = x[i].reshape(C, -1).numpy()
+        for q in range(1, h * w):
+            same = np.nonzero((vec[:, :q] == vec[:, q:q + 1]).all(0))[0]
+            if same.size:
+                assert np.array_equal(flat[:, same[0]], flat[:, q])
+        sets = pu.class_to_patch_index_dict(labels[i], h, w, K)
+        masks.append(pu.bitmask_from_dict(sets, h, w))
+        pu.update_prototypes_on_image_core(state, x[i].numpy(), d.permute(1, 2, 0).numpy(), labels[i], proto_class, K,
+                                           i, sets)
+        dists.append(d.numpy())
+    return dict(x=x.numpy(), protos=protos.numpy(), proto_class=proto_class, labels=labels, dist=np.stack(dists),
+                mask=np.stack(masks), global_min_proto_dist=state.global_min_proto_dist,
+                global_min_fmap_patches=state.global_min_fmap_patches.reshape(P, C), winner_patch=state.winner_patch,
+                proto_rf_boxes=state.proto_rf_boxes)
+
+
 def kld_case(B, h, w, P, K, seed):
     """module.py:167-208 on the distances of a trained-looking layer: labels in blocks with
     void, every class value and the skipped value K present; one class with a single pixel."""
@@ -131,6 +173,7 @@ CASES = {
     "l2_small": lambda: l2_case(2, 64, 17, 17, 38, 19, SEED),
     "l2_ragged": lambda: l2_case(3, 32, 7, 11, 21, 3, SEED + 7),
     "push_small": lambda: push_case(3, 64, 64, 128, 8, 16, 38, 19, SEED),
+    "push_ties": lambda: push_ties_case(3, 64, 64, 128, 8, 16, 38, 19, 6, SEED + 3),
     "kld_small": lambda: kld_case(2, 13, 17, 38, 19, SEED + 11),
     "knn_small": lambda: knn_case(7, 32, 60, 110, 9, 13, 38, 4, 5, SEED + 13),
     "bbox_small": lambda: bbox_case(6, 64, 72, 136, 9, 17, 38, 19, SEED + 17),

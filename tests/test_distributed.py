@@ -78,6 +78,14 @@ def _worker(rank, world, port, n_img, P, C, result_q):
         gb.allreduce()
         gb.wait()
         grads = [p.grad.clone() for p in params]
+        # a parameter with a gradient on rank 1 only (data-dependent use), and one on neither:
+        # the first gets the reduced gradient on EVERY rank, the second stays None everywhere
+        extra = [torch.nn.Parameter(torch.zeros(4)), torch.nn.Parameter(torch.zeros(3))]
+        extra[0].grad = torch.full((4,), 6.0) if rank == 1 else None
+        gb2 = GradientBuckets(extra, bucket_mb=1.0)
+        gb2.arm()  # hook path: rank 0 never fires extra[0]'s hook, so wait() launches the bucket
+        gb2.wait()
+        skipped = (None if extra[0].grad is None else extra[0].grad.clone(), extra[1].grad)
         # bound boxes: rank r owns the prototypes whose winning image lies in its shard
         boxes = torch.full((P, 6), -1, dtype=torch.int64)
         for j in range(P):
@@ -87,7 +95,7 @@ def _worker(rank, world, port, n_img, P, C, result_q):
         # every prototype's winning image has its geometry on every rank (rf boxes)
         geo_ok = all(st.geometry.get(int(i)) == (8, 8, 2, 2) for i in st.img.tolist() if i >= 0)
         result_q.put((rank, st.dist, st.img, st.patch, st.fmap, geo_ok, grads, len(gb.buckets), merged,
-                      st.second))
+                      st.second, skipped))
         dist.barrier()  # neither rank tears gloo down while the other is still in a collective
     finally:
         dist.destroy_process_group()
@@ -107,7 +115,9 @@ def test_sharded_push_reduction_equals_serial_scan(n_img):
         p.join(timeout=60)
         assert p.exitcode == 0
     best, img, patch, fmap, second = _serial_truth(_make_images(n_img, P, C))
-    for rank, d, im, pa, fm, ngeo, grads, nbuckets, boxes, sec in results:
+    for rank, d, im, pa, fm, ngeo, grads, nbuckets, boxes, sec, skipped in results:
+        assert skipped[0] is not None and torch.equal(skipped[0], torch.full((4,), 3.0))  # (0 + 6) / 2
+        assert skipped[1] is None
         assert sec.tolist() == second  # the sharded runner-up equals the serial one
         assert ngeo  # winners' geometry reached every rank
         for j in range(P):  # every rank holds the union of the per-shard bound boxes

@@ -71,3 +71,62 @@ def test_adam_rejects_non_f32(device):
     p.grad = torch.ones_like(p)
     with pytest.raises(_lib.ProtosegError):
         Adam([p]).step()
+
+
+def test_adam_state_dict_round_trip_with_torch(device):
+    """Checkpoint resume both ways: torch.optim.Adam -> ours -> torch, the bias correction
+    continuing from the saved per-parameter step (the step is in state_dict)."""
+    from protoseg_amd.optim import Adam
+    ours = _params(device, [(361, 64), (19, 361)], 5)
+    ref = [torch.nn.Parameter(p.detach().clone()) for p in ours]
+    opt_ref = torch.optim.Adam(ref, lr=2.5e-4, weight_decay=5e-4, foreach=False)
+    for step in range(3):
+        _grads(ref, step, 6)
+        opt_ref.step()
+    with torch.no_grad():
+        for a, b in zip(ours, ref):
+            a.copy_(b)
+    opt = Adam(ours, lr=2.5e-4, weight_decay=5e-4)
+    opt.load_state_dict(opt_ref.state_dict())
+    for step in range(3, 5):
+        _grads(ours, step, 6)
+        for a, b in zip(ref, ours):
+            a.grad = b.grad.clone()
+        opt.step()
+        opt_ref.step()
+    for a, b in zip(ours, ref):
+        assert torch.allclose(a, b, rtol=1e-6, atol=1e-7), (a - b).abs().max().item()
+    sd = opt.state_dict()
+    assert [float(s["step"]) for s in sd["state"].values()] == [5.0, 5.0]
+    # and back into torch
+    ref2 = [torch.nn.Parameter(p.detach().clone()) for p in ours]
+    opt_ref2 = torch.optim.Adam(ref2, lr=2.5e-4, weight_decay=5e-4, foreach=False)
+    opt_ref2.load_state_dict(sd)
+    _grads(ours, 9, 6)
+    for a, b in zip(ref2, ours):
+        a.grad = b.grad.clone()
+    opt.step()
+    opt_ref2.step()
+    for a, b in zip(ours, ref2):
+        assert torch.allclose(a, b, rtol=1e-6, atol=1e-7), (a - b).abs().max().item()
+
+
+def test_adam_per_parameter_step_counts(device):
+    """A parameter without a gradient on some steps keeps its own step count (torch semantics),
+    and an empty tensor still advances its count."""
+    from protoseg_amd.optim import Adam
+    ours = _params(device, [(40,), (33, 5)], 8) + [torch.nn.Parameter(torch.zeros(0, device=device))]
+    ref = [torch.nn.Parameter(p.detach().clone()) for p in ours]
+    opt, opt_ref = Adam(ours, lr=1e-3), torch.optim.Adam(ref, lr=1e-3, foreach=False)
+    for step in range(5):
+        _grads(ours, step, 9)
+        if step % 2 == 1:
+            ours[1].grad = None  # skipped on odd steps
+        for a, b in zip(ref, ours):
+            a.grad = None if b.grad is None else b.grad.clone()
+        opt.step()
+        opt_ref.step()
+    for a, b in zip(ours, ref):
+        assert torch.allclose(a, b, rtol=1e-6, atol=1e-7)
+    steps = [float(s["step"]) for s in opt.state_dict()["state"].values()]
+    assert steps == [float(s["step"]) for s in opt_ref.state_dict()["state"].values()] == [5.0, 3.0, 5.0]

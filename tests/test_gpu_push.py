@@ -238,8 +238,18 @@ def test_near_tie_flag_fires_on_constructed_ties(device):
     push.push_update(st2, x2.to(device), lab, protos.to(device), pc.to(device), 0)
     flags = push.near_ties(st2, protos)
     assert j in flags
-    assert int(st2.patch[j]) == min(q, same[0])  # exact tie inside an image -> lower patch index
+    assert int(st2.patch[j]) == min(q, same[0])  # the kernel's own pick: the lower patch index
     assert float(st2.second[j]) == float(st2.dist[j])
+    assert j in push.exact_tie_candidates(st2)
+    # resolved in the reference's order: the oracle's literal loop (list(set) + np.argmin)
+    push.resolve_exact_ties(st2, lambda i: (x2.to(device), lab), protos.to(device), pc)
+    ost = pu.PushOracleState(P, C)
+    d = po.l2_convolution(x2, protos[:, :, None, None], torch.ones(P, C, 1, 1))[0]
+    assert d.reshape(P, -1)[j, q] == d.reshape(P, -1)[j, same[0]]
+    pu.update_prototypes_on_image_core(ost, x2[0].numpy(), d.permute(1, 2, 0).numpy(), labels.numpy(), pc.numpy(),
+                                       K, 0)
+    assert int(st2.patch[j]) == int(ost.winner_patch[j])
+    assert torch.equal(st2.fmap[j].cpu(), x2.view(C, -1)[:, int(ost.winner_patch[j])])
     # (b) the same image twice: every found prototype ties across images, image 0 wins
     st3 = push.PushState.create(P, C, device)
     push.push_update(st3, torch.cat([x, x]).to(device), torch.stack([lab, lab]), protos.to(device), pc.to(device), 0)
@@ -251,3 +261,52 @@ def test_near_tie_flag_fires_on_constructed_ties(device):
     gap = (st.second - st.dist).cpu()
     for k in range(P):
         assert (k in base_flags) == bool(st.img[k] >= 0 and gap[k] <= band[k])
+
+
+def test_exact_ties_resolve_in_reference_order_golden(device):
+    """push_ties.npz (3 images, every minimum shared by several patches, equal minima across
+    images): kernel scan + resolve_exact_ties equals the oracle's literal push.py loop in every
+    winning image, patch, distance, feature vector and rf box."""
+    push = _push()
+    g = np.load(os.path.join(GOLDEN, "push_ties.npz"))
+    x = torch.from_numpy(g["x"]).to(device)
+    protos = torch.from_numpy(g["protos"]).to(device)
+    pc = torch.from_numpy(g["proto_class"]).to(device)
+    labels = torch.from_numpy(g["labels"]).to(device)
+    P, C = protos.shape
+    for per in (1, 3):  # one image per call (the drop-in) and the batched scan
+        state = push.PushState.create(P, C, device)
+        for i0 in range(0, x.shape[0], per):
+            push.push_update(state, x[i0:i0 + per], labels[i0:i0 + per], protos, pc, i0)
+        cand = push.exact_tie_candidates(state)
+        assert len(cand) == P  # every prototype holds a tie at its minimum
+        moved = push.resolve_exact_ties(state, lambda i: (x[i:i + 1], labels[i]), protos, pc)
+        assert len(moved) > 0
+        assert np.array_equal(state.img.cpu().numpy(), g["proto_rf_boxes"][:, 0])
+        assert np.array_equal(state.patch.cpu().numpy(), g["winner_patch"])
+        assert np.array_equal(push.rf_boxes(state, g["proto_class"]), g["proto_rf_boxes"])
+        assert np.array_equal(state.fmap.cpu().numpy(), g["global_min_fmap_patches"].astype(np.float32))
+        assert np.allclose(state.dist.cpu().numpy(), g["global_min_proto_dist"], rtol=1e-5, atol=1e-5)
+
+
+def test_push_distances_equal_the_argmin_kernel(device):
+    """push_distances reproduces push_argmin's keys bit for bit (same arithmetic)."""
+    push = _push()
+    C, h, w, P, K = 64, 33, 47, 57, 19
+    gen = torch.Generator().manual_seed(77)
+    x = torch.sigmoid(2 * torch.randn(1, C, h, w, generator=gen)).to(device)
+    protos = torch.rand(P, C, generator=gen).to(device)
+    pc = torch.argmax(po.class_identity(P, K), dim=1).to(torch.int32).to(device)
+    labels = torch.from_numpy(np.random.default_rng(1).integers(0, K + 1, size=(4 * h, 4 * w))).to(device)
+    mask = push.patch_class_mask(labels, h, w)
+    keys = push.push_argmin(x, protos, pc, mask)
+    dk, qk, fk = push.decode_keys(keys[0].cpu())
+    d = push.push_distances(x, protos).cpu()
+    m = mask.cpu().numpy().view(np.uint32)[0]
+    for j in range(P):
+        member = torch.from_numpy(((m >> int(pc[j])) & 1).astype(bool))
+        if not member.any():
+            continue
+        dj = torch.where(member, d[j], torch.tensor(float("inf")))
+        assert float(dj.min()) == float(dk[j])
+        assert int(torch.nonzero(dj == dj.min())[0]) == int(qk[j])

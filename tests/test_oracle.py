@@ -89,3 +89,31 @@ def test_masked_argmin_fast_matches_loop():
     pu.update_prototypes_on_image_core(st, np.zeros((1, h, w), np.float32), D, y, pc, K, 0, sets)
     assert np.array_equal(st.winner_patch, idx)
     assert np.array_equal(st.global_min_proto_dist.astype(np.float32), best)
+
+
+def test_push_oracle_reproduces_ties_golden():
+    """push_ties.npz: every prototype's minimum is shared by several patches of its winning
+    image; the literal push.py loop (list(set) order + np.argmin) picks the winners."""
+    g = np.load(os.path.join(GOLDEN, "push_ties.npz"))
+    x, labels = g["x"], g["labels"]
+    n_img, C, h, w = x.shape
+    P = g["protos"].shape[0]
+    state = pu.PushOracleState(P, C)
+    for i in range(n_img):
+        sets = pu.class_to_patch_index_dict(labels[i], h, w, 19)
+        pu.update_prototypes_on_image_core(state, x[i], g["dist"][i].transpose(1, 2, 0), labels[i],
+                                           g["proto_class"], 19, i, sets)
+    assert np.array_equal(state.winner_patch, g["winner_patch"])
+    assert np.array_equal(state.proto_rf_boxes, g["proto_rf_boxes"])
+
+
+@pytest.mark.parametrize("H,W,h,w", [(64, 128, 8, 16), (100, 37, 13, 5), (250, 513, 33, 65)])
+def test_reference_patch_order_is_the_set_order(H, W, h, w):
+    """protoseg_amd.push.reference_patch_order rebuilds list(set) of push.py:214-230 from the
+    first-pixel order of each patch: equal, element for element, to the literal loop's list."""
+    from protoseg_amd.push import reference_patch_order
+    rng = np.random.default_rng(H + 3)
+    y = np.repeat(np.repeat(rng.integers(0, 6, size=(H // 3 + 1, W // 3 + 1)), 3, 0), 3, 1)[:H, :W]
+    sets = pu.class_to_patch_index_dict(y, h, w, 5)
+    for c in range(5):
+        assert reference_patch_order(y, c, h, w) == sets[c]
