@@ -51,6 +51,20 @@ int launch_bwd_fused_bf16(const Geometry& g, bool x_bf16, const void* x, const f
                           float* g_protos, float* g_w, float* ws, hipStream_t stream, int accumulate = 0,
                           int reduce = 1);
 int bf16_bwd_fused_grid(const Geometry& g);
+// One-pass backward (l2_bwd_onepass.hip): bf16x3, P <= 384 in one launch (8 waves per
+// workgroup, all with the same roles); its own fragment-ordered operand block
+// (launch_prep_onepass); g_x (+= when accumulate) and a g_P / g_W slab per workgroup for
+// launch_bwd_reduce_bf16_chunks. bf16_onepass_npt: 16-prototype tiles per wave (Pp = 128 npt).
+int bf16_onepass_npt(int P);
+bool bf16_bwd_onepass_fits(const Geometry& g, int terms);
+int bf16_bwd_onepass_grid(const Geometry& g);
+size_t bf16_onepass_image_bytes(const Geometry& g);
+size_t bf16_bwd_onepass_slab_elems(const Geometry& g);
+int launch_prep_onepass(const Geometry& g, const float* protos, const float* w_last, int act_kind, float eps,
+                        void* img, hipStream_t stream);
+int launch_bwd_onepass_bf16(const Geometry& g, bool x_bf16, const void* x, const void* img, float eps, int act_kind,
+                            const float* g_logits, const float* g_dist, void* g_x, float* ws, hipStream_t stream,
+                            int accumulate = 0);
 // Fixed-order sum of `slabs` partial slabs in ws (+ 2p sum g_s) into g_protos / g_w.
 int launch_bwd_reduce_bf16(const Geometry& g, const float* ws, int slabs, const float* protos, int act_kind,
                            float* g_protos, float* g_w, hipStream_t stream);

@@ -20,9 +20,13 @@
 //                      partial slabs, reduced by l2_bwd_reduce_kernel in a fixed order
 //                      (bitwise reproducible, no atomics).
 #include "protoseg_device.h"
+#include <cstdlib>
+#include <cstring>
 #include <map>
 #include <mutex>
+#include <tuple>
 #include <utility>
+#include <vector>
 
 #include "l2_launch.h"
 #include "protoseg_host.h"
@@ -613,40 +617,70 @@ namespace {
 // kernel launches and can be captured in a HIP graph once the block exists.
 constexpr size_t kImageBlockMin = 512 * 1024;
 
+// Backward kernel choice for the bf16x3 training backward: the one-pass kernel for P > 192 (one
+// pass over X instead of 192-prototype chunks), the fused kernel below; PROTOSEG_BWD=onepass /
+// fused forces one (read per call: tests and measurement A/B switch it in one process).
+bool use_onepass(int P) {
+  const char* e = getenv("PROTOSEG_BWD");
+  if (e && !strcmp(e, "onepass")) return true;
+  if (e && !strcmp(e, "fused")) return false;
+  return P > 192;
+}
+
+// One grow-only block per (device, stream, kind). A call that needs more takes a NEW block and
+// retires the old one without freeing it: a HIP graph that captured an earlier call still
+// points there, and a replay must not read freed memory.
+int stream_block(size_t need, hipStream_t s, int kind, void** out) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, hipStream_t, int>, std::pair<void*, size_t>> blocks;
+  static std::vector<void*> retired;  // kept until the process exits
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return check_launch("hipGetDevice");
+  std::lock_guard<std::mutex> lock(mu);
+  auto& b = blocks[{dev, s, kind}];
+  if (b.second < need) {
+    if (b.first) retired.push_back(b.first);
+    b = {nullptr, 0};
+    const size_t bytes = need > kImageBlockMin ? need : kImageBlockMin;
+    const hipError_t e = hipMalloc(&b.first, bytes);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      b = {nullptr, 0};
+      return fail(PROTOSEG_ERR_HIP, "hipMalloc (operand images, %zu B): %s", bytes, hipGetErrorString(e));
+    }
+    b.second = bytes;
+  }
+  *out = b.first;
+  return PROTOSEG_OK;
+}
+
 struct ImageBlock {
   void* ptr = nullptr;
   // per > 0: the images of ceil(g.P / per) prototype chunks of `per` rows, one prep launch.
   int build(const Geometry& g, int terms, const float* protos, const float* w_last, int act_kind, float eps,
             hipStream_t s, int per = 0) {
-    static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> blocks;
     const int nchunk = per > 0 ? static_cast<int>(ceil_div(g.P, per)) : 1;
     const size_t need = per > 0 ? nchunk * bf16_image_bytes(geometry_of(1, g.C, 1, 1, per, g.K), terms)
                                 : bf16_image_bytes(g, terms);
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return check_launch("hipGetDevice");
-    {
-      std::lock_guard<std::mutex> lock(mu);
-      auto& b = blocks[{dev, s}];
-      if (b.second < need) {
-        if (b.first) {  // once per stream at most (kImageBlockMin covers one launch's images; chunked calls may grow it)
-          if (hipStreamSynchronize(s) != hipSuccess || hipFree(b.first) != hipSuccess)
-            return check_launch("image block regrow");
-          b = {nullptr, 0};
-        }
-        const size_t bytes = need > kImageBlockMin ? need : kImageBlockMin;
-        const hipError_t e = hipMalloc(&b.first, bytes);
-        if (e != hipSuccess) {
-          (void)hipGetLastError();
-          b = {nullptr, 0};
-          return fail(PROTOSEG_ERR_HIP, "hipMalloc (operand images, %zu B): %s", bytes, hipGetErrorString(e));
-        }
-        b.second = bytes;
-      }
-      ptr = b.first;
-    }
+    if (int st = stream_block(need, s, 0, &ptr)) return st;
     if (per > 0) return launch_prep_bf16_chunks(g, per, nchunk, terms, protos, w_last, act_kind, eps, ptr, s);
     return launch_prep_bf16(g, terms, protos, w_last, act_kind, eps, ptr, s);
+  }
+  // The fragment-ordered blocks of the one-pass backward (l2_bwd_onepass.hip): nchunk chunks of
+  // `per` prototypes (the last may be shorter), chunk c's block at c * chunk_bytes(per).
+  int build_onepass(const Geometry& g, int per, int nchunk, const float* protos, const float* w_last, int act_kind,
+                    float eps, hipStream_t s) {
+    const size_t cb = bf16_onepass_image_bytes(geometry_of(1, g.C, 1, 1, per, g.K));
+    if (int st = stream_block(cb * nchunk, s, 1, &ptr)) return st;
+    for (int c = 0; c < nchunk; ++c) {
+      const int p0 = c * per, pc = g.P - p0 < per ? g.P - p0 : per;
+      Geometry gc = geometry_of(1, g.C, 1, 1, pc, g.K);
+      gc.ldw = g.P;
+      if (int st = launch_prep_onepass(gc, protos + static_cast<size_t>(p0) * g.C, w_last ? w_last + p0 : nullptr,
+                                       act_kind, eps, static_cast<unsigned char*>(ptr) + c * cb, s))
+        return st;
+    }
+    return PROTOSEG_OK;
   }
 };
 }  // namespace
@@ -777,6 +811,14 @@ extern "C" size_t protoseg_l2_bwd_workspace_size(int B, int C, int H, int W, int
   size_t need = f32_pw_workspace(g);
   const size_t b16 = bf16_bwd_pw_workspace(g);
   if (C == 64 && b16 > need) need = b16;
+  if (C == 64) {  // one-pass backward: one slab per workgroup and prototype chunk of <= 384
+    const int nchunk = static_cast<int>(ceil_div(P, 384)), per = static_cast<int>(ceil_div(P, nchunk));
+    const Geometry gc = geometry_of(B, C, H, W, per, K);
+    if (bf16_bwd_onepass_fits(gc, 2)) {
+      const size_t q = static_cast<size_t>(nchunk) * bf16_bwd_onepass_slab_elems(gc) * sizeof(float);
+      if (q > need) need = q;
+    }
+  }
   if (C == 64) {  // fused backward: one slab per workgroup and prototype chunk (fused_chunks)
     const int nchunk = static_cast<int>(ceil_div(P, 192)), per = static_cast<int>(ceil_div(P, nchunk));
     const Geometry gc = geometry_of(B, C, H, W, per, K);
@@ -814,6 +856,34 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
   const int terms = terms_of(precision);
   const bool xb = x_dtype == PROTOSEG_BF16;
   float* ws = static_cast<float*>(workspace);
+  // Training backward at bf16x3: ONE pass over X for up to 384 prototypes (19 prototypes/class;
+  // l2_bwd_onepass.hip), prototype chunks of <= 384 beyond (chunk c > 0 adds its g_x), one slab
+  // reduce. P <= 192 keeps the 192-prototype fused kernel unless PROTOSEG_BWD=onepass.
+  if (terms == 2 && (xsig || (g_x && (g_protos || g_w))) && use_onepass(P)) {
+    const int nchunk = static_cast<int>(ceil_div(P, 384)), per = static_cast<int>(ceil_div(P, nchunk));
+    Geometry gc = geometry_of(B, C, H, W, per, K);
+    if (bf16_bwd_onepass_fits(gc, terms)) {
+      KernelSpan span(nchunk > 1 ? "l2_bwd_onepass_bf16_kernel" : "", "", s);
+      ImageBlock img;
+      if (int st = img.build_onepass(geo, per, nchunk, protos, g_logits ? w_last : nullptr, act_kind, eps, s))
+        return st;
+      const size_t cb = bf16_onepass_image_bytes(gc);
+      const size_t chunk_elems = bf16_bwd_onepass_slab_elems(gc);
+      const int grid = bf16_bwd_onepass_grid(gc);
+      for (int c = 0; c < nchunk; ++c) {
+        const int p0 = c * per, pc = P - p0 < per ? P - p0 : per;
+        Geometry gq = geometry_of(B, C, H, W, pc, K);
+        gq.ldw = gq.ldd = P;
+        gq.p0 = p0;
+        gq.xsig = xsig;
+        if (int st = launch_bwd_onepass_bf16(gq, xb, x, static_cast<unsigned char*>(img.ptr) + c * cb, eps, act_kind,
+                                             g_logits, g_dist, g_x, ws + c * chunk_elems, s, c > 0))
+          return st;
+      }
+      return launch_bwd_reduce_bf16_chunks(geo, per, nchunk, ws, grid, chunk_elems, protos, act_kind, g_protos,
+                                           g_logits ? g_w : nullptr, s);
+    }
+  }
   // Training backward (g_x and g_P / g_W) at bf16x3: one fused kernel per chunk of <= 192
   // prototypes (l2_bwd_fused.hip); chunk c > 0 adds its x-gradient to g_x.
   if (terms == 2 && C == 64 && bf16_sizes_ok(geo) && (xsig || (g_x && (g_protos || g_w)))) {

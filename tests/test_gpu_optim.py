@@ -2,6 +2,8 @@
 reference's optimizer (segmentation/module.py:391). Bar: parameters within 1e-6 relative (+1e-7
 absolute) of torch's after several steps (same f32 arithmetic up to the order of the bias
 correction's division); a HIP-graph capture of step() replays as successive steps."""
+import copy
+
 import pytest
 import torch
 
@@ -87,7 +89,7 @@ def test_adam_state_dict_round_trip_with_torch(device):
         for a, b in zip(ours, ref):
             a.copy_(b)
     opt = Adam(ours, lr=2.5e-4, weight_decay=5e-4)
-    opt.load_state_dict(opt_ref.state_dict())
+    opt.load_state_dict(copy.deepcopy(opt_ref.state_dict()))  # a checkpoint: no shared tensors
     for step in range(3, 5):
         _grads(ours, step, 6)
         for a, b in zip(ref, ours):
@@ -101,7 +103,7 @@ def test_adam_state_dict_round_trip_with_torch(device):
     # and back into torch
     ref2 = [torch.nn.Parameter(p.detach().clone()) for p in ours]
     opt_ref2 = torch.optim.Adam(ref2, lr=2.5e-4, weight_decay=5e-4, foreach=False)
-    opt_ref2.load_state_dict(sd)
+    opt_ref2.load_state_dict(copy.deepcopy(sd))
     _grads(ours, 9, 6)
     for a, b in zip(ref2, ours):
         a.grad = b.grad.clone()

@@ -1,0 +1,122 @@
+"""LDS bank-conflict checker for the one-pass backward's images (16x16x32 MFMA access
+patterns). Model: 64 banks x 4 B; ds_read_b128 in 4 lane groups of 16, ds_read_b64 /
+ds_read_b64_tr_b16 in 2 groups of 32 (MI355X_MICROARCH.md §LDS); a group is conflict-free
+when its byte ranges hit distinct banks. Prints the extra cycles per pattern for a swizzle."""
+import itertools
+import sys
+
+B128_GROUPS = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
+               list(range(4, 12)) + list(range(16, 20)) + list(range(28, 32))]
+B128_GROUPS += [[l + 32 for l in g] for g in B128_GROUPS]
+B64_GROUPS = [list(range(32)), list(range(32, 64))]
+
+
+def conflicts(addr_of_lane, nbytes, groups):
+    extra = 0
+    for g in groups:
+        use = {}
+        for l in g:
+            a = addr_of_lane(l)
+            if a is None:
+                continue
+            for b in range(a // 4, (a + nbytes) // 4):
+                use.setdefault(b % 64, set()).add(b)
+        extra += max(len(v) for v in use.values()) - 1
+    return extra
+
+
+def check(row_bytes, f, patterns):
+    tot = 0
+    for name, fn, nb, groups in patterns:
+        c = fn(row_bytes, f)
+        tot += c
+        if len(sys.argv) > 1:
+            print(f"  {name}: {c}")
+    return tot
+
+
+def xa_patterns():
+    # XA: [32 n][64 c] bf16, 128-B rows, 8 chunks of 16 B (chunk q = channels 8q..8q+7)
+    def off(row, chunk, f, half=0):
+        return row * 128 + ((chunk ^ f(row)) * 16) + half * 8
+    pats = []
+    for nt in (0, 1):
+        for ks in (0, 1):
+            pats.append((f"A n{nt} k{ks}", lambda rb, f, nt=nt, ks=ks: conflicts(
+                lambda l: off(16 * nt + (l & 15), 4 * ks + (l >> 4), f), 16, B128_GROUPS), 16, B128_GROUPS))
+    for ct in range(4):
+        for second in (0, 1):
+            def fn(rb, f, ct=ct, second=second):
+                def a(l):
+                    g, q, pp = l >> 4, (l >> 2) & 3, l & 3
+                    row = 16 * second + 4 * g + q
+                    slot = 4 * ct + pp
+                    return off(row, slot >> 1, f, slot & 1)
+                return conflicts(a, 8, B64_GROUPS)
+            pats.append((f"trP ct{ct} s{second}", fn, 8, B64_GROUPS))
+    return pats
+
+
+def ga_patterns():
+    # GA: [32 n][32 k] bf16, 64-B rows, 4 chunks
+    def off(row, chunk, f, half=0):
+        return row * 64 + ((chunk ^ f(row)) & 3) * 16 + half * 8
+    pats = []
+    for nt in (0, 1):
+        pats.append((f"A n{nt}", lambda rb, f, nt=nt: conflicts(
+            lambda l: off(16 * nt + (l & 15), l >> 4, f), 16, B128_GROUPS), 16, B128_GROUPS))
+    for kt in range(2):
+        for second in (0, 1):
+            def fn(rb, f, kt=kt, second=second):
+                def a(l):
+                    g, q, pp = l >> 4, (l >> 2) & 3, l & 3
+                    row = 16 * second + 4 * g + q
+                    slot = 4 * kt + pp
+                    return off(row, slot >> 1, f, slot & 1)
+                return conflicts(a, 8, B64_GROUPS)
+            pats.append((f"trG kt{kt} s{second}", fn, 8, B64_GROUPS))
+    return pats
+
+
+def gs_patterns():
+    # g_s: [p][32 n] bf16, 64-B rows of 8 slots of 8 B (4 pixels)
+    def off(row, slot, f):
+        return row * 64 + ((slot ^ f(row)) & 7) * 8
+    pats = []
+    for ks in range(2):
+        for nh in range(2):
+            for second in (0, 1):
+                def fn(rb, f, ks=ks, nh=nh, second=second):
+                    def a(l):
+                        g, q, pp = l >> 4, (l >> 2) & 3, l & 3
+                        row = 32 * ks + 8 * g + q + 4 * second
+                        return off(row, 4 * nh + pp, f)
+                    return conflicts(a, 8, B64_GROUPS)
+                pats.append((f"trS ks{ks} nh{nh} s{second}", fn, 8, B64_GROUPS))
+    # owner stores (ds_write_b64, groups of 16 contiguous lanes): lane (p = 16 pt + m, g) -> slot g or 4+g
+    W64 = [list(range(i, i + 16)) for i in range(0, 64, 16)]
+    for pt in range(3):
+        for nt in range(2):
+            pats.append((f"stS pt{pt} nt{nt}", lambda rb, f, pt=pt, nt=nt: conflicts(
+                lambda l: off(16 * pt + (l & 15), 4 * nt + (l >> 4), f), 8, W64), 8, W64))
+    return pats
+
+
+if __name__ == "__main__":
+    cands = {
+        "none": lambda r: 0,
+        "r>>1&7": lambda r: (r >> 1) & 7,
+        "r&7": lambda r: r & 7,
+    }
+    for img, pats in (("XA", xa_patterns()), ("GA", ga_patterns()), ("GS", gs_patterns())):
+        best = None
+        # search over XOR swizzles f(r) = sum_b bit_b(r) * v_b (linear over GF(2)), row bits 0..4
+        for vs in itertools.product(range(8), repeat=5):
+            f = lambda r, vs=vs: (((r & 1) * vs[0]) ^ (((r >> 1) & 1) * vs[1]) ^ (((r >> 2) & 1) * vs[2])
+                                  ^ (((r >> 3) & 1) * vs[3]) ^ (((r >> 4) & 1) * vs[4]))
+            c = check(0, f, pats)
+            if best is None or c < best[0]:
+                best = (c, vs)
+            if c == 0:
+                break
+        print(img, "best extra cycles", best)
