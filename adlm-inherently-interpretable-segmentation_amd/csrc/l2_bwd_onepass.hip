@@ -31,6 +31,26 @@
 // that make every access pattern above conflict-free.
 #include <type_traits>
 
+#ifdef PROTOSEG_STAMPS
+#include <hip/hip_runtime.h>
+namespace protoseg {
+__device__ unsigned long long g_stamps_onepass[1 << 17];
+}
+// 16 slots per wave (tools/stamps_onepass.py), fenced so the phases they bracket stay in place
+// (debug builds only: production code has neither stamps nor fences).
+#define OSTAMP(slot)                                                                                 \
+  do {                                                                                               \
+    __builtin_amdgcn_sched_barrier(0);                                                               \
+    const unsigned _w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);                         \
+    if ((threadIdx.x & 63) == 0 && _w * 16 + (slot) < (1u << 17))                                    \
+      ::protoseg::g_stamps_onepass[_w * 16 + (slot)] = __builtin_amdgcn_s_memtime();                 \
+    __builtin_amdgcn_sched_barrier(0);                                                               \
+  } while (0)
+#else
+#define OSTAMP(slot) \
+  do {               \
+  } while (0)
+#endif
 #include "bf16_split.h"
 #include "l2_bf16_common.h"
 #include "l2_launch.h"
@@ -77,8 +97,8 @@ __host__ __device__ constexpr OneLds one_lds(int Pp) {
   OneLds o{};
   o.ptimg = 0;                        // (-2P)^T fragments (the pt region), Pp / 32 * 8 KiB
   o.gs = o.ptimg + (Pp / 32) * 8192;  // [term][Pp][32 n] bf16, 64-B rows of 8-B slots
-  o.xa = o.gs + kOT * Pp * 64;        // [term][32 n][64 c] bf16, 128-B rows of 16-B chunks
-  o.ga = o.xa + kOT * 32 * 128;       // [term][32 n][32 k] bf16, 64-B rows of 16-B chunks
+  o.xa = o.gs + kOT * Pp * 64;        // [term][32 n][64 c] bf16, 160-B rows (128 B + 32 B pad)
+  o.ga = o.xa + kOT * 32 * 160;       // [term][32 n][32 k] bf16, 64-B rows of 16-B chunks
   o.x2s = o.ga + kOT * 32 * 64;       // [32] f32 ||x||^2
   o.ro = o.x2s + 32 * 4;              // [32] u32 g_dist byte offset per pixel
   o.sig = o.ro + 32 * 4;              // [2 slots][2 pixel halves][4 channel tiles][16] f32
@@ -86,9 +106,14 @@ __host__ __device__ constexpr OneLds one_lds(int Pp) {
   return o;
 }
 
-// Image offsets in bf16 elements (swizzles from tools/lds_swizzle_check.py).
-// x image: row n (64 channels), 16-B chunk q holds channels 8q .. 8q+7, at chunk q ^ (n & 6).
-__device__ __forceinline__ int xa_off(int n, int chunk) { return n * 64 + ((chunk ^ (n & 6)) << 3); }
+// Image offsets in bf16 elements (tools/lds_swizzle_check.py checks every access pattern).
+// x image: row n (64 channels) at a 160-B stride: the padding, not an XOR swizzle, makes the A
+// reads (16 rows x 16 B) and the transposed reads (4 rows x 4 slots per 16-lane group)
+// conflict-free, so every n-tile / k-step / channel-tile variant of an access is an immediate
+// offset from one per-lane base (no per-variant address registers).
+constexpr int kXaRow = 80;  // bf16 elements per x-image row
+constexpr int kXaPlane = 32 * kXaRow;
+__device__ __forceinline__ int xa_off(int n, int chunk) { return n * kXaRow + (chunk << 3); }
 // g_logits image: row n (32 classes), chunk k at (k ^ ((n >> 1) & 2)) & 3.
 __device__ __forceinline__ int ga_off(int n, int chunk) { return n * 32 + (((chunk ^ ((n >> 1) & 2)) & 3) << 3); }
 // g_s image: row p (32 pixels), 8-B slot s (pixels 4s .. 4s+3) at s ^ (((p >> 2) & 1) | ((p >> 1) & 4)).
@@ -153,19 +178,11 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
   // ---- prologue: (-2P)^T image -> LDS (for the launch); the owned S / g_act B fragments and
   // ||p||^2 -> registers -------------------------------------------------------------------------
   lds_copy(smem_raw + L.ptimg, img + io.pt, io.p2 - io.pt);
-  bf16x8 ps[NPT][2][kOT], wt[NPT][kOT];
+
   float p2[NPT];
 #pragma unroll
   for (int jt = 0; jt < NPT; ++jt) {
     const int ptile = wave * NPT + jt;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int t = 0; t < kOT; ++t)
-        ps[jt][ks][t] = *reinterpret_cast<const bf16x8*>(img + io.ps + ((ptile * 2 + ks) * kOT + t) * 1024 + lane * 16);
-#pragma unroll
-    for (int t = 0; t < kOT; ++t)
-      wt[jt][t] = *reinterpret_cast<const bf16x8*>(img + io.wt + (ptile * kOT + t) * 1024 + lane * 16);
     p2[jt] = reinterpret_cast<const float*>(img + io.p2)[ptile * 16 + m];
   }
 
@@ -184,9 +201,13 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
         const int b = gp / HW;
         off = static_cast<unsigned>((b * kC) * HW + (gp - b * HW)) * sz;
       }
+      // the channel offset depends on the lane (sch): it goes into the per-lane voffset, never
+      // the soffset (a divergent soffset makes hipcc emit a waterfall loop per load)
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        raw[e] = BufIO<TX>::load(rx, off, static_cast<unsigned>(chan_of(sch >> 1, sch & 1, e) * HW) * sz);
+      for (int e = 0; e < 8; ++e) {
+        const unsigned co = static_cast<unsigned>(chan_of(sch >> 1, sch & 1, e) * HW) * sz;
+        raw[e] = BufIO<TX>::load(rx, off == kOOB ? kOOB : off + co, 0u);
+      }
     } else {
       const int gg = t * 32 + gn;
       const bool ok = lane < 48 && gg < npix;
@@ -216,7 +237,7 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
         const int c = chan_of(q, hh, 4 * half);
 #pragma unroll
         for (int t2 = 0; t2 < kOT; ++t2)
-          store_half4(XA + t2 * 32 * 64 + xa_off(sn, c >> 3) + (c & 7), f[t2], half);
+          store_half4(XA + t2 * kXaPlane + xa_off(sn, c >> 3) + (c & 7), f[t2], half);
       }
       // ||x||^2 in the family's fixed order (chunk fma chains, then pairs, quads, halves)
       float s = chunk_sq(v);
@@ -255,6 +276,23 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
   }
   auto owner_tile = [&](int jt) __attribute__((always_inline)) {
     const int p = (wave * NPT + jt) * 16 + m;
+    // The x / g_logits operands are the same for every owned tile: an opaque zero in their LDS
+    // addresses makes each tile reload them instead of keeping their fragments live across the
+    // tiles (the compiler would hoist the loads out of the unrolled tile loop).
+    int z = 0;
+    asm volatile("" : "+v"(z));
+    const bf16* XAj = XA + z;
+    const bf16* GAj = GA + z;
+    bf16x8 psj[2][kOT];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int t = 0; t < kOT; ++t)
+        psj[ks][t] = *reinterpret_cast<const bf16x8*>(img + io.ps + (((wave * NPT + jt) * 2 + ks) * kOT + t) * 1024 + lane * 16);
+    bf16x8 wtj[kOT];  // this tile's g_act B fragments, streamed from the (L2-resident) operand block
+#pragma unroll
+    for (int t = 0; t < kOT; ++t)
+      wtj[t] = *reinterpret_cast<const bf16x8*>(img + io.wt + ((wave * NPT + jt) * kOT + t) * 1024 + lane * 16);
     f32x4 acc[2], gacc[2];
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
@@ -266,15 +304,15 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
         bf16x8 xa[kOT];
 #pragma unroll
         for (int t = 0; t < kOT; ++t)
-          xa[t] = *reinterpret_cast<const bf16x8*>(XA + t * 32 * 64 + xa_off(16 * nt + m, 4 * ks + g));
-        acc[nt] = mfma16(xa[1], ps[jt][ks][0], acc[nt]);
-        acc[nt] = mfma16(xa[0], ps[jt][ks][1], acc[nt]);
-        acc[nt] = mfma16(xa[0], ps[jt][ks][0], acc[nt]);
+          xa[t] = *reinterpret_cast<const bf16x8*>(XAj + t * kXaPlane + xa_off(16 * nt + m, 4 * ks + g));
+        acc[nt] = mfma16(xa[1], psj[ks][0], acc[nt]);
+        acc[nt] = mfma16(xa[0], psj[ks][1], acc[nt]);
+        acc[nt] = mfma16(xa[0], psj[ks][0], acc[nt]);
       }
       bf16x8 ga[kOT];
 #pragma unroll
-      for (int t = 0; t < kOT; ++t) ga[t] = *reinterpret_cast<const bf16x8*>(GA + t * 32 * 32 + ga_off(16 * nt + m, g));
-      gacc[nt] = mma16_split(ga, wt[jt], f32x4{0.f, 0.f, 0.f, 0.f});
+      for (int t = 0; t < kOT; ++t) ga[t] = *reinterpret_cast<const bf16x8*>(GAj + t * 32 * 32 + ga_off(16 * nt + m, g));
+      gacc[nt] = mma16_split(ga, wtj, f32x4{0.f, 0.f, 0.f, 0.f});
     }
     float gdv[8];
     if constexpr (GD) {
@@ -319,7 +357,7 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
       const int slot = 4 * ct + pp, chunk = slot >> 1, sub = (slot & 1) * 4;
 #pragma unroll
       for (int t = 0; t < kOT; ++t)
-        xb[t] = tr_pair(XA + t * 32 * 64 + xa_off(4 * g + qq, chunk) + sub, XA + t * 32 * 64 + xa_off(16 + 4 * g + qq, chunk) + sub);
+        xb[t] = tr_pair(XAj + t * kXaPlane + xa_off(4 * g + qq, chunk) + sub, XAj + t * kXaPlane + xa_off(16 + 4 * g + qq, chunk) + sub);
       gp[jt][ct] = mma16_split(gsf, xb, gp[jt][ct]);
     }
     // g_W[k][p] += g_logits^T act: A = g_logits[n][k] transposed (lane = class)
@@ -329,7 +367,7 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
       const int slot = 4 * kt + pp, chunk = slot >> 1, sub = (slot & 1) * 4;
 #pragma unroll
       for (int t = 0; t < kOT; ++t)
-        gl[t] = tr_pair(GA + t * 32 * 32 + ga_off(4 * g + qq, chunk) + sub, GA + t * 32 * 32 + ga_off(16 + 4 * g + qq, chunk) + sub);
+        gl[t] = tr_pair(GAj + t * 32 * 32 + ga_off(4 * g + qq, chunk) + sub, GAj + t * 32 * 32 + ga_off(16 + 4 * g + qq, chunk) + sub);
       gw[jt][kt] = mma16_split(gl, actf, gw[jt][kt]);
     }
   };
@@ -353,7 +391,11 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       xe[r] = BufIO<TX>::load(rx, o, static_cast<unsigned>(r * HW) * sz);
-      olde[r] = BufIO<TX>::load(rgx, accumulate ? o : kOOB, static_cast<unsigned>(r * HW) * sz);
+      olde[r] = 0.f;
+    }
+    if (accumulate) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) olde[r] = BufIO<TX>::load(rgx, o, static_cast<unsigned>(r * HW) * sz);
     }
     gx = f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 sg = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -394,26 +436,36 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
   // ---- main loop. Per tile: phase A(i) | barrier | raw loads of tile i+1, phase B(i), the
   // sum_p g_s partial, staging of tile i+1 | barrier | g_x epilogue(i). The raw loads and the
   // epilogue's x live only across phase B, where phase A's working registers are dead.
+  OSTAMP(0);
   load_raw(tile_of(0));
   convert(tile_of(0));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the (-2P)^T image DMA
   __syncthreads();
+  OSTAMP(1);
   for (int i = 0; i < iters; ++i) {
     const int t = tile_of(i);
+    if (i == 2) OSTAMP(2);
 #pragma unroll
     for (int jt = 0; jt < NPT; ++jt) {
       owner_tile(jt);
       OSCHED_FENCE();
+      if (i == 2) OSTAMP(3 + jt);
     }
     __syncthreads();  // g_s(i) complete; every wave's reads of the x / g_logits images done
+    if (i == 2) OSTAMP(6);
     if (i + 1 < iters) load_raw(tile_of(i + 1));
     phase_b(t, i & 1);
     OSCHED_FENCE();
+    if (i == 2) OSTAMP(7);
     if (i + 1 < iters) convert(tile_of(i + 1));
+    if (i == 2) OSTAMP(8);
     __syncthreads();  // g_s(i) reads done; images(i+1) and every sum_p g_s partial of tile i written
+    if (i == 2) OSTAMP(9);
     gx_epilogue(t, i & 1);
     OSCHED_FENCE();
+    if (i == 2) OSTAMP(10);
   }
+  OSTAMP(13);
 
   // ---- slab: this workgroup's g_P (x -2: the x image holds +x), g_W, sum_n g_s; stride Ps = P
   // rounded up to 32 (the reduce kernel's layout), rows past it skipped --------------------------
@@ -585,3 +637,16 @@ int launch_bwd_onepass_bf16(const Geometry& g, bool x_bf16, const void* x, const
 }
 
 }  // namespace protoseg
+
+#ifdef PROTOSEG_STAMPS
+// Debug builds only: copy (and clear) the one-pass kernel's per-wave phase stamps.
+extern "C" int protoseg_debug_stamps_onepass(void* dst, size_t bytes) {
+  using protoseg::g_stamps_onepass;
+  const size_t n = bytes < sizeof(g_stamps_onepass) ? bytes : sizeof(g_stamps_onepass);
+  if (hipDeviceSynchronize() != hipSuccess) return 3;
+  if (dst && hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps_onepass), n, 0, hipMemcpyDeviceToHost) != hipSuccess) return 3;
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamps_onepass)) != hipSuccess) return 3;
+  return hipMemset(p, 0, sizeof(g_stamps_onepass)) == hipSuccess ? 0 : 3;
+}
+#endif

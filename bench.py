@@ -174,8 +174,9 @@ class LayerStep:
 
     @property
     def fused(self):
-        """bf16x3 at C = 64: the training backward is one fused kernel per prototype chunk
-        (l2_bwd_fused.hip); other precisions run the two-kernel backward."""
+        """bf16x3 at C = 64: the training backward is one kernel (l2_bwd_onepass.hip for P > 192,
+        up to 384 prototypes per launch; l2_bwd_fused.hip at P <= 192); other precisions run
+        the two-kernel backward."""
         return self.prec == _lib.PRECISIONS["bf16x3"] and self.C == 64
 
     def kernel_names(self):
@@ -184,7 +185,7 @@ class LayerStep:
         precision select) and reports the full name it bracketed; the backward call also runs
         the operand-image prep and slab-reduce kernels, outside the bracket (inside it when the
         call runs over prototype chunks: then the bracket spans all chunks)."""
-        return ["l2_fwd", "l2_bwd_fused"] if self.fused else ["l2_fwd", "l2_bwd_x", "l2_bwd_pw"]
+        return ["l2_fwd", "l2_bwd"] if self.fused else ["l2_fwd", "l2_bwd_x", "l2_bwd_pw"]
 
     def timed_calls(self):
         return [self.fwd, self.bwd] if self.fused else [self.fwd, self.bwd_x, self.bwd_pw]
@@ -198,7 +199,7 @@ class LayerStep:
         fwd = (mm + last + 2.0 * n * self.C, n * self.C * xb + n * self.P * 4 + n * self.K * 4)
         if self.fused:  # S, g_act, g_x, g_P, g_W: 3 distance-sized + 2 class-sized products
             return {"l2_fwd": fwd,
-                    "l2_bwd_fused": (3 * mm + 2 * last, n * self.C * xb + n * self.K * 4 + n * self.C * xb)}
+                    "l2_bwd": (3 * mm + 2 * last, n * self.C * xb + n * self.K * 4 + n * self.C * xb)}
         return {
             "l2_fwd": fwd,
             "l2_bwd_x": (2 * mm + last, n * self.C * xb + n * self.K * 4 + n * self.C * xb),

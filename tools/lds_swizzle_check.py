@@ -120,3 +120,30 @@ if __name__ == "__main__":
             if c == 0:
                 break
         print(img, "best extra cycles", best)
+
+
+def padded_search():
+    """Row padding instead of XOR swizzles: every loop variant is then an immediate offset
+    (one address VGPR per access family)."""
+    for name, row_bytes, nchunk, ntile_col in (("XA", 128, 8, 4), ("GA", 64, 4, 2)):
+        for pad in range(0, 65, 4):
+            stride = row_bytes + pad
+            tot = 0
+            for nt in (0, 1):
+                for ks in range(nchunk // 4):
+                    tot += conflicts(lambda l: (16 * nt + (l & 15)) * stride + (4 * ks + (l >> 4)) * 16, 16, B128_GROUPS)
+            for ct in range(ntile_col):
+                for second in (0, 1):
+                    def a(l, ct=ct, second=second):
+                        g, q, pp = l >> 4, (l >> 2) & 3, l & 3
+                        return (16 * second + 4 * g + q) * stride + (16 * ct + 4 * pp) * 2
+                    tot += conflicts(a, 8, B64_GROUPS)
+            if tot == 0:
+                print(name, "conflict-free row stride", stride)
+                break
+        else:
+            print(name, "no padding found")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "pad":
+    padded_search()

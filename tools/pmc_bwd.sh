@@ -1,0 +1,21 @@
+#!/bin/bash
+# SQ counter passes over tools/bwd_driver.py (one counter group per pass; kernel trace only).
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${TAG:-bwd}
+OUT=$R/gpurun_out/pmc_$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+i=0
+for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+           "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA" \
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_VALU_MFMA_BUSY_CYCLES"; do
+  i=$((i+1))
+  echo "== pass $i: $grp"
+  timeout -k 10 120 rocprofv3 --kernel-trace --pmc $grp -d "$OUT/p$i" -o p$i --output-format csv -- \
+    python3 "$R/tools/bwd_driver.py" ${DRIVER_ARGS:-} > "$OUT/p$i.log" 2>&1
+  rc=$?
+  echo "rc=$rc"; tail -n 1 "$OUT/p$i.log"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done
+python3 "$R/tools/pmc_summary.py" "$OUT"
