@@ -14,16 +14,16 @@
 // roles, so the four SIMDs carry equal MFMA and VALU work and each SIMD's two waves cover each
 // other's epilogue:
 //   phase A (owner): wave w owns prototypes 16 NPT w .. +16 NPT (NPT = 3 at Pp = 384). Layout B
-//     (rows = pixels, columns = prototypes: the prototype is on the lane): S and g_act with the
-//     owned prototypes' (-2P) and W^T B fragments in registers for the whole launch, the
-//     epilogue, then g_P += g_s^T X and g_W += g_logits^T act with the accumulators as the A /
+//     (rows = pixels, columns = prototypes: the prototype is on the lane): S with the owned rows
+//     of the (-2P) image in LDS as B fragments, g_act with W^T B fragments streamed from the
+//     (L2-resident) operand block, the epilogue, then g_P += g_s^T X and g_W += g_logits^T act with the accumulators as the A /
 //     B operands (the contraction runs over their rows: k-slot (g, e) of a lane group g is pixel
 //     4g + e of n-tile 0 for e < 4, 16 + 4g + e - 4 of n-tile 1 after), so g_P / g_W stay in
 //     registers for the launch and go out once as this workgroup's slab. g_s goes to LDS as a
 //     [p][n] image.
 //   phase B (after a barrier): wave w computes g_x^T for channels 16 (w & 3) .. +15 and pixels
-//     16 (w >> 2) .. +15 over ALL prototypes: A from a (-2P)^T image that stays in LDS for the
-//     launch (fragment-ordered, 1 KiB contiguous reads), B from the g_s image by transposed reads
+//     16 (w >> 2) .. +15 over ALL prototypes: A from the same (-2P) image by transposed reads
+//     (one image in LDS for the launch serves both orientations), B from the g_s image by transposed reads
 //     (ds_read_b64_tr_b16). sum_p g_s (the 2 x sum_p g_s term) comes from the same B fragments
 //     times a ones A operand, each wave over a quarter of the k-steps; the four partials are
 //     added in a fixed order after the second barrier.
@@ -70,33 +70,35 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 
-// ---- operand block (l2_prep_onepass_kernel), fragment order: 1 KiB per fragment, lane l at 16 l.
-// g = l >> 4, m = l & 15.
-//   ps [ptile Pp/16][ks 2][term]: S B fragment, lane (p = 16 ptile + m), channels 32 ks + 8 g + e
-//   wt [ptile][term]:             g_act B fragment, lane (p), classes 8 g + e (grad_unit * W)
-//   pt [term][ks Pp/32][ct 4]:    g_x A fragment, lane (c = 16 ct + m), p = 32 ks + 8 g + e
-//   p2 [Pp]                       ||p||^2 in the family's order (the forward's)
+// ---- operand block (l2_prep_onepass_kernel). g = l >> 4, m = l & 15.
+//   wt [ptile Pp/16][term]: g_act B fragment (fragment order, 1 KiB, lane l at 16 l): lane (p =
+//                           16 ptile + m), classes 8 g + e (grad_unit * W)
+//   pi [term][Pp][64 c]:    the (-2P) image, bf16 rows of 128 B, 16-B chunk q (channels 8q ..
+//                           8q+7) at q ^ pi_swz(p); copied to LDS as is. S reads its B fragments
+//                           as rows (lane p, chunk 4 ks + g), phase B its (-2P)^T A fragments
+//                           by transposed reads (4 rows p x 16 channels per 16-lane group):
+//                           both conflict-free under the swizzle (tools/lds_swizzle_check.py pimg)
+//   p2 [Pp]                 ||p||^2 in the family's order (the forward's)
 struct OneOffsets {
-  int ps, wt, pt, p2, total;
+  int wt, pi, p2, total;
 };
 __host__ __device__ constexpr OneOffsets one_offsets(int Pp) {
   OneOffsets o{};
-  o.ps = 0;
-  o.wt = o.ps + (Pp / 16) * 2 * kOT * 1024;
-  o.pt = o.wt + (Pp / 16) * kOT * 1024;
-  o.p2 = o.pt + kOT * (Pp / 32) * 4 * 1024;
+  o.wt = 0;
+  o.pi = o.wt + (Pp / 16) * kOT * 1024;
+  o.p2 = o.pi + kOT * Pp * 128;
   o.total = o.p2 + ((Pp * 4 + 1023) & ~1023);
   return o;
 }
 
 // LDS regions (bytes)
 struct OneLds {
-  int ptimg, gs, xa, ga, x2s, ro, sig, total;
+  int pimg, gs, xa, ga, x2s, ro, sig, total;
 };
 __host__ __device__ constexpr OneLds one_lds(int Pp) {
   OneLds o{};
-  o.ptimg = 0;                        // (-2P)^T fragments (the pt region), Pp / 32 * 8 KiB
-  o.gs = o.ptimg + (Pp / 32) * 8192;  // [term][Pp][32 n] bf16, 64-B rows of 8-B slots
+  o.pimg = 0;                         // the (-2P) image (the pi region), Pp x 256 B
+  o.gs = o.pimg + kOT * Pp * 128;     // [term][Pp][32 n] bf16, 64-B rows of 8-B slots
   o.xa = o.gs + kOT * Pp * 64;        // [term][32 n][64 c] bf16, 160-B rows (128 B + 32 B pad)
   o.ga = o.xa + kOT * 32 * 160;       // [term][32 n][32 k] bf16, 64-B rows of 16-B chunks
   o.x2s = o.ga + kOT * 32 * 64;       // [32] f32 ||x||^2
@@ -120,6 +122,9 @@ __device__ __forceinline__ int ga_off(int n, int chunk) { return n * 32 + (((chu
 __device__ __forceinline__ int gs_off2(int p, int slot) {
   return p * 32 + ((slot ^ (((p >> 2) & 1) | ((p >> 1) & 4))) << 2);
 }
+// (-2P) image: row p (64 channels), 16-B chunk q at q ^ ((p & 2) | ((p >> 1) & 4)).
+__host__ __device__ __forceinline__ int pi_swz(int p) { return (p & 2) | ((p >> 1) & 4); }
+__device__ __forceinline__ int pi_off(int p, int chunk) { return p * 64 + (((chunk ^ pi_swz(p)) & 7) << 3); }
 
 __device__ __forceinline__ bf16x8 tr_pair(const bf16* lo, const bf16* hi) {
   const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(lo));
@@ -146,6 +151,9 @@ __device__ __forceinline__ void store_half4(bf16* dst, const bf16x8& f, int half
 }
 
 #define OSCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#ifndef PB_DEPTH
+#define PB_DEPTH 1  // phase B: k-steps of fragments in flight ahead of the one multiplying
+#endif
 
 template <typename TX, int ACT, bool GD, bool XSIG, int NPT>
 __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
@@ -158,7 +166,7 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   constexpr OneLds L = one_lds(Pp);
   constexpr OneOffsets io = one_offsets(Pp);
-  const bf16* PTimg = reinterpret_cast<const bf16*>(smem_raw + L.ptimg);
+  const bf16* PI = reinterpret_cast<const bf16*>(smem_raw + L.pimg);
   bf16* GS = reinterpret_cast<bf16*>(smem_raw + L.gs);
   bf16* XA = reinterpret_cast<bf16*>(smem_raw + L.xa);
   bf16* GA = reinterpret_cast<bf16*>(smem_raw + L.ga);
@@ -175,9 +183,8 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
   const rsrc_t rgd = make_rsrc(g_dist, gd_bytes), rgx = make_rsrc(g_x, g_x ? x_bytes : 0u);
   auto tile_of = [&](int i) __attribute__((always_inline)) { return static_cast<int>(blockIdx.x) + i * G; };
 
-  // ---- prologue: (-2P)^T image -> LDS (for the launch); the owned S / g_act B fragments and
-  // ||p||^2 -> registers -------------------------------------------------------------------------
-  lds_copy(smem_raw + L.ptimg, img + io.pt, io.p2 - io.pt);
+  // ---- prologue: the (-2P) image -> LDS (for the launch); the owned ||p||^2 -> registers ------
+  lds_copy(smem_raw + L.pimg, img + io.pi, io.p2 - io.pi);
 
   float p2[NPT];
 #pragma unroll
@@ -283,12 +290,12 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
     asm volatile("" : "+v"(z));
     const bf16* XAj = XA + z;
     const bf16* GAj = GA + z;
-    bf16x8 psj[2][kOT];
+    bf16x8 psj[2][kOT];  // S B fragments: rows p of the (-2P) image
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int t = 0; t < kOT; ++t)
-        psj[ks][t] = *reinterpret_cast<const bf16x8*>(img + io.ps + (((wave * NPT + jt) * 2 + ks) * kOT + t) * 1024 + lane * 16);
+        psj[ks][t] = *reinterpret_cast<const bf16x8*>(PI + t * Pp * 64 + pi_off(p, 4 * ks + g));
     bf16x8 wtj[kOT];  // this tile's g_act B fragments, streamed from the (L2-resident) operand block
 #pragma unroll
     for (int t = 0; t < kOT; ++t)
@@ -399,20 +406,45 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
     }
     gx = f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 sg = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-    for (int ks = 0; ks < KS; ++ks) {
-      bf16x8 a[kOT], b[kOT];
+    // g_x: the fully unrolled k-loop reads the fragments of k-step ks + PB_DEPTH while k-step ks
+    // multiplies (the LDS latency hides behind the MFMAs instead of being exposed once per
+    // k-step); every read is a per-lane base + an immediate offset (the image swizzles depend
+    // on row bits below 32, so a k-step moves every address by the same amount).
+    const int aslot = 4 * ct + pp, chunk = aslot >> 1, sub = (aslot & 1) * 4, row0 = 8 * g + qq;
+    int z = 0;
+    asm volatile("" : "+v"(z));  // the bases are rebuilt per tile, not held across phase A
+    const bf16* pa0 = PI + z + pi_off(row0, chunk) + sub;
+    const bf16* pa1 = PI + z + pi_off(row0 + 4, chunk) + sub;
+    const bf16* pb0 = GS + z + gs_off2(row0, 4 * nh + pp);
+    const bf16* pb1 = GS + z + gs_off2(row0 + 4, 4 * nh + pp);
+    auto ldk = [&](int ks, bf16x8 (&a)[kOT], bf16x8 (&b)[kOT]) __attribute__((always_inline)) {
 #pragma unroll
       for (int t2 = 0; t2 < kOT; ++t2) {
-        a[t2] = *reinterpret_cast<const bf16x8*>(PTimg + ((t2 * KS + ks) * 4 + ct) * 512 + lane * 8);
-        const int row = 32 * ks + 8 * g + qq;
-        b[t2] = tr_pair(GS + t2 * Pp * 32 + gs_off2(row, 4 * nh + pp), GS + t2 * Pp * 32 + gs_off2(row + 4, 4 * nh + pp));
+        a[t2] = tr_pair(pa0 + t2 * Pp * 64 + ks * 32 * 64, pa1 + t2 * Pp * 64 + ks * 32 * 64);
+        b[t2] = tr_pair(pb0 + t2 * Pp * 32 + ks * 32 * 32, pb1 + t2 * Pp * 32 + ks * 32 * 32);
       }
-      gx = mma16_split(a, b, gx);
-      if (ks / KSQ == ct) {  // wave-uniform: sum_p g_s over a quarter of the prototypes
-        sg = mfma16(ones, b[1], sg);
-        sg = mfma16(ones, b[0], sg);
-      }
+    };
+    constexpr int D = PB_DEPTH;
+    bf16x8 fa[D + 1][kOT], fb[D + 1][kOT];
+#pragma unroll
+    for (int j = 0; j < D; ++j) ldk(j, fa[j], fb[j]);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + D < KS) ldk(ks + D, fa[(ks + D) % (D + 1)], fb[(ks + D) % (D + 1)]);
+      gx = mma16_split(fa[ks % (D + 1)], fb[ks % (D + 1)], gx);
+      OSCHED_FENCE();
+    }
+    // sum_p g_s over this wave's quarter of the prototypes (k-steps ct KSQ ..): the g_s
+    // fragments again, times a ones A operand
+    const int qoff = ct * KSQ * 32 * 32;
+#pragma unroll
+    for (int kk = 0; kk < KSQ; ++kk) {
+      bf16x8 b[kOT];
+#pragma unroll
+      for (int t2 = 0; t2 < kOT; ++t2)
+        b[t2] = tr_pair(pb0 + qoff + t2 * Pp * 32 + kk * 32 * 32, pb1 + qoff + t2 * Pp * 32 + kk * 32 * 32);
+      sg = mfma16(ones, b[1], sg);
+      sg = mfma16(ones, b[0], sg);
     }
     if (lane < 16) SIG[((slot * 2 + nh) * 4 + ct) * 16 + m] = sg[0];
   };
@@ -439,7 +471,7 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
   OSTAMP(0);
   load_raw(tile_of(0));
   convert(tile_of(0));
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the (-2P)^T image DMA
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the (-2P) image DMA
   __syncthreads();
   OSTAMP(1);
   for (int i = 0; i < iters; ++i) {
@@ -491,7 +523,7 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
   }
 }
 
-// ---- prep: the fragment-ordered operand block --------------------------------------------------
+// ---- prep: the operand block -------------------------------------------------------------------
 __device__ float one_norm2(const float* __restrict__ protos, int p, bool valid) {
 #pragma clang fp contract(off)
   const float* row = protos + static_cast<size_t>(valid ? p : 0) * kC;
@@ -504,30 +536,29 @@ __device__ float one_norm2(const float* __restrict__ protos, int p, bool valid) 
   return valid ? s : 0.f;
 }
 
-// blockIdx.y: 0 = ps, 1 = wt, 2 = pt, 3 = p2; one thread per fragment lane (both terms).
+// blockIdx.y: 0 = the (-2P) image (one thread per row chunk, both terms), 1 = wt (one thread per
+// fragment lane), 2 = p2.
 __global__ __launch_bounds__(256) void l2_prep_onepass_kernel(const float* __restrict__ protos, int P, int Pp,
                                                               const float* __restrict__ w_last, int K, int ldw,
                                                               float wt_scale, unsigned char* __restrict__ block) {
   const OneOffsets o = one_offsets(Pp);
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int lane = tid & 63, frag = tid >> 6, g = lane >> 4, m = lane & 15;
   float v[8];
   bf16x8 f[kOT];
-  auto put = [&](int base, int stride) {
-    split8<kOT>(v, f);
-#pragma unroll
-    for (int t = 0; t < kOT; ++t) *reinterpret_cast<bf16x8*>(block + base + t * stride + lane * 16) = f[t];
-  };
   switch (blockIdx.y) {
-    case 0: {  // ps[ptile][ks]: lane (p = 16 ptile + m), channels 32 ks + 8 g + e
-      if (frag >= (Pp / 16) * 2) return;
-      const int ptile = frag >> 1, ks = frag & 1, p = 16 * ptile + m;
+    case 0: {  // pi[term][p][chunk q]: channels 8q .. 8q+7 of -2 p
+      if (tid >= Pp * 8) return;
+      const int p = tid >> 3, q = tid & 7;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = p < P ? -2.f * protos[static_cast<size_t>(p) * kC + 32 * ks + 8 * g + e] : 0.f;
-      put(o.ps + frag * kOT * 1024, 1024);
+      for (int e = 0; e < 8; ++e) v[e] = p < P ? -2.f * protos[static_cast<size_t>(p) * kC + 8 * q + e] : 0.f;
+      split8<kOT>(v, f);
+      const int off = o.pi + p * 128 + ((q ^ pi_swz(p)) & 7) * 16;
+#pragma unroll
+      for (int t = 0; t < kOT; ++t) *reinterpret_cast<bf16x8*>(block + off + t * Pp * 128) = f[t];
       break;
     }
     case 1: {  // wt[ptile]: lane (p), classes 8 g + e
+      const int lane = tid & 63, frag = tid >> 6, g = lane >> 4, m = lane & 15;
       if (frag >= Pp / 16) return;
       const int p = 16 * frag + m;
 #pragma unroll
@@ -535,18 +566,9 @@ __global__ __launch_bounds__(256) void l2_prep_onepass_kernel(const float* __res
         const int k = 8 * g + e;
         v[e] = (w_last && p < P && k < K) ? wt_scale * w_last[static_cast<size_t>(k) * ldw + p] : 0.f;
       }
-      put(o.wt + frag * kOT * 1024, 1024);
-      break;
-    }
-    case 2: {  // pt[ks][ct] (term planes of KS * 4 fragments): lane (c = 16 ct + m), p = 32 ks + 8 g + e
-      if (frag >= (Pp / 32) * 4) return;
-      const int ks = frag >> 2, ct = frag & 3, c = 16 * ct + m;
+      split8<kOT>(v, f);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int p = 32 * ks + 8 * g + e;
-        v[e] = p < P ? -2.f * protos[static_cast<size_t>(p) * kC + c] : 0.f;
-      }
-      put(o.pt + frag * 1024, (Pp / 32) * 4 * 1024);
+      for (int t = 0; t < kOT; ++t) *reinterpret_cast<bf16x8*>(block + o.wt + (frag * kOT + t) * 1024 + lane * 16) = f[t];
       break;
     }
     default: {
@@ -600,8 +622,7 @@ size_t bf16_bwd_onepass_slab_elems(const Geometry& g) {
 int launch_prep_onepass(const Geometry& g, const float* protos, const float* w_last, int act_kind, float eps,
                         void* img, hipStream_t stream) {
   const int Pp = kOW * bf16_onepass_npt(g.P) * 16;
-  const int frags = (Pp / 16) * 2;  // the largest region's fragment count
-  const dim3 grid(static_cast<unsigned>(ceil_div(static_cast<long long>(frags) * 64, 256)), 4);
+  const dim3 grid(static_cast<unsigned>(ceil_div(Pp * 8, 256)), 3);  // the image's Pp x 8 chunks: the largest region
   hipLaunchKernelGGL(l2_prep_onepass_kernel, grid, dim3(256), 0, stream, protos, g.P, Pp, w_last, g.K, g.ldw,
                      act_grad_unit(act_kind, eps), static_cast<unsigned char*>(img));
   return check_launch("l2_prep_onepass_kernel");

@@ -28,6 +28,35 @@ from torch import Tensor
 from .distributed import GradientBuckets, world_info
 
 
+def backbone_params(features, key: str):
+    """segmentation/utils.py:42-61 (``get_params``): "1x" = the conv parameters of the ResNet
+    layers, "10x" / "20x" = the ASPP conv weights / biases."""
+    for name, m in features.named_modules():
+        if not isinstance(m, torch.nn.Conv2d):
+            continue
+        if key == "1x" and "layer" in name:
+            yield from m.parameters()
+        elif key == "10x" and "aspp" in name:
+            yield m.weight
+        elif key == "20x" and "aspp" in name:
+            yield m.bias
+
+
+def joint_param_groups(ppnet, lr_features: float = 2.5e-5, lr_add_on_layers: float = 2.5e-4,
+                       lr_prototype_vectors: float = 2.5e-4, weight_decay: float = 5e-4):
+    """The joint-phase optimizer groups of module.py:357-382 (defaults: cityscapes_*_imnet.gin
+    joint_optimizer_*): backbone 1x / 10x / 20x, add-on layers, prototype vectors (no weight
+    decay). BatchNorm and the last layer get gradients but are not stepped, as in the reference."""
+    wd = weight_decay
+    return [
+        {"params": list(backbone_params(ppnet.features, "1x")), "lr": lr_features, "weight_decay": wd},
+        {"params": list(backbone_params(ppnet.features, "10x")), "lr": 10 * lr_features, "weight_decay": wd},
+        {"params": list(backbone_params(ppnet.features, "20x")), "lr": 10 * lr_features, "weight_decay": wd},
+        {"params": list(ppnet.add_on_layers.parameters()), "lr": lr_add_on_layers, "weight_decay": wd},
+        {"params": [ppnet.prototype_vectors], "lr": lr_prototype_vectors},
+    ]
+
+
 def _default_resize(labels: Tensor, h: int, w: int) -> Tensor:
     from .knn import resize_label
     return resize_label(labels, h, w)

@@ -39,7 +39,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from protoseg_amd import _lib  # noqa: E402
-from protoseg_amd.distributed import init_from_env  # noqa: E402
+from protoseg_amd.distributed import init_from_env, world_info  # noqa: E402
 
 PEAK_HBM_GBPS = 8000.0       # MI355X_MICROARCH.md chip table (spec)
 PEAK_F32_VALU_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 (vector), spec
@@ -95,7 +95,9 @@ class LayerStep:
         from protoseg_amd.optim import Adam
         self.params = [torch.nn.Parameter(self.protos), torch.nn.Parameter(self.w_last)]
         self.params[0].grad, self.params[1].grad = self.g_p, self.g_w
-        self.opt = Adam(self.params, lr=2.5e-4)
+        # weight decay: gin joint_optimizer_weight_decay = 5e-4 (module.py:359-375 passes it to
+        # every group but the prototype vectors'; one group here keeps one launch, same cost)
+        self.opt = Adam(self.params, lr=2.5e-4, weight_decay=5e-4)
         self.buckets = None
 
     def _stream(self):
@@ -711,6 +713,133 @@ def layer_report(step: LayerStep, per_kernel, actual, args):
     return roof, kernels
 
 
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` outside a launcher: start N ranks (one process per GPU) with
+    torch.distributed.run on 127.0.0.1 and return its exit code. Runs before anything touches the
+    GPU; the children are started as child processes (never exec'd over this one)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+
+
+def cpu_smoke(args, rank, world):
+    """--cpu-smoke: the multi-rank plumbing without a GPU (gloo): every rank runs `steps` of the
+    DP exchange of the layer step (GradientBuckets over g_P and g_W, CPU tensors of the headline
+    shapes) between the same barriers as the GPU bench, rank 0 prints the JSON line. The value is
+    the exchange rate only, labelled as such — it is a launcher test, not a measurement."""
+    from protoseg_amd.distributed import GradientBuckets
+    P, C, K = args.protos, args.channels, args.classes
+    params = [torch.nn.Parameter(torch.rand(P, C)), torch.nn.Parameter(torch.rand(K, P))]
+    buckets = GradientBuckets(params, average=True)
+    for p in params:
+        p.grad = torch.full_like(p, float(rank + 1))
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        buckets.allreduce()
+        buckets.wait()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    mean_rank = float(params[0].grad[0, 0])  # mean of 1..world after averaging (idempotent)
+    if rank == 0:
+        print(json.dumps({"metric": "cpu-smoke: DP gradient exchange only (no GPU)", "value":
+                          round(args.batch * world * args.steps / elapsed, 1), "unit": "img/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": 0, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+                          "data": "synthetic", "config": {"workload": "cpu-smoke", "parallelism": f"dp{world}",
+                                                          "backend": dist.get_backend() if world > 1 else None,
+                                                          "grad_mean_check": mean_rank}}))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def time_small_batches(args, device, batches=(2, 4), protos=(361, 190)):
+    """The layer step at the reference's per-GPU micro-batches (gin joint_batch_size = 2;
+    configs[2]: 32 images over 8 GPUs = 4 per GPU), where launch and tail costs dominate."""
+    x_dtype = torch.float32 if args.x_dtype == "f32" else torch.bfloat16
+    out = {}
+    for P in protos:
+        for B in batches:
+            s = LayerStep(B, args.channels, args.fmap, args.fmap, P, args.classes, x_dtype, device, SEED,
+                          args.precision)
+            e, k, a = time_layer(s, args.steps, args.warmup, 1, args.launch == "graph")
+            out[f"B{B}_P{P}"] = {"img_per_s": round(B * args.steps / e, 1), "ms_per_step": round(e / args.steps * 1e3, 4),
+                                 "kernels_ms": {a[n]: round(v * 1e3, 4) for n, v in k.items()}}
+            del s
+    return out
+
+
+def time_train_step(args, device, rank, world, accumulations=1, warm_accumulations=1, batch=4, P=190):
+    """BASELINE configs[2] (cityscapes_kld_imnet.gin) end to end, data-parallel: PPNet on the
+    in-tree DeepLabV2-ResNet101 (random init; deeplab_n_features 64, scales [], deeplab_simple
+    add-on), synthetic 513x513 batches of `batch` images per GPU with 19-class labels (0 = void),
+    train.PatchClassificationStep (module.py:118-243): cross entropy + KLD (0.25) + L1, loss /
+    iter_size backward, every iter_size = 5 micro-steps the bucketed RCCL all-reduce of the whole
+    gradient (GradientBuckets, launched from the backward's hooks) and the joint-phase Adam
+    (module.py:357-391, weight decay 5e-4) on the HIP kernel. Times `accumulations` optimizer
+    steps (x iter_size micro-steps) after `warm_accumulations`, between barriers; max over ranks."""
+    from protoseg_amd.deeplab import deeplabv2_resnet101_features
+    from protoseg_amd.model import construct_PPNet
+    from protoseg_amd.optim import Adam
+    from protoseg_amd.train import PatchClassificationStep, joint_param_groups
+    iter_size = 5
+    torch.manual_seed(SEED)  # identical initial weights on every rank
+    feats = deeplabv2_resnet101_features(pretrained=False, deeplab_n_features=64, scales=[])
+    net = construct_PPNet(img_size=513, prototype_shape=(P, 64, 1, 1), num_classes=args.classes,
+                          prototype_activation_function="log", add_on_layers_type="deeplab_simple",
+                          features=feats, bottleneck_stride=1, patch_classification=True).to(device)
+    net.train()
+    net.features.base.freeze_bn()  # module.py:127
+    opt = Adam(joint_param_groups(net))
+    step = PatchClassificationStep(net, opt, loss_weight_kld=0.25, loss_weight_l1=1e-4, iter_size=iter_size)
+    grad_mb = sum(p.numel() * p.element_size() for p in step.buckets.params) / 2 ** 20
+    gen = torch.Generator().manual_seed(SEED + 11 + rank)
+    images = torch.randn(iter_size, batch, 3, 513, 513, generator=gen).to(device)
+    blocks = torch.randint(0, args.classes + 1, (iter_size, batch, 33, 33), generator=gen)
+    targets = blocks.repeat_interleave(16, 2).repeat_interleave(16, 3)[:, :, :513, :513].contiguous().to(device)
+
+    def run(n_acc):
+        for _ in range(n_acc):
+            for i in range(iter_size):
+                step(images[i], targets[i])
+
+    run(warm_accumulations)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    run(accumulations)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    micro = accumulations * iter_size
+    return {"workload": "cityscapes_kld_imnet DP training step: DeepLabV2-R101 (PyTorch-ROCm) + prototype layer and "
+                        "KLD (HIP) + bucketed RCCL gradient all-reduce + HIP Adam, synthetic 513x513",
+            "img_per_s": round(world * batch * micro / elapsed, 2), "n_gpus": world, "per_gpu_batch": batch,
+            "global_batch": world * batch, "iter_size": iter_size, "prototypes": P,
+            "ms_per_micro_step": round(elapsed / micro * 1e3, 2),
+            "ms_per_optimizer_step": round(elapsed / accumulations * 1e3, 2),
+            "micro_steps_timed": micro, "grad_exchange_mb": round(grad_mb, 1),
+            "buckets": len(step.buckets.buckets), "backbone_dtype": "f32"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -735,7 +864,20 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="push CPU baseline time budget")
     ap.add_argument("--launch", choices=["graph", "eager"], default="graph",
                     help="graph: each step is one HIP graph replay of the three C-ABI calls")
+    ap.add_argument("--no-small-batch", action="store_true", help="skip the B=2/4 side lines")
+    ap.add_argument("--no-train", action="store_true", help="skip the DeepLabV2-R101 DP training-step side line")
+    ap.add_argument("--train-accumulations", type=int, default=1,
+                    help="optimizer steps (x iter_size 5 micro-steps) timed in the training side line")
+    ap.add_argument("--cpu-smoke", action="store_true",
+                    help="no GPU: launch the ranks and time only the gloo gradient exchange (launcher test)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: start the N ranks here, before any GPU call, and report theirs
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.cpu_smoke:
+        cpu_smoke(args, *init_from_env("gloo")[::2])
+        return
 
     rank, local_rank, world = init_from_env()
     if world != args.gpus and rank == 0:
@@ -786,6 +928,12 @@ def main():
     bboxes = None
     if not args.no_push and world == 1:
         bboxes = time_bound_boxes(3, 1, device)
+    small = None
+    if not args.no_small_batch and world == 1:
+        small = time_small_batches(args, device)
+    train = None
+    if not args.no_train:
+        train = time_train_step(args, device, rank, world, args.train_accumulations)
 
     if rank == 0:
         roof, kernels = layer_report(step, per_kernel, actual, args)
@@ -831,6 +979,10 @@ def main():
             out["eval"] = evaluation
         if bboxes is not None:
             out["push"]["bound_boxes"] = bboxes
+        if small is not None:
+            out["small_batch"] = small
+        if train is not None:
+            out["train_step"] = train
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_layer_baseline(args.batch, args.channels, args.fmap, args.fmap, args.protos,
                                                      args.classes)
