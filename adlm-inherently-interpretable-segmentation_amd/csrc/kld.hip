@@ -55,6 +55,9 @@ struct KldLayout {
   size_t part;   // float [B * K * S * kKldPartFloats]: per pixel-range partials
   size_t group;  // float [B * K * 2]: per (image, class) sum of exp(-kld) and pair count
   size_t stat;   // int [4]: [0] pair count, [1] a class holds more than max_per_class prototypes
+  size_t slot;   // int [P]: bucket * 256 + position in the bucket (the compact gradient's column)
+  size_t rcnt;   // int [B * K * S]: class pixels in each 1024-pixel range
+  size_t plist;  // int [B * K * HW]: per (image, class) the class pixels of range s at s * 1024 + q
   size_t total;
 };
 
@@ -78,6 +81,12 @@ KldLayout kld_layout(int B, int P, int HW, int K) {
   o = align256(o + static_cast<size_t>(B) * K * 2 * 4);
   l.stat = o;
   o = align256(o + 16);
+  l.slot = o;
+  o = align256(o + static_cast<size_t>(P) * 4);
+  l.rcnt = o;
+  o = align256(o + static_cast<size_t>(B) * K * kld_ranges(HW) * 4);
+  l.plist = o;
+  o = align256(o + static_cast<size_t>(B) * K * HW * 4);
   l.total = o;
   return l;
 }
@@ -85,6 +94,7 @@ KldLayout kld_layout(int B, int P, int HW, int K) {
 struct KldPtrs {
   int *off, *idx, *cnt, *stat;
   float *lse, *kl, *part, *group;
+  int *slot, *rcnt, *plist;
 };
 
 KldPtrs kld_ptrs(void* ws, const KldLayout& l) {
@@ -92,7 +102,9 @@ KldPtrs kld_ptrs(void* ws, const KldLayout& l) {
   return {reinterpret_cast<int*>(b + l.off),    reinterpret_cast<int*>(b + l.idx),
           reinterpret_cast<int*>(b + l.cnt),    reinterpret_cast<int*>(b + l.stat),
           reinterpret_cast<float*>(b + l.lse),  reinterpret_cast<float*>(b + l.kl),
-          reinterpret_cast<float*>(b + l.part), reinterpret_cast<float*>(b + l.group)};
+          reinterpret_cast<float*>(b + l.part), reinterpret_cast<float*>(b + l.group),
+          reinterpret_cast<int*>(b + l.slot),   reinterpret_cast<int*>(b + l.rcnt),
+          reinterpret_cast<int*>(b + l.plist)};
 }
 
 __device__ __forceinline__ int bucket_of(int pc, int K) { return (pc >= 0 && pc < K) ? pc : K; }
@@ -104,7 +116,8 @@ __device__ __forceinline__ int bucket_of(int pc, int K) { return (pc >= 0 && pc 
 constexpr int kKldListMaxP = 1 << 20;
 __global__ __launch_bounds__(64) void kld_lists_kernel(const int32_t* __restrict__ proto_class, int P, int K,
                                                        int max_per_class, int* __restrict__ off,
-                                                       int* __restrict__ idx, int* __restrict__ stat) {
+                                                       int* __restrict__ idx, int* __restrict__ stat,
+                                                       int* __restrict__ slot) {
   // Bucket c's running count and write position live in lane c's registers (no LDS, no
   // barriers): ballots give each chunk's members, a broadcast of lane c gives their base.
   const int lane = threadIdx.x;
@@ -134,11 +147,12 @@ __global__ __launch_bounds__(64) void kld_lists_kernel(const int32_t* __restrict
     for (int c = 0; c <= K; ++c) {
       const unsigned long long m = __ballot(bk == c);
       if (m == 0ull) continue;  // uniform
-      const int base = __shfl(next, c);
+      const int base = __shfl(next, c), start = __shfl(incl - cnt, c);
       if (bk == c) {
         const int below = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
                                                     __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0));
         idx[base + below] = p;
+        slot[p] = c * 256 + (base + below - start);  // the prototype's column of the compact gradient
       }
       if (lane == c) next += __popcll(m);
     }
@@ -154,6 +168,33 @@ __device__ __forceinline__ long long label_at(const TL* lab, int n) {
   return static_cast<long long>(lab[n]);
 }
 
+__device__ __forceinline__ int lane_rank(unsigned long long m) {  // set bits of m below this lane
+  return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0));
+}
+
+// Gathers rows[i][q] = d[s_proto[i]][list[q]] for i < npc, q < kq over the workgroup's threads
+// (q fastest: consecutive lanes read consecutive class pixels of one prototype row), four loads
+// in flight per thread.
+__device__ __forceinline__ void gather_tasks(const float* __restrict__ db, int HW, const int* list, int kq,
+                                             const int* s_proto, int npc, float* rows, int stride) {
+  const int T = npc * kq;
+  for (int t0 = threadIdx.x; t0 < T; t0 += 4 * kKldThreads) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + u * kKldThreads;
+      const int i = t / kq, q = t - i * kq;
+      v[u] = t < T ? db[static_cast<size_t>(s_proto[i]) * HW + list[q]] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + u * kKldThreads;
+      const int i = t / kq, q = t - i * kq;
+      if (t < T) rows[i * stride + q] = v[u];
+    }
+  }
+}
+
 // Merge of two (max, sum exp(. - max)) pairs; an empty side is (-inf, 0).
 __device__ __forceinline__ void lse_merge(float& m, float& s, float mo, float so) {
   const float mm = fmaxf(m, mo);
@@ -161,40 +202,86 @@ __device__ __forceinline__ void lse_merge(float& m, float& s, float mo, float so
   m = mm;
 }
 
-// One workgroup per (class c, image b, pixel range s). LDS (dynamic): [mpc][257] e | [mpc][257] z.
-// ONE pass over the range (online log-sum-exp): per 256-pixel chunk the class pixels' distances
-// are compacted into LDS, the chunk's max per prototype updates the running max m_i, the
-// accumulators S_i = sum e_i and T_ij = sum e_i (z_i - z_j) (e_i = exp(z_i - m_i)) are rescaled
-// by exp(m_old - m_new), and the chunk is added. The range partial (m_i, S_i, T_ij, count) is the
-// one a separate max pass would give, up to rounding.
+// One workgroup per (class c, image b, pixel range s of 1024). The range's class pixels are
+// compacted once (ballots, one prefix over the (row, wave) counts: pixel order kept) into an LDS
+// list, which also goes to plist / rcnt for the backward. Then ONE pass over the list (online
+// log-sum-exp): per chunk of 256 class pixels the distances are gathered into LDS, the chunk's
+// max per prototype updates the running max m_i, the accumulators S_i = sum e_i and T_ij = sum
+// e_i (z_i - z_j) (e_i = exp(z_i - m_i)) are rescaled by exp(m_old - m_new), and the chunk is
+// added. The range partial (m_i, S_i, T_ij, count) is the one a separate max pass would give, up
+// to rounding. LDS (dynamic): [mpc][257] e | [mpc][257] z.
 template <typename TL>
 __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* __restrict__ dist, int P, int HW,
                                                                   const TL* __restrict__ label, int K, int mpc,
                                                                   const int* __restrict__ off,
-                                                                  const int* __restrict__ idx, float* __restrict__ part) {
+                                                                  const int* __restrict__ idx,
+                                                                  float* __restrict__ part, int* __restrict__ rcnt,
+                                                                  int* __restrict__ plist) {
   extern __shared__ __attribute__((aligned(16))) float kld_smem[];
   __shared__ int s_proto[kKldMaxPerClass];
   __shared__ float s_m[kKldMaxPerClass];
   __shared__ float s_scale[kKldMaxPerClass];
-  __shared__ int s_cnt[4];
+  __shared__ int s_wc[kKldRange / 64];
+  __shared__ int s_list[kKldRange];
+  constexpr int kRows = kKldRange / kKldThreads;
   const int c = blockIdx.x, b = blockIdx.y, rs = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int o0 = off[c];
   const int npc_all = off[c + 1] - o0;
   const int npc = npc_all < mpc ? npc_all : mpc;
-  float* out = part + ((static_cast<size_t>(b) * K + c) * gridDim.z + rs) * kKldPartFloats;
+  const size_t bc = static_cast<size_t>(b) * K + c;
+  float* out = part + (bc * gridDim.z + rs) * kKldPartFloats;
+  int* rc = rcnt + bc * gridDim.z + rs;
   if (npc < 1 || npc_all > mpc) {  // no prototype of the class, or the overflow case (loss is NaN)
-    if (tid == 0) out[2 * kKldMaxPerClass] = 0.f;
+    if (tid == 0) {
+      out[2 * kKldMaxPerClass] = 0.f;
+      *rc = 0;
+    }
     return;
+  }
+  const TL* lab = label + static_cast<size_t>(b) * HW;
+  const int n0 = rs * kKldRange, n1 = min(HW, n0 + kKldRange);
+  bool in[kRows];
+  int below[kRows];
+#pragma unroll
+  for (int r = 0; r < kRows; ++r) {  // all label loads in flight together
+    const int n = n0 + r * kKldThreads + tid;
+    in[r] = n < n1 && label_at(lab, n) == c;
+  }
+#pragma unroll
+  for (int r = 0; r < kRows; ++r) {
+    const unsigned long long bal = __ballot(in[r]);
+    below[r] = lane_rank(bal);
+    if (lane == 0) s_wc[r * (kKldThreads / 64) + wave] = __popcll(bal);
   }
   if (tid < npc) {
     s_proto[tid] = idx[o0 + tid];
     s_m[tid] = -INFINITY;
   }
   __syncthreads();
-  const TL* lab = label + static_cast<size_t>(b) * HW;
+  int total = 0;
+  int* pl = plist + bc * HW + n0;
+#pragma unroll
+  for (int r = 0; r < kRows; ++r) {
+    int pos = total + below[r];
+    for (int w = 0; w < kKldThreads / 64; ++w) {
+      const int v = s_wc[r * (kKldThreads / 64) + w];
+      pos += w < wave ? v : 0;
+      total += v;
+    }
+    if (in[r]) {
+      const int n = n0 + r * kKldThreads + tid;
+      s_list[pos] = n;
+      pl[pos] = n;
+    }
+  }
+  if (tid == 0) *rc = total;
+  if (total == 0) {  // uniform
+    if (tid == 0) out[2 * kKldMaxPerClass] = 0.f;
+    return;
+  }
+  __syncthreads();
   const float* db = dist + static_cast<size_t>(b) * P * HW;
-  const int n0 = rs * kKldRange, n1 = min(HW, n0 + kKldRange);
 
   float* se = kld_smem;                          // [npc][257]
   float* sz = kld_smem + npc * kKldLdsStride;    // [npc][257]
@@ -203,27 +290,9 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
   G = G < 1 ? 1 : (G > 16 ? 16 : G);
   const int ntask = E * G;  // <= 1024
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  int total = 0;
-  for (int base = n0; base < n1; base += kKldThreads) {
-    // the chunk's class pixels, compacted in pixel order (wave ballots + prefix)
-    const int n = base + tid;
-    const bool in = n < n1 && label_at(lab, n) == c;
-    const unsigned long long bal = __ballot(in);
-    const int below = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(bal >> 32),
-                                                __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(bal), 0));
-    if (lane == 0) s_cnt[wave] = __popcll(bal);
-    __syncthreads();
-    const int kq = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
-    if (kq == 0) {  // uniform: no pixel of the class in this chunk
-      __syncthreads();
-      continue;
-    }
-    total += kq;
-    if (in) {
-      int pos = below;
-      for (int w = 0; w < wave; ++w) pos += s_cnt[w];
-      for (int i = 0; i < npc; ++i) sz[i * kKldLdsStride + pos] = db[static_cast<size_t>(s_proto[i]) * HW + n];
-    }
+  for (int base = 0; base < total; base += kKldThreads) {
+    const int kq = min(kKldThreads, total - base);
+    gather_tasks(db, HW, s_list + base, kq, s_proto, npc, sz, kKldLdsStride);
     __syncthreads();
     {  // chunk max per prototype (8 threads per row) -> running max and the rescale factor
       const int i = tid >> 3, l8 = tid & 7;
@@ -271,7 +340,6 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
     __syncthreads();
   }
   if (tid == 0) out[2 * kKldMaxPerClass] = static_cast<float>(total);
-  if (total == 0) return;  // uniform
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int task = tid + k * kKldThreads;
@@ -460,6 +528,85 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_kernel(
   }
 }
 
+// The same gradient in the compact layout the layer backward expands (l2_bwd_fused /
+// l2_bwd_onepass, protoseg_l2_bwd_kld): g_cls[g][slot] (g = b * HW + n, slot = the prototype's
+// position in its class) at each pixel of a contributing (image, class) group, pix_cls[g] = that
+// class. pix_cls is set to -1 everywhere first (one memset); one workgroup per (class c, image
+// b, pixel range s) of a contributing group then walks the range's class-pixel list the forward
+// left in plist, thread = pixel. LDS (dynamic): [mpc][257] p | [mpc][257] log p (each thread its
+// own column) | the group's (w_ij, KL_ij) pairs.
+__global__ __launch_bounds__(kKldThreads) void kld_grad_compact_kernel(
+    const float* __restrict__ dist, int P, int HW, int K, int mpc, const int* __restrict__ off,
+    const int* __restrict__ idx, const int* __restrict__ cnt, const float* __restrict__ lse,
+    const float2* __restrict__ coef, const int* __restrict__ stat, const int* __restrict__ rcnt,
+    const int* __restrict__ plist, float* __restrict__ g_cls, int32_t* __restrict__ pix_cls) {
+  extern __shared__ __attribute__((aligned(16))) float kld_smem[];
+  __shared__ int s_proto[kKldMaxPerClass];
+  __shared__ float s_lse[kKldMaxPerClass];
+  const int c = blockIdx.x, b = blockIdx.y, rs = blockIdx.z, tid = threadIdx.x;
+  const size_t bc = static_cast<size_t>(b) * K + c;
+  const int q1 = rcnt[bc * gridDim.z + rs];
+  if (q1 == 0) return;
+  const int o0 = off[c];
+  const int npc = off[c + 1] - o0;
+  if (npc < 2 || npc > mpc || stat[0] == 0 || cnt[bc] < 2) return;  // uniform: the group adds no pair
+  const int* pl = plist + bc * HW + rs * kKldRange;
+  int32_t* pc = pix_cls + static_cast<size_t>(b) * HW;
+  float* sp = kld_smem;
+  float* slp = sp + mpc * kKldLdsStride;
+  float2* scoef = reinterpret_cast<float2*>(slp + mpc * kKldLdsStride);
+  const float2* cb = coef + (static_cast<size_t>(b) * K + c) * kKldPair;
+  for (int e = tid; e < npc * npc; e += kKldThreads) scoef[e] = cb[e];
+  if (tid < npc) {
+    s_proto[tid] = idx[o0 + tid];
+    s_lse[tid] = lse[static_cast<size_t>(b) * P + idx[o0 + tid]];
+  }
+  __syncthreads();
+  const float* db = dist + static_cast<size_t>(b) * P * HW;
+  for (int base = 0; base < q1; base += kKldThreads) {  // chunks of 256 class pixels
+    const int kq = min(kKldThreads, q1 - base);
+    const int* lq = pl + base;
+    gather_tasks(db, HW, lq, kq, s_proto, npc, slp, kKldLdsStride);
+    for (int q = tid; q < kq; q += kKldThreads) pc[lq[q]] = c;
+    __syncthreads();
+    for (int t = tid; t < npc * kq; t += kKldThreads) {
+      const int i = t / kq, q = t - i * kq;
+      const float lp = slp[i * kKldLdsStride + q] - s_lse[i];
+      slp[i * kKldLdsStride + q] = lp;
+      sp[i * kKldLdsStride + q] = expf(lp);
+    }
+    __syncthreads();
+    // one task per (pixel, class slot), slot fastest: a pixel's row of g_cls is written by
+    // consecutive lanes
+    for (int t = tid; t < npc * kq; t += kKldThreads) {
+      const int q = t / npc, i = t - q * npc;
+      const float pi = sp[i * kKldLdsStride + q], li = slp[i * kKldLdsStride + q];
+      float g = 0.f;
+      for (int j = 0; j < npc; ++j) {
+        const float2 wk = scoef[i * npc + j];  // (w_ij, KL_ij); w_ii = 0
+        g = fmaf(wk.x, pi * (li - slp[j * kKldLdsStride + q] - wk.y + 1.f) - sp[j * kKldLdsStride + q], g);
+      }
+      g_cls[(static_cast<size_t>(b) * HW + lq[q]) * mpc + i] = 0.5f * g;
+    }
+    __syncthreads();
+  }
+}
+
+// Dense g_dist from the compact layout (protoseg_kld_expand): one thread per (image, prototype,
+// pixel), row segments coalesced.
+__global__ __launch_bounds__(256) void kld_expand_kernel(const float* __restrict__ g_cls,
+                                                         const int32_t* __restrict__ pix_cls,
+                                                         const int32_t* __restrict__ proto_slot, int P, int HW,
+                                                         int mpc, int accumulate, float* __restrict__ g_dist) {
+  const int n = blockIdx.x * 256 + threadIdx.x, p = blockIdx.y, b = blockIdx.z;
+  if (n >= HW) return;
+  const size_t g = static_cast<size_t>(b) * HW + n;
+  const int sl = proto_slot[p];
+  const float v = pix_cls[g] == (sl >> 8) ? g_cls[g * mpc + (sl & 255)] : 0.f;
+  float* o = g_dist + (static_cast<size_t>(b) * P + p) * HW + n;
+  *o = accumulate ? *o + v : v;
+}
+
 int kld_check(const float* dist, int B, int P, int HW, const void* label, int label_dtype, const int32_t* proto_class,
               int K, int max_per_class, const void* ws, size_t ws_bytes) {
   if (!dist || !label || !proto_class || !ws) return fail(PROTOSEG_ERR_INVALID, "null pointer argument");
@@ -512,14 +659,15 @@ extern "C" int protoseg_kld_forward(const float* dist, int B, int P, int HW, con
   const KldLayout l = kld_layout(B, P, HW, K);
   const KldPtrs w = kld_ptrs(workspace, l);
   const int S = kld_ranges(HW);
-  hipLaunchKernelGGL(kld_lists_kernel, dim3(1), dim3(64), 0, s, proto_class, P, K, max_per_class, w.off, w.idx, w.stat);
+  hipLaunchKernelGGL(kld_lists_kernel, dim3(1), dim3(64), 0, s, proto_class, P, K, max_per_class, w.off, w.idx, w.stat,
+                     w.slot);
   if (int st = check_launch("kld_lists_kernel")) return st;
   const size_t lds = static_cast<size_t>(2) * max_per_class * kKldLdsStride * sizeof(float);
   const int st = by_label(label_dtype, [&](auto tl) {
     using TL = std::remove_pointer_t<decltype(tl)>;
     if (int e = ensure_lds<kld_partial_kernel<TL>, kKldMaxDynLds>()) return e;
     hipLaunchKernelGGL(kld_partial_kernel<TL>, dim3(K, B, S), dim3(kKldThreads), lds, s, dist, P, HW,
-                       static_cast<const TL*>(label), K, max_per_class, w.off, w.idx, w.part);
+                       static_cast<const TL*>(label), K, max_per_class, w.off, w.idx, w.part, w.rcnt, w.plist);
     return check_launch("kld_partial_kernel");
   });
   if (st) return st;
@@ -555,4 +703,43 @@ extern "C" int protoseg_kld_backward(const float* dist, int B, int P, int HW, co
                        g_dist);
     return check_launch("kld_grad_kernel");
   });
+}
+
+extern "C" int protoseg_kld_backward_compact(const float* dist, int B, int P, int HW, const void* label,
+                                             int label_dtype, const int32_t* proto_class, int K, int max_per_class,
+                                             const float* g_loss, void* workspace, size_t workspace_bytes,
+                                             float* g_cls, int32_t* pix_cls, int32_t* proto_slot,
+                                             protoseg_stream_t stream) {
+  if (int st = kld_check(dist, B, P, HW, label, label_dtype, proto_class, K, max_per_class, workspace, workspace_bytes))
+    return st;
+  if (!g_cls || !pix_cls || !proto_slot) return fail(PROTOSEG_ERR_INVALID, "g_cls, pix_cls and proto_slot must be non-null");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const KldLayout l = kld_layout(B, P, HW, K);
+  const KldPtrs w = kld_ptrs(workspace, l);
+  if (hipMemcpyAsync(proto_slot, w.slot, static_cast<size_t>(P) * 4, hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return check_launch("proto_slot copy");
+  float2* coef = reinterpret_cast<float2*>(w.part);
+  hipLaunchKernelGGL(kld_coef_kernel, dim3(K, B), dim3(64), 0, s, K, max_per_class, w.off, w.cnt, w.kl, w.stat, g_loss,
+                     coef);
+  if (int st = check_launch("kld_coef_kernel")) return st;
+  const size_t lds = static_cast<size_t>(2) * max_per_class * kKldLdsStride * sizeof(float) +
+                     static_cast<size_t>(max_per_class) * max_per_class * sizeof(float2);
+  if (int e = ensure_lds<kld_grad_compact_kernel, kKldMaxDynLds + kKldPair * sizeof(float2)>()) return e;
+  if (hipMemsetAsync(pix_cls, 0xFF, static_cast<size_t>(B) * HW * 4, s) != hipSuccess)  // -1: no gradient
+    return check_launch("pix_cls memset");
+  hipLaunchKernelGGL(kld_grad_compact_kernel, dim3(K, B, kld_ranges(HW)), dim3(kKldThreads), lds, s, dist, P, HW, K,
+                     max_per_class, w.off, w.idx, w.cnt, w.lse, coef, w.stat, w.rcnt, w.plist, g_cls, pix_cls);
+  return check_launch("kld_grad_compact_kernel");
+}
+
+extern "C" int protoseg_kld_expand(const float* g_cls, const int32_t* pix_cls, const int32_t* proto_slot, int B, int P,
+                                   int HW, int max_per_class, int accumulate, float* g_dist, protoseg_stream_t stream) {
+  if (!g_cls || !pix_cls || !proto_slot || !g_dist) return fail(PROTOSEG_ERR_INVALID, "null pointer argument");
+  if (B <= 0 || P <= 0 || HW <= 0 || max_per_class < 1 || max_per_class > kKldMaxPerClass)
+    return fail(PROTOSEG_ERR_INVALID, "bad shape B=%d P=%d HW=%d max_per_class=%d", B, P, HW, max_per_class);
+  if (P > 65535) return fail(PROTOSEG_ERR_UNSUPPORTED, "P=%d > 65535", P);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(kld_expand_kernel, dim3(static_cast<unsigned>(ceil_div(HW, 256)), P, B), dim3(256), 0, s, g_cls,
+                     pix_cls, proto_slot, P, HW, max_per_class, accumulate, g_dist);
+  return check_launch("kld_expand_kernel");
 }

@@ -70,13 +70,15 @@ constexpr int kMaxPp = kOwners * 32;        // prototypes per launch
 // lands zero-extended in a dword), then g_logits as the tile's flat [32 n][K] run (K <= 32).
 constexpr int kRawPiece = 68;
 constexpr int kRawXDw = 32 * kRawPiece;
-constexpr int kRawSlot = (kRawXDw + 32 * 32) * 4;  // 12,800 B
+// + 64 dwords: the tile's KLD pixel classes (compact g_dist, GD = 2; one 64-lane DMA)
+constexpr int kRawClsDw = kRawXDw + 32 * 32;
+constexpr int kRawSlot = (kRawClsDw + 64) * 4;  // 13,056 B
 __device__ __forceinline__ constexpr int raw_x(int c, int n) { return (c >> 1) * kRawPiece + (c & 1) * 32 + n; }
 
 // LDS regions (bytes). The (-2P) and W^T images are adjacent, as in the operand-image block,
 // so one LDS-DMA copy fills both.
 struct FusedLds {
-  int pimg, wtimg, xa, ga, x2s, rowoff, gs, raw, total;
+  int pimg, wtimg, xa, ga, x2s, rowoff, rcls, gs, raw, total;
 };
 __host__ __device__ inline FusedLds fused_lds(int Pp) {
   FusedLds o;
@@ -86,7 +88,8 @@ __host__ __device__ inline FusedLds fused_lds(int Pp) {
   o.ga = o.xa + 2 * kT * 32 * 64 * 2;   // [2 slots][T][32 n][32 k] bf16, CPR 4
   o.x2s = o.ga + 2 * kT * 32 * 32 * 2;  // [2 slots][32] f32: ||x||^2 per pixel
   o.rowoff = o.x2s + 2 * 32 * 4;        // [2 slots][32] u32: g_dist byte offset per pixel
-  o.gs = o.rowoff + 2 * 32 * 4;         // [2 slots][T][Pp][32 n] bf16, 8-B slots swizzled
+  o.rcls = o.rowoff + 2 * 32 * 4;       // [2 slots][32] int: KLD pixel class (GD = 2)
+  o.gs = o.rcls + 2 * 32 * 4;           // [2 slots][T][Pp][32 n] bf16, 8-B slots swizzled
   o.total = o.gs + 2 * kT * Pp * 64;
   // Raw tiles (LDS-DMA targets, 2 slots). The operand images are read into registers in the
   // prologue, so their region is free afterwards and holds the raw slots when it is big enough.
@@ -129,11 +132,13 @@ __device__ __forceinline__ constexpr int chan_of_col(int u) { return chan_of(u >
 // the launch when known at compile time (6: Pp = 192, every chunk at P = 190 / 361 / 570), else
 // 0 (read from Pp): with it the x waves' g_x loop is one straight-line block instead of a
 // branch per prototype tile (each branch a scheduling boundary with its own s_waitcnt).
-template <typename TX, int ACT, bool GD, bool XSIG, int NPT>
+// GD: 0 no distance gradient, 1 a dense g_dist, 2 the KLD loss's compact one (CompactGd).
+template <typename TX, int ACT, int GD, bool XSIG, int NPT>
 __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
     const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const unsigned char* __restrict__ img, int P, int Pp,
     int K, float eps, const float* __restrict__ g_logits, unsigned gl_bytes, const float* __restrict__ g_dist,
-    unsigned gd_bytes, int gd_ld, int gd_p0, TX* __restrict__ g_x, int accumulate, float* __restrict__ slab) {
+    unsigned gd_bytes, int gd_ld, int gd_p0, CompactGd cg, TX* __restrict__ g_x, int accumulate,
+    float* __restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const FusedLds L = fused_lds(Pp);
   const ImgOffsets io = img_offsets(Pp, kT);
@@ -147,12 +152,15 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
   const int xw = wave - kOwners;  // x wave index (channel tile), valid when !owner
   const unsigned sz = sizeof(TX);
   const rsrc_t rx = make_rsrc(x, x_bytes), rg = make_rsrc(g_logits, gl_bytes);
-  const rsrc_t rgd = make_rsrc(g_dist, gd_bytes), rgx = make_rsrc(g_x, g_x ? x_bytes : 0u);
+  // GD = 2: g_dist points at the compact values (gd_bytes = npix * mpc * 4)
+  const rsrc_t rgd = make_rsrc(GD == 2 ? cg.val : g_dist, gd_bytes), rgx = make_rsrc(g_x, g_x ? x_bytes : 0u);
+  const rsrc_t rpc = make_rsrc(cg.pix, GD == 2 ? static_cast<unsigned>(npix) * 4u : 0u);
   auto tile_of = [&](int i) __attribute__((always_inline)) { return static_cast<int>(blockIdx.x) + i * static_cast<int>(gridDim.x); };
   auto xa_slot = [&](int sb) __attribute__((always_inline)) { return reinterpret_cast<bf16*>(smem_raw + L.xa) + sb * kT * 32 * kC; };
   auto ga_slot = [&](int sb) __attribute__((always_inline)) { return reinterpret_cast<bf16*>(smem_raw + L.ga) + sb * kT * 32 * 32; };
   auto x2_slot = [&](int sb) __attribute__((always_inline)) { return reinterpret_cast<float*>(smem_raw + L.x2s) + sb * 32; };
   auto ro_slot = [&](int sb) __attribute__((always_inline)) { return reinterpret_cast<unsigned*>(smem_raw + L.rowoff) + sb * 32; };
+  auto cl_slot = [&](int sb) __attribute__((always_inline)) { return reinterpret_cast<int*>(smem_raw + L.rcls) + sb * 32; };
   auto gs_slot = [&](int sb) __attribute__((always_inline)) { return reinterpret_cast<bf16*>(smem_raw + L.gs) + sb * kT * Pp * 32; };
 
   // ---- staging (all 8 waves) ------------------------------------------------------------------
@@ -179,6 +187,13 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
     for (int m = wave; m * 64 < 32 * K; m += 8)
       dma<float>(rg, RG + m * 64, m * 64 + lane < lim ? static_cast<unsigned>(lane * 4) : kOOB,
                  static_cast<unsigned>((t * 32 * K + m * 64) * 4));
+    if constexpr (GD == 2) {  // the tile's 32 contiguous pixel classes (lanes past them land 0)
+      if (wave == kOwners + kXWaves - 1) {
+        const int valid = t < ntiles ? min(32, npix - t * 32) : 0;
+        dma<float>(rpc, R + kRawClsDw, lane < valid ? static_cast<unsigned>(lane * 4) : kOOB,
+                   static_cast<unsigned>(t * 32 * 4));
+      }
+    }
   };
   // Raw slot rs -> split images of slot sb, pixels 4 wave .. 4 wave + 3 per wave: lanes 0..31
   // the 8 XA chunks of a pixel (lane = 8 (pixel) + chunk 2q + hh: channels chan_of(q, hh, 0..7)),
@@ -212,12 +227,19 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
       for (int e = 0; e < 8; ++e) v[e] = 8 * kc + e < K ? RG[n * K + 8 * kc + e] : 0.f;
       split8<kT>(v, f);
       store_frag<kT>(ga_slot(sb), 32 * 32, img_off<4>(n, kc), f);
-      if constexpr (GD) {
+      if constexpr (GD == 1) {
         if (kc == 0) {
           const int g = t * 32 + n;
           const bool ok = t < ntiles && g < npix;
           const int b = ok ? g / HW : 0;
           ro_slot(sb)[n] = ok ? static_cast<unsigned>(((b * gd_ld + gd_p0) * HW + (g - b * HW)) * 4) : kOOB;
+        }
+      } else if constexpr (GD == 2) {
+        if (kc == 0) {  // the pixel's compact row and class
+          const int g = t * 32 + n;
+          const int cl = (t < ntiles && g < npix) ? reinterpret_cast<const int*>(R + kRawClsDw)[n] : -1;
+          ro_slot(sb)[n] = cl >= 0 ? static_cast<unsigned>(g * cg.mpc * 4) : kOOB;
+          cl_slot(sb)[n] = cl;
         }
       }
     }
@@ -236,6 +258,14 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
   const int p = (owner ? wave : 0) * 32 + j;
   const bool pvalid = p < P;
   const float p2 = owner ? reinterpret_cast<const float*>(img + io.p2)[p] : 0.f;
+  int pcls = -2, pslot = 0;  // GD = 2: this lane's prototype's class (-2: none) and compact column
+  if constexpr (GD == 2) {
+    if (owner && pvalid) {
+      const int code = cg.slot[gd_p0 + p];
+      pcls = code >> 8;
+      pslot = (code & 255) * 4;
+    }
+  }
   // this wave's prototype-tile B fragments of S and g_act (registers, loaded in the prologue)
   bf16x8 preg[kNQ][kT], wreg[2][kT];
   auto owner_tile = [&](int sb, bool stamp) __attribute__((always_inline)) {
@@ -243,7 +273,14 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
     const bf16* GA = ga_slot(sb);
     float x2r[16], gdv[16];
     load_rows16(x2_slot(sb) + 4 * h, x2r);
-    if constexpr (GD) {
+    if constexpr (GD == 2) {
+      float rof[16], clf[16];
+      load_rows16(reinterpret_cast<const float*>(ro_slot(sb)) + 4 * h, rof);
+      load_rows16(reinterpret_cast<const float*>(cl_slot(sb)) + 4 * h, clf);
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        gdv[r] = BufIO<float>::load(rgd, __float_as_int(clf[r]) == pcls ? __float_as_uint(rof[r]) + pslot : kOOB, 0);
+    } else if constexpr (GD == 1) {
       float rof[16];
       load_rows16(reinterpret_cast<const float*>(ro_slot(sb)) + 4 * h, rof);
       const unsigned pcol = static_cast<unsigned>(p * HW * 4);
@@ -560,18 +597,20 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
   }
 }
 
-template <typename TX, int ACT, bool GD, bool XSIG, int NPT>
+template <typename TX, int ACT, int GD, bool XSIG, int NPT>
 int fused_t(const Geometry& g, const void* x, const unsigned char* img, float eps, const float* g_logits,
             const float* g_dist, void* g_x, int accumulate, float* ws, int grid, hipStream_t stream) {
   if (int st = ensure_lds<l2_bwd_fused_bf16_kernel<TX, ACT, GD, XSIG, NPT>>()) return st;
   const unsigned long long npix = static_cast<unsigned long long>(g.npix);
   const unsigned xb = static_cast<unsigned>(npix * kC * sizeof(TX));
   const unsigned glb = g_logits ? static_cast<unsigned>(npix * g.K * 4) : 0u;
-  const unsigned gdb = g_dist ? static_cast<unsigned>(npix * g.ldd * 4) : 0u;
+  const unsigned gdb = GD == 2 ? static_cast<unsigned>(npix * g.cgd.mpc * 4)
+                               : g_dist ? static_cast<unsigned>(npix * g.ldd * 4) : 0u;
   KernelTimer timer("l2_bwd_fused_bf16_kernel", stream);
   hipLaunchKernelGGL((l2_bwd_fused_bf16_kernel<TX, ACT, GD, XSIG, NPT>), dim3(grid), dim3(kThreads),
                      static_cast<size_t>(fused_lds(g.Pp).total), stream, static_cast<const TX*>(x), xb, g.HW, g.npix, img,
-                     g.P, g.Pp, g.K, eps, g_logits, glb, g_dist, gdb, g.ldd, g.p0, static_cast<TX*>(g_x), accumulate, ws);
+                     g.P, g.Pp, g.K, eps, g_logits, glb, g_dist, gdb, g.ldd, g.p0, g.cgd, static_cast<TX*>(g_x), accumulate,
+                     ws);
   return check_launch("l2_bwd_fused_bf16_kernel");
 }
 
@@ -592,7 +631,7 @@ int launch_bwd_fused_bf16(const Geometry& g, bool x_bf16, const void* x, const f
   auto go = [&](auto tx, auto aa, auto gd) __attribute__((always_inline)) {
     using TX = std::remove_pointer_t<decltype(tx)>;
     constexpr int kA = decltype(aa)::value;
-    constexpr bool kG = decltype(gd)::value;
+    constexpr int kG = decltype(gd)::value;
     const bool six = g.Pp == 6 * 32;
     if (g.xsig)
       return six ? fused_t<TX, kA, kG, true, 6>(g, x, blk, eps, g_logits, g_dist, g_x, accumulate, ws, grid, stream)
@@ -602,12 +641,16 @@ int launch_bwd_fused_bf16(const Geometry& g, bool x_bf16, const void* x, const f
   };
   using A0 = std::integral_constant<int, 0>;
   using A1 = std::integral_constant<int, 1>;
-  using GT = std::true_type;
-  using GF = std::false_type;
+  using GT = std::integral_constant<int, 1>;
+  using GF = std::integral_constant<int, 0>;
+  using GC = std::integral_constant<int, 2>;
   float* f = nullptr;
   uint16_t* b = nullptr;
   int st;
-  if (act_kind == 0)
+  if (g.cgd.val) {  // the compact KLD gradient: f32 x only
+    if (x_bf16 || g_dist) return fail(PROTOSEG_ERR_UNSUPPORTED, "compact g_dist: f32 x and no dense g_dist");
+    st = act_kind == 0 ? go(f, A0(), GC()) : go(f, A1(), GC());
+  } else if (act_kind == 0)
     st = x_bf16 ? (g_dist ? go(b, A0(), GT()) : go(b, A0(), GF())) : (g_dist ? go(f, A0(), GT()) : go(f, A0(), GF()));
   else
     st = x_bf16 ? (g_dist ? go(b, A1(), GT()) : go(b, A1(), GF())) : (g_dist ? go(f, A1(), GT()) : go(f, A1(), GF()));

@@ -93,7 +93,7 @@ __host__ __device__ constexpr OneOffsets one_offsets(int Pp) {
 
 // LDS regions (bytes)
 struct OneLds {
-  int pimg, gs, xa, ga, x2s, ro, sig, total;
+  int pimg, gs, xa, ga, x2s, ro, cl, sig, total;
 };
 __host__ __device__ constexpr OneLds one_lds(int Pp) {
   OneLds o{};
@@ -103,7 +103,8 @@ __host__ __device__ constexpr OneLds one_lds(int Pp) {
   o.ga = o.xa + kOT * 32 * 160;       // [term][32 n][32 k] bf16, 64-B rows of 16-B chunks
   o.x2s = o.ga + kOT * 32 * 64;       // [32] f32 ||x||^2
   o.ro = o.x2s + 32 * 4;              // [32] u32 g_dist byte offset per pixel
-  o.sig = o.ro + 32 * 4;              // [2 slots][2 pixel halves][4 channel tiles][16] f32
+  o.cl = o.ro + 32 * 4;               // [32] int: the pixel's KLD class (compact g_dist, GD = 2)
+  o.sig = o.cl + 32 * 4;              // [2 slots][2 pixel halves][4 channel tiles][16] f32
   o.total = o.sig + 2 * 2 * 4 * 16 * 4;
   return o;
 }
@@ -155,11 +156,13 @@ __device__ __forceinline__ void store_half4(bf16* dst, const bf16x8& f, int half
 #define PB_DEPTH 1  // phase B: k-steps of fragments in flight ahead of the one multiplying
 #endif
 
-template <typename TX, int ACT, bool GD, bool XSIG, int NPT>
+// GD: 0 no distance gradient, 1 a dense g_dist, 2 the KLD loss's compact one (CompactGd).
+template <typename TX, int ACT, int GD, bool XSIG, int NPT>
 __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
     const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const unsigned char* __restrict__ img, int P,
     int K, float eps, const float* __restrict__ g_logits, unsigned gl_bytes, const float* __restrict__ g_dist,
-    unsigned gd_bytes, int gd_ld, int gd_p0, TX* __restrict__ g_x, int accumulate, float* __restrict__ slab) {
+    unsigned gd_bytes, int gd_ld, int gd_p0, CompactGd cg, TX* __restrict__ g_x, int accumulate,
+    float* __restrict__ slab) {
   constexpr int Pp = kOW * NPT * 16;  // prototype columns of the images
   constexpr int KS = Pp / 32;         // g_x k-steps (a multiple of 4)
   constexpr int KSQ = KS / 4;         // sum_p g_s k-steps per channel-tile wave
@@ -172,6 +175,7 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
   bf16* GA = reinterpret_cast<bf16*>(smem_raw + L.ga);
   float* X2S = reinterpret_cast<float*>(smem_raw + L.x2s);
   unsigned* RO = reinterpret_cast<unsigned*>(smem_raw + L.ro);
+  int* CL = reinterpret_cast<int*>(smem_raw + L.cl);
   float* SIG = reinterpret_cast<float*>(smem_raw + L.sig);
 
   const int lane = threadIdx.x & 63, g = lane >> 4, m = lane & 15, wave = wave_id();
@@ -180,17 +184,25 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
   const int iters = (ntiles - static_cast<int>(blockIdx.x) + G - 1) / G;
   const unsigned sz = sizeof(TX);
   const rsrc_t rx = make_rsrc(x, x_bytes), rg = make_rsrc(g_logits, gl_bytes);
-  const rsrc_t rgd = make_rsrc(g_dist, gd_bytes), rgx = make_rsrc(g_x, g_x ? x_bytes : 0u);
+  // GD = 2: g_dist points at the compact values (gd_bytes = npix * mpc * 4)
+  const rsrc_t rgd = make_rsrc(GD == 2 ? cg.val : g_dist, gd_bytes), rgx = make_rsrc(g_x, g_x ? x_bytes : 0u);
   auto tile_of = [&](int i) __attribute__((always_inline)) { return static_cast<int>(blockIdx.x) + i * G; };
 
   // ---- prologue: the (-2P) image -> LDS (for the launch); the owned ||p||^2 -> registers ------
   lds_copy(smem_raw + L.pimg, img + io.pi, io.p2 - io.pi);
 
   float p2[NPT];
+  int pcls[NPT], pslot[NPT];  // GD = 2: the owned prototypes' class and compact column (bytes)
 #pragma unroll
   for (int jt = 0; jt < NPT; ++jt) {
     const int ptile = wave * NPT + jt;
     p2[jt] = reinterpret_cast<const float*>(img + io.p2)[ptile * 16 + m];
+    if constexpr (GD == 2) {
+      const int pp = ptile * 16 + m;
+      const int code = pp < P ? cg.slot[gd_p0 + pp] : 0;
+      pcls[jt] = pp < P ? code >> 8 : -2;  // never a pixel class (those are >= -1)
+      pslot[jt] = (code & 255) * 4;
+    }
   }
 
   // ---- staging: wave w stages pixels 4w .. 4w+3 of a tile. Lanes 0..31: x of pixel 4w + l/8,
@@ -200,6 +212,7 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
   const int sn = 4 * wave + ((lane & 31) >> 3), sch = lane & 7;
   const int gn = 4 * wave + ((lane - 32) >> 2), gkc = lane & 3;
   float raw[8];
+  int rcl = -1;  // GD = 2, lanes 48 .. 51: the KLD class of pixel 4 wave + lane - 48
   auto load_raw = [&](int t) __attribute__((always_inline)) {
     if (lane < 32) {
       const int gp = t * 32 + sn;
@@ -216,6 +229,10 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
         raw[e] = BufIO<TX>::load(rx, off == kOOB ? kOOB : off + co, 0u);
       }
     } else {
+      if constexpr (GD == 2) {
+        const int gc = t * 32 + 4 * wave + (lane - 48);
+        if (lane >= 48 && lane < 52) rcl = gc < npix ? cg.pix[gc] : -1;
+      }
       const int gg = t * 32 + gn;
       const bool ok = lane < 48 && gg < npix;
 #pragma unroll
@@ -256,7 +273,7 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
       split8<kOT>(v, f);
 #pragma unroll
       for (int t2 = 0; t2 < kOT; ++t2) *reinterpret_cast<bf16x8*>(GA + t2 * 32 * 32 + ga_off(gn, gkc)) = f[t2];
-      if constexpr (GD) {
+      if constexpr (GD == 1) {
         if (gkc == 0) {
           const int gg = t * 32 + gn;
           const bool ok = gg < npix;
@@ -264,6 +281,10 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
           RO[gn] = ok ? static_cast<unsigned>(((b * gd_ld + gd_p0) * HW + (gg - b * HW)) * 4) : kOOB;
         }
       }
+    } else if (GD == 2 && lane < 52) {  // the pixel's compact row and class
+      const int n = 4 * wave + (lane - 48);
+      RO[n] = rcl >= 0 ? static_cast<unsigned>((t * 32 + n) * cg.mpc * 4) : kOOB;
+      CL[n] = rcl;
     }
   };
 
@@ -322,7 +343,18 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
       gacc[nt] = mma16_split(ga, wtj, f32x4{0.f, 0.f, 0.f, 0.f});
     }
     float gdv[8];
-    if constexpr (GD) {
+    if constexpr (GD == 2) {
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const uint4 ro = *reinterpret_cast<const uint4*>(RO + 16 * nt + 4 * g);
+        const int4 cl = *reinterpret_cast<const int4*>(CL + 16 * nt + 4 * g);
+        const unsigned rv[4] = {ro.x, ro.y, ro.z, ro.w};
+        const int cv[4] = {cl.x, cl.y, cl.z, cl.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          gdv[4 * nt + r] = BufIO<float>::load(rgd, cv[r] == pcls[jt] ? rv[r] + pslot[jt] : kOOB, 0);
+      }
+    } else if constexpr (GD == 1) {
       const unsigned pcol = static_cast<unsigned>(p * HW * 4);
       const bool pvalid = p < P;
 #pragma unroll
@@ -578,7 +610,7 @@ __global__ __launch_bounds__(256) void l2_prep_onepass_kernel(const float* __res
   }
 }
 
-template <typename TX, int ACT, bool GD, bool XSIG, int NPT>
+template <typename TX, int ACT, int GD, bool XSIG, int NPT>
 int onepass_t(const Geometry& g, const void* x, const unsigned char* img, float eps, const float* g_logits,
               const float* g_dist, void* g_x, int accumulate, float* ws, int grid, hipStream_t stream) {
   constexpr int Pp = kOW * NPT * 16;
@@ -588,11 +620,12 @@ int onepass_t(const Geometry& g, const void* x, const unsigned char* img, float 
   const unsigned long long npix = static_cast<unsigned long long>(g.npix);
   const unsigned xb = static_cast<unsigned>(npix * kC * sizeof(TX));
   const unsigned glb = g_logits ? static_cast<unsigned>(npix * g.K * 4) : 0u;
-  const unsigned gdb = g_dist ? static_cast<unsigned>(npix * g.ldd * 4) : 0u;
+  const unsigned gdb = GD == 2 ? static_cast<unsigned>(npix * g.cgd.mpc * 4)
+                               : g_dist ? static_cast<unsigned>(npix * g.ldd * 4) : 0u;
   KernelTimer timer("l2_bwd_onepass_bf16_kernel", stream);
   hipLaunchKernelGGL((l2_bwd_onepass_bf16_kernel<TX, ACT, GD, XSIG, NPT>), dim3(grid), dim3(kOThreads), lds, stream,
                      static_cast<const TX*>(x), xb, g.HW, g.npix, img, g.P, g.K, eps, g_logits, glb, g_dist, gdb,
-                     g.ldd, g.p0, static_cast<TX*>(g_x), accumulate, ws);
+                     g.ldd, g.p0, g.cgd, static_cast<TX*>(g_x), accumulate, ws);
   return check_launch("l2_bwd_onepass_bf16_kernel");
 }
 
@@ -637,7 +670,7 @@ int launch_bwd_onepass_bf16(const Geometry& g, bool x_bf16, const void* x, const
   auto go = [&](auto tx, auto aa, auto gd) __attribute__((always_inline)) {
     using TX = std::remove_pointer_t<decltype(tx)>;
     constexpr int kA = decltype(aa)::value;
-    constexpr bool kG = decltype(gd)::value;
+    constexpr int kG = decltype(gd)::value;
     auto by_npt = [&](auto xs) __attribute__((always_inline)) {
       constexpr bool kX = decltype(xs)::value;
       if (npt == 3) return onepass_t<TX, kA, kG, kX, 3>(g, x, blk, eps, g_logits, g_dist, g_x, accumulate, ws, grid, stream);
@@ -648,13 +681,18 @@ int launch_bwd_onepass_bf16(const Geometry& g, bool x_bf16, const void* x, const
   };
   using A0 = std::integral_constant<int, 0>;
   using A1 = std::integral_constant<int, 1>;
-  using GT = std::true_type;
-  using GF = std::false_type;
+  using G0 = std::integral_constant<int, 0>;
+  using G1 = std::integral_constant<int, 1>;
+  using G2 = std::integral_constant<int, 2>;
   float* f = nullptr;
   uint16_t* b = nullptr;
+  if (g.cgd.val) {  // the compact KLD gradient: f32 x only (bf16_bwd_compact_ok)
+    if (x_bf16 || g_dist) return fail(PROTOSEG_ERR_UNSUPPORTED, "compact g_dist: f32 x and no dense g_dist");
+    return act_kind == 0 ? go(f, A0(), G2()) : go(f, A1(), G2());
+  }
   if (act_kind == 0)
-    return x_bf16 ? (g_dist ? go(b, A0(), GT()) : go(b, A0(), GF())) : (g_dist ? go(f, A0(), GT()) : go(f, A0(), GF()));
-  return x_bf16 ? (g_dist ? go(b, A1(), GT()) : go(b, A1(), GF())) : (g_dist ? go(f, A1(), GT()) : go(f, A1(), GF()));
+    return x_bf16 ? (g_dist ? go(b, A0(), G1()) : go(b, A0(), G0())) : (g_dist ? go(f, A0(), G1()) : go(f, A0(), G0()));
+  return x_bf16 ? (g_dist ? go(b, A1(), G1()) : go(b, A1(), G0())) : (g_dist ? go(f, A1(), G1()) : go(f, A1(), G0()));
 }
 
 }  // namespace protoseg

@@ -7,12 +7,23 @@
 
 namespace protoseg {
 
+// The KLD loss's distance gradient in its compact layout (kld.hip, protoseg_l2_bwd_kld): at
+// global pixel g and prototype p, g_dist = val[g * mpc + (slot[p] & 255)] when pix[g] ==
+// slot[p] >> 8, else 0. `slot` is indexed by the whole call's prototype (a chunk adds its p0).
+struct CompactGd {
+  const float* val = nullptr;  // [npix, mpc] f32
+  const int* pix = nullptr;    // [npix] int32: class of the pixel's contributing group, or -1
+  const int* slot = nullptr;   // [P] int32: class * 256 + position in the class
+  int mpc = 0;
+};
+
 struct Geometry {
   int C, P, Pp, K, HW;
   int npix, ntiles;  // B*H*W pixels, 32-pixel tiles
   int ldw = 0;       // row stride of w_last / g_w (= P, or the full P for a prototype chunk)
   int ldd = 0, p0 = 0;  // g_dist: prototypes per image (= P, or the full P) and the chunk's first
   int xsig = 0;         // x is the add-on's pre-activation: sigmoid on load (bf16 fwd + fused bwd)
+  CompactGd cgd;        // cgd.val != nullptr: the compact KLD gradient instead of a dense g_dist
 };
 
 // bf16 split family (C = 64). `terms` = 2 (3 products) or 3 (6 products).
@@ -76,5 +87,23 @@ int launch_bwd_reduce_bf16_chunks(const Geometry& g, int per, int nchunk, const 
 int launch_bwd_pw_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const float* protos, const void* img,
                        float eps, int act_kind, const float* g_logits, const float* g_dist, float* g_protos,
                        float* g_w, float* ws, hipStream_t stream);
+
+// Any C, any K (l2_wide.hip): exact f32 MFMA GEMMs with fused epilogues. Forward scratch: x2 / p2
+// (+ the distances when dist is null and logits are wanted); backward workspace: D, G_s, sums and
+// the split-K partial slabs.
+bool wide_family_fits(const Geometry& g);
+size_t wide_fwd_scratch_bytes(const Geometry& g, bool need_dist);
+size_t wide_bwd_workspace_bytes(const Geometry& g);
+int launch_fwd_wide(const Geometry& g, bool x_bf16, const void* x, const float* protos, const float* w_last, float eps,
+                    int act_kind, float* dist, float* act, float* logits, void* scratch, hipStream_t s);
+int launch_bwd_wide(const Geometry& g, bool x_bf16, const void* x, const float* protos, const float* w_last, float eps,
+                    int act_kind, const float* g_logits, const float* g_dist, void* g_x, float* g_protos, float* g_w,
+                    void* workspace, hipStream_t s);
+// The push's path for prototype depths push.hip does not hold (C outside {32, 64, 128}): the
+// image's distances by the wide GEMM, then a masked argmin per (image, prototype) with
+// protoseg_push_argmin's key contract; wide_push_distances_scratch = protoseg_push_distances.
+int wide_push_argmin(const float* x, int n_img, int C, int hw, const float* protos, int P, const int32_t* proto_class,
+                     const uint32_t* mask, int words, uint64_t* img_keys, uint64_t* img_second, hipStream_t s);
+int wide_push_distances_scratch(const float* x, int C, int hw, const float* protos, int m, float* dist, hipStream_t s);
 
 }  // namespace protoseg

@@ -697,20 +697,28 @@ int f32_launch_protos(int C) {
   return p;
 }
 
+// Bounds of the wide family (l2_wide.hip): every depth / class count the register- and
+// LDS-resident families do not hold.
+constexpr int kWideMaxC = 4096, kWideMaxP = 65536, kWideMaxK = 4096;
+
+// The C in {32, 64, 128}, K <= 32, P <= 4096 families (bf16 split and f32) vs the wide GEMM family.
+bool use_wide(int C, int K, int P) { return nc_of(C) == 0 || K > 32 || P > kMaxChunkedP; }
+
 extern "C" int protoseg_l2_supported(int C, int P, int K) {
-  if (nc_of(C) == 0 || P <= 0 || K < 0 || K > 32) return 0;
-  return P <= kMaxChunkedP ? 1 : 0;  // beyond one launch's LDS: prototype chunks (both families)
+  if (C <= 0 || P <= 0 || K < 0) return 0;
+  if (!use_wide(C, K, P)) return 1;  // beyond one launch's LDS: prototype chunks
+  return (C <= kWideMaxC && P <= kWideMaxP && K <= kWideMaxK) ? 1 : 0;
 }
 
 extern "C" int protoseg_l2_max_protos(int C, int precision) {
-  if (nc_of(C) == 0 || precision < PROTOSEG_PREC_BF16X3 || precision > PROTOSEG_PREC_F32) return 0;
-  return kMaxChunkedP;
+  if (C <= 0 || precision < PROTOSEG_PREC_BF16X3 || precision > PROTOSEG_PREC_F32) return 0;
+  return C <= kWideMaxC ? kWideMaxP : 0;  // the wide family beyond the chunked families' 4096
 }
 
 // PROTOSEG_X_SIGMOID in act_kind: x is the add-on's pre-activation and the kernels apply the
 // sigmoid on load (model.py:124-128). Served by the bf16 forward and the fused backward only.
 bool x_sigmoid_path(int B, int C, int H, int W, int P, int K, int precision) {
-  if (precision != PROTOSEG_PREC_BF16X3 || C != 64 || P <= 0 || P > kMaxChunkedP || K < 0 || K > 32) return false;
+  if (precision != PROTOSEG_PREC_BF16X3 || C != 64 || P <= 0 || P > kMaxChunkedP || K < 0 || K > 32) return false;  // not wide
   if (B <= 0 || H <= 0 || W <= 0 || static_cast<long long>(B) * H * W >= (1LL << 31)) return false;
   return bf16_sizes_ok(geometry_of(B, C, H, W, P, K));
 }
@@ -740,6 +748,14 @@ extern "C" int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, 
   if (logits_out && (!w_last || K <= 0)) return fail(PROTOSEG_ERR_INVALID, "logits_out needs w_last and K > 0");
   if (!dist_out && !act_out && !logits_out) return PROTOSEG_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (use_wide(C, K, P)) {  // any C / K: exact f32 GEMMs (l2_wide.hip), every precision request
+    if (xsig) return fail(PROTOSEG_ERR_UNSUPPORTED, "PROTOSEG_X_SIGMOID: C = 64, K <= 32 only");
+    if (!wide_family_fits(geo)) return fail(PROTOSEG_ERR_UNSUPPORTED, "B*H*W*max(P, C) >= 2^31 elements");
+    void* scratch = nullptr;
+    if (int st = stream_block(wide_fwd_scratch_bytes(geo, !dist_out && logits_out), s, 2, &scratch)) return st;
+    return launch_fwd_wide(geo, x_dtype == PROTOSEG_BF16, x, protos, w_last, eps, act_kind, dist_out, act_out,
+                           logits_out, scratch, s);
+  }
   const int terms = terms_of(precision);
   if (terms && bf16_fwd_fits(geo, terms)) {
     ImageBlock img;
@@ -808,6 +824,7 @@ extern "C" size_t protoseg_l2_bwd_workspace_size(int B, int C, int H, int W, int
   if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || P <= 0) return 0;
   if (static_cast<long long>(B) * H * W >= (1LL << 31)) return 0;
   const Geometry g = geometry_of(B, C, H, W, P, K);
+  if (use_wide(C, K, P)) return ((wide_bwd_workspace_bytes(g) + 255) / 256) * 256;
   size_t need = f32_pw_workspace(g);
   const size_t b16 = bf16_bwd_pw_workspace(g);
   if (C == 64 && b16 > need) need = b16;
@@ -829,23 +846,37 @@ extern "C" size_t protoseg_l2_bwd_workspace_size(int B, int C, int H, int W, int
   return ((need + 255) / 256) * 256;
 }
 
-extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P,
-                               const float* w_last, int K, float eps, int act_kind, int precision,
-                               const float* g_logits, const float* g_dist, void* g_x, float* g_protos, float* g_w,
-                               void* workspace, size_t workspace_bytes, protoseg_stream_t stream) {
+namespace {
+// The compact KLD gradient (protoseg_l2_bwd_kld) is expanded in the owners of the bf16x3 training
+// backward (one-pass and fused kernels), f32 x.
+bool kld_compact_path(const Geometry& geo, int x_dtype, int precision, int mpc) {
+  return terms_of(precision) == 2 && geo.C == 64 && x_dtype == PROTOSEG_F32 && bf16_sizes_ok(geo) && mpc >= 1 &&
+         mpc <= 32 && static_cast<long long>(geo.npix) * mpc * 4 < (1LL << 31);
+}
+
+int l2_bwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P, const float* w_last,
+                int K, float eps, int act_kind, int precision, const float* g_logits, const float* g_dist,
+                const CompactGd& cgd, void* g_x, float* g_protos, float* g_w, void* workspace, size_t workspace_bytes,
+                protoseg_stream_t stream) {
   const int xsig = split_x_sigmoid(act_kind, B, C, H, W, P, K, precision);
   if (xsig < 0) return -xsig;
   Geometry geo;
   if (int st = validate(x, x_dtype, B, C, H, W, protos, P, K, act_kind, precision, &geo)) return st;
+  if (cgd.val) {
+    if (g_dist) return fail(PROTOSEG_ERR_INVALID, "a dense g_dist and the compact KLD gradient together");
+    if (!kld_compact_path(geo, x_dtype, precision, cgd.mpc) || !(xsig || (g_x && (g_protos || g_w))))
+      return fail(PROTOSEG_ERR_UNSUPPORTED, "compact KLD gradient: needs BF16X3, C = 64, f32 x, g_x and g_protos / g_w "
+                                            "(protoseg_l2_bwd_kld_supported)");
+  }
   if (g_logits && (!w_last || K <= 0)) return fail(PROTOSEG_ERR_INVALID, "g_logits needs w_last and K > 0");
   if (g_w && !g_logits) return fail(PROTOSEG_ERR_INVALID, "g_w needs g_logits");
-  if (g_protos || g_w || xsig) {  // the fused kernel (every X_SIGMOID backward) writes its slab
+  if (g_protos || g_w || xsig || use_wide(C, K, P)) {  // slabs (fused kernel, every X_SIGMOID backward; wide family)
     const size_t need = protoseg_l2_bwd_workspace_size(B, C, H, W, P, K);
     if (!workspace || workspace_bytes < need)
       return fail(PROTOSEG_ERR_INVALID, "workspace %zu B < %zu B", workspace_bytes, need);
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (!g_logits && !g_dist) {  // no upstream gradient: every output is zero
+  if (!g_logits && !g_dist && !cgd.val) {  // no upstream gradient: every output is zero
     const size_t esz = x_dtype == PROTOSEG_F32 ? 4 : 2;
     if (g_x && hipMemsetAsync(g_x, 0, static_cast<size_t>(geo.npix) * C * esz, s) != hipSuccess)
       return check_launch("memset g_x");
@@ -856,6 +887,12 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
   const int terms = terms_of(precision);
   const bool xb = x_dtype == PROTOSEG_BF16;
   float* ws = static_cast<float*>(workspace);
+  if (use_wide(C, K, P)) {  // any C / K (l2_wide.hip)
+    if (xsig) return fail(PROTOSEG_ERR_UNSUPPORTED, "PROTOSEG_X_SIGMOID: C = 64, K <= 32 only");
+    if (!wide_family_fits(geo)) return fail(PROTOSEG_ERR_UNSUPPORTED, "B*H*W*max(P, C) >= 2^31 elements");
+    return launch_bwd_wide(geo, xb, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_x, g_protos,
+                           g_logits ? g_w : nullptr, workspace, s);
+  }
   // Training backward at bf16x3: ONE pass over X for up to 384 prototypes (19 prototypes/class;
   // l2_bwd_onepass.hip), prototype chunks of <= 384 beyond (chunk c > 0 adds its g_x), one slab
   // reduce. P <= 192 keeps the 192-prototype fused kernel unless PROTOSEG_BWD=onepass.
@@ -876,6 +913,7 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
         gq.ldw = gq.ldd = P;
         gq.p0 = p0;
         gq.xsig = xsig;
+        gq.cgd = cgd;
         if (int st = launch_bwd_onepass_bf16(gq, xb, x, static_cast<unsigned char*>(img.ptr) + c * cb, eps, act_kind,
                                              g_logits, g_dist, g_x, ws + c * chunk_elems, s, c > 0))
           return st;
@@ -906,6 +944,7 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
         gc.ldw = gc.ldd = P;
         gc.p0 = p0;
         gc.xsig = xsig;
+        gc.cgd = cgd;
         if (int st = launch_bwd_fused_bf16(gc, xb, x, protos + static_cast<size_t>(p0) * C,
                                            static_cast<unsigned char*>(img.ptr) + c * cb, eps, act_kind, g_logits,
                                            g_dist, g_x, nullptr, nullptr, ws + c * chunk_elems, s, c > 0, 0))
@@ -916,6 +955,7 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
     }
   }
   if (xsig) return fail(PROTOSEG_ERR_UNSUPPORTED, "PROTOSEG_X_SIGMOID: no fused backward for this shape");
+  if (cgd.val) return fail(PROTOSEG_ERR_UNSUPPORTED, "compact KLD gradient: no fused backward for this shape");
   // P too large for the bf16 backward's LDS images (e.g. P = 361, 19 prototypes/class): run it
   // over prototype chunks of <= 192. g_P rows and g_W columns are per prototype; g_x is a sum
   // over prototypes, so chunk c > 0 adds to it; g_dist rows are read at (b * P + p0 + p).
@@ -993,4 +1033,35 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
     });
   }
   return PROTOSEG_OK;
+}
+}  // namespace
+
+extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P,
+                               const float* w_last, int K, float eps, int act_kind, int precision,
+                               const float* g_logits, const float* g_dist, void* g_x, float* g_protos, float* g_w,
+                               void* workspace, size_t workspace_bytes, protoseg_stream_t stream) {
+  return l2_bwd_impl(x, x_dtype, B, C, H, W, protos, P, w_last, K, eps, act_kind, precision, g_logits, g_dist,
+                     CompactGd{}, g_x, g_protos, g_w, workspace, workspace_bytes, stream);
+}
+
+extern "C" int protoseg_l2_bwd_kld_supported(int B, int C, int H, int W, int P, int K, int x_dtype, int precision,
+                                             int max_per_class) {
+  if (B <= 0 || H <= 0 || W <= 0 || P <= 0 || !protoseg_l2_supported(C, P, K)) return 0;
+  if (static_cast<long long>(B) * H * W >= (1LL << 31)) return 0;
+  return kld_compact_path(geometry_of(B, C, H, W, P, K), x_dtype, precision, max_per_class) ? 1 : 0;
+}
+
+extern "C" int protoseg_l2_bwd_kld(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P,
+                                   const float* w_last, int K, float eps, int act_kind, int precision,
+                                   const float* g_logits, const float* g_cls, const int32_t* pix_cls,
+                                   const int32_t* proto_slot, int max_per_class, void* g_x, float* g_protos,
+                                   float* g_w, void* workspace, size_t workspace_bytes, protoseg_stream_t stream) {
+  if (!g_cls || !pix_cls || !proto_slot) return fail(PROTOSEG_ERR_INVALID, "g_cls, pix_cls and proto_slot must be non-null");
+  CompactGd cgd;
+  cgd.val = g_cls;
+  cgd.pix = pix_cls;
+  cgd.slot = proto_slot;
+  cgd.mpc = max_per_class;
+  return l2_bwd_impl(x, x_dtype, B, C, H, W, protos, P, w_last, K, eps, act_kind, precision, g_logits, nullptr, cgd,
+                     g_x, g_protos, g_w, workspace, workspace_bytes, stream);
 }

@@ -1,0 +1,534 @@
+// l2_wide.hip — the prototype layer for any prototype depth C and any class count K: the shapes
+// the C in {32, 64, 128}, K <= 32 families do not hold in registers / LDS. That includes the
+// reference's own construct_PPNet default, prototype_shape = (2000, 512, 1, 1) with 200 classes
+// (model.py:394), and the DenseNet-161 add-on depths of BASELINE configs[4].
+//
+// Exact f32 products (v_mfma_f32_32x32x2_f32: a k-ordered fma chain per output element), composed
+// as strided GEMMs whose epilogues carry the layer's elementwise math, reference model.py:
+//   forward   D[b]      = relu(x2 + p2 - 2 P X[b])                   M = P,  N = HW, K = C  (203-221)
+//             logits[b] = act(D[b])^T W^T  (act applied on the load)  M = HW, N = K,  K = P  (231-237, 266-278)
+//   backward (autograd of the same; D recomputed from x, never stored by the forward)
+//             G_s[b]    = (W^T GL[b]^T) act'(D) + g_dist, masked by D > 0             M = P, N = HW, K = K
+//             g_x[b]    = -2 P^T G_s[b] + 2 x sum_p G_s[b]                            M = C, N = HW, K = P
+//             g_P       = -2 sum_b G_s[b] X[b]^T + 2 p sum_{b,n} G_s                   M = P, N = C,  K = B HW
+//             g_W       = sum_b GL[b]^T act(D[b])^T                                    M = K, N = P,  K = B HW
+// The two contractions over pixels (g_P, g_W) are split over workgroups (partial slabs summed in
+// a fixed order: deterministic, no atomics). Every operand is addressed by (row, k, batch) strides,
+// so no tensor is transposed or copied; NCHW rows give coalesced loads and stores along pixels.
+#include "protoseg_device.h"
+#include "protoseg_host.h"
+#include "l2_launch.h"
+
+#include <map>
+#include <mutex>
+#include <utility>
+#include <vector>
+
+namespace protoseg {
+
+namespace {
+
+constexpr int kWT = 64;    // workgroup output tile (rows and columns)
+constexpr int kWKs = 16;   // contraction per LDS stage
+constexpr int kWThreads = 256;
+constexpr int kWLd = kWT + 4;  // LDS row pitch (floats)
+
+enum WideEpi { kEpiStore = 0, kEpiDist = 1, kEpiGs = 2, kEpiGx = 3 };
+
+// Element (r, k) of batch b at p[b * sb + r * sr + k * sk]; r is the output row (A) or column (B).
+struct Operand {
+  const void* p;
+  long long sr, sk, sb;
+};
+
+struct WideArgs {
+  Operand A, B;
+  int M, N, Kd, nb;  // per-batch contraction Kd; nb batches
+  int bk;            // 1: the contraction runs over (batch, k) and splits over blockIdx.z; 0: one output per batch
+  int ksplit;        // bk: workgroups along the contraction
+  void* out;         // element (m, n) of batch (or split) z at out[z * ob + m * om + n * on]
+  long long om, on, ob;
+  int accumulate;
+  float eps;
+  int act_kind;
+  const float* x2;   // kEpiDist: x2[b * x2b + n]
+  long long x2b;
+  const float* p2;   // kEpiDist: p2[m]
+  float* act;        // kEpiDist: optional activation output at act[b * ab + m * am + n * an]
+  long long am, an, ab;
+  const float* D;    // kEpiGs: the distance at the output's address
+  const float* gd;   // kEpiGs: dense g_dist at the output's address, or null
+  const void* xo;    // kEpiGx: x at the output's address
+  const float* cs;   // kEpiGx: column sums cs[b * csb + n]
+  long long csb;
+};
+
+template <typename T>
+__device__ __forceinline__ float load_elem(const void* p, long long i) {
+  return XIO<T>::load(static_cast<const T*>(p), static_cast<size_t>(i));
+}
+
+// ACT < 0: the value as stored; else the activation of a distance (model.py:231-237).
+template <int ACT>
+__device__ __forceinline__ float on_load(float v, float eps) {
+  if constexpr (ACT < 0) return v;
+  else return activation(v, eps, ACT);
+}
+
+// Stages rows [r0, r0 + 64) x contraction [k0, k0 + 16) of an operand into registers: four
+// elements per thread, the thread map coalesced along whichever index has stride 1.
+template <typename T, int ACT>
+__device__ __forceinline__ void load_tile(const Operand& o, int R, int Kd, int r0, int k0, int b, int bk, float eps,
+                                          float (&v)[4], int (&lr)[4], int (&lk)[4]) {
+  const int t = threadIdx.x;
+  const bool rows_fast = o.sr == 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = rows_fast ? (t & 63) : (t >> 4) + 16 * i;
+    const int k = rows_fast ? (t >> 6) + 4 * i : (t & 15);
+    lr[i] = r;
+    lk[i] = k;
+    const int rr = r0 + r;
+    int kk = k0 + k, bb = b;
+    bool ok = rr < R;
+    if (bk) {  // flattened (batch, k) contraction
+      bb = kk / Kd;
+      kk -= bb * Kd;
+      ok = ok && bb < b;  // b = the batch count here
+    } else {
+      ok = ok && kk < Kd;
+    }
+    float x = 0.f;
+    if (ok) x = on_load<ACT>(load_elem<T>(o.p, bb * o.sb + rr * o.sr + kk * o.sk), eps);
+    v[i] = x;
+  }
+}
+
+template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO>
+__global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
+  __shared__ float As[kWKs][kWLd];
+  __shared__ float Bs[kWKs][kWLd];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = lane & 31, h = lane >> 5;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int m0 = blockIdx.y * kWT, n0 = blockIdx.x * kWT, z = blockIdx.z;
+  // contraction range of this workgroup, in flattened (batch, k) units for bk
+  long long kbeg = 0, kend = a.Kd;
+  int bsel = z;
+  if (a.bk) {
+    const long long total = static_cast<long long>(a.nb) * a.Kd;
+    const long long chunks = (total + kWKs - 1) / kWKs;
+    kbeg = (chunks * z / a.ksplit) * kWKs;
+    kend = (chunks * (z + 1) / a.ksplit) * kWKs;
+    if (kend > total) kend = total;
+    bsel = a.nb;  // load_tile's batch bound
+  }
+  f32x16 acc = zero16();
+  float va[4], vb[4];
+  int ra[4], ka[4], rb[4], kb[4];
+  auto fetch = [&](long long k0) {
+    load_tile<TA, AACT>(a.A, a.M, a.Kd, m0, static_cast<int>(k0), bsel, a.bk, a.eps, va, ra, ka);
+    load_tile<TB, BACT>(a.B, a.N, a.Kd, n0, static_cast<int>(k0), bsel, a.bk, a.eps, vb, rb, kb);
+  };
+  if (kbeg < kend) fetch(kbeg);
+  for (long long k0 = kbeg; k0 < kend; k0 += kWKs) {
+    __syncthreads();  // the previous stage's MFMA reads are done
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      As[ka[i]][ra[i]] = va[i];
+      Bs[kb[i]][rb[i]] = vb[i];
+    }
+    __syncthreads();
+    if (k0 + kWKs < kend) fetch(k0 + kWKs);  // next stage's loads in flight under the MFMAs
+#pragma unroll
+    for (int kk = 0; kk < kWKs / 2; ++kk)
+      acc = mfma32(As[2 * kk + h][wm * 32 + j], Bs[2 * kk + h][wn * 32 + j], acc);
+  }
+
+  // epilogue: lane column n, rows acc_row(r, h)
+  const int n = n0 + wn * 32 + j;
+  if (n >= a.N) return;
+  const int bo = a.bk ? z : bsel;  // output batch (or split) index
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + wm * 32 + acc_row(r, h);
+    if (m >= a.M) continue;
+    const long long o = bo * a.ob + m * a.om + static_cast<long long>(n) * a.on;
+    float v = acc[r];
+    if constexpr (EPI == kEpiDist) {
+      const float d = l2_distance(a.x2[bo * a.x2b + n], a.p2[m], v);
+      v = d;
+      if (a.act) a.act[bo * a.ab + m * a.am + static_cast<long long>(n) * a.an] = activation(d, a.eps, a.act_kind);
+    } else if constexpr (EPI == kEpiGs) {
+      const float d = a.D[o];
+      float g = v * activation_grad(d, a.eps, a.act_kind);
+      if (a.gd) g += a.gd[o];
+      v = d > 0.f ? g : 0.f;  // relu backward
+    } else if constexpr (EPI == kEpiGx) {
+      // conv(x^2, ones) backward: 2x sum_p g_s; conv(x, P) backward: -2 P^T g_s
+      v = -2.f * v + 2.f * load_elem<TO>(a.xo, o) * a.cs[bo * a.csb + n];
+    }
+    TO* out = static_cast<TO*>(a.out);
+    if (a.accumulate) v += XIO<TO>::load(out, static_cast<size_t>(o));
+    XIO<TO>::store(out, static_cast<size_t>(o), v);
+  }
+}
+
+// Sums of squares: x2[b][n] = sum_c x[b][c][n]^2 (threads over (b, n)), p2[p] = sum_c P[p][c]^2.
+template <typename TX>
+__global__ __launch_bounds__(256) void wide_norms_kernel(const TX* __restrict__ x, int C, int HW, int npix,
+                                                         const float* __restrict__ protos, int P,
+                                                         float* __restrict__ x2, float* __restrict__ p2) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < npix) {
+    const int b = i / HW, n = i - b * HW;
+    const TX* xp = x + static_cast<size_t>(b) * C * HW + n;
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const float v = XIO<TX>::load(xp, static_cast<size_t>(c) * HW);
+      s = fmaf(v, v, s);
+    }
+    x2[i] = s;
+  } else if (i - npix < P && p2) {
+    const int p = i - npix;
+    const float* pp = protos + static_cast<size_t>(p) * C;
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s = fmaf(pp[c], pp[c], s);
+    p2[p] = s;
+  }
+}
+
+// cs[b][n] = sum_p G_s[b][p][n] (threads over (b, n): rows read coalesced along n).
+__global__ __launch_bounds__(256) void wide_colsum_kernel(const float* __restrict__ gs, int P, int HW, int npix,
+                                                          float* __restrict__ cs) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= npix) return;
+  const int b = i / HW, n = i - b * HW;
+  const float* g = gs + static_cast<size_t>(b) * P * HW + n;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += g[static_cast<size_t>(p) * HW];
+  cs[i] = s;
+}
+
+// rs[p] = sum_{b, n} G_s[b][p][n]: one workgroup per prototype, fixed-order tree.
+__global__ __launch_bounds__(256) void wide_rowsum_kernel(const float* __restrict__ gs, int P, int HW, int B,
+                                                          float* __restrict__ rs) {
+  __shared__ float red[256];
+  const int p = blockIdx.x;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float* g = gs + (static_cast<size_t>(b) * P + p) * HW;
+    for (int n = threadIdx.x; n < HW; n += 256) s += g[n];
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (static_cast<int>(threadIdx.x) < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) rs[p] = red[0];
+}
+
+// Split-K partial slabs [S][M][N] -> out[m][n] in slab order; kind 1 (g_P): -2 sum + 2 p rs[m].
+__global__ __launch_bounds__(256) void wide_finish_kernel(const float* __restrict__ part, int S, int M, int N, int kind,
+                                                          const float* __restrict__ protos, const float* __restrict__ rs,
+                                                          float* __restrict__ out, long long ldo) {
+  const long long e = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+  if (e >= static_cast<long long>(M) * N) return;
+  const int m = static_cast<int>(e / N), n = static_cast<int>(e - static_cast<long long>(m) * N);
+  float s = 0.f;
+  for (int i = 0; i < S; ++i) s += part[static_cast<size_t>(i) * M * N + e];
+  if (kind == 1) s = -2.f * s + 2.f * protos[e] * rs[m];
+  out[m * ldo + n] = s;
+}
+
+template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO>
+int gemm(const WideArgs& a, int grid_z, hipStream_t s) {
+  const dim3 grid(static_cast<unsigned>(ceil_div(a.N, kWT)), static_cast<unsigned>(ceil_div(a.M, kWT)),
+                  static_cast<unsigned>(grid_z));
+  hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO>), grid, dim3(kWThreads), 0, s, a);
+  return check_launch("wide_gemm_kernel");
+}
+
+// Workgroups along a pixel contraction: ~512 workgroups in all, at least 1, at most 64.
+int split_of(int M, int N, long long total) {
+  const long long tiles = ceil_div(M, kWT) * ceil_div(N, kWT);
+  long long s = 512 / (tiles > 0 ? tiles : 1);
+  const long long chunks = ceil_div(total, kWKs);
+  if (s > chunks) s = chunks;
+  if (s > 64) s = 64;
+  return static_cast<int>(s < 1 ? 1 : s);
+}
+
+struct WideBwdLayout {
+  size_t D, G, x2, p2, cs, rs, part, total;  // float offsets
+};
+WideBwdLayout wide_bwd_layout(const Geometry& g) {
+  WideBwdLayout l{};
+  const size_t dp = static_cast<size_t>(g.npix) * g.P;
+  const size_t sp = static_cast<size_t>(split_of(g.P, g.C, g.npix)) * g.P * g.C;
+  const size_t sw = static_cast<size_t>(split_of(g.K, g.P, g.npix)) * g.K * g.P;
+  auto al = [](size_t v) { return (v + 63) & ~static_cast<size_t>(63); };
+  l.D = 0;
+  l.G = al(dp);
+  l.x2 = l.G + al(dp);
+  l.p2 = l.x2 + al(g.npix);
+  l.cs = l.p2 + al(g.P);
+  l.rs = l.cs + al(g.npix);
+  l.part = l.rs + al(g.P);
+  l.total = l.part + al(sp > sw ? sp : sw);
+  return l;
+}
+
+Operand op(const void* p, long long sr, long long sk, long long sb) { return Operand{p, sr, sk, sb}; }
+
+// D[b][p][n] into `dist` (ld P per image), optional act[g][p]; x2 / p2 scratch given.
+template <typename TX>
+int wide_distances(const Geometry& g, const TX* x, const float* protos, float eps, int act_kind, float* dist,
+                   float* act, float* x2, float* p2, hipStream_t s) {
+  const int B = g.npix / g.HW;
+  hipLaunchKernelGGL(wide_norms_kernel<TX>, dim3(static_cast<unsigned>(ceil_div(g.npix + g.P, 256))), dim3(256), 0, s,
+                     x, g.C, g.HW, g.npix, protos, g.P, x2, p2);
+  if (int st = check_launch("wide_norms_kernel")) return st;
+  WideArgs a{};
+  a.A = op(protos, g.C, 1, 0);                                   // P[p][c]
+  a.B = op(x, 1, g.HW, static_cast<long long>(g.C) * g.HW);      // X[b][c][n]: (n, c)
+  a.M = g.P, a.N = g.HW, a.Kd = g.C, a.nb = B;
+  a.out = dist, a.om = g.HW, a.on = 1, a.ob = static_cast<long long>(g.P) * g.HW;
+  a.eps = eps, a.act_kind = act_kind;
+  a.x2 = x2, a.x2b = g.HW, a.p2 = p2;
+  a.act = act, a.am = 1, a.an = g.P, a.ab = static_cast<long long>(g.HW) * g.P;  // act[(b HW + n) P + p]
+  return gemm<kEpiDist, float, TX, -1, -1, float>(a, B, s);
+}
+
+}  // namespace
+
+bool wide_family_fits(const Geometry& g) {
+  return g.C >= 1 && g.P >= 1 && g.K >= 0 && static_cast<long long>(g.npix) * g.P < (1LL << 31) &&
+         static_cast<long long>(g.npix) * g.C < (1LL << 31);
+}
+
+size_t wide_fwd_scratch_bytes(const Geometry& g, bool need_dist) {
+  size_t f = static_cast<size_t>(g.npix) + g.P + 128;
+  if (need_dist) f += static_cast<size_t>(g.npix) * g.P;
+  return f * sizeof(float);
+}
+
+size_t wide_bwd_workspace_bytes(const Geometry& g) { return wide_bwd_layout(g).total * sizeof(float); }
+
+int launch_fwd_wide(const Geometry& g, bool x_bf16, const void* x, const float* protos, const float* w_last, float eps,
+                    int act_kind, float* dist, float* act, float* logits, void* scratch, hipStream_t s) {
+  float* sc = static_cast<float*>(scratch);
+  float* x2 = sc;
+  float* p2 = x2 + g.npix;
+  float* D = dist ? dist : p2 + g.P + 64;  // the logits read the distances back
+  const int st = x_bf16 ? wide_distances(g, static_cast<const uint16_t*>(x), protos, eps, act_kind, D, act, x2, p2, s)
+                        : wide_distances(g, static_cast<const float*>(x), protos, eps, act_kind, D, act, x2, p2, s);
+  if (st || !logits) return st;
+  // logits[b][n][k] = sum_p act(D[b][p][n]) W[k][p]
+  WideArgs a{};
+  a.A = op(D, 1, g.HW, static_cast<long long>(g.P) * g.HW);   // (n, p) of D[b][p][n]
+  a.B = op(w_last, g.ldw, 1, 0);                              // (k, p) of W[k][p]
+  a.M = g.HW, a.N = g.K, a.Kd = g.P, a.nb = g.npix / g.HW;
+  a.out = logits, a.om = g.K, a.on = 1, a.ob = static_cast<long long>(g.HW) * g.K;
+  a.eps = eps;
+  return act_kind == PROTOSEG_ACT_LOG ? gemm<kEpiStore, float, float, 0, -1, float>(a, a.nb, s)
+                                      : gemm<kEpiStore, float, float, 1, -1, float>(a, a.nb, s);
+}
+
+int launch_bwd_wide(const Geometry& g, bool x_bf16, const void* x, const float* protos, const float* w_last, float eps,
+                    int act_kind, const float* g_logits, const float* g_dist, void* g_x, float* g_protos, float* g_w,
+                    void* workspace, hipStream_t s) {
+  const WideBwdLayout l = wide_bwd_layout(g);
+  float* ws = static_cast<float*>(workspace);
+  float *D = ws + l.D, *G = ws + l.G, *x2 = ws + l.x2, *p2 = ws + l.p2, *cs = ws + l.cs, *rs = ws + l.rs;
+  float* part = ws + l.part;
+  const int B = g.npix / g.HW;
+  const long long img = static_cast<long long>(g.P) * g.HW;
+  int st = x_bf16 ? wide_distances(g, static_cast<const uint16_t*>(x), protos, eps, act_kind, D, nullptr, x2, p2, s)
+                  : wide_distances(g, static_cast<const float*>(x), protos, eps, act_kind, D, nullptr, x2, p2, s);
+  if (st) return st;
+  {  // G_s[b][p][n] = (sum_k W[k][p] GL[b][n][k]) act'(D) + g_dist, relu mask (K = 0: g_dist alone)
+    WideArgs a{};
+    a.A = op(w_last, 1, g.ldw, 0);                               // (p, k) of W[k][p]
+    a.B = op(g_logits, g.K, 1, static_cast<long long>(g.HW) * g.K);  // (n, k) of GL[b][n][k]
+    a.M = g.P, a.N = g.HW, a.Kd = g_logits ? g.K : 0, a.nb = B;
+    a.out = G, a.om = g.HW, a.on = 1, a.ob = img;
+    a.eps = eps, a.act_kind = act_kind, a.D = D, a.gd = g_dist;
+    if ((st = gemm<kEpiGs, float, float, -1, -1, float>(a, B, s))) return st;
+  }
+  if (g_x) {  // g_x[b][c][n] = -2 sum_p P[p][c] G_s[b][p][n] + 2 x cs[b][n]
+    hipLaunchKernelGGL(wide_colsum_kernel, dim3(static_cast<unsigned>(ceil_div(g.npix, 256))), dim3(256), 0, s, G, g.P,
+                       g.HW, g.npix, cs);
+    if ((st = check_launch("wide_colsum_kernel"))) return st;
+    WideArgs a{};
+    a.A = op(protos, 1, g.C, 0);          // (c, p) of P[p][c]
+    a.B = op(G, 1, g.HW, img);            // (n, p) of G_s[b][p][n]
+    a.M = g.C, a.N = g.HW, a.Kd = g.P, a.nb = B;
+    a.out = g_x, a.om = g.HW, a.on = 1, a.ob = static_cast<long long>(g.C) * g.HW;
+    a.xo = x, a.cs = cs, a.csb = g.HW;
+    st = x_bf16 ? gemm<kEpiGx, float, float, -1, -1, uint16_t>(a, B, s) : gemm<kEpiGx, float, float, -1, -1, float>(a, B, s);
+    if (st) return st;
+  }
+  if (g_protos) {  // g_P[p][c] = -2 sum_{b,n} G_s[b][p][n] x[b][c][n] + 2 p rs[p]
+    hipLaunchKernelGGL(wide_rowsum_kernel, dim3(static_cast<unsigned>(g.P)), dim3(256), 0, s, G, g.P, g.HW, B, rs);
+    if ((st = check_launch("wide_rowsum_kernel"))) return st;
+    const int S = split_of(g.P, g.C, g.npix);
+    WideArgs a{};
+    a.A = op(G, g.HW, 1, img);                                        // (p, n) of G_s[b][p][n]
+    a.B = op(x, g.HW, 1, static_cast<long long>(g.C) * g.HW);         // (c, n) of X[b][c][n]
+    a.M = g.P, a.N = g.C, a.Kd = g.HW, a.nb = B, a.bk = 1, a.ksplit = S;
+    a.out = part, a.om = g.C, a.on = 1, a.ob = static_cast<long long>(g.P) * g.C;
+    st = x_bf16 ? gemm<kEpiStore, float, uint16_t, -1, -1, float>(a, S, s)
+                : gemm<kEpiStore, float, float, -1, -1, float>(a, S, s);
+    if (st) return st;
+    const long long e = static_cast<long long>(g.P) * g.C;
+    hipLaunchKernelGGL(wide_finish_kernel, dim3(static_cast<unsigned>(ceil_div(e, 256))), dim3(256), 0, s, part, S,
+                       g.P, g.C, 1, protos, rs, g_protos, static_cast<long long>(g.C));
+    if ((st = check_launch("wide_finish_kernel"))) return st;
+  }
+  if (g_w && g_logits) {  // g_W[k][p] = sum_{b,n} GL[b][n][k] act(D[b][p][n])
+    const int S = split_of(g.K, g.P, g.npix);
+    WideArgs a{};
+    a.A = op(g_logits, 1, g.K, static_cast<long long>(g.HW) * g.K);  // (k, n) of GL[b][n][k]
+    a.B = op(D, g.HW, 1, img);                                       // (p, n) of D[b][p][n], act on load
+    a.M = g.K, a.N = g.P, a.Kd = g.HW, a.nb = B, a.bk = 1, a.ksplit = S;
+    a.out = part, a.om = g.P, a.on = 1, a.ob = static_cast<long long>(g.K) * g.P;
+    a.eps = eps;
+    st = act_kind == PROTOSEG_ACT_LOG ? gemm<kEpiStore, float, float, -1, 0, float>(a, S, s)
+                                      : gemm<kEpiStore, float, float, -1, 1, float>(a, S, s);
+    if (st) return st;
+    const long long e = static_cast<long long>(g.K) * g.P;
+    hipLaunchKernelGGL(wide_finish_kernel, dim3(static_cast<unsigned>(ceil_div(e, 256))), dim3(256), 0, s, part, S,
+                       g.K, g.P, 0, nullptr, nullptr, g_w, static_cast<long long>(g.ldw));
+    if ((st = check_launch("wide_finish_kernel"))) return st;
+  }
+  return PROTOSEG_OK;
+}
+
+namespace {
+
+// Grow-only scratch per (device, stream) for the wide push path; retired blocks are kept (a HIP
+// graph that captured an earlier call may still point at them).
+void* wide_scratch(size_t need, hipStream_t s, int* st) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> blocks;
+  static std::vector<void*> retired;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    *st = check_launch("hipGetDevice");
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lock(mu);
+  auto& b = blocks[{dev, s}];
+  if (b.second < need) {
+    if (b.first) retired.push_back(b.first);
+    b = {nullptr, 0};
+    if (hipMalloc(&b.first, need) != hipSuccess) {
+      (void)hipGetLastError();
+      b = {nullptr, 0};
+      *st = fail(PROTOSEG_ERR_HIP, "hipMalloc (wide push scratch, %zu B)", need);
+      return nullptr;
+    }
+    b.second = need;
+  }
+  *st = PROTOSEG_OK;
+  return b.first;
+}
+
+// One wave per (prototype, image): the masked minimum over the class patches as a key
+// (float_bits(d) << 32 | patch: the lowest patch wins an exact tie) and the runner-up distance
+// over the other class patches (protoseg_push_argmin's contract).
+__global__ __launch_bounds__(256) void wide_push_argmin_kernel(const float* __restrict__ dist, int P, int hw,
+                                                               const int32_t* __restrict__ proto_class,
+                                                               const uint32_t* __restrict__ mask, size_t plane, int words,
+                                                               unsigned long long* __restrict__ keys,
+                                                               unsigned long long* __restrict__ second) {
+  const int lane = threadIdx.x & 63;
+  const int p = blockIdx.x * 4 + (threadIdx.x >> 6), i = blockIdx.y;
+  if (p >= P) return;
+  const int pc = proto_class[p];
+  const unsigned long long kNone = ~0ull;
+  unsigned long long best = kNone;
+  unsigned sec = 0xFFFFFFFFu;  // runner-up distance bits (d >= 0: bits order like values)
+  if (pc >= 0 && (pc >> 5) < words) {
+    const float* d = dist + (static_cast<size_t>(i) * P + p) * hw;
+    const uint32_t* mk = mask + static_cast<size_t>(pc >> 5) * plane + static_cast<size_t>(i) * hw;  // word of the class
+    for (int n = lane; n < hw; n += 64) {
+      if (!((mk[n] >> (pc & 31)) & 1u)) continue;
+      const unsigned long long k = (static_cast<unsigned long long>(__float_as_uint(d[n])) << 32) | static_cast<unsigned>(n);
+      if (k < best) {
+        const unsigned ob = static_cast<unsigned>(best >> 32);
+        sec = best == kNone ? sec : (ob < sec ? ob : sec);
+        best = k;
+      } else {
+        const unsigned kb = static_cast<unsigned>(k >> 32);
+        sec = kb < sec ? kb : sec;
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {  // merge (best, runner-up) pairs across lanes
+    const unsigned long long ob = shfl_xor_u64(best, m);
+    const unsigned os = __shfl_xor(sec, m);
+    const unsigned long long lo = ob < best ? ob : best, hi = ob < best ? best : ob;
+    const unsigned hb = hi == kNone ? 0xFFFFFFFFu : static_cast<unsigned>(hi >> 32);
+    unsigned s2 = sec < os ? sec : os;
+    s2 = hb < s2 ? hb : s2;
+    best = lo;
+    sec = s2;
+  }
+  if (lane == 0) {
+    keys[static_cast<size_t>(i) * P + p] = best;
+    if (second)
+      second[static_cast<size_t>(i) * P + p] =
+          sec == 0xFFFFFFFFu ? kNone : ((static_cast<unsigned long long>(sec) << 32) | 0xFFFFFFFFull);
+  }
+}
+
+}  // namespace
+
+// Distances of n_img images [n_img][P][hw] (the push's wide-C path); x2 / p2 scratch given.
+int wide_push_distances(const float* x, int n_img, int C, int hw, const float* protos, int P, float* dist, float* x2,
+                        float* p2, hipStream_t s) {
+  Geometry g{};
+  g.C = C, g.P = P, g.K = 0, g.HW = hw, g.npix = n_img * hw;
+  return wide_distances(g, x, protos, 1e-4f, PROTOSEG_ACT_LOG, dist, nullptr, x2, p2, s);
+}
+
+int wide_push_distances_scratch(const float* x, int C, int hw, const float* protos, int m, float* dist, hipStream_t s) {
+  int st = PROTOSEG_OK;
+  float* sc = static_cast<float*>(wide_scratch((static_cast<size_t>(hw) + m + 128) * sizeof(float), s, &st));
+  if (st) return st;
+  return wide_push_distances(x, 1, C, hw, protos, m, dist, sc, sc + hw, s);
+}
+
+int wide_push_argmin(const float* x, int n_img, int C, int hw, const float* protos, int P, const int32_t* proto_class,
+                     const uint32_t* mask, int words, uint64_t* img_keys, uint64_t* img_second, hipStream_t s) {
+  // images per pass: the pass's distances within ~1 GiB of scratch
+  const size_t per_img = static_cast<size_t>(P) * hw;
+  int nb = static_cast<int>((static_cast<size_t>(1) << 28) / (per_img ? per_img : 1));
+  if (nb < 1) nb = 1;
+  if (nb > n_img) nb = n_img;
+  int st = PROTOSEG_OK;
+  float* sc = static_cast<float*>(
+      wide_scratch((per_img * nb + static_cast<size_t>(nb) * hw + P + 256) * sizeof(float), s, &st));
+  if (st) return st;
+  float* D = sc;
+  float* x2 = D + per_img * nb;
+  float* p2 = x2 + static_cast<size_t>(nb) * hw;
+  for (int i0 = 0; i0 < n_img; i0 += nb) {
+    const int ni = n_img - i0 < nb ? n_img - i0 : nb;
+    if ((st = wide_push_distances(x + static_cast<size_t>(i0) * C * hw, ni, C, hw, protos, P, D, x2, p2, s))) return st;
+    // mask planes [words][n_img][hw]: class c in word c >> 5
+    hipLaunchKernelGGL(wide_push_argmin_kernel, dim3(static_cast<unsigned>(ceil_div(P, 4)), ni), dim3(256), 0, s, D, P,
+                       hw, proto_class, mask + static_cast<size_t>(i0) * hw, static_cast<size_t>(n_img) * hw, words,
+                       reinterpret_cast<unsigned long long*>(img_keys) + static_cast<size_t>(i0) * P,
+                       img_second ? reinterpret_cast<unsigned long long*>(img_second) + static_cast<size_t>(i0) * P
+                                  : nullptr);
+    if ((st = check_launch("wide_push_argmin_kernel"))) return st;
+  }
+  return PROTOSEG_OK;
+}
+
+}  // namespace protoseg

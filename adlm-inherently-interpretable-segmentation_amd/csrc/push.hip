@@ -16,6 +16,7 @@
 #include "l2_bf16_common.h"
 #include "protoseg_device.h"
 #include "protoseg_host.h"
+#include "l2_launch.h"
 
 namespace protoseg {
 
@@ -24,7 +25,8 @@ namespace {
 template <typename TL>
 __global__ __launch_bounds__(256) void patch_mask_kernel(const TL* __restrict__ label, int H, int W, int h, int w,
                                                          const int32_t* __restrict__ lut, int lut_size,
-                                                         uint32_t* __restrict__ mask) {
+                                                         int base, uint32_t* __restrict__ mask) {
+  // base: this mask word's first class (32 per word; classes base+1 .. base+32 -> bits 0 .. 31)
   extern __shared__ uint32_t smask[];  // [w]
   const int pi = blockIdx.x;
   const int img = blockIdx.y;
@@ -59,7 +61,7 @@ __global__ __launch_bounds__(256) void patch_mask_kernel(const TL* __restrict__ 
       if (raw < 0 || raw >= lut_size) return 0u;
       c = lut[raw];
     }
-    return (c > 0 && c <= 32) ? 1u << (c - 1) : 0u;  // push.py:222-223: class c -> key c-1
+    return (c > base && c <= base + 32) ? 1u << (c - 1 - base) : 0u;  // push.py:222-223: class c -> key c-1
   };
   for (int c0 = 4 * static_cast<int>(threadIdx.x); c0 < W; c0 += 4 * static_cast<int>(blockDim.x)) {
     uint32_t b4[4] = {0u, 0u, 0u, 0u};
@@ -426,6 +428,13 @@ using namespace protoseg;
 extern "C" int protoseg_patch_class_mask(const void* label, int label_dtype, int n_img, int H_img, int W_img, int h,
                                          int w, const int32_t* lut, int lut_size, uint32_t* mask,
                                          protoseg_stream_t stream) {
+  return protoseg_patch_class_mask_words(label, label_dtype, n_img, H_img, W_img, h, w, lut, lut_size, 1, mask, stream);
+}
+
+extern "C" int protoseg_patch_class_mask_words(const void* label, int label_dtype, int n_img, int H_img, int W_img,
+                                               int h, int w, const int32_t* lut, int lut_size, int words,
+                                               uint32_t* mask, protoseg_stream_t stream) {
+  if (words < 1 || words > 64) return fail(PROTOSEG_ERR_INVALID, "words=%d outside [1, 64]", words);
   if (!label || !mask) return fail(PROTOSEG_ERR_INVALID, "label and mask must be non-null");
   if (n_img <= 0 || H_img <= 0 || W_img <= 0 || h <= 0 || w <= 0)
     return fail(PROTOSEG_ERR_INVALID, "bad shape n_img=%d H=%d W=%d h=%d w=%d", n_img, H_img, W_img, h, w);
@@ -434,21 +443,24 @@ extern "C" int protoseg_patch_class_mask(const void* label, int label_dtype, int
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const dim3 grid(h, n_img);
   const size_t lds = static_cast<size_t>(w) * sizeof(uint32_t);
-  switch (label_dtype) {
-    case PROTOSEG_I64:
-      hipLaunchKernelGGL(patch_mask_kernel<int64_t>, grid, dim3(256), lds, s, static_cast<const int64_t*>(label),
-                         H_img, W_img, h, w, lut, lut_size, mask);
-      break;
-    case PROTOSEG_I32:
-      hipLaunchKernelGGL(patch_mask_kernel<int32_t>, grid, dim3(256), lds, s, static_cast<const int32_t*>(label),
-                         H_img, W_img, h, w, lut, lut_size, mask);
-      break;
-    case PROTOSEG_U8:
-      hipLaunchKernelGGL(patch_mask_kernel<uint8_t>, grid, dim3(256), lds, s, static_cast<const uint8_t*>(label),
-                         H_img, W_img, h, w, lut, lut_size, mask);
-      break;
-    default:
-      return fail(PROTOSEG_ERR_UNSUPPORTED, "label_dtype %d", label_dtype);
+  for (int wd = 0; wd < words; ++wd) {  // word wd: classes 32 wd + 1 .. 32 wd + 32, plane [n_img][h*w]
+    uint32_t* mw = mask + static_cast<size_t>(wd) * n_img * h * w;
+    switch (label_dtype) {
+      case PROTOSEG_I64:
+        hipLaunchKernelGGL(patch_mask_kernel<int64_t>, grid, dim3(256), lds, s, static_cast<const int64_t*>(label),
+                           H_img, W_img, h, w, lut, lut_size, 32 * wd, mw);
+        break;
+      case PROTOSEG_I32:
+        hipLaunchKernelGGL(patch_mask_kernel<int32_t>, grid, dim3(256), lds, s, static_cast<const int32_t*>(label),
+                           H_img, W_img, h, w, lut, lut_size, 32 * wd, mw);
+        break;
+      case PROTOSEG_U8:
+        hipLaunchKernelGGL(patch_mask_kernel<uint8_t>, grid, dim3(256), lds, s, static_cast<const uint8_t*>(label),
+                           H_img, W_img, h, w, lut, lut_size, 32 * wd, mw);
+        break;
+      default:
+        return fail(PROTOSEG_ERR_UNSUPPORTED, "label_dtype %d", label_dtype);
+    }
   }
   return check_launch("patch_mask_kernel");
 }
@@ -491,12 +503,26 @@ void* push_scratch(size_t need, hipStream_t s, int* status) {
 extern "C" int protoseg_push_argmin(const float* x, int n_img, int C, int h, int w, const float* protos, int P,
                                     const int32_t* proto_class, const uint32_t* mask, uint64_t* img_keys,
                                     uint64_t* img_second, protoseg_stream_t stream) {
+  return protoseg_push_argmin_words(x, n_img, C, h, w, protos, P, proto_class, mask, 1, img_keys, img_second, stream);
+}
+
+extern "C" int protoseg_push_argmin_words(const float* x, int n_img, int C, int h, int w, const float* protos, int P,
+                                          const int32_t* proto_class, const uint32_t* mask, int words,
+                                          uint64_t* img_keys, uint64_t* img_second, protoseg_stream_t stream) {
+  if (words < 1 || words > 64) return fail(PROTOSEG_ERR_INVALID, "words=%d outside [1, 64]", words);
   if (!x || !protos || !proto_class || !mask || !img_keys)
     return fail(PROTOSEG_ERR_INVALID, "null pointer argument");
   if (n_img <= 0 || h <= 0 || w <= 0 || P <= 0) return fail(PROTOSEG_ERR_INVALID, "bad shape");
   const int nc = nc_of_push(C);
-  if (!nc) return fail(PROTOSEG_ERR_UNSUPPORTED, "C=%d", C);
   if (n_img > 65535) return fail(PROTOSEG_ERR_UNSUPPORTED, "n_img=%d per call", n_img);
+  if (!nc || words > 1) {  // other depths / more than 32 classes: the wide GEMM's distances + a masked argmin
+    if (C <= 0 || C > 4096) return fail(PROTOSEG_ERR_UNSUPPORTED, "C=%d", C);
+    const long long hwc = static_cast<long long>(h) * w;
+    if (hwc * C * n_img >= (1LL << 31) || hwc * P >= (1LL << 31))
+      return fail(PROTOSEG_ERR_UNSUPPORTED, "n_img*h*w*C or h*w*P >= 2^31");
+    return wide_push_argmin(x, n_img, C, static_cast<int>(hwc), protos, P, proto_class, mask, words, img_keys,
+                            img_second, reinterpret_cast<hipStream_t>(stream));
+  }
   if (reinterpret_cast<uintptr_t>(protos) % 16 != 0) return fail(PROTOSEG_ERR_INVALID, "protos must be 16-B aligned");
   const long long HW = static_cast<long long>(h) * w;
   if (HW >= (1LL << 31) / 2) return fail(PROTOSEG_ERR_UNSUPPORTED, "h*w=%lld", HW);
@@ -549,14 +575,23 @@ extern "C" int protoseg_push_argmin(const float* x, int n_img, int C, int h, int
 
 extern "C" int protoseg_push_distances(const float* x, int C, int h, int w, const float* protos, int m, float* dist,
                                        protoseg_stream_t stream) {
+  return protoseg_push_distances_words(x, C, h, w, protos, m, 1, dist, stream);
+}
+
+extern "C" int protoseg_push_distances_words(const float* x, int C, int h, int w, const float* protos, int m, int words,
+                                             float* dist, protoseg_stream_t stream) {
+  if (words < 1 || words > 64) return fail(PROTOSEG_ERR_INVALID, "words=%d outside [1, 64]", words);
   if (!x || !protos || !dist) return fail(PROTOSEG_ERR_INVALID, "null pointer argument");
   if (h <= 0 || w <= 0 || m <= 0) return fail(PROTOSEG_ERR_INVALID, "bad shape h=%d w=%d m=%d", h, w, m);
   const int nc = nc_of_push(C);
-  if (!nc) return fail(PROTOSEG_ERR_UNSUPPORTED, "C=%d", C);
-  if (reinterpret_cast<uintptr_t>(protos) % 16 != 0) return fail(PROTOSEG_ERR_INVALID, "protos must be 16-B aligned");
   const long long HW = static_cast<long long>(h) * w;
   if (HW * C >= (1LL << 31) || HW * m >= (1LL << 31)) return fail(PROTOSEG_ERR_UNSUPPORTED, "h*w=%lld too large", HW);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (!nc || words > 1) {  // the wide path's arithmetic, so ties here are the ties protoseg_push_argmin saw
+    if (C <= 0 || C > 4096) return fail(PROTOSEG_ERR_UNSUPPORTED, "C=%d", C);
+    return wide_push_distances_scratch(x, C, static_cast<int>(HW), protos, m, dist, s);
+  }
+  if (reinterpret_cast<uintptr_t>(protos) % 16 != 0) return fail(PROTOSEG_ERR_INVALID, "protos must be 16-B aligned");
   const dim3 grid(static_cast<unsigned>(ceil_div(HW, 32)), static_cast<unsigned>(ceil_div(m, 32)));
   const int n = static_cast<int>(HW);
   if (nc == 1)

@@ -49,13 +49,22 @@ SIGNATURES = {
     "protoseg_l2_bwd_workspace_size": (_sz, [_i, _i, _i, _i, _i, _i]),
     "protoseg_l2_bwd": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp,
                              _sz, _vp]),
+    "protoseg_l2_bwd_kld": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _i, _vp, _vp, _vp, _vp, _i, _vp,
+                                 _vp, _vp, _vp, _sz, _vp]),
+    "protoseg_l2_bwd_kld_supported": (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _i]),
     "protoseg_patch_class_mask": (_i, [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp]),
     "protoseg_push_argmin": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
     "protoseg_push_distances": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _vp]),
+    "protoseg_patch_class_mask_words": (_i, [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
+    "protoseg_push_argmin_words": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _i, _vp, _vp, _vp]),
+    "protoseg_push_distances_words": (_i, [_vp, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
     "protoseg_push_merge": (_i, [_vp, _vp, _i, _i64, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     "protoseg_kld_workspace_size": (_sz, [_i, _i, _i, _i]),
     "protoseg_kld_forward": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _vp, _sz, _vp]),
     "protoseg_kld_backward": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _sz, _vp, _vp]),
+    "protoseg_kld_backward_compact": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _sz, _vp, _vp, _vp,
+                                           _vp]),
+    "protoseg_kld_expand": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "protoseg_eval_counts": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _vp, _i, _vp, _vp, _vp]),
     "protoseg_resize_label": (_i, [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp]),
     "protoseg_knn_image_min": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),

@@ -105,6 +105,64 @@ def _backward(ctx, g_loss, g_npairs, g_ws):
 
 torch.library.register_autograd("protoseg::kld_forward", _backward, setup_context=_setup_context)
 
+
+def kld_backward_compact(distances: Tensor, target_img: Tensor, proto_class: Tensor, num_classes: int,
+                         max_per_class: int, workspace: Tensor, g_loss: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
+    """The backward in its compact layout (protoseg_kld_backward_compact): (g_cls [B*HW, mpc] f32,
+    pix_cls [B*HW] int32, proto_slot [P] int32); see include/protoseg_hip.h."""
+    dev = _lib.require_device(distances, target_img, proto_class, workspace, g_loss)
+    d = distances.contiguous().float()
+    B, P = d.shape[0], d.shape[1]
+    HW = d[0, 0].numel()
+    t, ldt = _labels(target_img, B)
+    pc = proto_class.to(torch.int32).contiguous()
+    g = g_loss.to(torch.float32).contiguous()
+    g_cls = torch.empty((B * HW, max_per_class), device=dev, dtype=torch.float32)
+    pix_cls = torch.empty((B * HW,), device=dev, dtype=torch.int32)
+    proto_slot = torch.empty((P,), device=dev, dtype=torch.int32)
+    with torch.cuda.device(dev):
+        _lib.call("protoseg_kld_backward_compact", _lib.ptr(d), B, P, HW, _lib.ptr(t), ldt, _lib.ptr(pc),
+                  int(num_classes), int(max_per_class), _lib.ptr(g), _lib.ptr(workspace), workspace.numel(),
+                  _lib.ptr(g_cls), _lib.ptr(pix_cls), _lib.ptr(proto_slot), _lib.stream_of(dev))
+    return g_cls, pix_cls, proto_slot
+
+
+class _KldToLayer(torch.autograd.Function):
+    """kld_forward whose backward hands the compact gradient to the prototype layer that produced
+    ``distances`` (ops.DistGradSink) instead of returning a dense [B, P, H, W] tensor."""
+
+    @staticmethod
+    def forward(ctx, distances, target_img, proto_class, num_classes, max_per_class, sink):
+        loss, npairs, ws = torch.ops.protoseg.kld_forward(distances, target_img, proto_class, num_classes,
+                                                          max_per_class)
+        ctx.save_for_backward(distances, target_img, proto_class, ws)
+        ctx.num_classes, ctx.max_per_class, ctx.sink = num_classes, max_per_class, sink
+        ctx.mark_non_differentiable(npairs)
+        return loss, npairs
+
+    @staticmethod
+    def backward(ctx, g_loss, g_npairs):
+        distances, target_img, proto_class, ws = ctx.saved_tensors
+        if g_loss is None or not ctx.needs_input_grad[0]:
+            return None, None, None, None, None, None
+        g_cls, pix_cls, proto_slot = kld_backward_compact(distances, target_img, proto_class, ctx.num_classes,
+                                                          ctx.max_per_class, ws, g_loss)
+        return (ctx.sink.deposit(g_cls, pix_cls, proto_slot, ctx.max_per_class, distances),
+                None, None, None, None, None)
+
+
+def kld_with_pairs(distances: Tensor, target_img: Tensor, proto_class: Tensor, num_classes: int,
+                   max_per_class: int) -> Tuple[Tensor, Tensor]:
+    """(loss, n_pairs) of module.py:167-208. When ``distances`` is the distances output of the
+    HIP prototype layer and its backward can take the compact gradient, the gradient goes to the
+    layer in that form (no [B, P, H, W] tensor); otherwise autograd gets the dense one."""
+    sink = getattr(distances, "_protoseg_sink", None)
+    if sink is not None and distances.requires_grad and torch.is_grad_enabled() and sink.accepts(max_per_class):
+        return _KldToLayer.apply(distances, target_img, proto_class, int(num_classes), int(max_per_class), sink)
+    loss, npairs, _ = torch.ops.protoseg.kld_forward(distances, target_img, proto_class, int(num_classes),
+                                                     int(max_per_class))
+    return loss, npairs
+
 _class_cache: dict = {}
 
 
@@ -144,6 +202,5 @@ def kld_loss(distances: Tensor, target_img: Tensor, prototype_class_identity: Te
     cols, mpc = prototype_columns(prototype_class_identity, distances.device)
     if max_per_class is not None:
         mpc = int(max_per_class)
-    loss, _, _ = torch.ops.protoseg.kld_forward(distances, target_img, cols, int(prototype_class_identity.shape[1]),
-                                                mpc)
+    loss, _ = kld_with_pairs(distances, target_img, cols, int(prototype_class_identity.shape[1]), mpc)
     return loss

@@ -107,8 +107,9 @@ def l2_backward(x: Tensor, protos: Tensor, w_last: Tensor, g_logits: Optional[Te
     if need_w is False and g_logits is None and need_protos is False and need_x is False:
         return g_x, g_p, g_w
     lib = _lib.load()
-    fused_sig = bool(act_kind & _lib.X_SIGMOID)
-    ws_bytes = lib.protoseg_l2_bwd_workspace_size(B, C, H, W, P, K) if (need_protos or need_w or fused_sig) else 0
+    # slabs of g_P / g_W, every X_SIGMOID backward, and the wide family's D / G_s buffers (any
+    # request, g_x alone included): the size query is host-only, torch's allocator caches the block
+    ws_bytes = lib.protoseg_l2_bwd_workspace_size(B, C, H, W, P, K)
     ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8) if ws_bytes else None
     with torch.cuda.device(dev):
         _lib.call("protoseg_l2_bwd", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P, _lib.ptr(w_last), K,
@@ -128,6 +129,101 @@ def _(x, protos, w_last, g_logits, g_dist, eps, act_kind, precision, need_x, nee
             x.new_empty((K, P), dtype=torch.float32) if need_w else x.new_empty(0, dtype=torch.float32))
 
 
+class DistGradSink:
+    """Hand-off of the KLD loss's distance gradient to this layer's backward in its compact layout.
+
+    The KLD gradient (module.py:167-208) is non-zero only at the prototypes of each pixel's own
+    class, so a dense [B, P, H, W] tensor is mostly zeros written and read back. ``l2_forward``
+    attaches one sink to its distances output; ``kld.kld_loss`` on those distances deposits the
+    compact (g_cls, pix_cls, proto_slot, max_per_class) triple here and returns an expanded zero
+    to autograd, and this layer's backward hands the deposit to ``protoseg_l2_bwd_kld``, which
+    expands it in registers. Gradients from any other consumer of the distances still arrive
+    densely through autograd and are added. If the layer backward cannot take the compact form
+    (a shape / precision the kernels do not serve, a gradient through the activations), the
+    deposits are expanded with ``protoseg_kld_expand`` first: same values either way."""
+
+    __slots__ = ("shape", "compact_ok", "deposits", "zero")
+
+    def __init__(self, shape, compact_ok: bool):
+        self.shape = shape          # (B, C, H, W, P, K, x_dtype, precision)
+        self.compact_ok = compact_ok
+        self.deposits = []
+        self.zero = None
+
+    def accepts(self, max_per_class: int) -> bool:
+        """Whether a KLD backward on these distances should deposit its compact form."""
+        if not self.compact_ok:
+            return False
+        return bool(_lib.load().protoseg_l2_bwd_kld_supported(*self.shape, int(max_per_class)))
+
+    def deposit(self, g_cls: Tensor, pix_cls: Tensor, proto_slot: Tensor, max_per_class: int, like: Tensor) -> Tensor:
+        self.deposits.append((g_cls, pix_cls, proto_slot, int(max_per_class)))
+        if self.zero is None or self.zero.device != like.device:
+            self.zero = torch.zeros((), device=like.device, dtype=like.dtype).expand(like.shape)
+        return self.zero
+
+    def is_zero(self, g: Optional[Tensor]) -> bool:
+        z = self.zero
+        return (g is not None and z is not None and g.shape == z.shape and g.stride() == z.stride()
+                and g.data_ptr() == z.data_ptr())
+
+    def take(self):
+        d, self.deposits = self.deposits, []
+        return d
+
+
+def expand_compact(deposit, B: int, P: int, HW: int, out: Optional[Tensor] = None) -> Tensor:
+    """Dense [B, P, HW] g_dist of a compact KLD deposit (protoseg_kld_expand); added to ``out``."""
+    g_cls, pix_cls, proto_slot, mpc = deposit
+    dev = g_cls.device
+    acc = out is not None
+    if out is None:
+        out = torch.empty((B, P, HW), device=dev, dtype=torch.float32)
+    with torch.cuda.device(dev):
+        _lib.call("protoseg_kld_expand", _lib.ptr(g_cls), _lib.ptr(pix_cls), _lib.ptr(proto_slot), B, P, HW, mpc,
+                  1 if acc else 0, _lib.ptr(out), _lib.stream_of(dev))
+    return out
+
+
+@torch.library.custom_op("protoseg::l2_backward_kld", mutates_args=(), device_types="cuda")
+def l2_backward_kld(x: Tensor, protos: Tensor, w_last: Tensor, g_logits: Optional[Tensor], g_cls: Tensor,
+                    pix_cls: Tensor, proto_slot: Tensor, max_per_class: int, eps: float, act_kind: int, precision: int,
+                    need_x: bool, need_protos: bool, need_w: bool) -> Tuple[Tensor, Tensor, Tensor]:
+    """l2_backward with the KLD loss's compact distance gradient (protoseg_l2_bwd_kld): the
+    kernels expand g_dist in registers instead of reading a dense [B, P, H, W] tensor."""
+    dev = _lib.require_device(x, protos, w_last, g_logits, g_cls, pix_cls, proto_slot)
+    x = x.contiguous()
+    protos = protos.contiguous()
+    w_last = w_last.contiguous()
+    g_logits = g_logits.contiguous().float() if g_logits is not None else None
+    B, C, H, W = x.shape
+    P, K = protos.shape[0], w_last.shape[0]
+    need_w = need_w and g_logits is not None
+    g_x = torch.empty_like(x) if need_x else x.new_empty(0)
+    g_p = torch.empty((P, C), device=dev, dtype=torch.float32) if need_protos else x.new_empty(0, dtype=torch.float32)
+    g_w = torch.empty((K, P), device=dev, dtype=torch.float32) if need_w else x.new_empty(0, dtype=torch.float32)
+    lib = _lib.load()
+    ws_bytes = lib.protoseg_l2_bwd_workspace_size(B, C, H, W, P, K)
+    ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
+    with torch.cuda.device(dev):
+        _lib.call("protoseg_l2_bwd_kld", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P, _lib.ptr(w_last),
+                  K, float(eps), int(act_kind), int(precision), _lib.ptr(g_logits), _lib.ptr(g_cls),
+                  _lib.ptr(pix_cls), _lib.ptr(proto_slot), int(max_per_class), _lib.ptr(g_x), _lib.ptr(g_p),
+                  _lib.ptr(g_w), _lib.ptr(ws), ws_bytes, _lib.stream_of(dev))
+    return g_x, g_p, g_w
+
+
+@l2_backward_kld.register_fake
+def _(x, protos, w_last, g_logits, g_cls, pix_cls, proto_slot, max_per_class, eps, act_kind, precision, need_x,
+      need_protos, need_w):
+    B, C, H, W = x.shape
+    P, K = protos.shape[0], w_last.shape[0]
+    need_w = need_w and g_logits is not None
+    return (torch.empty_like(x) if need_x else x.new_empty(0),
+            x.new_empty((P, C), dtype=torch.float32) if need_protos else x.new_empty(0, dtype=torch.float32),
+            x.new_empty((K, P), dtype=torch.float32) if need_w else x.new_empty(0, dtype=torch.float32))
+
+
 def _setup_context(ctx, inputs, output):
     x, protos, w_last, eps, act_kind, precision, with_dist, with_logits, with_act = inputs
     ctx.save_for_backward(x, protos, w_last)
@@ -135,6 +231,13 @@ def _setup_context(ctx, inputs, output):
     ctx.act_kind = act_kind
     ctx.precision = precision
     ctx.set_materialize_grads(False)  # unused outputs give None, not a zero-filled [B,P,H,W]
+    ctx.sink = None
+    dist = output[0]
+    if with_dist and dist.numel() and x.is_cuda:
+        B, C, H, W = x.shape
+        trains = x.requires_grad and (protos.requires_grad or w_last.requires_grad)
+        ctx.sink = DistGradSink((B, C, H, W, protos.shape[0], w_last.shape[0], _x_dtype(x), int(precision)), trains)
+        dist._protoseg_sink = ctx.sink
 
 
 def _act_grad_as_dist_grad(x, protos, w_last, g_act, eps, act_kind, precision):
@@ -154,13 +257,29 @@ def _act_grad_as_dist_grad(x, protos, w_last, g_act, eps, act_kind, precision):
 def _backward(ctx, g_dist, g_logits, g_act):
     x, protos, w_last = ctx.saved_tensors
     need_x, need_p, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+    sink = ctx.sink
+    compact = sink.take() if sink is not None else []
+    if sink is not None and sink.is_zero(g_dist):
+        g_dist = None  # only the KLD loss consumed the distances: its gradient is in `compact`
     if g_act is not None:
         extra = _act_grad_as_dist_grad(x, protos, w_last, g_act, ctx.eps, ctx.act_kind, ctx.precision)
         g_dist = extra if g_dist is None else g_dist + extra
-    if g_dist is None and g_logits is None:
+    B, _, H, W = x.shape
+    P = protos.shape[0]
+    if compact and (g_dist is not None or len(compact) > 1 or not (need_x and (need_p or need_w))):
+        dense = g_dist.reshape(B, P, H * W).float().contiguous() if g_dist is not None else None
+        for dep in compact:
+            dense = expand_compact(dep, B, P, H * W, dense)
+        g_dist, compact = dense.reshape(B, P, H, W), []
+    if g_dist is None and g_logits is None and not compact:
         return None, None, None, None, None, None, None, None, None
-    g_x, g_p, g_w = l2_backward(x, protos, w_last, g_logits, g_dist, ctx.eps, ctx.act_kind, ctx.precision, need_x,
-                                need_p, need_w and g_logits is not None)
+    if compact:
+        g_cls, pix_cls, proto_slot, mpc = compact[0]
+        g_x, g_p, g_w = l2_backward_kld(x, protos, w_last, g_logits, g_cls, pix_cls, proto_slot, mpc, ctx.eps,
+                                        ctx.act_kind, ctx.precision, need_x, need_p, need_w and g_logits is not None)
+    else:
+        g_x, g_p, g_w = l2_backward(x, protos, w_last, g_logits, g_dist, ctx.eps, ctx.act_kind, ctx.precision, need_x,
+                                    need_p, need_w and g_logits is not None)
     return (g_x if need_x else None, g_p if need_p else None, g_w if (need_w and g_w.numel()) else None,
             None, None, None, None, None, None)
 

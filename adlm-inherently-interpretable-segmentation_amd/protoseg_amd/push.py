@@ -48,10 +48,16 @@ def _label_dtype(t: Tensor) -> int:
     return {torch.int64: _lib.I64, torch.int32: _lib.I32, torch.uint8: _lib.U8}.get(t.dtype, -1)
 
 
-def patch_class_mask(labels: Tensor, h: int, w: int, lut: Optional[Tensor] = None) -> Tensor:
+def mask_words(num_classes: int) -> int:
+    """32-bit class-mask planes for ``num_classes`` classes (classes 0 .. K-1 = labels 1 .. K)."""
+    return max(1, (int(num_classes) + 31) // 32)
+
+
+def patch_class_mask(labels: Tensor, h: int, w: int, lut: Optional[Tensor] = None, words: int = 1) -> Tensor:
     """labels [n, H, W] (int64 / int32 / uint8, device) -> int32 [n, h*w] holding the uint32
     class bitmask of each patch (bit k <=> a pixel of class k+1). ``lut`` [L] int32 maps raw
-    label ids first (CITYSCAPES_19_EVAL_CATEGORIES / PASCAL_ID_MAPPING as a table)."""
+    label ids first (CITYSCAPES_19_EVAL_CATEGORIES / PASCAL_ID_MAPPING as a table). More than 32
+    classes: ``words`` planes, int32 [words, n, h*w] (plane q: classes 32q+1 .. 32q+32)."""
     dev = _lib.require_device(labels, lut)
     if labels.dim() == 2:
         labels = labels.unsqueeze(0)
@@ -60,11 +66,11 @@ def patch_class_mask(labels: Tensor, h: int, w: int, lut: Optional[Tensor] = Non
     if dt < 0:
         raise _lib.ProtosegError(f"label dtype {labels.dtype} unsupported (int64, int32, uint8)")
     n, H, W = labels.shape
-    mask = torch.empty((n, h * w), device=dev, dtype=torch.int32)
+    mask = torch.empty((n, h * w) if words == 1 else (words, n, h * w), device=dev, dtype=torch.int32)
     lut_c = lut.to(torch.int32).contiguous() if lut is not None else None
     with torch.cuda.device(dev):
-        _lib.call("protoseg_patch_class_mask", _lib.ptr(labels), dt, n, H, W, h, w, _lib.ptr(lut_c),
-                  0 if lut_c is None else lut_c.numel(), _lib.ptr(mask), _lib.stream_of(dev))
+        _lib.call("protoseg_patch_class_mask_words", _lib.ptr(labels), dt, n, H, W, h, w, _lib.ptr(lut_c),
+                  0 if lut_c is None else lut_c.numel(), int(words), _lib.ptr(mask), _lib.stream_of(dev))
     return mask
 
 
@@ -72,8 +78,10 @@ def push_argmin(x: Tensor, protos: Tensor, proto_class: Tensor, mask: Tensor, wi
     """Per image and prototype, the masked minimum key (float_bits(d) << 32 | patch) as int64
     storage of uint64 [n, P]; -1 (all ones) when the image has no patch of the class. With
     ``with_second`` also the runner-up of the same image (float_bits(d2) << 32 | 0xFFFFFFFF: the
-    second-smallest class-patch distance), as a pair."""
+    second-smallest class-patch distance), as a pair. A [words, n, h*w] mask (more than 32
+    classes) takes the wide path (protoseg_push_argmin_words)."""
     dev = _lib.require_device(x, protos, proto_class, mask)
+    words = 1 if mask.dim() == 2 else int(mask.shape[0])
     x = x.float().contiguous()
     protos = protos.reshape(protos.shape[0], -1).float().contiguous()
     n, C, h, w = x.shape
@@ -81,9 +89,9 @@ def push_argmin(x: Tensor, protos: Tensor, proto_class: Tensor, mask: Tensor, wi
     keys = torch.empty((n, P), device=dev, dtype=torch.int64)
     second = torch.empty_like(keys) if with_second else None
     with torch.cuda.device(dev):
-        _lib.call("protoseg_push_argmin", _lib.ptr(x), n, C, h, w, _lib.ptr(protos), P,
-                  _lib.ptr(proto_class.to(torch.int32).contiguous()), _lib.ptr(mask.contiguous()), _lib.ptr(keys),
-                  _lib.ptr(second), _lib.stream_of(dev))
+        _lib.call("protoseg_push_argmin_words", _lib.ptr(x), n, C, h, w, _lib.ptr(protos), P,
+                  _lib.ptr(proto_class.to(torch.int32).contiguous()), _lib.ptr(mask.contiguous()), words,
+                  _lib.ptr(keys), _lib.ptr(second), _lib.stream_of(dev))
     return (keys, second) if with_second else keys
 
 
@@ -119,14 +127,16 @@ class PushState:
 
 
 def push_update(state: PushState, x: Tensor, labels: Tensor, protos: Tensor, proto_class: Tensor, first_img: int,
-                lut: Optional[Tensor] = None) -> None:
+                lut: Optional[Tensor] = None, words: Optional[int] = None) -> None:
     """One batch of images (dataset indices first_img ..): mask -> argmin -> strict-'<' merge.
     This is push_prototypes' inner step (one call per batch of equal-geometry images)."""
     x = x.float().contiguous()
     n, C, h, w = x.shape
     if labels.dim() == 2:
         labels = labels.unsqueeze(0)
-    mask = patch_class_mask(labels, h, w, lut)
+    if words is None:  # class-mask planes (one below 33 classes); callers in a loop pass it
+        words = mask_words(int(proto_class.max()) + 1)
+    mask = patch_class_mask(labels, h, w, lut, words=words)
     keys, second = push_argmin(x, protos, proto_class, mask, with_second=True)
     dev = x.device
     P = keys.shape[1]
@@ -141,10 +151,10 @@ def push_update(state: PushState, x: Tensor, labels: Tensor, protos: Tensor, pro
         state.geometry[first_img + i] = (int(H), int(W), int(h), int(w))
 
 
-def push_distances(x: Tensor, protos: Tensor) -> Tensor:
+def push_distances(x: Tensor, protos: Tensor, words: int = 1) -> Tensor:
     """Distances [m, h*w] of ``protos`` [m, C] at every patch of ONE image x [1, C, h, w] (or
-    [C, h, w]) in push_argmin's arithmetic, operation for operation: a tie here is exactly a
-    tie that kernel saw."""
+    [C, h, w]) in push_argmin's arithmetic for a ``words``-plane mask, operation for operation: a
+    tie here is exactly a tie that kernel saw."""
     dev = _lib.require_device(x, protos)
     x = x.float().contiguous()
     if x.dim() == 4:
@@ -156,8 +166,8 @@ def push_distances(x: Tensor, protos: Tensor) -> Tensor:
     m = protos.shape[0]
     out = torch.empty((m, h * w), device=dev, dtype=torch.float32)
     with torch.cuda.device(dev):
-        _lib.call("protoseg_push_distances", _lib.ptr(x), C, h, w, _lib.ptr(protos), m, _lib.ptr(out),
-                  _lib.stream_of(dev))
+        _lib.call("protoseg_push_distances_words", _lib.ptr(x), C, h, w, _lib.ptr(protos), m, int(words),
+                  _lib.ptr(out), _lib.stream_of(dev))
     return out
 
 
@@ -210,6 +220,7 @@ def resolve_exact_ties(state: PushState, load: Callable, protos: Tensor, proto_c
     pcls = np.asarray(proto_class.cpu() if isinstance(proto_class, Tensor) else proto_class).astype(np.int64)
     lut_np = lut.cpu().numpy() if lut is not None else None
     pv = protos.detach().reshape(protos.shape[0], -1).float()
+    words = mask_words(int(pcls.max()) + 1)  # the scan's mask planes, hence its arithmetic
     moved = []
     for im in np.unique(img[cand]):
         ids = cand[img[cand] == im]
@@ -220,7 +231,7 @@ def resolve_exact_ties(state: PushState, load: Callable, protos: Tensor, proto_c
         if lut_np is not None:  # the scan's table (dataset.convert_targets); ids outside it: no class
             ok = (lab >= 0) & (lab < lut_np.size)
             lab = np.where(ok, lut_np[np.clip(lab, 0, lut_np.size - 1)], -1)
-        d = push_distances(x, pv[torch.as_tensor(ids, device=pv.device)]).cpu().numpy()
+        d = push_distances(x, pv[torch.as_tensor(ids, device=pv.device)], words).cpu().numpy()
         for k, j in enumerate(ids.tolist()):
             order = reference_patch_order(lab, int(pcls[j]), h, w)
             if not order:
@@ -442,6 +453,7 @@ def push_prototypes(dataset, prototype_network_parallel, prototype_layer_stride=
     P, C = ppnet.num_prototypes, ppnet.prototype_shape[1]
     proto_class_t = prototype_classes(ppnet).to(device)
     proto_class = proto_class_t.cpu().numpy()
+    words = mask_words(int(proto_class.max()) + 1)
     state = PushState.create(P, C, device)
 
     proto_epoch_dir = None
@@ -491,7 +503,7 @@ def push_prototypes(dataset, prototype_network_parallel, prototype_layer_stride=
                 imgs = torch.cat([r[0] for r in run], 0)
                 labels = torch.stack([r[1] for r in run], 0)
                 push_update(state, ppnet.conv_features(imgs), labels, ppnet.prototype_vectors, proto_class_t,
-                            run[0][2], lut)
+                            run[0][2], lut, words)
                 run.clear()
 
         for push_iter in range(lo, hi):

@@ -64,10 +64,9 @@ def _default_resize(labels: Tensor, h: int, w: int) -> Tensor:
 
 def _default_kld(distances: Tensor, target_img: Tensor, class_identity: Tensor):
     """(loss, n_pairs): module.py:167-208 on the HIP kernels."""
-    from .kld import prototype_columns
+    from .kld import kld_with_pairs, prototype_columns
     cols, mpc = prototype_columns(class_identity, distances.device)
-    loss, npairs, _ = torch.ops.protoseg.kld_forward(distances, target_img, cols, int(class_identity.shape[1]), mpc)
-    return loss, npairs
+    return kld_with_pairs(distances, target_img, cols, int(class_identity.shape[1]), mpc)
 
 
 class PatchClassificationStep:

@@ -143,6 +143,10 @@ class LayerStep:
         self.kld_loss = torch.empty((), device=self.device, dtype=torch.float32)
         self.kld_gloss = torch.full((), weight, device=self.device, dtype=torch.float32)
         self.g_dist = torch.empty_like(self.dist)
+        n = self.B * self.h * self.w
+        self.g_cls = torch.empty(n, self.mpc, device=self.device, dtype=torch.float32)
+        self.pix_cls = torch.empty(n, device=self.device, dtype=torch.int32)
+        self.proto_slot = torch.empty(self.P, device=self.device, dtype=torch.int32)
 
     def kld_fwd(self):
         _lib.call("protoseg_kld_forward", _lib.ptr(self.dist), self.B, self.P, self.h * self.w, _lib.ptr(self.target),
@@ -153,6 +157,21 @@ class LayerStep:
         _lib.call("protoseg_kld_backward", _lib.ptr(self.dist), self.B, self.P, self.h * self.w, _lib.ptr(self.target),
                   _lib.I64, _lib.ptr(self.proto_class), self.K, self.mpc, _lib.ptr(self.kld_gloss),
                   _lib.ptr(self.kld_ws), self.kld_ws_bytes, _lib.ptr(self.g_dist), self._stream())
+
+    def kld_bwd_compact(self):
+        """The KLD gradient in its compact per-pixel class-slot layout (no [B, P, H, W] tensor)."""
+        _lib.call("protoseg_kld_backward_compact", _lib.ptr(self.dist), self.B, self.P, self.h * self.w,
+                  _lib.ptr(self.target), _lib.I64, _lib.ptr(self.proto_class), self.K, self.mpc,
+                  _lib.ptr(self.kld_gloss), _lib.ptr(self.kld_ws), self.kld_ws_bytes, _lib.ptr(self.g_cls),
+                  _lib.ptr(self.pix_cls), _lib.ptr(self.proto_slot), self._stream())
+
+    def bwd_kld(self):
+        """Backward with the compact KLD gradient expanded in the kernels (protoseg_l2_bwd_kld)."""
+        _lib.call("protoseg_l2_bwd_kld", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w,
+                  _lib.ptr(self.protos), self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec,
+                  _lib.ptr(self.g_logits), _lib.ptr(self.g_cls), _lib.ptr(self.pix_cls), _lib.ptr(self.proto_slot),
+                  self.mpc, _lib.ptr(self.g_x), _lib.ptr(self.g_p), _lib.ptr(self.g_w), _lib.ptr(self.ws),
+                  self.ws_bytes, self._stream())
 
     def bwd_gd(self):
         """Backward with the KLD distance gradient (protoseg_l2_bwd g_dist)."""
@@ -318,11 +337,14 @@ def time_layer(step: LayerStep, steps: int, warmup: int, world: int, use_graph: 
     return elapsed, {n: float(np.mean(v)) for n, v in per_kernel.items()}, actual
 
 
-def time_kld_step(step: LayerStep, steps: int, warmup: int):
+def time_kld_step(step: LayerStep, steps: int, warmup: int, compact: bool = True):
     """BASELINE configs[2] step on one GPU: forward, KLD loss (module.py:167-208) forward and
-    backward, layer backward with g_logits and the KLD g_dist, as one HIP graph per step.
+    backward, layer backward with g_logits and the KLD gradient, Adam, as one HIP graph per step.
+    compact: the KLD gradient in its per-pixel class-slot layout, expanded in the layer backward's
+    kernels (what kld.kld_loss on PPNet's distances does); else the dense [B, P, H, W] g_dist.
     Returns ms per step and the per-launch event times of the two KLD calls."""
-    calls = [step.fwd, step.kld_fwd, step.kld_bwd, step.bwd_gd, step.opt_step]
+    kbwd = step.kld_bwd_compact if compact else step.kld_bwd
+    calls = [step.fwd, step.kld_fwd, kbwd, step.bwd_kld if compact else step.bwd_gd, step.opt_step]
     stream = torch.cuda.Stream(step.device)
     with torch.cuda.stream(stream):
         for _ in range(max(1, warmup)):
@@ -330,7 +352,7 @@ def time_kld_step(step: LayerStep, steps: int, warmup: int):
                 c()
         torch.cuda.synchronize()
         g = capture(lambda: [c() for c in calls], stream)
-        g_kf, g_kb = capture(step.kld_fwd, stream), capture(step.kld_bwd, stream)
+        g_kf, g_kb = capture(step.kld_fwd, stream), capture(kbwd, stream)
         for _ in range(warmup):
             g.replay()
         torch.cuda.synchronize()
@@ -353,11 +375,14 @@ def time_kld_step(step: LayerStep, steps: int, warmup: int):
     loss = float(step.kld_loss)
     n = step.B * step.h * step.w
     kb = float(np.mean(ms_b)) * 1e-3
-    return {"workload": "cityscapes_kld_imnet step on 1 GPU: fwd + KLD fwd/bwd (loss_weight_kld 0.25) + bwd with g_dist "
-                        "+ Adam update",
-            "ms_per_step": round(elapsed / steps * 1e3, 4), "img_per_s": round(step.B * steps / elapsed, 1),
-            "kld_forward_ms": round(float(np.mean(ms_f)), 4), "kld_backward_ms": round(kb * 1e3, 4),
-            "kld_backward_gbps": round(n * step.P * 4 / kb / 1e9, 1), "loss": round(loss, 6)}
+    out = {"workload": "cityscapes_kld_imnet step on 1 GPU: fwd + KLD fwd/bwd (loss_weight_kld 0.25) + bwd with the "
+                       + ("compact KLD gradient (protoseg_l2_bwd_kld)" if compact else "dense g_dist") + " + Adam update",
+           "ms_per_step": round(elapsed / steps * 1e3, 4), "img_per_s": round(step.B * steps / elapsed, 1),
+           "kld_forward_ms": round(float(np.mean(ms_f)), 4), "kld_backward_ms": round(kb * 1e3, 4),
+           "loss": round(loss, 6), "prototypes": step.P}
+    if not compact:
+        out["kld_backward_gbps"] = round(n * step.P * 4 / kb / 1e9, 1)
+    return out
 
 
 def time_sigmoid_step(step: LayerStep, steps: int, warmup: int):
@@ -907,10 +932,21 @@ def main():
 
     kld = None
     if not args.no_kld and world == 1:
-        kstep = side if (side is not None and side.P == 190) else step
-        kstep.setup_kld(SEED + rank)
-        kld = time_kld_step(kstep, max(5, args.steps // 4), 3)
-        kld["prototypes"] = kstep.P
+        # configs[2] binds 10 prototypes/class (P = 190); the metric's 19/class beside it. Each
+        # against the plain layer step of the same P (ratio_to_plain_step), the dense-g_dist
+        # variant as the before/after of the compact gradient.
+        kld = {}
+        for kstep, e_plain in ((side, e_side if side is not None else None), (step, elapsed)):
+            if kstep is None:
+                continue
+            kstep.setup_kld(SEED + rank)
+            line = time_kld_step(kstep, max(5, args.steps // 4), 3)
+            dense = time_kld_step(kstep, max(5, args.steps // 4), 3, compact=False)
+            line["dense_g_dist_ms_per_step"] = dense["ms_per_step"]
+            line["dense_kld_backward_ms"] = dense["kld_backward_ms"]
+            line["plain_step_ms"] = round(e_plain / args.steps * 1e3, 4)
+            line["ratio_to_plain_step"] = round(line["ms_per_step"] / line["plain_step_ms"], 3)
+            kld[f"P{kstep.P}"] = line
 
     sigmoid = None
     if world == 1 and args.precision == "bf16x3" and args.channels == 64:

@@ -95,11 +95,14 @@ int protoseg_timing_launches(void);
  *   dist_out   [B, P, H, W]   f32 or NULL   distances (model.py:219, NCHW)
  *   act_out    [B*H*W, P]     f32 or NULL   prototype activations (model.py:273)
  *   logits_out [B, H, W, K]   f32 or NULL   logits NHWC (model.py:278)
- * Supported (protoseg_l2_supported() is authoritative): K <= 32, P <= 4096 and
- *   - C = 64, BF16X3 / BF16X6: prototypes beyond one launch's LDS images run as prototype chunks
- *     inside the call (forward chunks of <= 384 rows at BF16X3, fewer at BF16X6);
- *   - C in {32, 64, 128}, F32 (and the bf16 requests the bf16 family cannot serve, C != 64): the
- *     f32 family, over prototype chunks of what one launch's LDS holds (C = 64: 384, C = 128: 224);
+ * Supported (protoseg_l2_supported() is authoritative):
+ *   - K <= 32, P <= 4096, C = 64, BF16X3 / BF16X6: prototypes beyond one launch's LDS images run
+ *     as prototype chunks inside the call (forward chunks of <= 384 rows at BF16X3, fewer at BF16X6);
+ *   - K <= 32, P <= 4096, C in {32, 64, 128}, F32 (and the bf16 requests the bf16 family cannot
+ *     serve, C != 64): the f32 family, over prototype chunks of what one launch's LDS holds;
+ *   - any other C <= 4096, K <= 4096, P <= 65536 (e.g. the reference's default prototype_shape
+ *     (2000, 512) with 200 classes, model.py:394), every precision request: the wide family
+ *     (exact f32 MFMA GEMMs with fused epilogues, l2_wide.hip; scratch per stream, graph-safe);
  *   - every tensor addressed by the kernels (B*H*W*max(P, C)*4 bytes) below 2^31 bytes.
  */
 int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, int W,
@@ -128,6 +131,29 @@ int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, int W,
                     void* workspace, size_t workspace_bytes,
                     protoseg_stream_t stream);
 
+/*
+ * The same backward with the KLD loss's distance gradient in its compact layout
+ * (protoseg_kld_backward_compact) instead of a dense [B, P, H, W] g_dist: the kernels expand
+ * g_dist[b][p][n] = g_cls[g][proto_slot[p] & 255] where pix_cls[g] == proto_slot[p] >> 8
+ * (g = b*H*W + n), 0 elsewhere, in registers. Same outputs as protoseg_l2_bwd given that dense
+ * tensor (protoseg_kld_expand). Served by the bf16x3 training backward (g_x with g_protos /
+ * g_w, C = 64, f32 x): protoseg_l2_bwd_kld_supported says whether a shape qualifies, otherwise
+ * the call returns PROTOSEG_ERR_UNSUPPORTED before launching anything.
+ *   g_cls      [B*H*W, max_per_class] f32
+ *   pix_cls    [B*H*W] int32: class of the pixel's contributing (image, class) group, or -1
+ *   proto_slot [P] int32: class * 256 + position of the prototype in its class
+ */
+int protoseg_l2_bwd_kld(const void* x, int x_dtype, int B, int C, int H, int W,
+                        const float* protos, int P, const float* w_last, int K,
+                        float eps, int act_kind, int precision,
+                        const float* g_logits, const float* g_cls, const int32_t* pix_cls,
+                        const int32_t* proto_slot, int max_per_class,
+                        void* g_x, float* g_protos, float* g_w,
+                        void* workspace, size_t workspace_bytes,
+                        protoseg_stream_t stream);
+int protoseg_l2_bwd_kld_supported(int B, int C, int H, int W, int P, int K, int x_dtype, int precision,
+                                  int max_per_class);
+
 /* 1 if (C, P, K) is inside the compiled kernel family, else 0. */
 int protoseg_l2_supported(int C, int P, int K);
 
@@ -155,6 +181,12 @@ int protoseg_l2_x_sigmoid_supported(int B, int C, int H, int W, int P, int K, in
 int protoseg_patch_class_mask(const void* label, int label_dtype, int n_img, int H_img, int W_img,
                               int h, int w, const int32_t* lut, int lut_size,
                               uint32_t* mask, protoseg_stream_t stream);
+/* More than 32 classes (e.g. 200): `words` 32-bit mask planes, mask [words][n_img][h*w], plane wd
+ * holding classes 32 wd + 1 .. 32 wd + 32 (bit k of plane wd <=> class 32 wd + k + 1).
+ * words = 1 is protoseg_patch_class_mask. */
+int protoseg_patch_class_mask_words(const void* label, int label_dtype, int n_img, int H_img, int W_img,
+                                    int h, int w, const int32_t* lut, int lut_size, int words,
+                                    uint32_t* mask, protoseg_stream_t stream);
 
 /*
  * Push, step 2: for every image and prototype, the masked argmin of the distance over the
@@ -163,7 +195,7 @@ int protoseg_patch_class_mask(const void* label, int label_dtype, int n_img, int
  * Distances are computed in-kernel (f32 MFMA, an exact f32 fma chain) with the reference's
  * rounding order for relu(||x||^2 + (||p||^2 - 2 x.p)), model.py:217-219.
  *
- *   x           [n_img, C, h, w] f32, C in {32, 64, 128}
+ *   x           [n_img, C, h, w] f32 (C in {32, 64, 128}: the fused kernel; other C: the wide path)
  *   proto_class [P] int32: argmax(prototype_class_identity[p]) (push.py:251); <0 = never pushed
  *   mask        [n_img, h*w] uint32 from protoseg_patch_class_mask
  *   img_keys    [n_img, P] uint64 out: (float_bits(d_min) << 32) | patch_index, or
@@ -184,6 +216,14 @@ int protoseg_push_argmin(const float* x, int n_img, int C, int h, int w,
                          const float* protos, int P, const int32_t* proto_class,
                          const uint32_t* mask, uint64_t* img_keys, uint64_t* img_second,
                          protoseg_stream_t stream);
+/* The same with a protoseg_patch_class_mask_words mask of `words` planes (prototype class c reads
+ * plane c >> 5). Prototype depths outside {32, 64, 128}, and every words > 1 call, take the wide
+ * path: the image's distances by the exact-f32 GEMM of l2_wide.hip, then a masked top-2 per
+ * (image, prototype), same key contract and tie rule (lowest patch index). */
+int protoseg_push_argmin_words(const float* x, int n_img, int C, int h, int w,
+                               const float* protos, int P, const int32_t* proto_class,
+                               const uint32_t* mask, int words, uint64_t* img_keys, uint64_t* img_second,
+                               protoseg_stream_t stream);
 
 /*
  * Push, exact-tie resolution: distances of m prototypes at every patch of ONE image in
@@ -192,12 +232,15 @@ int protoseg_push_argmin(const float* x, int n_img, int C, int h, int w,
  * first in the reference's list(set) order (push.py:214-230 insertion order, np.argmin at
  * 259-262). Replaces the reference's proto_dist_[patch_i, patch_j, j] gather (push.py:259-260)
  * for those prototypes only.
- *   x      [C, h, w] f32 (one image), C in {32, 64, 128}
+ *   x      [C, h, w] f32 (one image); C outside {32, 64, 128}: the wide path's arithmetic
  *   protos [m, C] f32, 16-B aligned (the gathered prototypes)
  *   dist   [m, h*w] f32 out
  */
 int protoseg_push_distances(const float* x, int C, int h, int w, const float* protos, int m, float* dist,
                             protoseg_stream_t stream);
+/* protoseg_push_distances in protoseg_push_argmin_words' arithmetic for the same (C, words). */
+int protoseg_push_distances_words(const float* x, int C, int h, int w, const float* protos, int m, int words,
+                                  float* dist, protoseg_stream_t stream);
 
 /*
  * Push, step 3: fold a batch of per-image keys into the running global minimum in image
@@ -253,6 +296,25 @@ int protoseg_kld_backward(const float* dist, int B, int P, int HW, const void* l
                           const int32_t* proto_class, int K, int max_per_class, const float* g_loss,
                           void* workspace, size_t workspace_bytes, float* g_dist,
                           protoseg_stream_t stream);
+/*
+ * The backward in the compact layout protoseg_l2_bwd_kld consumes (no [B, P, HW] tensor): the
+ * gradient is non-zero only at the prototypes of each pixel's own class (module.py:173-178), so
+ * it is stored per pixel and class slot. Same values as protoseg_kld_backward's g_dist:
+ *   g_cls      [B*HW, max_per_class] f32 out: g_cls[g][i] = d loss / d dist[b][idx_c[i]][n] for
+ *              the pixels of a contributing group (other entries are not written)
+ *   pix_cls    [B*HW] int32 out: the pixel's class c when its (image, class) group adds pairs, else -1
+ *   proto_slot [P] int32 out: class * 256 + position of the prototype among its class's prototypes
+ *              (ascending prototype id); prototypes outside [0, K) get class K
+ * protoseg_kld_expand writes (accumulate = 0) or adds (1) the dense g_dist these describe.
+ */
+int protoseg_kld_backward_compact(const float* dist, int B, int P, int HW, const void* label, int label_dtype,
+                                  const int32_t* proto_class, int K, int max_per_class, const float* g_loss,
+                                  void* workspace, size_t workspace_bytes,
+                                  float* g_cls, int32_t* pix_cls, int32_t* proto_slot,
+                                  protoseg_stream_t stream);
+int protoseg_kld_expand(const float* g_cls, const int32_t* pix_cls, const int32_t* proto_slot,
+                        int B, int P, int HW, int max_per_class, int accumulate, float* g_dist,
+                        protoseg_stream_t stream);
 
 /*
  * Segmentation evaluation counts. Replaces segmentation/eval_valid.py:159-197: bilinear upsample

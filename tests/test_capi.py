@@ -33,16 +33,20 @@ def test_version_and_supported_shapes():
     assert lib.protoseg_l2_supported(64, 361, 19) == 1
     assert lib.protoseg_l2_supported(32, 38, 3) == 1
     assert lib.protoseg_l2_supported(128, 64, 32) == 1
-    assert lib.protoseg_l2_supported(48, 190, 19) == 0    # C outside the kernel family
-    assert lib.protoseg_l2_supported(64, 190, 33) == 0    # more than 32 classes
     assert lib.protoseg_l2_supported(64, 570, 19) == 1    # 30 prototypes/class: bf16 prototype chunks
-    assert lib.protoseg_l2_supported(64, 5000, 19) == 0   # beyond the chunked bound
     assert lib.protoseg_l2_supported(128, 1000, 19) == 1  # f32 family over prototype chunks
-    assert lib.protoseg_l2_max_protos(64, _lib.PREC_BF16X3) == 4096
-    assert lib.protoseg_l2_max_protos(64, _lib.PREC_BF16X6) == 4096
-    assert lib.protoseg_l2_max_protos(64, _lib.PREC_F32) == 4096  # f32 family chunks too
-    assert lib.protoseg_l2_max_protos(128, _lib.PREC_BF16X3) == 4096
-    assert lib.protoseg_l2_max_protos(48, _lib.PREC_F32) == 0
+    # the wide family (l2_wide.hip): any depth, any class count, P beyond the chunked bound
+    assert lib.protoseg_l2_supported(48, 190, 19) == 1
+    assert lib.protoseg_l2_supported(64, 190, 33) == 1
+    assert lib.protoseg_l2_supported(64, 5000, 19) == 1
+    assert lib.protoseg_l2_supported(256, 2000, 200) == 1  # construct_PPNet's default, model.py:394
+    assert lib.protoseg_l2_supported(512, 2000, 200) == 1
+    assert lib.protoseg_l2_supported(0, 190, 19) == 0
+    assert lib.protoseg_l2_supported(8192, 190, 19) == 0
+    assert lib.protoseg_l2_supported(64, 100000, 19) == 0
+    for C in (48, 64, 128, 512):
+        assert lib.protoseg_l2_max_protos(C, _lib.PREC_BF16X3) == 65536
+    assert lib.protoseg_l2_max_protos(0, _lib.PREC_F32) == 0
     assert lib.protoseg_l2_max_protos(64, 9) == 0
     for C in (32, 64, 128):
         m = lib.protoseg_l2_max_protos(C, _lib.PREC_F32)
@@ -71,7 +75,7 @@ def test_argument_validation_returns_status_without_gpu():
     dummy = ctypes.c_void_p(16)  # never dereferenced: validation fails first
     st = lib.protoseg_l2_fwd(dummy, 7, 1, 64, 2, 2, dummy, 19, dummy, 19, 1e-4, 0, 0, null, null, null, null)
     assert st == _lib.ERR_UNSUPPORTED
-    st = lib.protoseg_l2_fwd(dummy, 0, 1, 48, 2, 2, dummy, 19, dummy, 19, 1e-4, 0, 0, null, null, null, null)
+    st = lib.protoseg_l2_fwd(dummy, 0, 1, 8192, 2, 2, dummy, 19, dummy, 19, 1e-4, 0, 0, null, null, null, null)
     assert st == _lib.ERR_UNSUPPORTED
     st = lib.protoseg_l2_fwd(dummy, 0, 1, 64, 2, 2, dummy, 19, dummy, 19, 1e-4, 0, 9, null, null, null, null)
     assert st == _lib.ERR_UNSUPPORTED and b"precision" in lib.protoseg_last_error()
@@ -82,7 +86,9 @@ def test_argument_validation_returns_status_without_gpu():
     assert st == _lib.ERR_INVALID
     st = lib.protoseg_patch_class_mask(null, 2, 1, 4, 4, 2, 2, null, 0, null, null)
     assert st == _lib.ERR_INVALID
-    st = lib.protoseg_push_argmin(dummy, 1, 48, 2, 2, dummy, 3, dummy, dummy, dummy, null, null)
+    st = lib.protoseg_push_argmin(dummy, 1, 8192, 2, 2, dummy, 3, dummy, dummy, dummy, null, null)
     assert st == _lib.ERR_UNSUPPORTED
+    st = lib.protoseg_push_argmin_words(dummy, 1, 64, 2, 2, dummy, 3, dummy, dummy, 0, dummy, null, null)
+    assert st == _lib.ERR_INVALID
     with pytest.raises(_lib.ProtosegError, match="status 1"):
         _lib.call("protoseg_push_merge", null, null, 1, 0, null, 64, 4, 3, null, null, null, null, null, null)

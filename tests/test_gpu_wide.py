@@ -1,0 +1,159 @@
+"""The wide family (l2_wide.hip): any prototype depth C and any class count K.
+
+The reference's own construct_PPNet default is prototype_shape = (2000, 512, 1, 1) with 200
+classes (model.py:394); the C in {32, 64, 128}, K <= 32 kernels do not hold it. These tests run
+that shape (and C = 256, odd depths, K > 32 at C = 64) through PPNet's layer op and the push
+argmin, against the oracle (model.py:203-283 restated op for op, autograd for the backward;
+push.py:195-263 restated). Products are exact f32 (v_mfma_f32_32x32x2_f32 fma chains): distances
+within 1e-4 relative (+ a floor of 1e-6 (||x||^2 + ||p||^2) for the expanded form's
+cancellation), logits and gradients within 1e-4 of their own scale (f32 sums over C / P / pixels
+in a different order than torch-CPU's).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import protoseg_oracle as po
+from oracle import push_oracle as pu
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(got, ref, name, rel=1e-4):
+    got = got.detach().double().cpu()
+    ref = ref.double()
+    scale = ref.abs().max().item()
+    err = (got - ref).abs().max().item()
+    assert err <= rel * max(scale, 1e-30), f"{name}: max err {err:.3e} (scale {scale:.3e})"
+
+
+def _inputs(B, C, h, w, P, K, seed):
+    gen = torch.Generator().manual_seed(seed)
+    x = torch.sigmoid(2.0 * torch.randn(B, C, h, w, generator=gen))
+    protos = torch.rand(P, C, generator=gen)
+    ident = torch.zeros(P, K)
+    for p in range(P):
+        ident[p, p % K] = 1  # every class holds prototypes even when P is not a multiple of K
+    w_last = po.last_layer_init(ident)
+    g_logits = torch.randn(B, h, w, K, generator=gen) / (B * h * w)
+    g_dist = torch.randn(B, P, h, w, generator=gen) * 1e-3
+    return x, protos, w_last, g_logits, g_dist
+
+
+@pytest.mark.parametrize("B,C,h,w,P,K", [
+    (1, 512, 7, 9, 2000, 200),   # construct_PPNet's default (model.py:394)
+    (2, 256, 9, 11, 2000, 200),
+    (2, 48, 13, 7, 190, 19),     # a depth outside {32, 64, 128}
+    (2, 64, 9, 10, 120, 40),     # more than 32 classes at C = 64
+    (1, 96, 5, 6, 4500, 19),     # P beyond the chunked families' 4096
+])
+def test_wide_layer_forward_backward_vs_oracle(device, B, C, h, w, P, K):
+    from protoseg_amd import _lib, ops
+    assert _lib.load().protoseg_l2_supported(C, P, K) == 1
+    x, protos, w_last, g_logits, g_dist = _inputs(B, C, h, w, P, K, seed=C + P + K)
+    xd = x.to(device).requires_grad_(True)
+    pd = protos.to(device).requires_grad_(True)
+    wd = w_last.to(device).requires_grad_(True)
+    dist, logits, _ = ops.prototype_layer(xd, pd, wd)
+    torch.autograd.backward([logits, dist], [g_logits.to(device), g_dist.to(device)])
+    torch.cuda.synchronize()
+    r_logits, r_dist, r_gx, r_gp, r_gw = po.forward_backward(x, protos, w_last, g_logits, g_dist)
+    floor = 1e-6 * ((x ** 2).sum(1).max() + (protos ** 2).sum(1).max()).item()
+    derr = (dist.detach().cpu() - r_dist).abs()
+    assert bool((derr <= 1e-4 * r_dist.abs() + floor).all()), f"distances: max err {derr.max().item():.3e}"
+    _close(logits, r_logits, "logits")
+    _close(xd.grad, r_gx, "g_x")
+    _close(pd.grad, r_gp, "g_protos")
+    _close(wd.grad, r_gw, "g_w")
+
+
+def test_wide_layer_bf16_x_and_activations(device):
+    """bf16 feature maps (widened exactly), the activation output and the linear activation."""
+    from protoseg_amd import ops
+    B, C, h, w, P, K = 2, 160, 6, 7, 300, 37
+    x, protos, w_last, g_logits, _ = _inputs(B, C, h, w, P, K, seed=3)
+    xb = x.to(torch.bfloat16)
+    xd = xb.to(device).requires_grad_(True)
+    pd = protos.to(device).requires_grad_(True)
+    wd = w_last.to(device).requires_grad_(True)
+    _, logits, acts = ops.prototype_layer(xd, pd, wd, with_dist=False, with_act=True)
+    logits.backward(g_logits.to(device))
+    r_logits, r_act = po.forward_from_conv_features(xb.float(), protos, w_last, return_activations=True)
+    _close(logits, r_logits, "logits")
+    _close(acts, r_act, "activations")
+    _, _, r_gx, r_gp, r_gw = po.forward_backward(xb.float(), protos, w_last, g_logits, None)
+    _close(xd.grad.float(), r_gx, "g_x (bf16)", rel=1e-2)  # g_x is stored in bf16
+    _close(pd.grad, r_gp, "g_protos")
+    _close(wd.grad, r_gw, "g_w")
+    dist_lin, logits_lin, _ = ops.prototype_layer(xd.detach(), pd.detach(), wd.detach(), activation="linear")
+    r_ll, r_dl = po.forward_from_conv_features(xb.float(), protos, w_last, activation="linear")
+    _close(logits_lin, r_ll, "logits (linear)")
+
+
+def _bitmask_words(labels, h, w, words):
+    """Multi-plane class bitmask [words, h*w] from the reference's class -> patch sets."""
+    sets = pu.class_to_patch_index_dict(labels, h, w, 32 * words)
+    out = np.zeros((words, h * w), dtype=np.uint32)
+    for k, patches in sets.items():
+        for (i, j) in patches:
+            out[k >> 5, i * w + j] |= np.uint32(1 << (k & 31))
+    return out
+
+
+@pytest.mark.parametrize("C,P,K", [(256, 2000, 200), (512, 400, 200), (48, 190, 19), (64, 190, 19)])
+def test_wide_push_argmin_vs_oracle(device, C, P, K):
+    """push.py:195-263 at >32 classes / wide depths: class planes bit-exact, minima and (where
+    separated) patch indices equal to the oracle's, runner-ups, and push_distances reproducing
+    exactly the distances the argmin saw (the exact-tie resolution's premise)."""
+    from protoseg_amd import push
+    n, h, w, H, W = 2, 9, 11, 40, 47
+    words = push.mask_words(K)
+    rng = np.random.default_rng(C + K)
+    labels = rng.integers(0, K + 1, size=(n, H, W)).astype(np.int64)
+    x, protos, _, _, _ = _inputs(n, C, h, w, P, K, seed=P)
+    pcls = (torch.arange(P) % K).to(torch.int32)
+    mask = push.patch_class_mask(torch.from_numpy(labels).to(device), h, w, words=words)
+    mk = mask.cpu().numpy().view(np.uint32)
+    if words == 1:
+        mk = mk[None]
+    for i in range(n):
+        assert np.array_equal(mk[:, i], _bitmask_words(labels[i], h, w, words))
+    xd, pd, pcd = x.to(device), protos.to(device), pcls.to(device)
+    keys, second = push.push_argmin(xd, pd, pcd, mask, with_second=True)
+    d, patch, found = push.decode_keys(keys.cpu())
+    ds, _, fs = push.decode_keys(second.cpu())
+    r_dist = po.l2_convolution(x, protos[:, :, None, None], torch.ones(P, C, 1, 1))
+    exact = 0
+    for i in range(n):
+        sets = pu.class_to_patch_index_dict(labels[i], h, w, K)
+        dm = r_dist[i].reshape(P, -1).numpy()
+        dk = push.push_distances(xd[i], pd, words).cpu().numpy()  # the argmin's own arithmetic
+        for p in range(0, P, max(1, P // 97)):
+            cand = sorted(pi * w + pj for pi, pj in sets[int(pcls[p])])
+            assert bool(found[i, p]) == (len(cand) > 0)
+            if not cand:
+                continue
+            ref = dm[p, cand]
+            assert abs(float(d[i, p]) - ref.min()) <= 1e-4 * ref.min() + 1e-4
+            own = dk[p, cand]
+            assert float(d[i, p]) == own.min() and int(patch[i, p]) == cand[int(np.argmin(own))]
+            if len(cand) > 1:
+                assert bool(fs[i, p]) and float(ds[i, p]) == np.sort(own)[1]
+            srt = np.sort(ref)
+            if len(cand) == 1 or srt[1] - srt[0] > 1e-5 * (1 + srt[0]) + 1e-4:
+                assert int(patch[i, p]) == cand[int(np.argmin(ref))]
+                exact += 1
+    assert exact > 0
+
+
+def test_ppnet_default_shape_constructs(device):
+    """construct_PPNet's reference default (prototype_shape (2000, 512, 1, 1), 200 classes) runs
+    a forward + backward on the HIP path."""
+    from protoseg_amd import ops
+    x, protos, w_last, g_logits, _ = _inputs(1, 512, 4, 5, 2000, 200, seed=9)
+    xd = x.to(device).requires_grad_(True)
+    dist, logits, _ = ops.prototype_layer(xd, protos.to(device), w_last.to(device))
+    logits.backward(g_logits.to(device))
+    torch.cuda.synchronize()
+    assert dist.shape == (1, 2000, 4, 5) and logits.shape == (1, 4, 5, 200)
+    assert torch.isfinite(xd.grad).all()
