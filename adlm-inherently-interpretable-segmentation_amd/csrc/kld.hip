@@ -109,57 +109,39 @@ KldPtrs kld_ptrs(void* ws, const KldLayout& l) {
 
 __device__ __forceinline__ int bucket_of(int pc, int K) { return (pc >= 0 && pc < K) ? pc : K; }
 
-// One wave: prototypes are scanned 64 at a time (lane = prototype); for each bucket c a ballot
-// gives the bucket's members of the chunk, appended in ascending prototype order
-// (module.py:173: nonzero of the identity column = the prototypes whose class is c). Bucket K
-// collects prototypes with no class in [0, K). Two sweeps: counts, then positions.
 constexpr int kKldListMaxP = 1 << 20;
+
+// One wave per bucket c (grid K + 1): prototypes scanned 64 at a time (lane = prototype), a
+// ballot per chunk for the bucket's members (module.py:173: nonzero of the identity column = the
+// prototypes whose class is c, ascending) and for the prototypes of lower buckets (the bucket's
+// start). Bucket K collects prototypes with no class in [0, K). Two sweeps: counts, then places.
 __global__ __launch_bounds__(64) void kld_lists_kernel(const int32_t* __restrict__ proto_class, int P, int K,
-                                                       int max_per_class, int* __restrict__ off,
-                                                       int* __restrict__ idx, int* __restrict__ stat,
+                                                       int* __restrict__ off, int* __restrict__ idx,
                                                        int* __restrict__ slot) {
-  // Bucket c's running count and write position live in lane c's registers (no LDS, no
-  // barriers): ballots give each chunk's members, a broadcast of lane c gives their base.
-  const int lane = threadIdx.x;
-  int cnt = 0;
+  const int lane = threadIdx.x, c = blockIdx.x;
+  int start = 0, cnt = 0;
   for (int p0 = 0; p0 < P; p0 += 64) {
     const int p = p0 + lane;
-    const int bk = p < P ? bucket_of(proto_class[p], K) : -1;
-    for (int c = 0; c <= K; ++c) {
-      const unsigned long long m = __ballot(bk == c);
-      if (lane == c) cnt += __popcll(m);
-    }
-  }
-  int incl = cnt;
-#pragma unroll
-  for (int sft = 1; sft < 64; sft <<= 1) {
-    const int v = __shfl_up(incl, sft);
-    if (lane >= sft) incl += v;
-  }
-  if (lane <= K) off[lane] = incl - cnt;
-  if (lane == K) off[K + 1] = incl;
-  const bool over = lane < K && cnt > max_per_class;
-  const unsigned long long any_over = __ballot(over);
-  int next = incl - cnt;  // lane c: next free slot of bucket c
-  for (int p0 = 0; p0 < P; p0 += 64) {
-    const int p = p0 + lane;
-    const int bk = p < P ? bucket_of(proto_class[p], K) : -1;
-    for (int c = 0; c <= K; ++c) {
-      const unsigned long long m = __ballot(bk == c);
-      if (m == 0ull) continue;  // uniform
-      const int base = __shfl(next, c), start = __shfl(incl - cnt, c);
-      if (bk == c) {
-        const int below = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0));
-        idx[base + below] = p;
-        slot[p] = c * 256 + (base + below - start);  // the prototype's column of the compact gradient
-      }
-      if (lane == c) next += __popcll(m);
-    }
+    const int bk = p < P ? bucket_of(proto_class[p], K) : K + 1;
+    start += __popcll(__ballot(bk < c));
+    cnt += __popcll(__ballot(bk == c));
   }
   if (lane == 0) {
-    stat[0] = 0;
-    stat[1] = any_over != 0ull ? 1 : 0;
+    off[c] = start;
+    if (c == K) off[K + 1] = start + cnt;
+  }
+  int pos = start;
+  for (int p0 = 0; p0 < P; p0 += 64) {
+    const int p = p0 + lane;
+    const bool in = p < P && bucket_of(proto_class[p], K) == c;
+    const unsigned long long m = __ballot(in);
+    if (in) {
+      const int r = pos + __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0));
+      idx[r] = p;
+      slot[p] = c * 256 + (r - start);  // the prototype's column of the compact gradient
+    }
+    pos += __popcll(m);
   }
 }
 
@@ -329,12 +311,28 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
         const float* zi = sz + i * kKldLdsStride;
         const float* zj = sz + j * kKldLdsStride;
         float a = acc[k];
+        // four independent chains (the LDS reads of a step do not wait for the previous fma);
+        // summed in a fixed order, so the result is deterministic
+        float a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        int q = g;
         if (i == j) {
-          for (int q = g; q < kq; q += G) a += ei[q];
+          for (; q + 3 * G < kq; q += 4 * G) {
+            a += ei[q];
+            a1 += ei[q + G];
+            a2 += ei[q + 2 * G];
+            a3 += ei[q + 3 * G];
+          }
+          for (; q < kq; q += G) a += ei[q];
         } else {
-          for (int q = g; q < kq; q += G) a = fmaf(ei[q], zi[q] - zj[q], a);
+          for (; q + 3 * G < kq; q += 4 * G) {
+            a = fmaf(ei[q], zi[q] - zj[q], a);
+            a1 = fmaf(ei[q + G], zi[q + G] - zj[q + G], a1);
+            a2 = fmaf(ei[q + 2 * G], zi[q + 2 * G] - zj[q + 2 * G], a2);
+            a3 = fmaf(ei[q + 3 * G], zi[q + 3 * G] - zj[q + 3 * G], a3);
+          }
+          for (; q < kq; q += G) a = fmaf(ei[q], zi[q] - zj[q], a);
         }
-        acc[k] = a;
+        acc[k] = a + ((a1 + a2) + a3);
       }
     }
     __syncthreads();
@@ -423,6 +421,7 @@ __global__ __launch_bounds__(64) void kld_merge_kernel(int P, int K, int S, int 
 // Mean over all pairs of exp(-kld) (module.py:202-206): the per-(image, class) sums of
 // kld_merge_kernel added in a fixed order.
 __global__ __launch_bounds__(256) void kld_finalize_kernel(int groups, const float* __restrict__ group_sums,
+                                                           const int* __restrict__ off, int K, int mpc,
                                                            int* __restrict__ stat, float* __restrict__ loss_out,
                                                            int32_t* __restrict__ npairs_out) {
   __shared__ float s_sum[256], s_n[256];
@@ -444,8 +443,11 @@ __global__ __launch_bounds__(256) void kld_finalize_kernel(int groups, const flo
   if (threadIdx.x == 0) {
     const int np = static_cast<int>(s_n[0]);
     float loss = np > 0 ? s_sum[0] / static_cast<float>(np) : 0.f;
-    if (stat[1]) loss = __builtin_nanf("");
+    bool over = false;  // a class holding more than max_per_class prototypes: the loss is NaN
+    for (int c = 0; c < K; ++c) over = over || off[c + 1] - off[c] > mpc;
+    if (over) loss = __builtin_nanf("");
     stat[0] = np;
+    stat[1] = over ? 1 : 0;
     loss_out[0] = loss;
     if (npairs_out) npairs_out[0] = np;
   }
@@ -510,12 +512,23 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_kernel(
     const float2* cb = coef + (static_cast<size_t>(b) * K + c) * kKldPair;
     for (int i = 0; i < npc; ++i) {
       const float pi = sp[i * kKldLdsStride + tid], li = slp[i * kKldLdsStride + tid];
-      float g = 0.f;
-      for (int j = 0; j < npc; ++j) {
-        const float2 wk = cb[i * npc + j];  // (w_ij, KL_ij); w_ii = 0
-        g = fmaf(wk.x, pi * (li - slp[j * kKldLdsStride + tid] - wk.y + 1.f) - sp[j * kKldLdsStride + tid], g);
+      // the compact kernel's order (four chains over j, fixed-order sum): both layouts hold the
+      // same f32 values
+      float gj[4] = {0.f, 0.f, 0.f, 0.f};
+      int j = 0;
+      for (; j + 3 < npc; j += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float2 wk = cb[i * npc + j + u];  // (w_ij, KL_ij); w_ii = 0
+          gj[u] = fmaf(wk.x, pi * (li - slp[(j + u) * kKldLdsStride + tid] - wk.y + 1.f) - sp[(j + u) * kKldLdsStride + tid],
+                       gj[u]);
+        }
       }
-      sg[i * kKldLdsStride + tid] = 0.5f * g;
+      for (; j < npc; ++j) {
+        const float2 wk = cb[i * npc + j];
+        gj[0] = fmaf(wk.x, pi * (li - slp[j * kKldLdsStride + tid] - wk.y + 1.f) - sp[j * kKldLdsStride + tid], gj[0]);
+      }
+      sg[i * kKldLdsStride + tid] = 0.5f * ((gj[0] + gj[1]) + (gj[2] + gj[3]));
     }
   }
   float* gb = g_dist + static_cast<size_t>(b) * P * HW + n;
@@ -581,11 +594,21 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_compact_kernel(
     for (int t = tid; t < npc * kq; t += kKldThreads) {
       const int q = t / npc, i = t - q * npc;
       const float pi = sp[i * kKldLdsStride + q], li = slp[i * kKldLdsStride + q];
-      float g = 0.f;
-      for (int j = 0; j < npc; ++j) {
-        const float2 wk = scoef[i * npc + j];  // (w_ij, KL_ij); w_ii = 0
-        g = fmaf(wk.x, pi * (li - slp[j * kKldLdsStride + q] - wk.y + 1.f) - sp[j * kKldLdsStride + q], g);
+      float gj[4] = {0.f, 0.f, 0.f, 0.f};  // four independent chains over j, summed in fixed order
+      int j = 0;
+      for (; j + 3 < npc; j += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float2 wk = scoef[i * npc + j + u];  // (w_ij, KL_ij); w_ii = 0
+          gj[u] = fmaf(wk.x, pi * (li - slp[(j + u) * kKldLdsStride + q] - wk.y + 1.f) - sp[(j + u) * kKldLdsStride + q],
+                       gj[u]);
+        }
       }
+      for (; j < npc; ++j) {
+        const float2 wk = scoef[i * npc + j];
+        gj[0] = fmaf(wk.x, pi * (li - slp[j * kKldLdsStride + q] - wk.y + 1.f) - sp[j * kKldLdsStride + q], gj[0]);
+      }
+      const float g = (gj[0] + gj[1]) + (gj[2] + gj[3]);
       g_cls[(static_cast<size_t>(b) * HW + lq[q]) * mpc + i] = 0.5f * g;
     }
     __syncthreads();
@@ -659,8 +682,7 @@ extern "C" int protoseg_kld_forward(const float* dist, int B, int P, int HW, con
   const KldLayout l = kld_layout(B, P, HW, K);
   const KldPtrs w = kld_ptrs(workspace, l);
   const int S = kld_ranges(HW);
-  hipLaunchKernelGGL(kld_lists_kernel, dim3(1), dim3(64), 0, s, proto_class, P, K, max_per_class, w.off, w.idx, w.stat,
-                     w.slot);
+  hipLaunchKernelGGL(kld_lists_kernel, dim3(K + 1), dim3(64), 0, s, proto_class, P, K, w.off, w.idx, w.slot);
   if (int st = check_launch("kld_lists_kernel")) return st;
   const size_t lds = static_cast<size_t>(2) * max_per_class * kKldLdsStride * sizeof(float);
   const int st = by_label(label_dtype, [&](auto tl) {
@@ -674,7 +696,8 @@ extern "C" int protoseg_kld_forward(const float* dist, int B, int P, int HW, con
   hipLaunchKernelGGL(kld_merge_kernel, dim3(K, B), dim3(64), 0, s, P, K, S, max_per_class, w.off, w.idx, w.part, w.cnt,
                      w.lse, w.kl, w.group);
   if (int e = check_launch("kld_merge_kernel")) return e;
-  hipLaunchKernelGGL(kld_finalize_kernel, dim3(1), dim3(256), 0, s, B * K, w.group, w.stat, loss_out, npairs_out);
+  hipLaunchKernelGGL(kld_finalize_kernel, dim3(1), dim3(256), 0, s, B * K, w.group, w.off, K, max_per_class, w.stat,
+                     loss_out, npairs_out);
   return check_launch("kld_finalize_kernel");
 }
 

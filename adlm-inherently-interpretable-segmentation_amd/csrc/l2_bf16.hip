@@ -309,13 +309,42 @@ __global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
     const unsigned dbase = valid ? static_cast<unsigned>(((b * ld + p0 + 4 * h) * HW + n) * 4) : kOOB;
     const unsigned abase = valid ? static_cast<unsigned>((g * ld + p0 + 4 * h) * 4) : kOOB;
     f32x16 lacc = zero16();
+    // The (-2P) fragments of the next prototype tile are read from LDS while this tile's
+    // epilogue runs (one LDS round trip per tile off the MFMA chain), and the W fragments of the
+    // logits before the epilogue's VALU, not after it.
+    // (bf16x3 only: the 3-term fragments would not fit the 256 registers beside the logits.)
+    constexpr bool kPf = T == 2;
+    bf16x8 pf[kNQ][T];
+    auto load_pf = [&](int pt) __attribute__((always_inline)) {
+#pragma unroll
+      for (int q = 0; q < kNQ; ++q) load_frag<T>(Pimg, Pp * kC, img_off<8>(pt * 32 + j, 2 * q + h), pf[q]);
+    };
+    if (kPf && pt0 < npt) load_pf(pt0);
     // Prototype tiles entirely below P store without a row predicate; only the last one (when
     // P is not a multiple of 32) pays for it. The body is instantiated for both cases.
     auto proto_tile = [&](int pt, auto full_tag) {
       constexpr bool kFull = decltype(full_tag)::value;
       float p2r[16];
       load_rows16(p2s + pt * 32 + 4 * h, p2r);
-      f32x16 acc = s_tile<T>(Pimg, Pp, pt, xb, x2, p2r);
+      f32x16 acc;
+      {
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {  // v_pk_add_f32: two rows per VALU op
+          const f32x2 v = f32x2{x2, x2} + f32x2{p2r[r], p2r[r + 1]};
+          acc[r] = v.x;
+          acc[r + 1] = v.y;
+        }
+      }
+      if constexpr (!kPf) load_pf(pt);
+#pragma unroll
+      for (int q = 0; q < kNQ; ++q) acc = mma_split<T>(pf[q], xb[q], acc);
+      if (kPf && pt + dpt < npt) load_pf(pt + dpt);
+      bf16x8 wa[2][T];
+      if constexpr (LOGITS && kPf) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) load_frag<T>(Wimg, Pp * 32, img_off<4>(pt * 32 + j, 2 * s + h), wa[s]);
+      }
       const int prem = P - pt * 32 - 4 * h;  // rows of this tile (and half) below P
       // No branches per element: a null output has a zero-size buffer resource (its stores are
       // dropped), rows past P get an out-of-range offset.
@@ -332,10 +361,10 @@ __global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
       if constexpr (LOGITS) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          bf16x8 ab[T], wa[T];
+          bf16x8 ab[T];
           acc_operand<T>(acc, s, ab);
-          load_frag<T>(Wimg, Pp * 32, img_off<4>(pt * 32 + j, 2 * s + h), wa);
-          lacc = mma_split<T>(wa, ab, lacc);
+          if constexpr (!kPf) load_frag<T>(Wimg, Pp * 32, img_off<4>(pt * 32 + j, 2 * s + h), wa[s]);
+          lacc = mma_split<T>(wa[s], ab, lacc);
         }
       }
     };

@@ -9,6 +9,6 @@ mkdir -p "$d"
 cp "$src" "$d/l2_bwd_onepass.hip"
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function "$@" -I"$C/../../include" -I"$C" -c "$d/l2_bwd_onepass.hip" -o "$d/l2_bwd_onepass.o"
 objs=""
-for o in capi l2_layer l2_bf16 l2_bwd_fused push kld eval knn bbox adam; do objs="$objs $C/$o.o"; done
+for o in capi l2_layer l2_wide l2_bf16 l2_bwd_fused push kld eval knn bbox adam; do objs="$objs $C/$o.o"; done
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fPIC $objs "$d/l2_bwd_onepass.o" -o "$d/libprotoseg_hip.so"
 echo "built $d"

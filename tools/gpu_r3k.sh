@@ -9,3 +9,5 @@ for P in 190 361; do
 P=$P timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/r3k_prof_$P" -o kp --output-format csv -- python3 "$R/tools/kld_prof.py" > "$R/gpurun_out/r3k_prof_$P.log" 2>&1 || { tail -20 "$R/gpurun_out/r3k_prof_$P.log"; exit 1; }
 python3 "$R/tools/kstats.py" "$R/gpurun_out/r3k_prof_$P/kp_kernel_stats.csv" | grep kld
 done
+cd "$R"
+timeout -k 10 300 python3 tools/ab_libs.py --protos 361 --call bwd_full --reps 40 2>&1 | grep -v amdgpu.ids | tee gpurun_out/r3k_ab_prio.log
