@@ -116,8 +116,11 @@ __global__ __launch_bounds__(256) void patch_mask_kernel(const TL* __restrict__ 
 // all ones) the half-waves merge and each (stripe, part) writes a partial top-2 that
 // push_top2_kernel folds. The runner-up distance lets the host flag near-ties (SURVEY.md §7,
 // hard part 2).
-constexpr int kPushBlk = 4;                 // 32-pixel tiles per staged block
-constexpr int kPushBlkPix = kPushBlk * 32;  // 128 pixels
+#ifndef PUSH_BLK
+#define PUSH_BLK 4
+#endif
+constexpr int kPushBlk = PUSH_BLK;          // 32-pixel tiles per staged block
+constexpr int kPushBlkPix = kPushBlk * 32;  // 128 pixels (at 4 tiles)
 constexpr int kPushXS = kPushBlkPix + 2;    // LDS row stride (floats): 16 * XS = 32 (mod 64) banks
 constexpr int kPushMaxTiles = 8;            // prototype tiles per chunk
 #ifndef PUSH_SPLIT
@@ -557,11 +560,12 @@ extern "C" int protoseg_push_argmin_words(const float* x, int n_img, int C, int 
     launch(push_argmin_kernel<1>, full, 0, per);
     launch(push_argmin_kernel<1>, rem ? 1 : 0, full * per, rem);
   } else if (nc == 2) {
-    if (int e = ensure_lds<push_argmin_kernel<2>, 72 * 1024>()) return e;
+    if (int e = ensure_lds<push_argmin_kernel<2>>()) return e;
     launch(push_argmin_kernel<2>, full, 0, per);
     launch(push_argmin_kernel<2>, rem ? 1 : 0, full * per, rem);
   } else {
-    if (int e = ensure_lds<push_argmin_kernel<4>, 140 * 1024>()) return e;
+    if (push_lds_bytes(C, per * kPushSplit) > kMaxLds) return fail(PROTOSEG_ERR_UNSUPPORTED, "push LDS at C=%d", C);
+    if (int e = ensure_lds<push_argmin_kernel<4>>()) return e;
     launch(push_argmin_kernel<4>, full, 0, per);
     launch(push_argmin_kernel<4>, rem ? 1 : 0, full * per, rem);
   }

@@ -434,7 +434,7 @@ def push_prototypes(dataset, prototype_network_parallel, prototype_layer_stride=
                     root_dir_for_saving_prototypes=None, epoch_number=None, prototype_img_filename_prefix=None,
                     prototype_self_act_filename_prefix=None, proto_bound_boxes_filename_prefix=None,
                     save_prototype_class_identity=True, log=print, pascal=False,
-                    prototype_activation_function_in_numpy=None, images_per_batch: int = 1,
+                    prototype_activation_function_in_numpy=None, images_per_batch: int = 8,
                     process_group=None):
     """Drop-in for segmentation/push.py:24-158 (same arguments and side effects, minus the
     visualisation PNGs). With torch.distributed initialised (or ``process_group`` given) and

@@ -558,23 +558,28 @@ def time_push(n_img, steps, warmup, device, C=64, H=1024, W=2048, h=129, w=257, 
 
 
 def cpu_push_baseline(budget_s, C=64, H=1024, W=2048, h=129, w=257, P=190, K=19):
-    """Oracle restatement of push.py:184-281 (Python loops, single thread) on one image."""
+    """Oracle restatement of push.py:184-281 on one image, op for op as the reference runs it on
+    the CPU: distances (torch-CPU conv, model.py:203-221), the label map as a torch.LongTensor
+    with one `.item()` per pixel for the class -> patch sets (push.py:186, 214-230), then the
+    per-prototype Python argmin (push.py:235-281). Single thread."""
     from oracle import protoseg_oracle as po
     from oracle import push_oracle as pu
     x, protos, labels, pc = make_push_inputs(1, C, H, W, h, w, P, K, "cpu", SEED)
+    lab = labels[0].numpy()
     n, t0 = 0, time.perf_counter()
     while True:
         d = po.l2_convolution(x, protos[:, :, None, None], torch.ones(P, C, 1, 1))[0]
         st = pu.PushOracleState(P, C)
-        pu.update_prototypes_on_image_core(st, x[0].numpy(), d.permute(1, 2, 0).numpy(), labels[0].numpy(),
-                                           pc.numpy(), K, 0)
+        sets = pu.class_to_patch_index_dict_torch(lab, h, w, K)
+        pu.update_prototypes_on_image_core(st, x[0].numpy(), d.permute(1, 2, 0).numpy(), lab, pc.numpy(), K, 0,
+                                           sets=sets)
         n += 1
         if time.perf_counter() - t0 >= budget_s:
             break
     dt = time.perf_counter() - t0
     return {"ms_per_img": round(dt / n * 1e3, 1), "cores": 1, "kind": "port",
-            "sample": f"{n} image(s): oracle push.py:184-281 loops (per-pixel patch sets + per-prototype argmin), "
-                      f"{H}x{W} labels, {C}x{h}x{w} map, P={P}"}
+            "sample": f"{n} image(s): push.py:184-281 on the CPU as the reference runs it (torch.LongTensor labels, "
+                      f"per-pixel .item() patch sets, per-prototype argmin), {H}x{W} labels, {C}x{h}x{w} map, P={P}"}
 
 
 def _timed_calls(run, steps, warmup):
@@ -890,6 +895,7 @@ def main():
     ap.add_argument("--launch", choices=["graph", "eager"], default="graph",
                     help="graph: each step is one HIP graph replay of the three C-ABI calls")
     ap.add_argument("--no-small-batch", action="store_true", help="skip the B=2/4 side lines")
+    ap.add_argument("--no-sigmoid", action="store_true", help="skip the fused add-on sigmoid side line")
     ap.add_argument("--no-train", action="store_true", help="skip the DeepLabV2-R101 DP training-step side line")
     ap.add_argument("--train-accumulations", type=int, default=1,
                     help="optimizer steps (x iter_size 5 micro-steps) timed in the training side line")
@@ -949,12 +955,15 @@ def main():
             kld[f"P{kstep.P}"] = line
 
     sigmoid = None
-    if world == 1 and args.precision == "bf16x3" and args.channels == 64:
+    if world == 1 and args.precision == "bf16x3" and args.channels == 64 and not args.no_sigmoid:
         sigmoid = time_sigmoid_step(step, max(5, args.steps // 2), 3)
 
     push = None
     if not args.no_push:
         push = time_push(args.push_images, args.push_steps, 1, device)
+        if world == 1 and args.push_images != 1:  # the 1-image call (push_prototypes(images_per_batch=1))
+            one = time_push(1, args.push_steps, 1, device)
+            push["images_per_call_1"] = {k: one[k] for k in ("ms_per_img", "argmin_kernel_ms_per_img", "roofline")}
 
     knn = evaluation = None
     if not args.no_knn and world == 1:

@@ -46,6 +46,25 @@ def class_to_patch_index_dict(img_y: np.ndarray, h: int, w: int, num_classes: in
     return {k: list(v) for k, v in sets.items()}
 
 
+def class_to_patch_index_dict_torch(img_y, h: int, w: int, num_classes: int) -> Dict[int, List[tuple]]:
+    """push.py:186 + 214-230 as the reference runs them: the label map as a torch.LongTensor and
+    one `int(img_y[i, j].item())` per pixel (the CPU baseline's timed loop; same sets as
+    class_to_patch_index_dict)."""
+    import torch
+    img_y = torch.LongTensor(np.asarray(img_y))
+    patch_height = img_y.shape[0] / h
+    patch_width = img_y.shape[1] / w
+    sets = {key: set() for key in range(num_classes)}
+    for pixel_i in range(img_y.shape[0]):
+        patch_i = int(pixel_i / patch_height)
+        for pixel_j in range(img_y.shape[1]):
+            patch_j = int(pixel_j / patch_width)
+            pixel_cls = int(img_y[pixel_i, pixel_j].item())
+            if pixel_cls > 0:
+                sets[pixel_cls - 1].add((patch_i, patch_j))
+    return {k: list(v) for k, v in sets.items()}
+
+
 def class_patch_bitmask_fast(img_y: np.ndarray, h: int, w: int) -> np.ndarray:
     """Vectorised class bitmask per patch, uint32 [h*w]: bit c-1 set iff a pixel of class c>0
     maps to the patch (same float64 division as push.py:217-219)."""

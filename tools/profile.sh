@@ -7,11 +7,12 @@
 # counters never share a pass with tracing domains other than the kernel trace).
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-TAG=${TAG:-r02}
+TAG=${TAG:-r03}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-B=(python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline)
+# one configuration per workload: no side lines that launch the same kernels at other shapes
+B=(python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-small-batch --no-train --no-sigmoid)
 declare -A ARGS
 ARGS[p361]="--protos 361 --side-protos 0 --no-kld --no-push --no-knn --no-eval"
 ARGS[p190]="--protos 190 --side-protos 0 --no-kld --no-push --no-knn --no-eval"
