@@ -157,3 +157,28 @@ def test_ppnet_default_shape_constructs(device):
     torch.cuda.synchronize()
     assert dist.shape == (1, 2000, 4, 5) and logits.shape == (1, 4, 5, 200)
     assert torch.isfinite(xd.grad).all()
+
+
+def test_densenet_config_depth_fp16(device):
+    """BASELINE configs[4] (DenseNet-161, 30 prototypes/class, fp16): the depth is not stated
+    (the add-on maps the 1024-channel features to prototype_shape[1]); at the full 1024 the layer
+    runs on the wide family, fp16 feature maps widened exactly at the boundary and g_x returned
+    in fp16."""
+    from protoseg_amd import ops
+    B, C, h, w, P, K = 2, 1024, 8, 8, 570, 19
+    x, protos, w_last, g_logits, _ = _inputs(B, C, h, w, P, K, seed=161)
+    xh = x.half()
+    xd = xh.to(device).requires_grad_(True)
+    pd = protos.to(device).requires_grad_(True)
+    wd = w_last.to(device).requires_grad_(True)
+    dist, logits, _ = ops.prototype_layer(xd, pd, wd)
+    logits.backward(g_logits.to(device))
+    r_logits, r_dist, r_gx, r_gp, r_gw = po.forward_backward(xh.float(), protos, w_last, g_logits, None)
+    floor = 1e-6 * ((xh.float() ** 2).sum(1).max() + (protos ** 2).sum(1).max()).item()
+    derr = (dist.detach().cpu() - r_dist).abs()
+    assert bool((derr <= 1e-4 * r_dist.abs() + floor).all()), f"distances: max err {derr.max().item():.3e}"
+    _close(logits, r_logits, "logits")
+    assert xd.grad.dtype == torch.float16
+    _close(xd.grad.float(), r_gx, "g_x (fp16)", rel=2e-3)
+    _close(pd.grad, r_gp, "g_protos")
+    _close(wd.grad, r_gw, "g_w")
