@@ -69,6 +69,7 @@ constexpr int kOThreads = kOW * 64;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 // ---- operand block (l2_prep_onepass_kernel). g = l >> 4, m = l & 15.
 //   wt [ptile Pp/16][term]: g_act B fragment (fragment order, 1 KiB, lane l at 16 l): lane (p =
@@ -183,9 +184,11 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
   const int G = static_cast<int>(gridDim.x);
   const int iters = (ntiles - static_cast<int>(blockIdx.x) + G - 1) / G;
   const unsigned sz = sizeof(TX);
+  const unsigned chs = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(HW) * sz);  // one channel plane
   const rsrc_t rx = make_rsrc(x, x_bytes), rg = make_rsrc(g_logits, gl_bytes);
   // GD = 2: g_dist points at the compact values (gd_bytes = npix * mpc * 4)
   const rsrc_t rgd = make_rsrc(GD == 2 ? cg.val : g_dist, gd_bytes), rgx = make_rsrc(g_x, g_x ? x_bytes : 0u);
+  const rsrc_t rimg = make_rsrc(img, static_cast<unsigned>(io.total));
   auto tile_of = [&](int i) __attribute__((always_inline)) { return static_cast<int>(blockIdx.x) + i * G; };
 
   // ---- prologue: the (-2P) image -> LDS (for the launch); the owned ||p||^2 -> registers ------
@@ -205,15 +208,25 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
     }
   }
 
+  // Lane-derived LDS / buffer addresses are loop-invariant; held across the tile loop they are the
+  // first values the allocator spills (a spilled address costs a scratch reload and a vmcnt(0)
+  // per tile), so each phase rebuilds them from the lane id plus an opaque zero (a few VALU).
+  auto opaque_lane = [&]() __attribute__((always_inline)) {
+    int z = 0;
+    asm volatile("" : "+v"(z));
+    return lane + z;
+  };
+
   // ---- staging: wave w stages pixels 4w .. 4w+3 of a tile. Lanes 0..31: x of pixel 4w + l/8,
   // chunk ch = l & 7 = channels chan_of(ch >> 1, ch & 1, 0..7) (the family's ||x||^2 order);
   // lanes 32..47: 8 classes (8 kc ..) of pixel 4w + (l - 32) / 4. Raw values go to registers
   // first (issued one phase ahead), then split into the images.
-  const int sn = 4 * wave + ((lane & 31) >> 3), sch = lane & 7;
-  const int gn = 4 * wave + ((lane - 32) >> 2), gkc = lane & 3;
   float raw[8];
   int rcl = -1;  // GD = 2, lanes 48 .. 51: the KLD class of pixel 4 wave + lane - 48
   auto load_raw = [&](int t) __attribute__((always_inline)) {
+    const int lz = opaque_lane();
+    const int sn = 4 * wave + ((lz & 31) >> 3), sch = lz & 7;
+    const int gn = 4 * wave + ((lz - 32) >> 2), gkc = lz & 3;
     if (lane < 32) {
       const int gp = t * 32 + sn;
       unsigned off = kOOB;
@@ -221,13 +234,13 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
         const int b = gp / HW;
         off = static_cast<unsigned>((b * kC) * HW + (gp - b * HW)) * sz;
       }
-      // the channel offset depends on the lane (sch): it goes into the per-lane voffset, never
-      // the soffset (a divergent soffset makes hipcc emit a waterfall loop per load)
+      // channel chan_of(q, h, e) = lane part (q, h) + element part (e): the lane part goes into
+      // the per-lane voffset (a divergent soffset makes hipcc emit a waterfall loop per load),
+      // the uniform element part into the soffset, so no per-element offsets stay live
+      const unsigned vo = off == kOOB ? kOOB : off + static_cast<unsigned>(chan_of(sch >> 1, sch & 1, 0) * HW) * sz;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const unsigned co = static_cast<unsigned>(chan_of(sch >> 1, sch & 1, e) * HW) * sz;
-        raw[e] = BufIO<TX>::load(rx, off == kOOB ? kOOB : off + co, 0u);
-      }
+      for (int e = 0; e < 8; ++e)
+        raw[e] = BufIO<TX>::load(rx, vo, __builtin_amdgcn_readfirstlane(static_cast<unsigned>(chan_of(0, 0, e)) * chs));
     } else {
       if constexpr (GD == 2) {
         const int gc = t * 32 + 4 * wave + (lane - 48);
@@ -245,6 +258,9 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
   auto convert = [&](int t) __attribute__((always_inline)) {
     float v[8];
     bf16x8 f[kOT];
+    const int lz = opaque_lane();
+    const int sn = 4 * wave + ((lz & 31) >> 3), sch = lz & 7;
+    const int gn = 4 * wave + ((lz - 32) >> 2), gkc = lz & 3;
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = raw[e];
     if (lane < 32) {
@@ -290,7 +306,6 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
 
   // transposed-read lane roles: lane 4 qq + pp of group g supplies row qq of its 4-row block,
   // 8-B slot pp of the block's 16 columns
-  const int qq = (lane >> 2) & 3, pp = lane & 3;
 
   // ---- phase A: owned prototype tile jt (16 prototypes) against the staged 32 pixels ---------
   f32x4 gp[NPT][4], gw[NPT][2];
@@ -303,14 +318,14 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
     gsum[jt] = 0.f;
   }
   auto owner_tile = [&](int jt) __attribute__((always_inline)) {
+    // The x / g_logits operands are the same for every owned tile: the opaque lane id in their
+    // LDS addresses makes each tile reload them instead of keeping their fragments live across
+    // the tiles (the compiler would hoist the loads out of the unrolled tile loop).
+    const int lz = opaque_lane();
+    const int m = lz & 15, g = lz >> 4, qq = (lz >> 2) & 3, pp = lz & 3;
     const int p = (wave * NPT + jt) * 16 + m;
-    // The x / g_logits operands are the same for every owned tile: an opaque zero in their LDS
-    // addresses makes each tile reload them instead of keeping their fragments live across the
-    // tiles (the compiler would hoist the loads out of the unrolled tile loop).
-    int z = 0;
-    asm volatile("" : "+v"(z));
-    const bf16* XAj = XA + z;
-    const bf16* GAj = GA + z;
+    const bf16* XAj = XA;
+    const bf16* GAj = GA;
     bf16x8 psj[2][kOT];  // S B fragments: rows p of the (-2P) image
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -319,8 +334,10 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
         psj[ks][t] = *reinterpret_cast<const bf16x8*>(PI + t * Pp * 64 + pi_off(p, 4 * ks + g));
     bf16x8 wtj[kOT];  // this tile's g_act B fragments, streamed from the (L2-resident) operand block
 #pragma unroll
-    for (int t = 0; t < kOT; ++t)
-      wtj[t] = *reinterpret_cast<const bf16x8*>(img + io.wt + ((wave * NPT + jt) * kOT + t) * 1024 + lane * 16);
+    for (int t = 0; t < kOT; ++t)  // lane part in the voffset, the tile's (uniform) part in the soffset
+      wtj[t] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rimg, static_cast<unsigned>(lz * 16),
+                                              static_cast<unsigned>(io.wt + ((wave * NPT + jt) * kOT + t) * 1024), 0));
     f32x4 acc[2], gacc[2];
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
@@ -413,20 +430,19 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
 
   // ---- phase B: g_x^T of channels 16 ct .. +15, pixels 16 nh .. +15, over all Pp prototypes ----
   const int ct = wave & 3, nh = wave >> 2;
-  bf16x8 ones;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = static_cast<bf16>(1.f);
   f32x4 gx;
   float xe[4], olde[4];  // x (and the earlier chunks' g_x) at the lane's output elements
   // output element r: channel 16 ct + 4 g + r, pixel 16 nh + m of the tile
-  auto out_off = [&](int t) __attribute__((always_inline)) -> unsigned {
+  auto out_off = [&](int t, int m, int g) __attribute__((always_inline)) -> unsigned {
     const int gp = t * 32 + 16 * nh + m;
     if (gp >= npix) return kOOB;
     const int b = gp / HW;
     return static_cast<unsigned>((b * kC + 16 * ct + 4 * g) * HW + (gp - b * HW)) * sz;
   };
   auto phase_b = [&](int t, int slot) __attribute__((always_inline)) {
-    const unsigned o = out_off(t);
+    const int lz = opaque_lane();
+    const int m = lz & 15, g = lz >> 4, qq = (lz >> 2) & 3, pp = lz & 3;
+    const unsigned o = out_off(t, m, g);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       xe[r] = BufIO<TX>::load(rx, o, static_cast<unsigned>(r * HW) * sz);
@@ -443,12 +459,10 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
     // k-step); every read is a per-lane base + an immediate offset (the image swizzles depend
     // on row bits below 32, so a k-step moves every address by the same amount).
     const int aslot = 4 * ct + pp, chunk = aslot >> 1, sub = (aslot & 1) * 4, row0 = 8 * g + qq;
-    int z = 0;
-    asm volatile("" : "+v"(z));  // the bases are rebuilt per tile, not held across phase A
-    const bf16* pa0 = PI + z + pi_off(row0, chunk) + sub;
-    const bf16* pa1 = PI + z + pi_off(row0 + 4, chunk) + sub;
-    const bf16* pb0 = GS + z + gs_off2(row0, 4 * nh + pp);
-    const bf16* pb1 = GS + z + gs_off2(row0 + 4, 4 * nh + pp);
+    const bf16* pa0 = PI + pi_off(row0, chunk) + sub;  // rebuilt per tile (opaque lane), not held across phase A
+    const bf16* pa1 = PI + pi_off(row0 + 4, chunk) + sub;
+    const bf16* pb0 = GS + gs_off2(row0, 4 * nh + pp);
+    const bf16* pb1 = GS + gs_off2(row0 + 4, 4 * nh + pp);
     auto ldk = [&](int ks, bf16x8 (&a)[kOT], bf16x8 (&b)[kOT]) __attribute__((always_inline)) {
 #pragma unroll
       for (int t2 = 0; t2 < kOT; ++t2) {
@@ -469,6 +483,8 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
     // sum_p g_s over this wave's quarter of the prototypes (k-steps ct KSQ ..): the g_s
     // fragments again, times a ones A operand
     const int qoff = ct * KSQ * 32 * 32;
+    const unsigned one2 = 0x3F803F80u + static_cast<unsigned>(lz - lane);  // bf16 (1, 1), built per tile, not held
+    const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{one2, one2, one2, one2});
 #pragma unroll
     for (int kk = 0; kk < KSQ; ++kk) {
       bf16x8 b[kOT];
@@ -481,9 +497,11 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
     if (lane < 16) SIG[((slot * 2 + nh) * 4 + ct) * 16 + m] = sg[0];
   };
   auto gx_epilogue = [&](int t, int slot) __attribute__((always_inline)) {
+    const int lz = opaque_lane();
+    const int m = lz & 15, g = lz >> 4;
     const float* sp = SIG + (slot * 2 + nh) * 64 + m;
     const float sn2 = ((sp[0] + sp[16]) + sp[32]) + sp[48];  // fixed order over the channel tiles
-    const unsigned o = out_off(t);
+    const unsigned o = out_off(t, m, g);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float v;
