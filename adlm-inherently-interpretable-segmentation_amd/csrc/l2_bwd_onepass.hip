@@ -153,6 +153,9 @@ __device__ __forceinline__ void store_half4(bf16* dst, const bf16x8& f, int half
 }
 
 #define OSCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#ifndef ONEPASS_PIPE
+#define ONEPASS_PIPE 1  // owned tile jt + 1's products issued before tile jt's epilogue
+#endif
 #ifndef PB_DEPTH
 #define PB_DEPTH 1  // phase B: k-steps of fragments in flight ahead of the one multiplying
 #endif
@@ -317,15 +320,27 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
     gw[jt][0] = gw[jt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     gsum[jt] = 0.f;
   }
-  auto owner_tile = [&](int jt) __attribute__((always_inline)) {
-    // The x / g_logits operands are the same for every owned tile: the opaque lane id in their
-    // LDS addresses makes each tile reload them instead of keeping their fragments live across
-    // the tiles (the compiler would hoist the loads out of the unrolled tile loop).
-    const int lz = opaque_lane();
-    const int m = lz & 15, g = lz >> 4, qq = (lz >> 2) & 3, pp = lz & 3;
+  // lz: the opaque lane id of this pixel tile's phase A (one per tile, shared by the owned
+  // prototype tiles, whose addresses differ by immediates: the swizzles use row bits below 16).
+  // An owned tile runs in two halves: the front (S and g_act products, the g_dist loads) and the
+  // back (epilogue, g_s image, g_P / g_W products). The main loop issues tile jt + 1's front
+  // before tile jt's back, so the epilogue's VALU runs beside the next tile's MFMAs.
+  struct Front {
+    f32x4 acc[2], gacc[2];
+    float gdv[8];
+  };
+  auto owner_front = [&](int jt, int lz, Front& fr) __attribute__((always_inline)) {
+    const int m = lz & 15, g = lz >> 4;
     const int p = (wave * NPT + jt) * 16 + m;
-    const bf16* XAj = XA;
-    const bf16* GAj = GA;
+    // the x / g_logits operands are the same for every owned tile: an opaque zero on their image
+    // bases makes each tile reload them instead of keeping their fragments live across the tiles
+    int zj = 0;
+    asm volatile("" : "+v"(zj));
+    const bf16* XAj = XA + zj;
+    const bf16* GAj = GA + zj;
+    f32x4 (&acc)[2] = fr.acc;
+    f32x4 (&gacc)[2] = fr.gacc;
+    float (&gdv)[8] = fr.gdv;
     bf16x8 psj[2][kOT];  // S B fragments: rows p of the (-2P) image
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -338,7 +353,6 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
       wtj[t] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
                                               rimg, static_cast<unsigned>(lz * 16),
                                               static_cast<unsigned>(io.wt + ((wave * NPT + jt) * kOT + t) * 1024), 0));
-    f32x4 acc[2], gacc[2];
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
       const float4 x2 = *reinterpret_cast<const float4*>(X2S + 16 * nt + 4 * g);
@@ -359,7 +373,6 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
       for (int t = 0; t < kOT; ++t) ga[t] = *reinterpret_cast<const bf16x8*>(GAj + t * 32 * 32 + ga_off(16 * nt + m, g));
       gacc[nt] = mma16_split(ga, wtj, f32x4{0.f, 0.f, 0.f, 0.f});
     }
-    float gdv[8];
     if constexpr (GD == 2) {
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
@@ -383,7 +396,17 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
           gdv[4 * nt + r] = BufIO<float>::load(rgd, (rv[r] != kOOB && pvalid) ? rv[r] + pcol : kOOB, 0);
       }
     }
-    OSCHED_FENCE();
+  };
+  auto owner_back = [&](int jt, int lz, Front& fr) __attribute__((always_inline)) {
+    const int m = lz & 15, g = lz >> 4, qq = (lz >> 2) & 3, pp = lz & 3;
+    const int p = (wave * NPT + jt) * 16 + m;
+    int zj = 0;
+    asm volatile("" : "+v"(zj));
+    const bf16* XAj = XA + zj;
+    const bf16* GAj = GA + zj;
+    const f32x4 (&acc)[2] = fr.acc;
+    const f32x4 (&gacc)[2] = fr.gacc;
+    const float (&gdv)[8] = fr.gdv;
     // epilogue: element e = 4 nt + r is pixel (16 nt + 4 g + r): the A / B k-slot order
     float gs[8], av[8];
 #pragma unroll
@@ -527,12 +550,28 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
   for (int i = 0; i < iters; ++i) {
     const int t = tile_of(i);
     if (i == 2) OSTAMP(2);
+    const int lzA = opaque_lane();
+#if ONEPASS_PIPE
+    Front fr[2];
+    owner_front(0, lzA, fr[0]);
 #pragma unroll
     for (int jt = 0; jt < NPT; ++jt) {
-      owner_tile(jt);
+      if (jt + 1 < NPT) owner_front(jt + 1, lzA, fr[(jt + 1) & 1]);
+      owner_back(jt, lzA, fr[jt & 1]);
+      if (i == 2) OSTAMP(3 + jt);
+    }
+    OSCHED_FENCE();
+#else
+#pragma unroll
+    for (int jt = 0; jt < NPT; ++jt) {
+      Front fr;
+      owner_front(jt, lzA, fr);
+      OSCHED_FENCE();
+      owner_back(jt, lzA, fr);
       OSCHED_FENCE();
       if (i == 2) OSTAMP(3 + jt);
     }
+#endif
     __syncthreads();  // g_s(i) complete; every wave's reads of the x / g_logits images done
     if (i == 2) OSTAMP(6);
     if (i + 1 < iters) load_raw(tile_of(i + 1));
