@@ -181,7 +181,7 @@ __device__ __forceinline__ unsigned x_lane_off(int t, int ntiles, int npix, int 
   const int j = threadIdx.x & 31, h = (threadIdx.x & 63) >> 5;
   const int g = t * 32 + j;
   if (t >= ntiles || g >= npix) return kOOB;
-  const int b = g / HW, n = g - b * HW;
+  const int b = div_pix(g, HW), n = g - b * HW;
   return static_cast<unsigned>(((b * kC + 4 * h) * HW + n) * static_cast<int>(sizeof(TX)));
 }
 
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
     const float x2 = x_frags<T>(xv, xb);
     const int g = t * 32 + j;
     const bool valid = g < npix;
-    const int b = valid ? g / HW : 0;
+    const int b = valid ? div_pix(g, HW) : 0;
     const int n = valid ? g - b * HW : 0;
     // ld = prototypes per image / pixel row of the outputs (= P, or the full P for a chunk
     // starting at prototype p0)
@@ -478,7 +478,7 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
   auto run_tile = [&](int t, const float (&raw)[kNQ * 8], int pt0, int dpt, f32x16 (&gx)[2], float& gsum) {
     const int g = t * 32 + j;
     const bool valid = g < npix;
-    const int b = valid ? g / HW : 0;
+    const int b = valid ? div_pix(g, HW) : 0;
     const int n = valid ? g - b * HW : 0;
     // B operand of g_act^T: lane (h, j) holds g_logits[pixel j][16s + 8h + jj]
     bf16x8 glb[2][T];
@@ -682,7 +682,7 @@ __global__ __launch_bounds__(MAXT) void l2_bwd_pw_bf16_kernel(
     const int g = t * 32 + j;
     unsigned xo = kOOB;
     if (t < ntiles && g < npix) {
-      const int b = g / HW;
+      const int b = div_pix(g, HW);
       xo = static_cast<unsigned>(((b * kC + h) * HW + (g - b * HW)) * static_cast<int>(sizeof(TX)));
     }
     const int lim = t < ntiles ? min(32, npix - t * 32) : 0;  // valid pixels of this tile
@@ -748,7 +748,7 @@ __global__ __launch_bounds__(MAXT) void l2_bwd_pw_bf16_kernel(
       if (w == npt - 1 && lane < 32) {  // per-row g_dist offset (b, n) of this tile
         const int g = t * 32 + lane;
         const bool ok = t < ntiles && g < npix;
-        const int b = ok ? g / HW : 0;
+        const int b = ok ? div_pix(g, HW) : 0;
         rowoff[lane] = ok ? static_cast<unsigned>(((b * gd_ld + gd_p0) * HW + (g - b * HW)) * 4) : kOOB;
       }
     }

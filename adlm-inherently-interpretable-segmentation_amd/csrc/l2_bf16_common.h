@@ -118,5 +118,18 @@ __device__ __forceinline__ float x2_tree_halves(const float (&s)[4]) {
   return (u[0] + u[1]) + (u[2] + u[3]);
 }
 
+// n / d for 0 <= n < 2^23 and a wave-uniform d >= 1 (the family's pixel indices: bf16_sizes_ok
+// keeps B H W below 2^23): a v_rcp_f32 estimate (1 ulp; the quotient estimate is within 0.75 of
+// n / d), truncation and one correction step, in place of the ~25-instruction signed division
+// the compiler emits for a runtime divisor. Exact, as the integer division.
+__device__ __forceinline__ int div_pix(int n, int d) {
+  const float r = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(__builtin_amdgcn_rcpf(static_cast<float>(d)))));
+  int q = static_cast<int>(static_cast<float>(n) * r);
+  const int rem = n - __mul24(q, d);
+  q += rem >= d ? 1 : 0;
+  q -= rem < 0 ? 1 : 0;
+  return q;
+}
+
 }  // namespace bf16l
 }  // namespace protoseg

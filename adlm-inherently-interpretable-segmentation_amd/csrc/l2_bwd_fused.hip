@@ -174,7 +174,7 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
     const int n = lane & 31, g = t * 32 + n;
     unsigned off = kOOB;
     if (t < ntiles && g < npix) {
-      const int b = g / HW;
+      const int b = div_pix(g, HW);
       off = static_cast<unsigned>((b * kC + (lane >> 5)) * HW + (g - b * HW)) * sz;
     }
 #pragma unroll
@@ -204,8 +204,13 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
     const XS* R = raw_slot(rs);
     float v[8];
     bf16x8 f[kT];
+    // lane-derived addresses rebuilt per tile from an opaque lane id: held across the loop they
+    // are what the allocator spills first (a scratch reload + vmcnt(0) per tile)
+    int z = 0;
+    asm volatile("" : "+v"(z));
+    const int lz = lane + z;
     if (lane < 32) {
-      const int n = 4 * wave + (lane >> 3), ch = lane & 7;
+      const int n = 4 * wave + (lz >> 3), ch = lz & 7;
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = lds_val(R + raw_x(chan_of(ch >> 1, ch & 1, e), n));
       if constexpr (XSIG) {  // pixels past the map stay 0 (their g_s is 0 anyway)
@@ -221,7 +226,7 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
       s += __shfl_xor(s, 4);
       if (ch == 0) x2_slot(sb)[n] = s;
     } else if (lane < 48) {
-      const int n = 4 * wave + ((lane - 32) >> 2), kc = lane & 3;
+      const int n = 4 * wave + ((lz - 32) >> 2), kc = lz & 3;
       const float* RG = reinterpret_cast<const float*>(R + kRawXDw);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = 8 * kc + e < K ? RG[n * K + 8 * kc + e] : 0.f;
@@ -231,7 +236,7 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
         if (kc == 0) {
           const int g = t * 32 + n;
           const bool ok = t < ntiles && g < npix;
-          const int b = ok ? g / HW : 0;
+          const int b = ok ? div_pix(g, HW) : 0;
           ro_slot(sb)[n] = ok ? static_cast<unsigned>(((b * gd_ld + gd_p0) * HW + (g - b * HW)) * 4) : kOOB;
         }
       } else if constexpr (GD == 2) {
@@ -273,13 +278,18 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
     const bf16* GA = ga_slot(sb);
     float x2r[16], gdv[16];
     load_rows16(x2_slot(sb) + 4 * h, x2r);
-    if constexpr (GD == 2) {
-      float rof[16], clf[16];
-      load_rows16(reinterpret_cast<const float*>(ro_slot(sb)) + 4 * h, rof);
-      load_rows16(reinterpret_cast<const float*>(cl_slot(sb)) + 4 * h, clf);
+    if constexpr (GD == 2) {  // four rows at a time: the row offsets / classes are not all live at once
+      const unsigned* ros = ro_slot(sb) + 4 * h;
+      const int* cls = cl_slot(sb) + 4 * h;
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        gdv[r] = BufIO<float>::load(rgd, __float_as_int(clf[r]) == pcls ? __float_as_uint(rof[r]) + pslot : kOOB, 0);
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const uint4 ro = *reinterpret_cast<const uint4*>(ros + 8 * g4);
+        const int4 cl = *reinterpret_cast<const int4*>(cls + 8 * g4);
+        const unsigned rv[4] = {ro.x, ro.y, ro.z, ro.w};
+        const int cv[4] = {cl.x, cl.y, cl.z, cl.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) gdv[4 * g4 + e] = BufIO<float>::load(rgd, cv[e] == pcls ? rv[e] + pslot : kOOB, 0);
+      }
     } else if constexpr (GD == 1) {
       float rof[16];
       load_rows16(reinterpret_cast<const float*>(ro_slot(sb)) + 4 * h, rof);
@@ -398,7 +408,7 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
     const int g = t * 32 + j;
     unsigned pix = kOOB;
     if (g < npix) {
-      const int b = g / HW;
+      const int b = div_pix(g, HW);
       pix = static_cast<unsigned>((b * kC + 32 * xw + 8 * h) * HW + (g - b * HW)) * sz;
     }
     // x (for the 2 x s term) and, for chunk c > 0, the earlier chunks' g_x: loads issued before

@@ -1,0 +1,8 @@
+#!/bin/bash
+# fused backward without spills: parity, then interleaved A/B against the previous build
+set -u
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_l2.py tests/test_gpu_kld_compact.py tests/test_gpu_kld.py tests/test_gpu_onepass.py > gpurun_out/r3t_tests.log 2>&1 || { tail -40 gpurun_out/r3t_tests.log; exit 1; }
+tail -1 gpurun_out/r3t_tests.log
+timeout -k 10 300 python3 tools/ab_libs.py --protos 190 --call bwd_full --reps 40 2>&1 | grep -v amdgpu.ids | tee gpurun_out/r3t_ab_bwd190.log
+timeout -k 10 300 python3 tools/ab_libs.py --protos 120 --call bwd_full --reps 40 2>&1 | grep -v amdgpu.ids | tee gpurun_out/r3t_ab_bwd120.log
