@@ -154,26 +154,38 @@ __device__ __forceinline__ int lane_rank(unsigned long long m) {  // set bits of
   return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0));
 }
 
+// n / d for 0 <= n < 2^23, d >= 1 with r = 1/d (v_rcp_f32, 1 ulp): the quotient estimate is
+// within 1 of n / d, one correction step makes it exact; replaces the ~25-instruction integer
+// division the compiler emits for a runtime divisor in the per-element task decompositions.
+__device__ __forceinline__ int qdiv(int n, int d, float r) {
+  int q = static_cast<int>(static_cast<float>(n) * r);
+  const int rem = n - __mul24(q, d);
+  q += rem >= d ? 1 : 0;
+  q -= rem < 0 ? 1 : 0;
+  return q;
+}
+__device__ __forceinline__ float qrcp(int d) { return __builtin_amdgcn_rcpf(static_cast<float>(d)); }
+
 // Gathers rows[i][q] = d[s_proto[i]][list[q]] for i < npc, q < kq over the workgroup's threads
 // (q fastest: consecutive lanes read consecutive class pixels of one prototype row), four loads
 // in flight per thread.
 __device__ __forceinline__ void gather_tasks(const float* __restrict__ db, int HW, const int* list, int kq,
                                              const int* s_proto, int npc, float* rows, int stride) {
   const int T = npc * kq;
+  const float rk = qrcp(kq);
   for (int t0 = threadIdx.x; t0 < T; t0 += 4 * kKldThreads) {
     float v[4];
+    int ro[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int t = t0 + u * kKldThreads;
-      const int i = t / kq, q = t - i * kq;
-      v[u] = t < T ? db[static_cast<size_t>(s_proto[i]) * HW + list[q]] : 0.f;
+      const int i = qdiv(t, kq, rk), q = t - i * kq;
+      ro[u] = i * stride + q;
+      v[u] = t < T ? db[static_cast<size_t>(s_proto[i < npc ? i : 0]) * HW + list[q]] : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int t = t0 + u * kKldThreads;
-      const int i = t / kq, q = t - i * kq;
-      if (t < T) rows[i * stride + q] = v[u];
-    }
+    for (int u = 0; u < 4; ++u)
+      if (t0 + u * kKldThreads < T) rows[ro[u]] = v[u];
   }
 }
 
@@ -268,10 +280,29 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
   float* se = kld_smem;                          // [npc][257]
   float* sz = kld_smem + npc * kKldLdsStride;    // [npc][257]
   const int E = npc * npc;
-  int G = kKldThreads / E;  // pixel groups per (i, j) entry
-  G = G < 1 ? 1 : (G > 16 ? 16 : G);
-  const int ntask = E * G;  // <= 1024
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  // T_ij in 4 x 4 register blocks: thread = (block (bi, bj), pixel group g); per pixel it reads
+  // e and z of its 4 rows and z of its 4 columns (12 LDS values for 16 fma, where one thread per
+  // entry read 3 per fma: the LDS reads, not the fma, bounded the chunk) and the 4 rows' sum e_i.
+  const int nbi = (npc + 3) >> 2, nblk = nbi * nbi;
+  int G = kKldThreads / nblk;
+  G = G > 64 ? 64 : G;
+  const int blk = tid / G, g = tid - blk * G;  // G >= 4: the divisions are by small powers / ints once
+  const bool worker = blk < nblk;
+  const int bi = worker ? blk / nbi : 0, bj = worker ? blk - bi * nbi : 0;
+  const int i0 = 4 * bi, j0 = 4 * bj;
+  int ri[4], rj[4];  // LDS row offsets, clamped into the class's rows (rows past npc are discarded)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    ri[r] = min(i0 + r, npc - 1) * kKldLdsStride;
+    rj[r] = min(j0 + r, npc - 1) * kKldLdsStride;
+  }
+  float acc[4][4], ssum[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    ssum[r] = 0.f;
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) acc[r][cc] = 0.f;
+  }
   for (int base = 0; base < total; base += kKldThreads) {
     const int kq = min(kKldThreads, total - base);
     gather_tasks(db, HW, s_list + base, kq, s_proto, npc, sz, kKldLdsStride);
@@ -292,62 +323,54 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int task = tid + k * kKldThreads;
-      if (task < ntask) acc[k] *= s_scale[(task / G) / npc];
+    for (int r = 0; r < 4; ++r) {
+      const float sc = s_scale[min(i0 + r, npc - 1)];
+      ssum[r] *= sc;
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) acc[r][cc] *= sc;
     }
-    for (int t = tid; t < npc * kq; t += kKldThreads) {
-      const int i = t / kq, q = t - i * kq;
-      se[i * kKldLdsStride + q] = expf(sz[i * kKldLdsStride + q] - s_m[i]);
+    {
+      const float rk = qrcp(kq);
+      for (int t = tid; t < npc * kq; t += kKldThreads) {
+        const int i = qdiv(t, kq, rk), q = t - i * kq;
+        se[i * kKldLdsStride + q] = expf(sz[i * kKldLdsStride + q] - s_m[i]);
+      }
     }
     __syncthreads();
+    if (worker) {
+      for (int q = g; q < kq; q += G) {
+        float e[4], zi[4], zj[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int task = tid + k * kKldThreads;
-      if (task < ntask) {
-        const int e = task / G, g = task - e * G;
-        const int i = e / npc, j = e - i * npc;
-        const float* ei = se + i * kKldLdsStride;
-        const float* zi = sz + i * kKldLdsStride;
-        const float* zj = sz + j * kKldLdsStride;
-        float a = acc[k];
-        // four independent chains (the LDS reads of a step do not wait for the previous fma);
-        // summed in a fixed order, so the result is deterministic
-        float a1 = 0.f, a2 = 0.f, a3 = 0.f;
-        int q = g;
-        if (i == j) {
-          for (; q + 3 * G < kq; q += 4 * G) {
-            a += ei[q];
-            a1 += ei[q + G];
-            a2 += ei[q + 2 * G];
-            a3 += ei[q + 3 * G];
-          }
-          for (; q < kq; q += G) a += ei[q];
-        } else {
-          for (; q + 3 * G < kq; q += 4 * G) {
-            a = fmaf(ei[q], zi[q] - zj[q], a);
-            a1 = fmaf(ei[q + G], zi[q + G] - zj[q + G], a1);
-            a2 = fmaf(ei[q + 2 * G], zi[q + 2 * G] - zj[q + 2 * G], a2);
-            a3 = fmaf(ei[q + 3 * G], zi[q + 3 * G] - zj[q + 3 * G], a3);
-          }
-          for (; q < kq; q += G) a = fmaf(ei[q], zi[q] - zj[q], a);
+        for (int r = 0; r < 4; ++r) {
+          e[r] = se[ri[r] + q];
+          zi[r] = sz[ri[r] + q];
+          zj[r] = sz[rj[r] + q];
         }
-        acc[k] = a + ((a1 + a2) + a3);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          ssum[r] += e[r];
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) acc[r][cc] = fmaf(e[r], zi[r] - zj[cc], acc[r][cc]);
+        }
       }
     }
     __syncthreads();
   }
   if (tid == 0) out[2 * kKldMaxPerClass] = static_cast<float>(total);
+  // the pixel groups' blocks -> LDS [block][g][16], then a fixed-order sum over g per entry
+  float* red = kld_smem;
+  if (worker) {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int task = tid + k * kKldThreads;
-    if (task < ntask) kld_smem[task] = acc[k];
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) red[(blk * G + g) * 16 + r * 4 + cc] = (bi == bj && r == cc) ? ssum[r] : acc[r][cc];
   }
   __syncthreads();
   for (int e = tid; e < E; e += kKldThreads) {
-    float v = 0.f;
-    for (int g = 0; g < G; ++g) v += kld_smem[e * G + g];
     const int i = e / npc, j = e - i * npc;
+    const int b2 = (i >> 2) * nbi + (j >> 2), sl = (i & 3) * 4 + (j & 3);
+    float v = 0.f;
+    for (int gg = 0; gg < G; ++gg) v += red[(b2 * G + gg) * 16 + sl];
     if (i == j) {
       out[i] = s_m[i];
       out[kKldMaxPerClass + i] = v;
@@ -582,34 +605,59 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_compact_kernel(
     gather_tasks(db, HW, lq, kq, s_proto, npc, slp, kKldLdsStride);
     for (int q = tid; q < kq; q += kKldThreads) pc[lq[q]] = c;
     __syncthreads();
+    const float rk = qrcp(kq);
     for (int t = tid; t < npc * kq; t += kKldThreads) {
-      const int i = t / kq, q = t - i * kq;
+      const int i = qdiv(t, kq, rk), q = t - i * kq;
       const float lp = slp[i * kKldLdsStride + q] - s_lse[i];
       slp[i * kKldLdsStride + q] = lp;
       sp[i * kKldLdsStride + q] = expf(lp);
     }
     __syncthreads();
-    // one task per (pixel, class slot), slot fastest: a pixel's row of g_cls is written by
-    // consecutive lanes
-    for (int t = tid; t < npc * kq; t += kKldThreads) {
-      const int q = t / npc, i = t - q * npc;
-      const float pi = sp[i * kKldLdsStride + q], li = slp[i * kKldLdsStride + q];
-      float gj[4] = {0.f, 0.f, 0.f, 0.f};  // four independent chains over j, summed in fixed order
+    // one task per (pixel, block of 4 class slots), pixel fastest: a wave's lanes share the slot
+    // block, so the (w_ij, KL_ij) reads are broadcasts, and a pixel's lp_j / p_j are read once
+    // for its 4 slots (the LDS reads bounded the chunk). Each slot's sum is kld_grad_kernel's
+    // sequence (four chains over j, the same expression), so compact == dense bit for bit.
+    const int nib = (npc + 3) >> 2;
+    for (int t = tid; t < nib * kq; t += kKldThreads) {
+      const int ib = qdiv(t, kq, rk), q = t - ib * kq;
+      int ii[4];
+      float pi[4], li[4], gj[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        ii[r] = min(4 * ib + r, npc - 1);  // slots past npc repeat the last one (not stored)
+        pi[r] = sp[ii[r] * kKldLdsStride + q];
+        li[r] = slp[ii[r] * kKldLdsStride + q];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) gj[r][u] = 0.f;
+      }
       int j = 0;
       for (; j + 3 < npc; j += 4) {
+        float lj[4], pj[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const float2 wk = scoef[i * npc + j + u];  // (w_ij, KL_ij); w_ii = 0
-          gj[u] = fmaf(wk.x, pi * (li - slp[(j + u) * kKldLdsStride + q] - wk.y + 1.f) - sp[(j + u) * kKldLdsStride + q],
-                       gj[u]);
+          lj[u] = slp[(j + u) * kKldLdsStride + q];
+          pj[u] = sp[(j + u) * kKldLdsStride + q];
         }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float2 wk = scoef[ii[r] * npc + j + u];  // (w_ij, KL_ij); w_ii = 0
+            gj[r][u] = fmaf(wk.x, pi[r] * (li[r] - lj[u] - wk.y + 1.f) - pj[u], gj[r][u]);
+          }
       }
       for (; j < npc; ++j) {
-        const float2 wk = scoef[i * npc + j];
-        gj[0] = fmaf(wk.x, pi * (li - slp[j * kKldLdsStride + q] - wk.y + 1.f) - sp[j * kKldLdsStride + q], gj[0]);
+        const float lj = slp[j * kKldLdsStride + q], pj = sp[j * kKldLdsStride + q];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float2 wk = scoef[ii[r] * npc + j];
+          gj[r][0] = fmaf(wk.x, pi[r] * (li[r] - lj - wk.y + 1.f) - pj, gj[r][0]);
+        }
       }
-      const float g = (gj[0] + gj[1]) + (gj[2] + gj[3]);
-      g_cls[(static_cast<size_t>(b) * HW + lq[q]) * mpc + i] = 0.5f * g;
+      float* row = g_cls + (static_cast<size_t>(b) * HW + lq[q]) * mpc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (4 * ib + r < npc) row[4 * ib + r] = 0.5f * ((gj[r][0] + gj[r][1]) + (gj[r][2] + gj[r][3]));
     }
     __syncthreads();
   }
@@ -684,7 +732,8 @@ extern "C" int protoseg_kld_forward(const float* dist, int B, int P, int HW, con
   const int S = kld_ranges(HW);
   hipLaunchKernelGGL(kld_lists_kernel, dim3(K + 1), dim3(64), 0, s, proto_class, P, K, w.off, w.idx, w.slot);
   if (int st = check_launch("kld_lists_kernel")) return st;
-  const size_t lds = static_cast<size_t>(2) * max_per_class * kKldLdsStride * sizeof(float);
+  const size_t lds = std::max(static_cast<size_t>(2) * max_per_class * kKldLdsStride * sizeof(float),
+                              static_cast<size_t>(kKldThreads) * 16 * sizeof(float));
   const int st = by_label(label_dtype, [&](auto tl) {
     using TL = std::remove_pointer_t<decltype(tl)>;
     if (int e = ensure_lds<kld_partial_kernel<TL>, kKldMaxDynLds>()) return e;

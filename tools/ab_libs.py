@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--fmap", type=int, default=65)
     ap.add_argument("--reps", type=int, default=40)
-    ap.add_argument("--call", default="bwd_full", choices=["bwd_full", "bwd_full_xsig", "fwd", "fwd_xsig", "push", "mask", "kld", "kldb"])
+    ap.add_argument("--call", default="bwd_full", choices=["bwd_full", "bwd_full_xsig", "fwd", "fwd_xsig", "push", "mask", "kld", "kldb", "kldc"])
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     B, C, h, w, P, K = args.batch, 64, args.fmap, args.fmap, args.protos, 19
@@ -65,7 +65,7 @@ def main():
         st = libs["main"].protoseg_patch_class_mask(P_(lab), _lib.U8, n_img, 1024, 2048, ph, pw, None, 0, P_(mask), s)
         assert st == 0
 
-    if args.call in ("kld", "kldb"):  # KLD forward (kldb: + backward) on the layer's distances (bench.py setup_kld: 8x8 label blocks)
+    if args.call in ("kld", "kldb", "kldc"):  # KLD forward (kldb: + backward, kldc: + compact backward) on the layer's distances (bench.py setup_kld: 8x8 label blocks)
         blocks = torch.randint(0, K + 1, (B, (h + 7) // 8, (w + 7) // 8), generator=gen)
         tgt = blocks.repeat_interleave(8, 1).repeat_interleave(8, 2)[:, :h, :w].reshape(B, -1).contiguous().to(dev)
         pcls = torch.clamp(torch.arange(P) // (P // K), max=K - 1).to(torch.int32).to(dev)
@@ -75,6 +75,9 @@ def main():
         kloss = torch.empty((), device=dev)
         kg = torch.full((), 0.25, device=dev)
         gdist = torch.empty_like(dist)
+        gcls = torch.empty(B * h * w, mpc, device=dev)
+        pixc = torch.empty(B * h * w, device=dev, dtype=torch.int32)
+        pslot = torch.empty(P, device=dev, dtype=torch.int32)
         st = libs["main"].protoseg_l2_fwd(P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 0,
                                           _lib.PRECISIONS["bf16x3"], P_(dist), None, P_(logits), s)
         assert st == 0
@@ -82,12 +85,15 @@ def main():
     def call(lib):
         if args.call == "mask":
             st = lib.protoseg_patch_class_mask(P_(lab), _lib.U8, n_img, 1024, 2048, ph, pw, None, 0, P_(mask), s)
-        elif args.call in ("kld", "kldb"):
+        elif args.call in ("kld", "kldb", "kldc"):
             st = lib.protoseg_kld_forward(P_(dist), B, P, h * w, P_(tgt), _lib.I64, P_(pcls), K, mpc, P_(kloss), None,
                                           P_(kws), kws_b, s)
             if args.call == "kldb" and st == 0:
                 st = lib.protoseg_kld_backward(P_(dist), B, P, h * w, P_(tgt), _lib.I64, P_(pcls), K, mpc, P_(kg),
                                                P_(kws), kws_b, P_(gdist), s)
+            if args.call == "kldc" and st == 0:
+                st = lib.protoseg_kld_backward_compact(P_(dist), B, P, h * w, P_(tgt), _lib.I64, P_(pcls), K, mpc,
+                                                       P_(kg), P_(kws), kws_b, P_(gcls), P_(pixc), P_(pslot), s)
         elif args.call == "push":
             st = lib.protoseg_push_argmin(P_(xp), n_img, C, ph, pw, P_(protos), P, P_(pcls), P_(mask), P_(keys),
                                           P_(second), s)
@@ -103,7 +109,7 @@ def main():
     for name, lib in libs.items():  # warm-up + the variants agree with main
         call(lib)
         torch.cuda.synchronize()
-        out = (gdist if args.call == "kldb" else mask.float() if args.call == "mask" else
+        out = (gdist if args.call == "kldb" else gcls if args.call == "kldc" else mask.float() if args.call == "mask" else
                kloss.reshape(1) if args.call == "kld" else keys.float() if args.call == "push" else
                gx if args.call.startswith("bwd") else logits).clone()
         if ref is None:
