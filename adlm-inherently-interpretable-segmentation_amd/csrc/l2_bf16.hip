@@ -247,6 +247,9 @@ struct TileSchedule {
   }
 };
 
+#ifndef FWD_DIST_CPOL
+#define FWD_DIST_CPOL 0  // cache policy of the distance stores (measured variants: tools/gpu_r3aa.sh)
+#endif
 // Forward, one pixel tile per wave per round: distances (NCHW stores), activation in registers,
 // logits = W . act with the accumulator as B operand. Remainder tiles: see TileSchedule; the
 // per-wave logits partials are summed in LDS in a fixed order (deterministic).
@@ -352,7 +355,8 @@ __global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
       for (int r = 0; r < 16; ++r) {
         const float d = relu_f(acc[r]);  // F.relu (model.py:219)
         const unsigned row_ok = (kFull || row_of(r) < prem) ? 0u : kOOB;
-        BufIO<float>::store(rd, d, dbase | row_ok, static_cast<unsigned>((pt * 32 + row_of(r)) * HW * 4));
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(d), rd, dbase | row_ok,
+                                              static_cast<unsigned>((pt * 32 + row_of(r)) * HW * 4), FWD_DIST_CPOL);
         const float a = act_base<ACT>(d, eps);  // act_unit lives in the W image
         if constexpr (ACTS)
           BufIO<float>::store(ra, a * act_unit(ACT), abase | row_ok, static_cast<unsigned>((pt * 32 + row_of(r)) * 4));
