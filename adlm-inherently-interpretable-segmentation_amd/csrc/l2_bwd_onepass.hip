@@ -153,6 +153,12 @@ __device__ __forceinline__ void store_half4(bf16* dst, const bf16x8& f, int half
 }
 
 #define OSCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#ifndef ONEPASS_PB_FREE
+#define ONEPASS_PB_FREE 0  // 1: no scheduling fence per phase-B k-step (measured variant)
+#endif
+#ifndef ONEPASS_PRIO
+#define ONEPASS_PRIO 0  // 1: s_setprio 1 for waves 4..7 (measured variant)
+#endif
 #ifndef ONEPASS_PIPE
 #define ONEPASS_PIPE 1  // owned tile jt + 1's products issued before tile jt's epilogue
 #endif
@@ -501,7 +507,9 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
     for (int ks = 0; ks < KS; ++ks) {
       if (ks + D < KS) ldk(ks + D, fa[(ks + D) % (D + 1)], fb[(ks + D) % (D + 1)]);
       gx = mma16_split(fa[ks % (D + 1)], fb[ks % (D + 1)], gx);
+#if !ONEPASS_PB_FREE
       OSCHED_FENCE();
+#endif
     }
     // sum_p g_s over this wave's quarter of the prototypes (k-steps ct KSQ ..): the g_s
     // fragments again, times a ones A operand
@@ -541,6 +549,9 @@ __global__ __launch_bounds__(kOThreads, 1) void l2_bwd_onepass_bf16_kernel(
   // ---- main loop. Per tile: phase A(i) | barrier | raw loads of tile i+1, phase B(i), the
   // sum_p g_s partial, staging of tile i+1 | barrier | g_x epilogue(i). The raw loads and the
   // epilogue's x live only across phase B, where phase A's working registers are dead.
+#if ONEPASS_PRIO
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the second-dispatched half
+#endif
   OSTAMP(0);
   load_raw(tile_of(0));
   convert(tile_of(0));

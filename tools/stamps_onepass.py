@@ -72,6 +72,16 @@ def main():
     seg(7, 8, "staging")
     seg(8, 9, "barrier 2 wait")
     seg(9, 10, "g_x epilogue")
+    # by wave index in the workgroup (waves w and w + 4 share a SIMD): p50 cycles
+    widx = np.nonzero(live)[0] % 8
+    print("  wave  owner A  barrier1  phase B  staging  barrier2")
+    for wv in range(8):
+        r = s[widx == wv]
+        ok = (r[:, 2] != 0) & (r[:, 10] != 0)
+        r = r[ok]
+        if len(r):
+            p50 = lambda a, b: np.percentile(r[:, b] - r[:, a], 50)
+            print(f"  {wv:4d} {p50(2, 5):8.0f} {p50(5, 6):9.0f} {p50(6, 7):8.0f} {p50(7, 8):8.0f} {p50(8, 9):9.0f}")
 
 
 if __name__ == "__main__":
