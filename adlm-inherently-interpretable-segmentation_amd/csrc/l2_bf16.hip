@@ -247,6 +247,9 @@ struct TileSchedule {
   }
 };
 
+#ifndef FWD_REM_ROUNDS
+#define FWD_REM_ROUNDS 3  // small-batch forward: remainder rounds preferred over one full round
+#endif
 #ifndef FWD_DIST_CPOL
 #define FWD_DIST_CPOL 0  // cache policy of the distance stores (measured variants: tools/gpu_r3aa.sh)
 #endif
@@ -984,8 +987,19 @@ int fwd_t(const Geometry& g, const Bytes& nb, const void* x, const unsigned char
   // prefetch their next tile.
   const int cap = resident_blocks<l2_fwd_bf16_kernel<TX, T, ACT, ACTS, LOGITS>>(kWavesF * 64, lds);
   const int want = static_cast<int>(ceil_div(g.ntiles, kWavesF));
+  // Fewer tiles than one full round over the resident grid (batches below ≈ 16 images; the
+  // drop-in runs 2-4 per GPU): ceil(ntiles / 8) workgroups would leave the schedule with no full
+  // round and every tile in the remainder path, 8 rounds deep. A full-round tile costs one wave
+  // ≈ 2.6x a remainder tile (one workgroup, the prototype tiles split over its waves; stamps in
+  // DESIGN.md §5.3), so: up to FWD_REM_ROUNDS remainder rounds over the resident grid, else
+  // floor(ntiles / 8) workgroups for one full round and fewer than 8 remainder tiles.
+  int grid = want < cap ? want : cap;
+  if (g.ntiles <= FWD_REM_ROUNDS * cap)
+    grid = g.ntiles < cap ? g.ntiles : cap;
+  else if (g.ntiles < kWavesF * cap)
+    grid = g.ntiles / kWavesF;
   KernelTimer timer("l2_fwd_bf16_kernel", stream);
-  hipLaunchKernelGGL((l2_fwd_bf16_kernel<TX, T, ACT, ACTS, LOGITS>), dim3(want < cap ? want : cap), dim3(kWavesF * 64), lds,
+  hipLaunchKernelGGL((l2_fwd_bf16_kernel<TX, T, ACT, ACTS, LOGITS>), dim3(grid), dim3(kWavesF * 64), lds,
                      stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, img, g.P, g.Pp, g.K, eps, dist, nb.d, act,
                      nb.a, logits, nb.l, g.ldd, g.p0, accumulate, g.xsig);
   return check_launch("l2_fwd_bf16_kernel");

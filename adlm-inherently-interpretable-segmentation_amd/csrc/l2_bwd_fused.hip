@@ -631,7 +631,11 @@ bool bf16_bwd_fused_fits(const Geometry& g, int terms) {
          bf16_sizes_ok(g);
 }
 
-int bf16_bwd_fused_grid(const Geometry& g) { return g.ntiles < 256 ? g.ntiles : 256; }
+// as many workgroups as the rounds of 256 need (fewer slabs for the reduce at small batches)
+int bf16_bwd_fused_grid(const Geometry& g) {
+  const int rounds = static_cast<int>(ceil_div(g.ntiles, 256));
+  return static_cast<int>(ceil_div(g.ntiles, rounds > 0 ? rounds : 1));
+}
 
 int launch_bwd_fused_bf16(const Geometry& g, bool x_bf16, const void* x, const float* protos, const void* img,
                           float eps, int act_kind, const float* g_logits, const float* g_dist, void* g_x,

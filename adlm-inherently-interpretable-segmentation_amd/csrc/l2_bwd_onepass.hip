@@ -708,7 +708,10 @@ bool bf16_bwd_onepass_fits(const Geometry& g, int terms) {
 int bf16_bwd_onepass_grid(const Geometry& g) {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  return g.ntiles < cus ? g.ntiles : cus;
+  // as many workgroups as the rounds need, no more: at small batches every slab the reduce reads
+  // belongs to a workgroup that did work (e.g. 265 tiles: 133 workgroups x 2, not 256 + 9)
+  const int rounds = static_cast<int>(ceil_div(g.ntiles, cus));
+  return static_cast<int>(ceil_div(g.ntiles, rounds > 0 ? rounds : 1));
 }
 
 size_t bf16_onepass_image_bytes(const Geometry& g) {
