@@ -978,6 +978,17 @@ struct Bytes {
   unsigned x, d, a, l, gl, gd;
 };
 
+// Grid of the layout-A kernels (TileSchedule): ceil(ntiles / waves) workgroups up to the resident
+// cap, except below one full round over the cap, where that grid leaves no full round and every
+// tile in the remainder path, rounds deep: then up to FWD_REM_ROUNDS remainder rounds over the
+// whole cap, else floor(ntiles / waves) workgroups (one full round, < waves remainder tiles).
+static int layout_a_grid(int ntiles, int waves, int cap) {
+  if (ntiles <= FWD_REM_ROUNDS * cap) return ntiles < cap ? ntiles : cap;
+  if (ntiles < waves * cap) return ntiles / waves;
+  const int want = static_cast<int>(ceil_div(ntiles, waves));
+  return want < cap ? want : cap;
+}
+
 template <typename TX, int T, int ACT, bool ACTS, bool LOGITS>
 int fwd_t(const Geometry& g, const Bytes& nb, const void* x, const unsigned char* img, float eps, float* dist,
           float* act, float* logits, int accumulate, hipStream_t stream) {
@@ -986,18 +997,10 @@ int fwd_t(const Geometry& g, const Bytes& nb, const void* x, const unsigned char
   // Persistent: one generation of resident workgroups; waves stride over the tiles and
   // prefetch their next tile.
   const int cap = resident_blocks<l2_fwd_bf16_kernel<TX, T, ACT, ACTS, LOGITS>>(kWavesF * 64, lds);
-  const int want = static_cast<int>(ceil_div(g.ntiles, kWavesF));
-  // Fewer tiles than one full round over the resident grid (batches below ≈ 16 images; the
-  // drop-in runs 2-4 per GPU): ceil(ntiles / 8) workgroups would leave the schedule with no full
-  // round and every tile in the remainder path, 8 rounds deep. A full-round tile costs one wave
+  // Small batches (the drop-in runs 2-4 images per GPU): a full-round tile costs one wave
   // ≈ 2.6x a remainder tile (one workgroup, the prototype tiles split over its waves; stamps in
-  // DESIGN.md §5.3), so: up to FWD_REM_ROUNDS remainder rounds over the resident grid, else
-  // floor(ntiles / 8) workgroups for one full round and fewer than 8 remainder tiles.
-  int grid = want < cap ? want : cap;
-  if (g.ntiles <= FWD_REM_ROUNDS * cap)
-    grid = g.ntiles < cap ? g.ntiles : cap;
-  else if (g.ntiles < kWavesF * cap)
-    grid = g.ntiles / kWavesF;
+  // DESIGN.md §5.3), hence layout_a_grid's small-batch rule.
+  const int grid = layout_a_grid(g.ntiles, kWavesF, cap);
   KernelTimer timer("l2_fwd_bf16_kernel", stream);
   hipLaunchKernelGGL((l2_fwd_bf16_kernel<TX, T, ACT, ACTS, LOGITS>), dim3(grid), dim3(kWavesF * 64), lds,
                      stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, img, g.P, g.Pp, g.K, eps, dist, nb.d, act,
@@ -1011,9 +1014,9 @@ int bwd_x_t(const Geometry& g, const Bytes& nb, const void* x, const unsigned ch
   if (int st = ensure_lds<l2_bwd_x_bf16_kernel<TX, T, ACT, GD>>()) return st;
   const size_t lds = bwd_x_lds(g, T);
   const int cap = resident_blocks<l2_bwd_x_bf16_kernel<TX, T, ACT, GD>>(kWavesA * 64, lds);
-  const int want = static_cast<int>(ceil_div(g.ntiles, kWavesA));
   KernelTimer timer("l2_bwd_x_bf16_kernel", stream);
-  hipLaunchKernelGGL((l2_bwd_x_bf16_kernel<TX, T, ACT, GD>), dim3(want < cap ? want : cap), dim3(kWavesA * 64), lds,
+  hipLaunchKernelGGL((l2_bwd_x_bf16_kernel<TX, T, ACT, GD>), dim3(layout_a_grid(g.ntiles, kWavesA, cap)),
+                     dim3(kWavesA * 64), lds,
                      stream, static_cast<const TX*>(x), nb.x, g.HW, g.npix, img, g.P, g.Pp, g.K, eps, g_logits, nb.gl,
                      g_dist, nb.gd, g.ldd, g.p0, static_cast<TX*>(g_x), accumulate);
   return check_launch("l2_bwd_x_bf16_kernel");
