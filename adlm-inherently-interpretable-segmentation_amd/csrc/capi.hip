@@ -2,7 +2,9 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <tuple>
 #include <string>
 #include <vector>
 
@@ -25,6 +27,36 @@ int fail(int code, const char* fmt, ...) {
 int check_launch(const char* what) {
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(PROTOSEG_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+  return PROTOSEG_OK;
+}
+
+int stream_scratch(ScratchKind kind, size_t need, size_t min_bytes, hipStream_t s, void** out) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, hipStream_t, int>, std::pair<void*, size_t>> blocks;
+  static std::vector<void*> retired;  // kept until the process exits (captured graphs may point there)
+  int dev = 0;
+  *out = nullptr;
+  if (hipGetDevice(&dev) != hipSuccess) return check_launch("hipGetDevice");
+  std::lock_guard<std::mutex> lock(mu);
+  auto& b = blocks[{dev, s, static_cast<int>(kind)}];
+  if (b.second < need) {
+    // 1.5x geometric growth: a sequence of ever larger calls retires O(log) blocks whose total
+    // stays within ~3x the largest, not the sum of every size seen
+    size_t bytes = b.second + b.second / 2;
+    if (bytes < need) bytes = need;
+    if (bytes < min_bytes) bytes = min_bytes;
+    bytes = (bytes + 4095) & ~static_cast<size_t>(4095);
+    void* p = nullptr;
+    const hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(PROTOSEG_ERR_HIP, "hipMalloc (scratch kind %d, %zu B): %s", static_cast<int>(kind), bytes,
+                  hipGetErrorString(e));
+    }
+    if (b.first) retired.push_back(b.first);
+    b = {p, bytes};
+  }
+  *out = b.first;
   return PROTOSEG_OK;
 }
 

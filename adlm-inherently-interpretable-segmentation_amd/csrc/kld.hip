@@ -139,7 +139,10 @@ __global__ __launch_bounds__(64) void kld_lists_kernel(const int32_t* __restrict
       const int r = pos + __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
                                                     __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0));
       idx[r] = p;
-      slot[p] = c * 256 + (r - start);  // the prototype's column of the compact gradient
+      // the prototype's column of the compact gradient: class * 256 + rank. A rank past 255 would
+      // wrap into the next class's code; such a class holds more prototypes than any max_per_class
+      // (its groups add no pairs), so its prototypes get class -2, which no pixel carries.
+      slot[p] = r - start < 256 ? c * 256 + (r - start) : -2 * 256;
     }
     pos += __popcll(m);
   }

@@ -627,31 +627,8 @@ bool use_onepass(int P) {
   return P > 192;
 }
 
-// One grow-only block per (device, stream, kind). A call that needs more takes a NEW block and
-// retires the old one without freeing it: a HIP graph that captured an earlier call still
-// points there, and a replay must not read freed memory.
 int stream_block(size_t need, hipStream_t s, int kind, void** out) {
-  static std::mutex mu;
-  static std::map<std::tuple<int, hipStream_t, int>, std::pair<void*, size_t>> blocks;
-  static std::vector<void*> retired;  // kept until the process exits
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return check_launch("hipGetDevice");
-  std::lock_guard<std::mutex> lock(mu);
-  auto& b = blocks[{dev, s, kind}];
-  if (b.second < need) {
-    if (b.first) retired.push_back(b.first);
-    b = {nullptr, 0};
-    const size_t bytes = need > kImageBlockMin ? need : kImageBlockMin;
-    const hipError_t e = hipMalloc(&b.first, bytes);
-    if (e != hipSuccess) {
-      (void)hipGetLastError();
-      b = {nullptr, 0};
-      return fail(PROTOSEG_ERR_HIP, "hipMalloc (operand images, %zu B): %s", bytes, hipGetErrorString(e));
-    }
-    b.second = bytes;
-  }
-  *out = b.first;
-  return PROTOSEG_OK;
+  return stream_scratch(static_cast<ScratchKind>(kind), need, kImageBlockMin, s, out);
 }
 
 struct ImageBlock {
@@ -849,8 +826,10 @@ extern "C" size_t protoseg_l2_bwd_workspace_size(int B, int C, int H, int W, int
 namespace {
 // The compact KLD gradient (protoseg_l2_bwd_kld) is expanded in the owners of the bf16x3 training
 // backward (one-pass and fused kernels), f32 x.
+// Not on the wide family (K > 32 or P > 4096 run there): its GEMM chain reads a dense g_dist only.
 bool kld_compact_path(const Geometry& geo, int x_dtype, int precision, int mpc) {
-  return terms_of(precision) == 2 && geo.C == 64 && x_dtype == PROTOSEG_F32 && bf16_sizes_ok(geo) && mpc >= 1 &&
+  return terms_of(precision) == 2 && geo.C == 64 && !use_wide(geo.C, geo.K, geo.P) && x_dtype == PROTOSEG_F32 &&
+         bf16_sizes_ok(geo) && mpc >= 1 &&
          mpc <= 32 && static_cast<long long>(geo.npix) * mpc * 4 < (1LL << 31);
 }
 
@@ -889,6 +868,7 @@ int l2_bwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const fl
   float* ws = static_cast<float*>(workspace);
   if (use_wide(C, K, P)) {  // any C / K (l2_wide.hip)
     if (xsig) return fail(PROTOSEG_ERR_UNSUPPORTED, "PROTOSEG_X_SIGMOID: C = 64, K <= 32 only");
+    if (cgd.val) return fail(PROTOSEG_ERR_UNSUPPORTED, "compact KLD gradient on the wide family (K > 32 or P > 4096)");
     if (!wide_family_fits(geo)) return fail(PROTOSEG_ERR_UNSUPPORTED, "B*H*W*max(P, C) >= 2^31 elements");
     return launch_bwd_wide(geo, xb, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_x, g_protos,
                            g_logits ? g_w : nullptr, workspace, s);

@@ -408,32 +408,11 @@ int launch_bwd_wide(const Geometry& g, bool x_bf16, const void* x, const float* 
 
 namespace {
 
-// Grow-only scratch per (device, stream) for the wide push path; retired blocks are kept (a HIP
-// graph that captured an earlier call may still point at them).
+// Grow-only scratch per (device, stream) for the wide push path (stream_scratch).
 void* wide_scratch(size_t need, hipStream_t s, int* st) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> blocks;
-  static std::vector<void*> retired;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) {
-    *st = check_launch("hipGetDevice");
-    return nullptr;
-  }
-  std::lock_guard<std::mutex> lock(mu);
-  auto& b = blocks[{dev, s}];
-  if (b.second < need) {
-    if (b.first) retired.push_back(b.first);
-    b = {nullptr, 0};
-    if (hipMalloc(&b.first, need) != hipSuccess) {
-      (void)hipGetLastError();
-      b = {nullptr, 0};
-      *st = fail(PROTOSEG_ERR_HIP, "hipMalloc (wide push scratch, %zu B)", need);
-      return nullptr;
-    }
-    b.second = need;
-  }
-  *st = PROTOSEG_OK;
-  return b.first;
+  void* p = nullptr;
+  *st = stream_scratch(ScratchKind::kWidePush, need, 0, s, &p);
+  return p;
 }
 
 // One wave per (prototype, image): the masked minimum over the class patches as a key

@@ -475,31 +475,9 @@ namespace {
 // more takes a NEW block and retires the old one without freeing it: a graph that captured an
 // earlier call still points there, and replaying it must not write into freed memory.
 void* push_scratch(size_t need, hipStream_t s, int* status) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> blocks;
-  static std::vector<void*> retired;  // kept until the process exits
-  int dev = 0;
-  *status = PROTOSEG_OK;
-  if (hipGetDevice(&dev) != hipSuccess) {
-    *status = check_launch("hipGetDevice");
-    return nullptr;
-  }
-  std::lock_guard<std::mutex> lock(mu);
-  auto& b = blocks[{dev, s}];
-  if (b.second < need) {
-    if (b.first) retired.push_back(b.first);
-    b = {nullptr, 0};
-    const size_t bytes = need < (1u << 20) ? (1u << 20) : need;
-    const hipError_t e = hipMalloc(&b.first, bytes);
-    if (e != hipSuccess) {
-      (void)hipGetLastError();
-      b = {nullptr, 0};
-      *status = fail(PROTOSEG_ERR_HIP, "hipMalloc (push scratch, %zu B): %s", bytes, hipGetErrorString(e));
-      return nullptr;
-    }
-    b.second = bytes;
-  }
-  return b.first;
+  void* p = nullptr;
+  *status = stream_scratch(ScratchKind::kPush, need, 1u << 20, s, &p);
+  return p;
 }
 }  // namespace
 

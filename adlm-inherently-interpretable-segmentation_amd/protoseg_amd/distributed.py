@@ -107,16 +107,25 @@ class GradientBuckets:
     and bench.py's multi-GPU step).
 
     Buckets are filled in reverse registration order (the order backward produces grads), each
-    up to ``bucket_mb`` MiB; xGMI rings are per-link bound, so few large collectives beat many
-    small ones. ``arm()`` before the backward of the step that ends a gradient accumulation
-    (module.py:235-243: the optimizer steps every iter_size micro-steps) makes each bucket's
-    all-reduce start from the gradient hook of its last parameter, so the exchange overlaps the
-    rest of the backward; buckets are always launched in index order, so every rank issues the
-    same collective sequence. ``wait()`` launches whatever has not started, waits, and writes
-    the reduced gradients back: a parameter that got no gradient on a rank contributes zeros
-    there, and it gets the reduced gradient on every rank when any rank had one (a had-gradient
-    flag per parameter is summed with the bucket), so no replica skips an update the others
-    make. Without ``arm()``, ``allreduce()`` + ``wait()`` do the same after backward.
+    up to ``bucket_mb`` MiB of one dtype; xGMI rings are per-link bound, so few large collectives
+    beat many small ones. ``arm()`` before the backward of the step that ends a gradient
+    accumulation (module.py:235-243: the optimizer steps every iter_size micro-steps) makes each
+    bucket's all-reduce start from the gradient hook of its last parameter, so the exchange
+    overlaps the rest of the backward; buckets are always launched in index order, so every rank
+    issues the same collective sequence. Without ``arm()``, ``allreduce()`` + ``wait()`` do the
+    same after backward.
+
+    Each bucket owns one persistent flat buffer, and after its first exchange every gradient of
+    the bucket IS a view into it (DDP's gradient-as-bucket-view): backward accumulates straight
+    into the buffer, the all-reduce runs on it in place and the reduced values are already where
+    ``p.grad`` points, so an exchange is one collective (+ the averaging scale) per bucket, with
+    no concatenation copy and no device -> host read. Zeroing the gradients in place
+    (``zero_grad(set_to_none=False)``, the reference's torch-1.10 default) keeps the views.
+
+    A parameter that got no gradient on a rank contributes zeros there, and it gets the reduced
+    gradient on every rank when any rank had one (a had-gradient flag per parameter is summed
+    with the bucket), so no replica skips an update the others make. Only then is a flag read
+    on the host: for parameters whose local gradient is None.
     """
 
     def __init__(self, params: Iterable[torch.nn.Parameter], bucket_mb: float = 64.0, group=None,
@@ -129,7 +138,7 @@ class GradientBuckets:
         cur, size = [], 0
         for p in reversed(self.params):
             nbytes = p.numel() * p.element_size()
-            if cur and size + nbytes > limit:
+            if cur and (size + nbytes > limit or p.dtype != cur[0].dtype or p.device != cur[0].device):
                 self.buckets.append(cur)
                 cur, size = [], 0
             cur.append(p)
@@ -137,6 +146,8 @@ class GradientBuckets:
         if cur:
             self.buckets.append(cur)
         self._bucket_of = {id(p): b for b, bucket in enumerate(self.buckets) for p in bucket}
+        self._numel = [sum(p.numel() for p in bucket) for bucket in self.buckets]
+        self._flat: List[Optional[torch.Tensor]] = [None] * len(self.buckets)
         self._hooks = []
         self._armed = False
         self._ready = [0] * len(self.buckets)
@@ -164,17 +175,51 @@ class GradientBuckets:
         while self._next < len(self.buckets) and self._ready[self._next] == len(self.buckets[self._next]):
             self._launch(self._next)
 
+    def flat(self, b: int) -> torch.Tensor:
+        """Bucket b's persistent buffer: the parameters' gradients in bucket order, then one
+        had-gradient flag per parameter."""
+        if self._flat[b] is None:
+            ref = self.buckets[b][0]
+            self._flat[b] = torch.zeros(self._numel[b] + len(self.buckets[b]), dtype=ref.dtype, device=ref.device)
+        return self._flat[b]
+
+    def bind_grads(self) -> None:
+        """Make every parameter's .grad a view into its bucket's buffer now (existing values
+        copied; None becomes zeros): a caller whose kernels write gradients into fixed buffers
+        (bench.py's captured step) then writes them straight into the exchange buffers."""
+        for b, bucket in enumerate(self.buckets):
+            flat, off = self.flat(b), 0
+            for p in bucket:
+                n = p.numel()
+                seg = flat[off:off + n]
+                if p.grad is None:
+                    seg.zero_()
+                elif p.grad.data_ptr() != seg.data_ptr():
+                    seg.copy_(p.grad.reshape(-1))
+                p.grad = seg.view_as(p)
+                off += n
+
     def _launch(self, b: int) -> None:
-        bucket = self.buckets[b]
-        # one had-gradient flag per parameter travels at the end of the bucket: after the SUM a
-        # parameter gets the reduced gradient on EVERY rank as soon as any rank had one, so the
-        # replicas' optimizers skip (or update) the same parameters
-        flags = [1.0 if p.grad is not None else 0.0 for p in bucket]
-        ref = bucket[0]
-        flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in bucket]
-                         + [torch.tensor(flags, dtype=ref.dtype, device=ref.device)])
+        bucket, flat = self.buckets[b], self.flat(b)
+        n_total = self._numel[b]
+        missing, off = [], 0
+        for i, p in enumerate(bucket):
+            n = p.numel()
+            seg = flat[off:off + n]
+            g = p.grad
+            if g is None:
+                seg.zero_()
+                missing.append(i)
+            elif g.data_ptr() != seg.data_ptr() or g.shape != p.shape:
+                seg.copy_(g.reshape(-1))   # first exchange (or a replaced .grad): alias it from now on
+                p.grad = seg.view_as(p)
+            off += n
+        flags = flat[n_total:]
+        flags.fill_(1.0)
+        for i in missing:
+            flags[i:i + 1].zero_()
         work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-        self._pending[b] = (flat, work)
+        self._pending[b] = (work, missing)
         self._next = b + 1
 
     def allreduce(self) -> None:
@@ -185,26 +230,26 @@ class GradientBuckets:
             self._launch(self._next)
 
     def wait(self) -> None:
+        """Completes the exchange on the current stream (no host synchronisation unless a
+        parameter's local gradient is None)."""
         world = self._world()
         if world == 1:
             return
         self.allreduce()
         for b, bucket in enumerate(self.buckets):
-            flat, work = self._pending[b]
+            work, missing = self._pending[b]
             work.wait()
-            had = flat[-len(bucket):].tolist()
+            flat = self._flat[b]
             if self.average:
                 flat.div_(world)
-            off = 0
-            for p, h in zip(bucket, had):
-                n = p.numel()
-                if h > 0:  # some rank had a gradient: every rank takes the reduced one
-                    red = flat[off:off + n].view_as(p)
-                    if p.grad is None:
-                        p.grad = red.clone()
-                    else:
-                        p.grad.copy_(red)
-                off += n  # no rank had one: left without a gradient everywhere
+            if missing:  # some rank may have had a gradient for a parameter this rank lacks
+                had = flat[self._numel[b]:][missing].tolist()
+                offs = [0]
+                for p in bucket:
+                    offs.append(offs[-1] + p.numel())
+                for i, h in zip(missing, had):
+                    if h > 0:  # every rank takes the reduced gradient; otherwise none has one
+                        bucket[i].grad = flat[offs[i]:offs[i + 1]].view_as(bucket[i])
         self._pending = [None] * len(self.buckets)
         self._next = 0
         self._armed = False

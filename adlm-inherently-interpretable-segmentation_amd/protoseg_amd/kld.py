@@ -127,28 +127,55 @@ def kld_backward_compact(distances: Tensor, target_img: Tensor, proto_class: Ten
     return g_cls, pix_cls, proto_slot
 
 
+def _layer_backward_runs(layer_node) -> bool:
+    """Whether the current backward pass will run the prototype layer's backward past its own
+    node, i.e. consume a deposit: some node behind it (x's producer, the prototypes' or the last
+    layer's AccumulateGrad) executes. ``autograd.grad(loss, distances)`` and
+    ``backward(inputs=[distances])`` stop at the distances: the layer never runs."""
+    if layer_node is None:
+        return False
+    try:
+        return any(torch._C._will_engine_execute_node(n) for n, _ in layer_node.next_functions if n is not None)
+    except (AttributeError, RuntimeError):  # no engine introspection: always the dense gradient
+        return False
+
+
 class _KldToLayer(torch.autograd.Function):
     """kld_forward whose backward hands the compact gradient to the prototype layer that produced
-    ``distances`` (ops.DistGradSink) instead of returning a dense [B, P, H, W] tensor."""
+    ``distances`` (ops.DistGradSink) instead of returning a dense [B, P, H, W] tensor.
+
+    The hand-off is taken only when the layer's backward consumes it in the same backward pass
+    and nothing observes the gradient at ``distances`` itself (``retain_grad`` or a tensor hook):
+    otherwise this returns the dense gradient, so ``autograd.grad(kld, distances)``, hooks and
+    ``backward(inputs=[distances])`` see the real values. Deposits carry the backward pass's
+    graph-task id and the layer takes only its own pass's, so a ``retain_graph`` replay never
+    sums a stale deposit."""
 
     @staticmethod
-    def forward(ctx, distances, target_img, proto_class, num_classes, max_per_class, sink):
+    def forward(ctx, distances, target_img, proto_class, num_classes, max_per_class, sink, layer_node):
         loss, npairs, ws = torch.ops.protoseg.kld_forward(distances, target_img, proto_class, num_classes,
                                                           max_per_class)
         ctx.save_for_backward(distances, target_img, proto_class, ws)
         ctx.num_classes, ctx.max_per_class, ctx.sink = num_classes, max_per_class, sink
+        ctx.layer_node = layer_node
+        ctx.dist_ref = sink.dist_ref
         ctx.mark_non_differentiable(npairs)
         return loss, npairs
 
     @staticmethod
     def backward(ctx, g_loss, g_npairs):
         distances, target_img, proto_class, ws = ctx.saved_tensors
+        none = (None,) * 6
         if g_loss is None or not ctx.needs_input_grad[0]:
-            return None, None, None, None, None, None
+            return (None,) + none
+        d = ctx.dist_ref() if ctx.dist_ref is not None else None
+        observed = d is not None and (d.retains_grad or bool(getattr(d, "_backward_hooks", None)))
+        if observed or not _layer_backward_runs(ctx.layer_node):
+            g = kld_backward(distances, target_img, proto_class, ctx.num_classes, ctx.max_per_class, ws, g_loss)
+            return (g.to(distances.dtype),) + none
         g_cls, pix_cls, proto_slot = kld_backward_compact(distances, target_img, proto_class, ctx.num_classes,
                                                           ctx.max_per_class, ws, g_loss)
-        return (ctx.sink.deposit(g_cls, pix_cls, proto_slot, ctx.max_per_class, distances),
-                None, None, None, None, None)
+        return (ctx.sink.deposit(g_cls, pix_cls, proto_slot, ctx.max_per_class, distances),) + none
 
 
 def kld_with_pairs(distances: Tensor, target_img: Tensor, proto_class: Tensor, num_classes: int,
@@ -158,7 +185,8 @@ def kld_with_pairs(distances: Tensor, target_img: Tensor, proto_class: Tensor, n
     layer in that form (no [B, P, H, W] tensor); otherwise autograd gets the dense one."""
     sink = getattr(distances, "_protoseg_sink", None)
     if sink is not None and distances.requires_grad and torch.is_grad_enabled() and sink.accepts(max_per_class):
-        return _KldToLayer.apply(distances, target_img, proto_class, int(num_classes), int(max_per_class), sink)
+        return _KldToLayer.apply(distances, target_img, proto_class, int(num_classes), int(max_per_class), sink,
+                                 distances.grad_fn)
     loss, npairs, _ = torch.ops.protoseg.kld_forward(distances, target_img, proto_class, int(num_classes),
                                                      int(max_per_class))
     return loss, npairs

@@ -11,6 +11,7 @@ autograd graph of those ops (the reference has no custom backward).
 from __future__ import annotations
 
 import os
+import weakref
 from typing import Optional, Tuple
 
 import torch
@@ -142,13 +143,14 @@ class DistGradSink:
     (a shape / precision the kernels do not serve, a gradient through the activations), the
     deposits are expanded with ``protoseg_kld_expand`` first: same values either way."""
 
-    __slots__ = ("shape", "compact_ok", "deposits", "zero")
+    __slots__ = ("shape", "compact_ok", "deposits", "zero", "dist_ref")
 
     def __init__(self, shape, compact_ok: bool):
         self.shape = shape          # (B, C, H, W, P, K, x_dtype, precision)
         self.compact_ok = compact_ok
-        self.deposits = []
+        self.deposits = []          # (graph task id, (g_cls, pix_cls, proto_slot, max_per_class))
         self.zero = None
+        self.dist_ref = None        # weak reference to the distances tensor (retain_grad / hook checks)
 
     def accepts(self, max_per_class: int) -> bool:
         """Whether a KLD backward on these distances should deposit its compact form."""
@@ -157,7 +159,7 @@ class DistGradSink:
         return bool(_lib.load().protoseg_l2_bwd_kld_supported(*self.shape, int(max_per_class)))
 
     def deposit(self, g_cls: Tensor, pix_cls: Tensor, proto_slot: Tensor, max_per_class: int, like: Tensor) -> Tensor:
-        self.deposits.append((g_cls, pix_cls, proto_slot, int(max_per_class)))
+        self.deposits.append((_graph_task(), (g_cls, pix_cls, proto_slot, int(max_per_class))))
         if self.zero is None or self.zero.device != like.device:
             self.zero = torch.zeros((), device=like.device, dtype=like.dtype).expand(like.shape)
         return self.zero
@@ -168,8 +170,18 @@ class DistGradSink:
                 and g.data_ptr() == z.data_ptr())
 
     def take(self):
+        """This backward pass's deposits (older passes' stale ones, e.g. of a pass that stopped at
+        the distances, are dropped)."""
+        task = _graph_task()
         d, self.deposits = self.deposits, []
-        return d
+        return [dep for t, dep in d if t == task]
+
+
+def _graph_task() -> int:
+    try:
+        return int(torch._C._current_graph_task_id())
+    except (AttributeError, RuntimeError):
+        return -1
 
 
 def expand_compact(deposit, B: int, P: int, HW: int, out: Optional[Tensor] = None) -> Tensor:
@@ -237,6 +249,7 @@ def _setup_context(ctx, inputs, output):
         B, C, H, W = x.shape
         trains = x.requires_grad and (protos.requires_grad or w_last.requires_grad)
         ctx.sink = DistGradSink((B, C, H, W, protos.shape[0], w_last.shape[0], _x_dtype(x), int(precision)), trains)
+        ctx.sink.dist_ref = weakref.ref(dist)
         dist._protoseg_sink = ctx.sink
 
 

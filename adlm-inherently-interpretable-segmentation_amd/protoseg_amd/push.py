@@ -126,6 +126,21 @@ class PushState:
                    second=torch.full((P,), math.inf, device=device, dtype=torch.float32))
 
 
+_words_cache: Dict[tuple, int] = {}
+
+
+def _class_words(proto_class: Tensor) -> int:
+    """mask_words(max class + 1), cached per (tensor, version): reading the maximum of a device
+    tensor is a device -> host sync, paid once per prototype-class tensor, not once per batch."""
+    key = (proto_class.data_ptr(), proto_class._version, proto_class.numel(), str(proto_class.device))
+    w = _words_cache.get(key)
+    if w is None:
+        if len(_words_cache) > 64:
+            _words_cache.clear()
+        w = _words_cache[key] = mask_words(int(proto_class.max()) + 1)
+    return w
+
+
 def push_update(state: PushState, x: Tensor, labels: Tensor, protos: Tensor, proto_class: Tensor, first_img: int,
                 lut: Optional[Tensor] = None, words: Optional[int] = None) -> None:
     """One batch of images (dataset indices first_img ..): mask -> argmin -> strict-'<' merge.
@@ -135,7 +150,7 @@ def push_update(state: PushState, x: Tensor, labels: Tensor, protos: Tensor, pro
     if labels.dim() == 2:
         labels = labels.unsqueeze(0)
     if words is None:  # class-mask planes (one below 33 classes); callers in a loop pass it
-        words = mask_words(int(proto_class.max()) + 1)
+        words = _class_words(proto_class)
     mask = patch_class_mask(labels, h, w, lut, words=words)
     keys, second = push_argmin(x, protos, proto_class, mask, with_second=True)
     dev = x.device

@@ -160,7 +160,9 @@ class PatchClassificationStep:
 
     def __call__(self, image: Tensor, target: Tensor) -> Dict[str, Tensor]:
         if self.iter_steps == 0:
-            self.optimizer.zero_grad(set_to_none=True)
+            # in place, as the reference's optimizer.zero_grad() (module.py:122; torch 1.10's
+            # default): the gradients stay views into the exchange buckets' buffers
+            self.optimizer.zero_grad(set_to_none=False)
         boundary = self.iter_steps + 1 == self.iter_size
         if boundary:
             self.buckets.arm()  # the exchange rides on this backward's gradient hooks

@@ -190,6 +190,9 @@ class LayerStep:
             if self.buckets is None:
                 from protoseg_amd.distributed import GradientBuckets
                 self.buckets = GradientBuckets(self.params, average=True)
+                # the backward writes g_P / g_W straight into the exchange buffers (no copy)
+                self.buckets.bind_grads()
+                self.g_p, self.g_w = self.params[0].grad, self.params[1].grad
             self.buckets.allreduce()
             self.buckets.wait()
 
@@ -281,6 +284,11 @@ def time_layer(step: LayerStep, steps: int, warmup: int, world: int, use_graph: 
         torch.cuda.synchronize()
         if use_graph and world == 1:
             g_step = capture(lambda: [step.fwd(), step.bwd(), step.opt_step()], stream)
+            run_step = g_step.replay
+        elif use_graph and os.environ.get("PROTOSEG_DP_CAPTURE", "1") == "1":
+            # the whole step, RCCL all-reduce included, as one graph: the exchange is sync-free
+            # (GradientBuckets: gradients are views into its buffers, no host reads)
+            g_step = capture(lambda: [step.fwd(), step.bwd(), step.exchange(world), step.opt_step()], stream)
             run_step = g_step.replay
         elif use_graph:
             g_grad = capture(lambda: [step.fwd(), step.bwd()], stream)
@@ -533,9 +541,10 @@ def time_push(n_img, steps, warmup, device, C=64, H=1024, W=2048, h=129, w=257, 
     from protoseg_amd import push as dpush
     x, protos, labels, pc = make_push_inputs(n_img, C, H, W, h, w, P, K, device, SEED)
     state = dpush.PushState.create(P, C, device)
+    words = dpush.mask_words(K)  # push_prototypes computes it once per push (no per-call host sync)
 
     def run():
-        dpush.push_update(state, x, labels, protos, pc, 0)
+        dpush.push_update(state, x, labels, protos, pc, 0, words=words)
 
     for _ in range(warmup):
         run()

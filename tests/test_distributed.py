@@ -132,3 +132,53 @@ def test_sharded_push_reduction_equals_serial_scan(n_img):
         assert nbuckets == 3
         for k, g in enumerate(grads):
             assert torch.allclose(g, torch.full_like(g, 1.5 * (k + 1)))  # mean of rank+1 over 2 ranks
+
+
+def _bucket_view_worker(rank, world, port, result_q):
+    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+    dist.init_process_group("gloo", init_method=f"file://{port}", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(0)
+        params = [torch.nn.Parameter(torch.rand(5, 3)), torch.nn.Parameter(torch.rand(7)),
+                  torch.nn.Parameter(torch.rand(4, 4))]
+        gb = GradientBuckets(params, bucket_mb=100 / 2 ** 20, average=True)  # 2 buckets (64 + 28 B, 60 B)
+        rounds = []
+        for step in range(3):
+            for p in params:  # zero_grad(set_to_none=False) after the first step: views survive
+                if p.grad is not None:
+                    p.grad.zero_()
+            loss = sum(((rank + 1) * (step + 1) * p * torch.arange(p.numel()).view_as(p)).sum() for p in params)
+            gb.arm()
+            loss.backward()
+            gb.wait()
+            in_flat = all(any(f is not None and f.data_ptr() <= p.grad.data_ptr() < f.data_ptr() + f.numel() * 4
+                              for f in gb._flat) for p in params)
+            rounds.append(([p.grad.clone() for p in params], in_flat))
+        result_q.put((rank, rounds, len(gb.buckets)))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gradient_buckets_alias_grads_across_steps():
+    """After the first exchange every .grad is a view into its bucket's persistent buffer, and
+    later steps (gradients zeroed in place, accumulated by backward into the buffer) reduce
+    correctly with no copy: mean over ranks of (rank + 1) * (step + 1) * arange."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bucket_view_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    mean = sum(r + 1 for r in range(world)) / world
+    for rank, rounds, nb in results:
+        assert nb == 2
+        for step, (grads, in_flat) in enumerate(rounds):
+            assert in_flat
+            for g, shape in zip(grads, [(5, 3), (7,), (4, 4)]):
+                ref = mean * (step + 1) * torch.arange(g.numel(), dtype=torch.float32).view(shape)
+                assert torch.equal(g, ref)

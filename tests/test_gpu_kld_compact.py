@@ -154,3 +154,97 @@ def test_autograd_hand_off_with_fused_sigmoid(device):
     ref = _train_grads(device, 190, False, dense_only=True, x_sigmoid=True)
     for a, b in zip(got, ref):
         assert torch.equal(a, b)
+
+
+def _layer_and_kld(device, P, K, seed=21):
+    _lib, kld, ops = _mods()
+    B, h, w = 2, 33, 35
+    x, protos, w_last, g_logits = _layer_inputs(B, h, w, P, K, seed=seed)
+    xd = x.to(device).requires_grad_(True)
+    pd = protos.to(device).requires_grad_(True)
+    wd = w_last.to(device).requires_grad_(True)
+    target = ko.synthetic_targets(B, h, w, K, seed=seed + 1, block=5).to(device)
+    ident = po.class_identity(P, K)
+    dist, logits, _ = ops.prototype_layer(xd, pd, wd)
+    return (xd, pd, wd), dist, logits, g_logits.to(device), target, ident
+
+
+def _dense_kld_grad(dist, target, ident, g_loss=0.25):
+    _, kld, _ = _mods()
+    cols, mpc = kld.prototype_columns(ident, dist.device)
+    K = ident.shape[1]
+    _, _, ws = torch.ops.protoseg.kld_forward(dist.detach(), target, cols, K, mpc)
+    return torch.ops.protoseg.kld_backward(dist.detach(), target, cols, K, mpc, ws,
+                                           torch.full((), g_loss, device=dist.device))
+
+
+def test_wide_family_takes_the_dense_kld_gradient(device):
+    """K = 40 classes at C = 64 runs the layer on the wide family, which reads a dense g_dist only:
+    protoseg_l2_bwd_kld_supported refuses, so kld_loss hands autograd the dense gradient and the
+    layer's gradients equal the dense-only path's (the compact gradient was dropped)."""
+    _lib, kld, ops = _mods()
+    P, K = 80, 40
+    assert _lib.load().protoseg_l2_bwd_kld_supported(2, 64, 33, 35, P, K, _lib.F32, _lib.PREC_BF16X3, 2) == 0
+
+    def grads(dense_only):
+        leaves, dist, logits, gl, target, ident = _layer_and_kld(device, P, K)
+        d_in = dist * 1.0 if dense_only else dist
+        loss = (logits * gl).sum() + 0.25 * kld.kld_loss(d_in, target, ident)
+        loss.backward()
+        torch.cuda.synchronize()
+        return [t.grad.clone() for t in leaves]
+
+    got, ref = grads(False), grads(True)
+    for name, a, b in zip(("g_x", "g_protos", "g_w"), got, ref):
+        assert torch.equal(a, b), name
+    assert ref[1].abs().max().item() > 0
+
+
+def test_hand_off_autograd_grad_on_distances(device):
+    """autograd.grad(kld, distances) never runs the layer backward: the KLD node returns the dense
+    gradient (not the hand-off's zero) and leaves no deposit behind."""
+    _, kld, _ = _mods()
+    _, dist, _, _, target, ident = _layer_and_kld(device, 190, 19)
+    loss = 0.25 * kld.kld_loss(dist, target, ident)
+    (g,) = torch.autograd.grad(loss, dist)
+    torch.cuda.synchronize()
+    assert torch.equal(g, _dense_kld_grad(dist, target, ident))
+    assert dist._protoseg_sink.deposits == []
+
+
+def test_hand_off_retain_grad_and_hooks_see_real_values(device):
+    _, kld, _ = _mods()
+    leaves, dist, logits, gl, target, ident = _layer_and_kld(device, 190, 19)
+    dist.retain_grad()
+    seen = []
+    dist.register_hook(lambda g: seen.append(g.clone()))
+    loss = 0.25 * kld.kld_loss(dist, target, ident) + (logits * gl).sum()
+    loss.backward()
+    torch.cuda.synchronize()
+    dense = _dense_kld_grad(dist, target, ident)
+    assert torch.equal(dist.grad, dense) and torch.equal(seen[0], dense)
+    leaves2, dist2, logits2, gl2, target2, ident2 = _layer_and_kld(device, 190, 19)
+    loss2 = 0.25 * kld.kld_loss(dist2 * 1.0, target2, ident2) + (logits2 * gl2).sum()
+    loss2.backward()
+    for a, b in zip(leaves, leaves2):
+        assert torch.equal(a.grad, b.grad)
+
+
+def test_hand_off_retain_graph_and_partial_passes(device):
+    """A retain_graph replay sums each pass's gradient once, and a pass that stops at the distances
+    (backward(inputs=[dist])) leaves no deposit for the next full pass."""
+    _, kld, _ = _mods()
+    leaves, dist, logits, gl, target, ident = _layer_and_kld(device, 361, 19)
+    loss = 0.25 * kld.kld_loss(dist, target, ident) + (logits * gl).sum()
+    loss.backward(inputs=[dist], retain_graph=True)
+    assert torch.equal(dist.grad, _dense_kld_grad(dist, target, ident))
+    loss.backward(retain_graph=True)
+    first = [t.grad.clone() for t in leaves]
+    loss.backward()
+    torch.cuda.synchronize()
+    leaves2, dist2, logits2, gl2, target2, ident2 = _layer_and_kld(device, 361, 19)
+    loss2 = 0.25 * kld.kld_loss(dist2 * 1.0, target2, ident2) + (logits2 * gl2).sum()
+    loss2.backward()
+    for a, b, f in zip(leaves, leaves2, first):
+        assert torch.equal(f, b.grad)
+        assert torch.equal(a.grad, b.grad + b.grad)
