@@ -13,6 +13,7 @@ class-0 prototypes and label value ``num_classes`` is skipped (module.py:170-178
 """
 from __future__ import annotations
 
+import weakref
 from typing import Optional, Tuple
 
 import torch
@@ -201,10 +202,12 @@ def prototype_columns(prototype_class_identity: Tensor, device) -> Tuple[Tensor,
     reference's one-hot identity (model.py:66-71) that is argmax(identity[p]) == c. Cached per
     identity tensor version, so a training loop pays the host reduction once."""
     ident = prototype_class_identity
-    key = (id(ident), ident._version, ident.data_ptr(), str(device))
+    key = (id(ident), ident._version, ident.data_ptr(), tuple(ident.shape), str(device))
     hit = _class_cache.get(key)
-    if hit is not None:
-        return hit
+    # the entry holds a weak reference to its tensor: a new tensor that reuses a freed one's id
+    # and storage address is a miss, not the freed tensor's columns
+    if hit is not None and hit[0]() is ident:
+        return hit[1]
     host = ident.detach().to("cpu")
     if host.dim() != 2 or not bool(((host != 0).sum(1) == 1).all()):
         raise _lib.ProtosegError("prototype_class_identity must be one-hot per prototype (model.py:66-71)")
@@ -215,7 +218,7 @@ def prototype_columns(prototype_class_identity: Tensor, device) -> Tuple[Tensor,
     cols = host.abs().argmax(1).to(torch.int32).to(device)
     if len(_class_cache) > 16:
         _class_cache.clear()
-    _class_cache[key] = (cols, mpc)
+    _class_cache[key] = (weakref.ref(ident), (cols, mpc))
     return cols, mpc
 
 

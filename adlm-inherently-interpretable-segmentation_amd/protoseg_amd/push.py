@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import json
 import math
+import weakref
 import os
 import time
 from dataclasses import dataclass, field
@@ -126,18 +127,20 @@ class PushState:
                    second=torch.full((P,), math.inf, device=device, dtype=torch.float32))
 
 
-_words_cache: Dict[tuple, int] = {}
+_words_cache: Dict[tuple, tuple] = {}
 
 
 def _class_words(proto_class: Tensor) -> int:
     """mask_words(max class + 1), cached per (tensor, version): reading the maximum of a device
     tensor is a device -> host sync, paid once per prototype-class tensor, not once per batch."""
-    key = (proto_class.data_ptr(), proto_class._version, proto_class.numel(), str(proto_class.device))
-    w = _words_cache.get(key)
-    if w is None:
-        if len(_words_cache) > 64:
-            _words_cache.clear()
-        w = _words_cache[key] = mask_words(int(proto_class.max()) + 1)
+    key = (id(proto_class), proto_class.data_ptr(), proto_class._version, proto_class.numel(), str(proto_class.device))
+    hit = _words_cache.get(key)
+    if hit is not None and hit[0]() is proto_class:  # not a new tensor reusing a freed one's id / address
+        return hit[1]
+    if len(_words_cache) > 64:
+        _words_cache.clear()
+    w = mask_words(int(proto_class.max()) + 1)
+    _words_cache[key] = (weakref.ref(proto_class), w)
     return w
 
 

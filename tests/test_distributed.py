@@ -52,6 +52,24 @@ def _make_images(n_img, P, C):
     return out
 
 
+def _wire(obj):
+    """Tensors -> numpy (pickled by value): a tensor put on a multiprocessing queue travels as a
+    shared-memory handle that dies with the sending rank, which may exit before the parent reads."""
+    if isinstance(obj, torch.Tensor):
+        return ("__t", obj.detach().cpu().numpy().copy())
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_wire(o) for o in obj)
+    return obj
+
+
+def _unwire(obj):
+    if isinstance(obj, tuple) and len(obj) == 2 and isinstance(obj[0], str) and obj[0] == "__t":
+        return torch.from_numpy(obj[1])
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_unwire(o) for o in obj)
+    return obj
+
+
 def _worker(rank, world, port, n_img, P, C, result_q):
     # file rendezvous (no TCP port to race for) and gloo's pair sockets on loopback
     os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
@@ -94,8 +112,8 @@ def _worker(rank, world, port, n_img, P, C, result_q):
         merged = reduce_bound_boxes(boxes.numpy())
         # every prototype's winning image has its geometry on every rank (rf boxes)
         geo_ok = all(st.geometry.get(int(i)) == (8, 8, 2, 2) for i in st.img.tolist() if i >= 0)
-        result_q.put((rank, st.dist, st.img, st.patch, st.fmap, geo_ok, grads, len(gb.buckets), merged,
-                      st.second, skipped))
+        result_q.put(_wire((rank, st.dist, st.img, st.patch, st.fmap, geo_ok, grads, len(gb.buckets), merged,
+                            st.second, skipped)))
         dist.barrier()  # neither rank tears gloo down while the other is still in a collective
     finally:
         dist.destroy_process_group()
@@ -110,7 +128,7 @@ def test_sharded_push_reduction_equals_serial_scan(n_img):
     procs = [ctx.Process(target=_worker, args=(r, world, port, n_img, P, C, q)) for r in range(world)]
     for p in procs:
         p.start()
-    results = [q.get(timeout=120) for _ in range(world)]
+    results = [_unwire(q.get(timeout=120)) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -153,7 +171,7 @@ def _bucket_view_worker(rank, world, port, result_q):
             gb.wait()
             in_flat = all(any(f is not None and f.data_ptr() <= p.grad.data_ptr() < f.data_ptr() + f.numel() * 4
                               for f in gb._flat) for p in params)
-            rounds.append(([p.grad.clone() for p in params], in_flat))
+            rounds.append(([p.grad.tolist() for p in params], in_flat))  # plain lists: no shared memory
         result_q.put((rank, rounds, len(gb.buckets)))
         dist.barrier()
     finally:
@@ -180,5 +198,6 @@ def test_gradient_buckets_alias_grads_across_steps():
         for step, (grads, in_flat) in enumerate(rounds):
             assert in_flat
             for g, shape in zip(grads, [(5, 3), (7,), (4, 4)]):
+                g = torch.tensor(g)
                 ref = mean * (step + 1) * torch.arange(g.numel(), dtype=torch.float32).view(shape)
                 assert torch.equal(g, ref)
