@@ -122,7 +122,14 @@ class LayerStep:
 
     def bwd(self):
         """One backward call for g_x, g_prototypes and g_last_layer, as the autograd op makes it
-        (ops.l2_backward): one operand-image prep shared by the two backward kernels."""
+        (ops.l2_backward with the forward's saved distances: protoseg_l2_bwd_saved)."""
+        _lib.call("protoseg_l2_bwd_saved", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w,
+                  _lib.ptr(self.protos), self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec,
+                  _lib.ptr(self.dist), _lib.ptr(self.g_logits), ctypes.c_void_p(None), _lib.ptr(self.g_x),
+                  _lib.ptr(self.g_p), _lib.ptr(self.g_w), _lib.ptr(self.ws), self.ws_bytes, self._stream())
+
+    def bwd_recompute(self):
+        """The same backward recomputing the distances from x (protoseg_l2_bwd: no saved tensor)."""
         _lib.call("protoseg_l2_bwd", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w, _lib.ptr(self.protos),
                   self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec, _lib.ptr(self.g_logits),
                   ctypes.c_void_p(None), _lib.ptr(self.g_x), _lib.ptr(self.g_p), _lib.ptr(self.g_w),
@@ -166,19 +173,19 @@ class LayerStep:
                   _lib.ptr(self.pix_cls), _lib.ptr(self.proto_slot), self._stream())
 
     def bwd_kld(self):
-        """Backward with the compact KLD gradient expanded in the kernels (protoseg_l2_bwd_kld)."""
-        _lib.call("protoseg_l2_bwd_kld", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w,
+        """Backward with the compact KLD gradient expanded in the kernels (protoseg_l2_bwd_kld_saved)."""
+        _lib.call("protoseg_l2_bwd_kld_saved", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w,
                   _lib.ptr(self.protos), self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec,
-                  _lib.ptr(self.g_logits), _lib.ptr(self.g_cls), _lib.ptr(self.pix_cls), _lib.ptr(self.proto_slot),
-                  self.mpc, _lib.ptr(self.g_x), _lib.ptr(self.g_p), _lib.ptr(self.g_w), _lib.ptr(self.ws),
-                  self.ws_bytes, self._stream())
+                  _lib.ptr(self.dist), _lib.ptr(self.g_logits), _lib.ptr(self.g_cls), _lib.ptr(self.pix_cls),
+                  _lib.ptr(self.proto_slot), self.mpc, _lib.ptr(self.g_x), _lib.ptr(self.g_p), _lib.ptr(self.g_w),
+                  _lib.ptr(self.ws), self.ws_bytes, self._stream())
 
     def bwd_gd(self):
-        """Backward with the KLD distance gradient (protoseg_l2_bwd g_dist)."""
-        _lib.call("protoseg_l2_bwd", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w, _lib.ptr(self.protos),
-                  self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec, _lib.ptr(self.g_logits),
-                  _lib.ptr(self.g_dist), _lib.ptr(self.g_x), _lib.ptr(self.g_p), _lib.ptr(self.g_w),
-                  _lib.ptr(self.ws), self.ws_bytes, self._stream())
+        """Backward with the KLD distance gradient (protoseg_l2_bwd_saved g_dist)."""
+        _lib.call("protoseg_l2_bwd_saved", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w,
+                  _lib.ptr(self.protos), self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec,
+                  _lib.ptr(self.dist), _lib.ptr(self.g_logits), _lib.ptr(self.g_dist), _lib.ptr(self.g_x),
+                  _lib.ptr(self.g_p), _lib.ptr(self.g_w), _lib.ptr(self.ws), self.ws_bytes, self._stream())
 
     def opt_step(self):
         self.opt.step()
@@ -221,9 +228,10 @@ class LayerStep:
         mm = 2.0 * n * self.P * self.C
         last = 2.0 * n * self.P * self.K
         fwd = (mm + last + 2.0 * n * self.C, n * self.C * xb + n * self.P * 4 + n * self.K * 4)
-        if self.fused:  # S, g_act, g_x, g_P, g_W: 3 distance-sized + 2 class-sized products
+        if self.fused:  # from the saved distances: g_act, g_x, g_P, g_W (2 distance-sized + 2 class-sized
+            # products); bytes X, g_logits, D (the forward's distances) read, g_X written
             return {"l2_fwd": fwd,
-                    "l2_bwd": (3 * mm + 2 * last, n * self.C * xb + n * self.K * 4 + n * self.C * xb)}
+                    "l2_bwd": (2 * mm + 2 * last, n * self.C * xb + n * self.K * 4 + n * self.P * 4 + n * self.C * xb)}
         return {
             "l2_fwd": fwd,
             "l2_bwd_x": (2 * mm + last, n * self.C * xb + n * self.K * 4 + n * self.C * xb),
@@ -410,10 +418,10 @@ def time_sigmoid_step(step: LayerStep, steps: int, warmup: int):
         _lib.call("protoseg_l2_fwd", _lib.ptr(x), step.xdt, step.B, step.C, step.h, step.w, _lib.ptr(step.protos),
                   step.P, _lib.ptr(step.w_last), step.K, 1e-4, act, step.prec, _lib.ptr(step.dist), null,
                   _lib.ptr(step.logits), step._stream())
-        _lib.call("protoseg_l2_bwd", _lib.ptr(x), step.xdt, step.B, step.C, step.h, step.w, _lib.ptr(step.protos),
-                  step.P, _lib.ptr(step.w_last), step.K, 1e-4, act, step.prec, _lib.ptr(step.g_logits), null,
-                  _lib.ptr(gx), _lib.ptr(step.g_p), _lib.ptr(step.g_w), _lib.ptr(step.ws), step.ws_bytes,
-                  step._stream())
+        _lib.call("protoseg_l2_bwd_saved", _lib.ptr(x), step.xdt, step.B, step.C, step.h, step.w,
+                  _lib.ptr(step.protos), step.P, _lib.ptr(step.w_last), step.K, 1e-4, act, step.prec,
+                  _lib.ptr(step.dist), _lib.ptr(step.g_logits), null, _lib.ptr(gx), _lib.ptr(step.g_p),
+                  _lib.ptr(step.g_w), _lib.ptr(step.ws), step.ws_bytes, step._stream())
         step.opt_step()
 
     def fused():

@@ -18,6 +18,12 @@ for step in "$@"; do
         tests/test_gpu_headline_parity.py tests/test_gpu_kld_compact.py tests/test_checkpoint.py tests/test_gpu_dp_capture.py \
         > gpurun_out/${T}_tests_new.log 2>&1 || { tail -60 gpurun_out/${T}_tests_new.log; exit 1; }
       tail -30 gpurun_out/${T}_tests_new.log ;;
+    diag)
+      timeout -k 10 300 python -u tools/debug/kld_compact_diag.py > gpurun_out/${T}_diag.log 2>&1; tail -30 gpurun_out/${T}_diag.log ;;
+    owner)
+      timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+        tests/test_gpu_owner.py tests/test_gpu_headline_parity.py > gpurun_out/${T}_owner.log 2>&1 || { tail -60 gpurun_out/${T}_owner.log; exit 1; }
+      tail -30 gpurun_out/${T}_owner.log ;;
     smoke)
       timeout -k 10 300 python -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/${T}_smoke.log 2>&1 \
         || { tail -20 gpurun_out/${T}_smoke.log; exit 1; }
