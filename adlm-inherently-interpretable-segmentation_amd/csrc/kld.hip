@@ -494,7 +494,9 @@ __global__ __launch_bounds__(64) void kld_coef_kernel(int K, int mpc, const int*
   float2* cb = coef + (static_cast<size_t>(b) * K + c) * kKldPair;
   for (int e = threadIdx.x; e < npc * npc; e += 64) {
     const int i = e / npc, j = e - i * npc;
-    const float kij = klb[i * kKldMaxPerClass + j], kji = klb[j * kKldMaxPerClass + i];
+    // the merge kernel leaves KL's diagonal unwritten (workspace garbage, possibly NaN): the
+    // pair (w_ii, KL_ii) = (0, 0) keeps 0 * KL_ii out of the gradient sums
+    const float kij = i == j ? 0.f : klb[i * kKldMaxPerClass + j], kji = i == j ? 0.f : klb[j * kKldMaxPerClass + i];
     const float w = i == j ? 0.f : -(gl / static_cast<float>(np)) * expf(-((kji + kij) / 2.f));
     cb[i * npc + j] = make_float2(w, kij);
   }

@@ -109,6 +109,21 @@ __device__ __forceinline__ void store_half4(bf16* dst, const bf16x8& f, int half
   const s16x8 v = __builtin_bit_cast(s16x8, f);
   *reinterpret_cast<s16x4*>(dst) = half ? __builtin_shufflevector(v, v, 4, 5, 6, 7) : __builtin_shufflevector(v, v, 0, 1, 2, 3);
 }
+// Timing-only ablations (wrong results; measured variants built by tools/build_var.sh):
+//   OWNER_ABL_NO_D: no distance loads; OWNER_ABL_NO_PA: no (-2P)^T fragment loads;
+//   OWNER_ABL_NO_GX: no g_x partial / reduce; OWNER_TILES_RR: round-robin tiles instead of runs.
+#ifndef OWNER_ABL_NO_D
+#define OWNER_ABL_NO_D 0
+#endif
+#ifndef OWNER_ABL_NO_PA
+#define OWNER_ABL_NO_PA 0
+#endif
+#ifndef OWNER_ABL_NO_GX
+#define OWNER_ABL_NO_GX 0
+#endif
+#ifndef OWNER_TILES_RR
+#define OWNER_TILES_RR 0
+#endif
 #ifndef OWNER_PIPE
 #define OWNER_PIPE 0  // 1: owned tile jt+1's g_act products issued before tile jt's epilogue
 #endif
@@ -141,8 +156,15 @@ __global__ __launch_bounds__(kQThreads, 1) void l2_bwd_owner_bf16_kernel(
   // contiguous runs: workgroup b takes tiles [first, first + iters)
   const int G = static_cast<int>(gridDim.x), bq = ntiles / G, br = ntiles - bq * G;
   const int bid = static_cast<int>(blockIdx.x);
+#if OWNER_TILES_RR
+  const int first = bid;  // tile first + i * G (round robin)
+  const int iters = (ntiles - bid + G - 1) / G;
+  auto tile_at = [&](int i) __attribute__((always_inline)) { return first + i * G; };
+#else
   const int first = bid * bq + (bid < br ? bid : br);
   const int iters = bq + (bid < br ? 1 : 0);
+  auto tile_at = [&](int i) __attribute__((always_inline)) { return first + i; };
+#endif
   const unsigned sz = sizeof(TX);
   const unsigned chs = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(HW) * sz);
   const rsrc_t rx = make_rsrc(x, x_bytes), rg = make_rsrc(g_logits, gl_bytes), rd = make_rsrc(dist, d_bytes);
@@ -158,6 +180,13 @@ __global__ __launch_bounds__(kQThreads, 1) void l2_bwd_owner_bf16_kernel(
   // ---- the owned (-2P)^T A fragments of g_x, streamed from the (L2-resident) operand block per
   // tile and owned tile (12 KiB per wave: held for the launch they would cost 48 VGPRs)
   auto load_pa = [&](int jt, bf16x8 (&dst)[2][kQT]) __attribute__((always_inline)) {
+    if (OWNER_ABL_NO_PA) {
+#pragma unroll
+      for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+        for (int t = 0; t < kQT; ++t) dst[ci][t] = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u + jt, 0u, 0u, 0u});
+      return;
+    }
 #pragma unroll
     for (int ci = 0; ci < 2; ++ci)
 #pragma unroll
@@ -184,6 +213,11 @@ __global__ __launch_bounds__(kQThreads, 1) void l2_bwd_owner_bf16_kernel(
   float dv[NPT][8];
   const unsigned drow = static_cast<unsigned>((m * HW + 4 * g) * 4);  // lane part
   auto load_d = [&](int t, int jt) __attribute__((always_inline)) {
+    if (OWNER_ABL_NO_D) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dv[jt][e] = static_cast<float>(t & 7) + 0.5f * e;
+      return;
+    }
     const int gp0 = t * 32;
     const int b0 = div_pix(gp0, HW);
     const int pl = (wave * NPT + jt) * 16;  // the owned tile's first prototype (chunk-local)
@@ -480,16 +514,16 @@ __global__ __launch_bounds__(kQThreads, 1) void l2_bwd_owner_bf16_kernel(
 
   // ---- main loop -------------------------------------------------------------------------
   if (iters > 0) {
-    load_raw(first);
+    load_raw(tile_at(0));
 #pragma unroll
-    for (int jt = 0; jt < NPT; ++jt) load_d(first, jt);
-    convert(first, 0);
+    for (int jt = 0; jt < NPT; ++jt) load_d(tile_at(0), jt);
+    convert(tile_at(0), 0);
   }
   __syncthreads();
   for (int i = 0; i < iters; ++i) {
-    const int t = first + i;
+    const int t = tile_at(i), tn = tile_at(i + 1);
     const bool more = i + 1 < iters;
-    if (more) load_raw(t + 1);  // x / g_logits of the next tile, converted after the barrier
+    if (more) load_raw(tn);  // x / g_logits of the next tile, converted after the barrier
     const int lzA = opaque_lane();
 #if OWNER_PIPE
     Front fr[2];
@@ -498,7 +532,7 @@ __global__ __launch_bounds__(kQThreads, 1) void l2_bwd_owner_bf16_kernel(
     for (int jt = 0; jt < NPT; ++jt) {
       if (jt + 1 < NPT) owner_front(jt + 1, lzA, fr[(jt + 1) & 1]);
       owner_back(jt, lzA, fr[jt & 1]);
-      if (more) load_d(t + 1, jt);  // dv[jt] is consumed: the next tile's distances go there
+      if (more) load_d(tn, jt);  // dv[jt] is consumed: the next tile's distances go there
     }
 #else
 #pragma unroll
@@ -506,16 +540,18 @@ __global__ __launch_bounds__(kQThreads, 1) void l2_bwd_owner_bf16_kernel(
       Front fr;
       owner_front(jt, lzA, fr);
       owner_back(jt, lzA, fr);
-      if (more) load_d(t + 1, jt);  // dv[jt] is consumed: the next tile's distances go there
+      if (more) load_d(tn, jt);  // dv[jt] is consumed: the next tile's distances go there
     }
 #endif
-    bf16x8 pa0[2][kQT];
-    load_pa(0, pa0);
-    mem_fence_compiler();  // the g_s image writes above, the transposed reads below (same wave)
-    gx_partial(pa0);
+    if (!OWNER_ABL_NO_GX) {
+      bf16x8 pa0[2][kQT];
+      load_pa(0, pa0);
+      mem_fence_compiler();  // the g_s image writes above, the transposed reads below (same wave)
+      gx_partial(pa0);
+    }
     __syncthreads();  // every wave's partial written; every read of the x / g_logits images done
-    gx_reduce(t, i & 1);
-    if (more) convert(t + 1, (i + 1) & 1);
+    if (!OWNER_ABL_NO_GX) gx_reduce(t, i & 1);
+    if (more) convert(tn, (i + 1) & 1);
     __syncthreads();  // images of tile t+1 written; every read of the partials done
   }
 

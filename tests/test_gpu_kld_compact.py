@@ -248,3 +248,28 @@ def test_hand_off_retain_graph_and_partial_passes(device):
     for a, b, f in zip(leaves, leaves2, first):
         assert torch.equal(f, b.grad)
         assert torch.equal(a.grad, b.grad + b.grad)
+
+
+def test_kld_gradient_ignores_stale_workspace(device):
+    """The KLD workspace comes from torch's caching allocator uninitialised. The merge kernel never
+    writes KL's diagonal; a NaN left there by an earlier tensor once reached the gradient through
+    w_ii * KL_ii = 0 * NaN (found when this file ran after the B = 32 parity tests)."""
+    _lib, kld, ops = _mods()
+    junk = [torch.full((n,), float("nan"), device=device) for n in (1 << 12, 1 << 16, 1 << 20, 1 << 23)]
+    del junk
+    B, h, w, P, K = 2, 9, 11, 38, 19
+    x, protos, _ = po.synthetic_inputs(B, 64, h, w, P, K, seed=B * 5 + P)
+    dist = po.l2_convolution(x, protos[:, :, None, None], torch.ones(P, 64, 1, 1)).to(device)
+    target = ko.synthetic_targets(B, h, w, K, seed=h + w, block=3).to(device)
+    ident = po.class_identity(P, K)
+    cols, mpc = kld.prototype_columns(ident, device)
+    _, _, ws = torch.ops.protoseg.kld_forward(dist, target, cols, K, mpc)
+    g_loss = torch.full((), 0.25, device=device)
+    dense = torch.ops.protoseg.kld_backward(dist, target, cols, K, mpc, ws, g_loss)
+    g_cls, pix_cls, proto_slot = kld.kld_backward_compact(dist, target, cols, K, mpc, ws, g_loss)
+    expanded = ops.expand_compact((g_cls, pix_cls, proto_slot, mpc), B, P, h * w).reshape(B, P, h, w)
+    torch.cuda.synchronize()
+    assert not bool(torch.isnan(dense).any()) and not bool(torch.isnan(expanded).any())
+    assert torch.equal(expanded, dense)
+    _, _, ref = ko.kld_loss_and_grad(dist.cpu(), target.long().cpu(), ident, 0.25)
+    assert (dense.cpu() - ref).abs().max().item() <= 1e-4 * ref.abs().max().item()

@@ -24,6 +24,18 @@ for step in "$@"; do
       timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
         tests/test_gpu_owner.py tests/test_gpu_headline_parity.py > gpurun_out/${T}_owner.log 2>&1 || { tail -60 gpurun_out/${T}_owner.log; exit 1; }
       tail -30 gpurun_out/${T}_owner.log ;;
+    ab-owner)
+      timeout -k 10 300 python -u tools/ab_libs.py --protos 361 --call bwd_saved --reps 30 > gpurun_out/${T}_ab_owner.log 2>&1 \
+        || { tail -20 gpurun_out/${T}_ab_owner.log; exit 1; }
+      cat gpurun_out/${T}_ab_owner.log ;;
+    sq-owner)
+      TAG=owner361_$T DRIVER_ARGS="--P 361 --fwd" bash tools/pmc_bwd.sh > gpurun_out/${T}_pmc_owner.log 2>&1 \
+        || { tail -20 gpurun_out/${T}_pmc_owner.log; exit 1; }
+      tail -25 gpurun_out/${T}_pmc_owner.log ;;
+    kldtest)
+      timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_headline_parity.py tests/test_gpu_kld_compact.py \
+        > gpurun_out/${T}_kldtest.log 2>&1 || { tail -40 gpurun_out/${T}_kldtest.log; exit 1; }
+      tail -3 gpurun_out/${T}_kldtest.log ;;
     smoke)
       timeout -k 10 300 python -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/${T}_smoke.log 2>&1 \
         || { tail -20 gpurun_out/${T}_smoke.log; exit 1; }
