@@ -63,7 +63,12 @@ def _(distances, target_img, proto_class, num_classes, max_per_class):
             distances.new_empty((n,), dtype=torch.uint8))
 
 
-@torch.library.custom_op("protoseg::kld_backward", mutates_args=("workspace",), device_types="cuda")
+# The backward writes its per-pair coefficients into the workspace's range-partial region, which
+# the forward leaves dead; every value the forward produced for the backward (lists, counts,
+# log-sum-exps, KL matrices, pair count) is only read. So the op does not count as mutating the
+# workspace: a second backward over a retained graph (retain_graph=True) recomputes the same
+# coefficients from the same forward results.
+@torch.library.custom_op("protoseg::kld_backward", mutates_args=(), device_types="cuda")
 def kld_backward(distances: Tensor, target_img: Tensor, proto_class: Tensor, num_classes: int, max_per_class: int,
                  workspace: Tensor, g_loss: Tensor) -> Tensor:
     """d(g_loss * loss) / d distances, dense, shaped like ``distances``."""
