@@ -68,8 +68,9 @@ __host__ __device__ constexpr QOffsets q_offsets(int Pp) {
 // its g_x partial ([32 n][68] f32) and its 32 pixel sums.
 constexpr int kPartRow = 68;                    // floats per partial / x-copy row (64 + 4 pad)
 constexpr int kPartBytes = 32 * kPartRow * 4 + 32 * 4;
+constexpr int kMaxWtBytes = (kQW * 3 * 16 / 16) * kQT * 1024;  // Pp = 384
 struct QLds {
-  int xa, ga, xs, wave, ro, cl, total;
+  int xa, ga, xs, wave, wt, ro, cl, total;
 };
 __host__ __device__ constexpr QLds q_lds() {
   QLds o{};
@@ -77,7 +78,8 @@ __host__ __device__ constexpr QLds q_lds() {
   o.ga = o.xa + kQT * 32 * 160;          // [term][32 n][32 k] bf16
   o.xs = o.ga + kQT * 32 * 64;           // [2][32 n][68] f32: x (sigmoid(x) with XSIG) per tile
   o.wave = o.xs + 2 * 32 * kPartRow * 4;  // [8][kPartBytes]
-  o.ro = o.wave + kQW * kPartBytes;      // [32] u32 g_dist row offset per pixel
+  o.wt = o.wave + kQW * kPartBytes;      // the operand block's wt region (W^T fragments), copied once
+  o.ro = o.wt + kMaxWtBytes;             // [32] u32 g_dist row offset per pixel
   o.cl = o.ro + 32 * 4;                  // [32] int KLD class per pixel
   o.total = o.cl + 32 * 4;
   return o;
@@ -151,6 +153,7 @@ __global__ __launch_bounds__(kQThreads, 1) void l2_bwd_owner_bf16_kernel(
   bf16* GW = reinterpret_cast<bf16*>(WREG);                            // [term][16 NPT][32]
   float* PART = reinterpret_cast<float*>(WREG);                        // [32][68] after the g_x products
   float* PSUM = PART + 32 * kPartRow;                                  // [32]
+  const bf16* WT = reinterpret_cast<const bf16*>(smem_raw + L.wt);       // wt fragments, 1 KiB each
 
   const int ntiles = (npix + 31) / 32;
   // contiguous runs: workgroup b takes tiles [first, first + iters)
@@ -345,12 +348,10 @@ __global__ __launch_bounds__(kQThreads, 1) void l2_bwd_owner_bf16_kernel(
     int zj = 0;
     asm volatile("" : "+v"(zj));
     const bf16* GAj = GA + zj;
-    bf16x8 wtj[kQT];
+    bf16x8 wtj[kQT];  // from LDS: no vector-memory wait here (the distance prefetch is in flight)
 #pragma unroll
     for (int t = 0; t < kQT; ++t)
-      wtj[t] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                                              rimg, static_cast<unsigned>(lz * 16),
-                                              static_cast<unsigned>(io.wt + ((wave * NPT + jt) * kQT + t) * 1024), 0));
+      wtj[t] = *reinterpret_cast<const bf16x8*>(WT + ((wave * NPT + jt) * kQT + t) * 512 + lz * 8);
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
       bf16x8 ga[kQT];
@@ -432,7 +433,7 @@ __global__ __launch_bounds__(kQThreads, 1) void l2_bwd_owner_bf16_kernel(
   };
 
   // ---- g_x^T partial over the owned prototypes (32x32x16): out[c][n], c = 32 ci + row ---------
-  auto gx_partial = [&](bf16x8 (&pa0)[2][kQT]) __attribute__((always_inline)) {
+  auto gx_partial = [&](bf16x8 (&pa0)[2][kQT], auto&& after_loads) __attribute__((always_inline)) {
     const int lz = opaque_lane();
     const int h = lz >> 5, G = (lz >> 4) & 1, q = (lz >> 2) & 3, pq = lz & 3;
     f32x16 acc[2] = {zero16(), zero16()};
@@ -462,6 +463,11 @@ __global__ __launch_bounds__(kQThreads, 1) void l2_bwd_owner_bf16_kernel(
       sacc = mfma_bf16(ones, bs[1], sacc);
       sacc = mfma_bf16(ones, bs[0], sacc);
     }
+    // the next tile's distances are issued behind the last fragment load (vmcnt counts in issue
+    // order: a wait for the fragments never waits for them), with the fragment registers dead
+    __builtin_amdgcn_sched_barrier(0);
+    after_loads();
+    __builtin_amdgcn_sched_barrier(0);
     // every read of the g_s image (this wave's) is done before the partial overwrites it
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const int n = lz & 31;
@@ -513,12 +519,14 @@ __global__ __launch_bounds__(kQThreads, 1) void l2_bwd_owner_bf16_kernel(
   };
 
   // ---- main loop -------------------------------------------------------------------------
+  lds_copy(smem_raw + L.wt, img + io.wt, io.pa - io.wt);
   if (iters > 0) {
     load_raw(tile_at(0));
 #pragma unroll
     for (int jt = 0; jt < NPT; ++jt) load_d(tile_at(0), jt);
     convert(tile_at(0), 0);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wt DMA (and tile 0's distances)
   __syncthreads();
   for (int i = 0; i < iters; ++i) {
     const int t = tile_at(i), tn = tile_at(i + 1);
@@ -532,7 +540,6 @@ __global__ __launch_bounds__(kQThreads, 1) void l2_bwd_owner_bf16_kernel(
     for (int jt = 0; jt < NPT; ++jt) {
       if (jt + 1 < NPT) owner_front(jt + 1, lzA, fr[(jt + 1) & 1]);
       owner_back(jt, lzA, fr[jt & 1]);
-      if (more) load_d(tn, jt);  // dv[jt] is consumed: the next tile's distances go there
     }
 #else
 #pragma unroll
@@ -540,14 +547,20 @@ __global__ __launch_bounds__(kQThreads, 1) void l2_bwd_owner_bf16_kernel(
       Front fr;
       owner_front(jt, lzA, fr);
       owner_back(jt, lzA, fr);
-      if (more) load_d(tn, jt);  // dv[jt] is consumed: the next tile's distances go there
     }
 #endif
     if (!OWNER_ABL_NO_GX) {
       bf16x8 pa0[2][kQT];
       load_pa(0, pa0);
       mem_fence_compiler();  // the g_s image writes above, the transposed reads below (same wave)
-      gx_partial(pa0);
+      gx_partial(pa0, [&]() __attribute__((always_inline)) {
+        if (more)
+#pragma unroll
+          for (int jt = 0; jt < NPT; ++jt) load_d(tn, jt);  // dv is consumed: the next tile's go there
+      });
+    } else if (more) {
+#pragma unroll
+      for (int jt = 0; jt < NPT; ++jt) load_d(tn, jt);
     }
     __syncthreads();  // every wave's partial written; every read of the x / g_logits images done
     if (!OWNER_ABL_NO_GX) gx_reduce(t, i & 1);

@@ -25,7 +25,7 @@ for step in "$@"; do
         tests/test_gpu_owner.py tests/test_gpu_headline_parity.py > gpurun_out/${T}_owner.log 2>&1 || { tail -60 gpurun_out/${T}_owner.log; exit 1; }
       tail -30 gpurun_out/${T}_owner.log ;;
     ab-owner)
-      timeout -k 10 300 python -u tools/ab_libs.py --protos 361 --call bwd_saved --reps 30 > gpurun_out/${T}_ab_owner.log 2>&1 \
+      timeout -k 10 300 python -u tools/ab_libs.py --protos 361 --call bwd_saved --reps 30 --also-recompute > gpurun_out/${T}_ab_owner.log 2>&1 \
         || { tail -20 gpurun_out/${T}_ab_owner.log; exit 1; }
       cat gpurun_out/${T}_ab_owner.log ;;
     sq-owner)
