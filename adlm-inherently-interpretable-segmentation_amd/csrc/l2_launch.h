@@ -77,19 +77,6 @@ int launch_bwd_onepass_bf16(const Geometry& g, bool x_bf16, const void* x, const
                             const float* g_logits, const float* g_dist, void* g_x, float* ws, hipStream_t stream,
                             int accumulate = 0);
 // Fixed-order sum of `slabs` partial slabs in ws (+ 2p sum g_s) into g_protos / g_w.
-// Owner backward (l2_bwd_owner.hip): bf16x3, P <= 384 per launch, from the forward's saved
-// distances (no recompute of S); operand block by launch_prep_owner; g_x (+= when accumulate) and
-// the same per-workgroup slab as the one-pass kernel (launch_bwd_reduce_bf16_chunks).
-int bf16_owner_npt(int P);
-bool bf16_bwd_owner_fits(const Geometry& g, int terms);
-int bf16_bwd_owner_grid(const Geometry& g);
-size_t bf16_owner_image_bytes(const Geometry& g);
-size_t bf16_bwd_owner_slab_elems(const Geometry& g);
-int launch_prep_owner(const Geometry& g, const float* protos, const float* w_last, int act_kind, float eps, void* img,
-                      hipStream_t stream);
-int launch_bwd_owner_bf16(const Geometry& g, bool x_bf16, const void* x, const float* dist, const void* img, float eps,
-                          int act_kind, const float* g_logits, const float* g_dist, void* g_x, float* ws,
-                          hipStream_t stream, int accumulate);
 int launch_bwd_reduce_bf16(const Geometry& g, const float* ws, int slabs, const float* protos, int act_kind,
                            float* g_protos, float* g_w, hipStream_t stream);
 // nchunk chunks of `per` prototypes (g.P in all, g_w columns at stride g.ldw); chunk c's slabs

@@ -620,11 +620,6 @@ constexpr size_t kImageBlockMin = 512 * 1024;
 // Backward kernel choice for the bf16x3 training backward: the one-pass kernel for P > 192 (one
 // pass over X instead of 192-prototype chunks), the fused kernel below; PROTOSEG_BWD=onepass /
 // fused forces one (read per call: tests and measurement A/B switch it in one process).
-int getenv_flag(const char* name) {
-  const char* e = getenv(name);
-  return (e && *e && strcmp(e, "0") != 0) ? 1 : 0;
-}
-
 bool use_onepass(int P) {
   const char* e = getenv("PROTOSEG_BWD");
   if (e && !strcmp(e, "onepass")) return true;
@@ -660,21 +655,6 @@ struct ImageBlock {
       gc.ldw = g.P;
       if (int st = launch_prep_onepass(gc, protos + static_cast<size_t>(p0) * g.C, w_last ? w_last + p0 : nullptr,
                                        act_kind, eps, static_cast<unsigned char*>(ptr) + c * cb, s))
-        return st;
-    }
-    return PROTOSEG_OK;
-  }
-  // The owner backward's blocks (l2_bwd_owner.hip), same chunking.
-  int build_owner(const Geometry& g, int per, int nchunk, const float* protos, const float* w_last, int act_kind,
-                  float eps, hipStream_t s) {
-    const size_t cb = bf16_owner_image_bytes(geometry_of(1, g.C, 1, 1, per, g.K));
-    if (int st = stream_block(cb * nchunk, s, static_cast<int>(ScratchKind::kOwnerImages), &ptr)) return st;
-    for (int c = 0; c < nchunk; ++c) {
-      const int p0 = c * per, pc = g.P - p0 < per ? g.P - p0 : per;
-      Geometry gc = geometry_of(1, g.C, 1, 1, pc, g.K);
-      gc.ldw = g.P;
-      if (int st = launch_prep_owner(gc, protos + static_cast<size_t>(p0) * g.C, w_last ? w_last + p0 : nullptr,
-                                     act_kind, eps, static_cast<unsigned char*>(ptr) + c * cb, s))
         return st;
     }
     return PROTOSEG_OK;
@@ -833,15 +813,6 @@ extern "C" size_t protoseg_l2_bwd_workspace_size(int B, int C, int H, int W, int
       if (q > need) need = q;
     }
   }
-  if (C == 64) {  // owner backward: one slab per workgroup and prototype chunk of <= 384
-    const int nchunk = static_cast<int>(ceil_div(P, 384)), per = static_cast<int>(ceil_div(P, nchunk));
-    Geometry gc = geometry_of(B, C, H, W, per, K);
-    gc.ldd = P;
-    if (bf16_bwd_owner_fits(gc, 2)) {
-      const size_t q = static_cast<size_t>(nchunk) * bf16_bwd_owner_slab_elems(gc) * sizeof(float);
-      if (q > need) need = q;
-    }
-  }
   if (C == 64) {  // fused backward: one slab per workgroup and prototype chunk (fused_chunks)
     const int nchunk = static_cast<int>(ceil_div(P, 192)), per = static_cast<int>(ceil_div(P, nchunk));
     const Geometry gc = geometry_of(B, C, H, W, per, K);
@@ -865,7 +836,7 @@ bool kld_compact_path(const Geometry& geo, int x_dtype, int precision, int mpc) 
 int l2_bwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P, const float* w_last,
                 int K, float eps, int act_kind, int precision, const float* g_logits, const float* g_dist,
                 const CompactGd& cgd, void* g_x, float* g_protos, float* g_w, void* workspace, size_t workspace_bytes,
-                protoseg_stream_t stream, const float* dist = nullptr) {
+                protoseg_stream_t stream) {
   const int xsig = split_x_sigmoid(act_kind, B, C, H, W, P, K, precision);
   if (xsig < 0) return -xsig;
   Geometry geo;
@@ -901,34 +872,6 @@ int l2_bwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const fl
     if (!wide_family_fits(geo)) return fail(PROTOSEG_ERR_UNSUPPORTED, "B*H*W*max(P, C) >= 2^31 elements");
     return launch_bwd_wide(geo, xb, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_x, g_protos,
                            g_logits ? g_w : nullptr, workspace, s);
-  }
-  // Training backward at bf16x3 from the forward's distances (the owner kernel, l2_bwd_owner.hip):
-  // one pass over X per chunk of <= 384 prototypes (chunk c > 0 adds its g_x), one slab reduce.
-  if (dist && terms == 2 && (xsig || (g_x && (g_protos || g_w))) && getenv_flag("PROTOSEG_NO_OWNER") == 0) {
-    const int nchunk = static_cast<int>(ceil_div(P, 384)), per = static_cast<int>(ceil_div(P, nchunk));
-    Geometry gc = geometry_of(B, C, H, W, per, K);
-    gc.ldd = P;
-    if (bf16_bwd_owner_fits(gc, terms)) {
-      KernelSpan span(nchunk > 1 ? "l2_bwd_owner_bf16_kernel" : "", "", s);
-      ImageBlock img;
-      if (int st = img.build_owner(geo, per, nchunk, protos, g_logits ? w_last : nullptr, act_kind, eps, s)) return st;
-      const size_t cb = bf16_owner_image_bytes(gc);
-      const size_t chunk_elems = bf16_bwd_owner_slab_elems(gc);
-      const int grid = bf16_bwd_owner_grid(gc);
-      for (int c = 0; c < nchunk; ++c) {
-        const int p0 = c * per, pc = P - p0 < per ? P - p0 : per;
-        Geometry gq = geometry_of(B, C, H, W, pc, K);
-        gq.ldw = gq.ldd = P;
-        gq.p0 = p0;
-        gq.xsig = xsig;
-        gq.cgd = cgd;
-        if (int st = launch_bwd_owner_bf16(gq, xb, x, dist, static_cast<unsigned char*>(img.ptr) + c * cb, eps, act_kind,
-                                           g_logits, g_dist, g_x, ws + c * chunk_elems, s, c > 0))
-          return st;
-      }
-      return launch_bwd_reduce_bf16_chunks(geo, per, nchunk, ws, grid, chunk_elems, protos, act_kind, g_protos,
-                                           g_logits ? g_w : nullptr, s);
-    }
   }
   // Training backward at bf16x3: ONE pass over X for up to 384 prototypes (19 prototypes/class;
   // l2_bwd_onepass.hip), prototype chunks of <= 384 beyond (chunk c > 0 adds its g_x), one slab
@@ -1081,16 +1024,6 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
                      CompactGd{}, g_x, g_protos, g_w, workspace, workspace_bytes, stream);
 }
 
-extern "C" int protoseg_l2_bwd_saved(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos,
-                                     int P, const float* w_last, int K, float eps, int act_kind, int precision,
-                                     const float* dist, const float* g_logits, const float* g_dist, void* g_x,
-                                     float* g_protos, float* g_w, void* workspace, size_t workspace_bytes,
-                                     protoseg_stream_t stream) {
-  if (!dist) return fail(PROTOSEG_ERR_INVALID, "dist must be non-null (protoseg_l2_bwd recomputes it)");
-  return l2_bwd_impl(x, x_dtype, B, C, H, W, protos, P, w_last, K, eps, act_kind, precision, g_logits, g_dist,
-                     CompactGd{}, g_x, g_protos, g_w, workspace, workspace_bytes, stream, dist);
-}
-
 extern "C" int protoseg_l2_bwd_kld_supported(int B, int C, int H, int W, int P, int K, int x_dtype, int precision,
                                              int max_per_class) {
   if (B <= 0 || H <= 0 || W <= 0 || P <= 0 || !protoseg_l2_supported(C, P, K)) return 0;
@@ -1111,21 +1044,4 @@ extern "C" int protoseg_l2_bwd_kld(const void* x, int x_dtype, int B, int C, int
   cgd.mpc = max_per_class;
   return l2_bwd_impl(x, x_dtype, B, C, H, W, protos, P, w_last, K, eps, act_kind, precision, g_logits, nullptr, cgd,
                      g_x, g_protos, g_w, workspace, workspace_bytes, stream);
-}
-
-extern "C" int protoseg_l2_bwd_kld_saved(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos,
-                                         int P, const float* w_last, int K, float eps, int act_kind, int precision,
-                                         const float* dist, const float* g_logits, const float* g_cls,
-                                         const int32_t* pix_cls, const int32_t* proto_slot, int max_per_class,
-                                         void* g_x, float* g_protos, float* g_w, void* workspace,
-                                         size_t workspace_bytes, protoseg_stream_t stream) {
-  if (!g_cls || !pix_cls || !proto_slot) return fail(PROTOSEG_ERR_INVALID, "g_cls, pix_cls and proto_slot must be non-null");
-  if (!dist) return fail(PROTOSEG_ERR_INVALID, "dist must be non-null (protoseg_l2_bwd_kld recomputes it)");
-  CompactGd cgd;
-  cgd.val = g_cls;
-  cgd.pix = pix_cls;
-  cgd.slot = proto_slot;
-  cgd.mpc = max_per_class;
-  return l2_bwd_impl(x, x_dtype, B, C, H, W, protos, P, w_last, K, eps, act_kind, precision, g_logits, nullptr, cgd,
-                     g_x, g_protos, g_w, workspace, workspace_bytes, stream, dist);
 }

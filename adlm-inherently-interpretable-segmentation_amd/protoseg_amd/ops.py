@@ -24,9 +24,6 @@ PRECISIONS = _lib.PRECISIONS
 # bf16x3: bf16 MFMA on 2-term split operands (|rel err| ~1e-5 on distances, the default);
 # bf16x6: 3-term split (f32-class); f32: v_mfma_f32_32x32x2_f32 (exact f32 fma chain).
 DEFAULT_PRECISION = os.environ.get("PROTOSEG_PRECISION", "bf16x3")
-# The backward reads the forward's saved distances (protoseg_l2_bwd_saved) unless
-# PROTOSEG_SAVE_DISTANCES=0 (then it recomputes them from x: protoseg_l2_bwd).
-SAVE_DISTANCES = os.environ.get("PROTOSEG_SAVE_DISTANCES", "1") != "0"
 
 
 def precision_code(precision: Optional[str]) -> int:
@@ -93,12 +90,10 @@ def _(x, protos, w_last, eps, act_kind, precision, with_dist, with_logits, with_
 @torch.library.custom_op("protoseg::l2_backward", mutates_args=(), device_types="cuda")
 def l2_backward(x: Tensor, protos: Tensor, w_last: Tensor, g_logits: Optional[Tensor], g_dist: Optional[Tensor],
                 eps: float, act_kind: int, precision: int, need_x: bool, need_protos: bool,
-                need_w: bool, dist: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor]:
+                need_w: bool) -> Tuple[Tensor, Tensor, Tensor]:
     """Backward of l2_forward with respect to (x, protos, w_last); unrequested grads are empty.
-    With X_SIGMOID in act_kind, g_x is the gradient w.r.t. the pre-activation. ``dist``: the
-    forward's distances (autograd's saved relu output, model.py:219); given, the kernels read them
-    instead of recomputing S (protoseg_l2_bwd_saved)."""
-    dev = _lib.require_device(x, protos, w_last, g_logits, g_dist, dist)
+    With X_SIGMOID in act_kind, g_x is the gradient w.r.t. the pre-activation."""
+    dev = _lib.require_device(x, protos, w_last, g_logits, g_dist)
     x = x.contiguous()
     protos = protos.contiguous()
     w_last = w_last.contiguous()
@@ -118,20 +113,14 @@ def l2_backward(x: Tensor, protos: Tensor, w_last: Tensor, g_logits: Optional[Te
     ws_bytes = lib.protoseg_l2_bwd_workspace_size(B, C, H, W, P, K)
     ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8) if ws_bytes else None
     with torch.cuda.device(dev):
-        if dist is not None:
-            _lib.call("protoseg_l2_bwd_saved", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P,
-                      _lib.ptr(w_last), K, float(eps), int(act_kind), int(precision), _lib.ptr(dist.contiguous()),
-                      _lib.ptr(g_logits), _lib.ptr(g_dist), _lib.ptr(g_x), _lib.ptr(g_p), _lib.ptr(g_w), _lib.ptr(ws),
-                      ws_bytes, _lib.stream_of(dev))
-        else:
-            _lib.call("protoseg_l2_bwd", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P, _lib.ptr(w_last),
-                      K, float(eps), int(act_kind), int(precision), _lib.ptr(g_logits), _lib.ptr(g_dist),
-                      _lib.ptr(g_x), _lib.ptr(g_p), _lib.ptr(g_w), _lib.ptr(ws), ws_bytes, _lib.stream_of(dev))
+        _lib.call("protoseg_l2_bwd", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P, _lib.ptr(w_last),
+                  K, float(eps), int(act_kind), int(precision), _lib.ptr(g_logits), _lib.ptr(g_dist),
+                  _lib.ptr(g_x), _lib.ptr(g_p), _lib.ptr(g_w), _lib.ptr(ws), ws_bytes, _lib.stream_of(dev))
     return g_x, g_p, g_w
 
 
 @l2_backward.register_fake
-def _(x, protos, w_last, g_logits, g_dist, eps, act_kind, precision, need_x, need_protos, need_w, dist=None):
+def _(x, protos, w_last, g_logits, g_dist, eps, act_kind, precision, need_x, need_protos, need_w):
     B, C, H, W = x.shape
     P, K = protos.shape[0], w_last.shape[0]
     need_w = need_w and g_logits is not None
@@ -210,8 +199,7 @@ def expand_compact(deposit, B: int, P: int, HW: int, out: Optional[Tensor] = Non
 @torch.library.custom_op("protoseg::l2_backward_kld", mutates_args=(), device_types="cuda")
 def l2_backward_kld(x: Tensor, protos: Tensor, w_last: Tensor, g_logits: Optional[Tensor], g_cls: Tensor,
                     pix_cls: Tensor, proto_slot: Tensor, max_per_class: int, eps: float, act_kind: int, precision: int,
-                    need_x: bool, need_protos: bool, need_w: bool,
-                    dist: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor]:
+                    need_x: bool, need_protos: bool, need_w: bool) -> Tuple[Tensor, Tensor, Tensor]:
     """l2_backward with the KLD loss's compact distance gradient (protoseg_l2_bwd_kld): the
     kernels expand g_dist in registers instead of reading a dense [B, P, H, W] tensor."""
     dev = _lib.require_device(x, protos, w_last, g_logits, g_cls, pix_cls, proto_slot)
@@ -229,23 +217,16 @@ def l2_backward_kld(x: Tensor, protos: Tensor, w_last: Tensor, g_logits: Optiona
     ws_bytes = lib.protoseg_l2_bwd_workspace_size(B, C, H, W, P, K)
     ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
     with torch.cuda.device(dev):
-        if dist is not None:
-            _lib.call("protoseg_l2_bwd_kld_saved", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P,
-                      _lib.ptr(w_last), K, float(eps), int(act_kind), int(precision), _lib.ptr(dist.contiguous()),
-                      _lib.ptr(g_logits), _lib.ptr(g_cls), _lib.ptr(pix_cls), _lib.ptr(proto_slot),
-                      int(max_per_class), _lib.ptr(g_x), _lib.ptr(g_p), _lib.ptr(g_w), _lib.ptr(ws), ws_bytes,
-                      _lib.stream_of(dev))
-        else:
-            _lib.call("protoseg_l2_bwd_kld", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P,
-                      _lib.ptr(w_last), K, float(eps), int(act_kind), int(precision), _lib.ptr(g_logits),
-                      _lib.ptr(g_cls), _lib.ptr(pix_cls), _lib.ptr(proto_slot), int(max_per_class), _lib.ptr(g_x),
-                      _lib.ptr(g_p), _lib.ptr(g_w), _lib.ptr(ws), ws_bytes, _lib.stream_of(dev))
+        _lib.call("protoseg_l2_bwd_kld", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P,
+                  _lib.ptr(w_last), K, float(eps), int(act_kind), int(precision), _lib.ptr(g_logits),
+                  _lib.ptr(g_cls), _lib.ptr(pix_cls), _lib.ptr(proto_slot), int(max_per_class), _lib.ptr(g_x),
+                  _lib.ptr(g_p), _lib.ptr(g_w), _lib.ptr(ws), ws_bytes, _lib.stream_of(dev))
     return g_x, g_p, g_w
 
 
 @l2_backward_kld.register_fake
 def _(x, protos, w_last, g_logits, g_cls, pix_cls, proto_slot, max_per_class, eps, act_kind, precision, need_x,
-      need_protos, need_w, dist=None):
+      need_protos, need_w):
     B, C, H, W = x.shape
     P, K = protos.shape[0], w_last.shape[0]
     need_w = need_w and g_logits is not None
@@ -256,10 +237,7 @@ def _(x, protos, w_last, g_logits, g_cls, pix_cls, proto_slot, max_per_class, ep
 
 def _setup_context(ctx, inputs, output):
     x, protos, w_last, eps, act_kind, precision, with_dist, with_logits, with_act = inputs
-    # the distances are saved as the reference's autograd saves relu's output (model.py:219): the
-    # backward reads them instead of recomputing S; in-place edits of them are caught by autograd
-    saved_dist = output[0] if (with_dist and output[0].numel() and SAVE_DISTANCES) else None
-    ctx.save_for_backward(x, protos, w_last, saved_dist)
+    ctx.save_for_backward(x, protos, w_last)
     ctx.eps = eps
     ctx.act_kind = act_kind
     ctx.precision = precision
@@ -289,7 +267,7 @@ def _act_grad_as_dist_grad(x, protos, w_last, g_act, eps, act_kind, precision):
 
 
 def _backward(ctx, g_dist, g_logits, g_act):
-    x, protos, w_last, dist = ctx.saved_tensors
+    x, protos, w_last = ctx.saved_tensors
     need_x, need_p, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
     sink = ctx.sink
     compact = sink.take() if sink is not None else []
@@ -310,11 +288,10 @@ def _backward(ctx, g_dist, g_logits, g_act):
     if compact:
         g_cls, pix_cls, proto_slot, mpc = compact[0]
         g_x, g_p, g_w = l2_backward_kld(x, protos, w_last, g_logits, g_cls, pix_cls, proto_slot, mpc, ctx.eps,
-                                        ctx.act_kind, ctx.precision, need_x, need_p, need_w and g_logits is not None,
-                                        dist)
+                                        ctx.act_kind, ctx.precision, need_x, need_p, need_w and g_logits is not None)
     else:
         g_x, g_p, g_w = l2_backward(x, protos, w_last, g_logits, g_dist, ctx.eps, ctx.act_kind, ctx.precision, need_x,
-                                    need_p, need_w and g_logits is not None, dist)
+                                    need_p, need_w and g_logits is not None)
     return (g_x if need_x else None, g_p if need_p else None, g_w if (need_w and g_w.numel()) else None,
             None, None, None, None, None, None)
 

@@ -122,14 +122,7 @@ class LayerStep:
 
     def bwd(self):
         """One backward call for g_x, g_prototypes and g_last_layer, as the autograd op makes it
-        (ops.l2_backward with the forward's saved distances: protoseg_l2_bwd_saved)."""
-        _lib.call("protoseg_l2_bwd_saved", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w,
-                  _lib.ptr(self.protos), self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec,
-                  _lib.ptr(self.dist), _lib.ptr(self.g_logits), ctypes.c_void_p(None), _lib.ptr(self.g_x),
-                  _lib.ptr(self.g_p), _lib.ptr(self.g_w), _lib.ptr(self.ws), self.ws_bytes, self._stream())
-
-    def bwd_recompute(self):
-        """The same backward recomputing the distances from x (protoseg_l2_bwd: no saved tensor)."""
+        (ops.l2_backward): one operand-image prep shared by the two backward kernels."""
         _lib.call("protoseg_l2_bwd", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w, _lib.ptr(self.protos),
                   self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec, _lib.ptr(self.g_logits),
                   ctypes.c_void_p(None), _lib.ptr(self.g_x), _lib.ptr(self.g_p), _lib.ptr(self.g_w),
@@ -173,19 +166,19 @@ class LayerStep:
                   _lib.ptr(self.pix_cls), _lib.ptr(self.proto_slot), self._stream())
 
     def bwd_kld(self):
-        """Backward with the compact KLD gradient expanded in the kernels (protoseg_l2_bwd_kld_saved)."""
-        _lib.call("protoseg_l2_bwd_kld_saved", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w,
+        """Backward with the compact KLD gradient expanded in the kernels (protoseg_l2_bwd_kld)."""
+        _lib.call("protoseg_l2_bwd_kld", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w,
                   _lib.ptr(self.protos), self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec,
-                  _lib.ptr(self.dist), _lib.ptr(self.g_logits), _lib.ptr(self.g_cls), _lib.ptr(self.pix_cls),
-                  _lib.ptr(self.proto_slot), self.mpc, _lib.ptr(self.g_x), _lib.ptr(self.g_p), _lib.ptr(self.g_w),
-                  _lib.ptr(self.ws), self.ws_bytes, self._stream())
+                  _lib.ptr(self.g_logits), _lib.ptr(self.g_cls), _lib.ptr(self.pix_cls), _lib.ptr(self.proto_slot),
+                  self.mpc, _lib.ptr(self.g_x), _lib.ptr(self.g_p), _lib.ptr(self.g_w), _lib.ptr(self.ws),
+                  self.ws_bytes, self._stream())
 
     def bwd_gd(self):
-        """Backward with the KLD distance gradient (protoseg_l2_bwd_saved g_dist)."""
-        _lib.call("protoseg_l2_bwd_saved", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w,
-                  _lib.ptr(self.protos), self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec,
-                  _lib.ptr(self.dist), _lib.ptr(self.g_logits), _lib.ptr(self.g_dist), _lib.ptr(self.g_x),
-                  _lib.ptr(self.g_p), _lib.ptr(self.g_w), _lib.ptr(self.ws), self.ws_bytes, self._stream())
+        """Backward with the KLD distance gradient (protoseg_l2_bwd g_dist)."""
+        _lib.call("protoseg_l2_bwd", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w, _lib.ptr(self.protos),
+                  self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec, _lib.ptr(self.g_logits),
+                  _lib.ptr(self.g_dist), _lib.ptr(self.g_x), _lib.ptr(self.g_p), _lib.ptr(self.g_w),
+                  _lib.ptr(self.ws), self.ws_bytes, self._stream())
 
     def opt_step(self):
         self.opt.step()
@@ -228,10 +221,9 @@ class LayerStep:
         mm = 2.0 * n * self.P * self.C
         last = 2.0 * n * self.P * self.K
         fwd = (mm + last + 2.0 * n * self.C, n * self.C * xb + n * self.P * 4 + n * self.K * 4)
-        if self.fused:  # from the saved distances: g_act, g_x, g_P, g_W (2 distance-sized + 2 class-sized
-            # products); bytes X, g_logits, D (the forward's distances) read, g_X written
+        if self.fused:  # S, g_act, g_x, g_P, g_W: 3 distance-sized + 2 class-sized products
             return {"l2_fwd": fwd,
-                    "l2_bwd": (2 * mm + 2 * last, n * self.C * xb + n * self.K * 4 + n * self.P * 4 + n * self.C * xb)}
+                    "l2_bwd": (3 * mm + 2 * last, n * self.C * xb + n * self.K * 4 + n * self.C * xb)}
         return {
             "l2_fwd": fwd,
             "l2_bwd_x": (2 * mm + last, n * self.C * xb + n * self.K * 4 + n * self.C * xb),
@@ -418,10 +410,10 @@ def time_sigmoid_step(step: LayerStep, steps: int, warmup: int):
         _lib.call("protoseg_l2_fwd", _lib.ptr(x), step.xdt, step.B, step.C, step.h, step.w, _lib.ptr(step.protos),
                   step.P, _lib.ptr(step.w_last), step.K, 1e-4, act, step.prec, _lib.ptr(step.dist), null,
                   _lib.ptr(step.logits), step._stream())
-        _lib.call("protoseg_l2_bwd_saved", _lib.ptr(x), step.xdt, step.B, step.C, step.h, step.w,
-                  _lib.ptr(step.protos), step.P, _lib.ptr(step.w_last), step.K, 1e-4, act, step.prec,
-                  _lib.ptr(step.dist), _lib.ptr(step.g_logits), null, _lib.ptr(gx), _lib.ptr(step.g_p),
-                  _lib.ptr(step.g_w), _lib.ptr(step.ws), step.ws_bytes, step._stream())
+        _lib.call("protoseg_l2_bwd", _lib.ptr(x), step.xdt, step.B, step.C, step.h, step.w, _lib.ptr(step.protos),
+                  step.P, _lib.ptr(step.w_last), step.K, 1e-4, act, step.prec, _lib.ptr(step.g_logits), null,
+                  _lib.ptr(gx), _lib.ptr(step.g_p), _lib.ptr(step.g_w), _lib.ptr(step.ws), step.ws_bytes,
+                  step._stream())
         step.opt_step()
 
     def fused():
@@ -812,6 +804,55 @@ def cpu_smoke(args, rank, world):
         dist.destroy_process_group()
 
 
+def time_wide(device, B, C, h, w, P, K, x_dtype, steps=10, warmup=3, label=""):
+    """The layer step on the wide family (l2_wide.hip: any C / K, exact f32 MFMA GEMMs with fused
+    epilogues): BASELINE configs[4]'s DenseNet depth and the reference's own construct_PPNet default
+    (model.py:394). Whole fwd / bwd calls are event-timed (each is a chain of GEMM launches); the
+    roofline is the call's algorithmic FLOPs against the f32 MFMA peak (f32 products)."""
+    step = LayerStep(B, C, h, w, P, K, x_dtype, device, SEED)
+    stream = torch.cuda.Stream(device)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    t_f, t_b = [], []
+    with torch.cuda.stream(stream):
+        for _ in range(warmup):
+            step.fwd()
+            step.bwd()
+            step.opt_step()
+        torch.cuda.synchronize()
+        g = capture(lambda: [step.fwd(), step.bwd(), step.opt_step()], stream)
+        for _ in range(warmup):
+            g.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            g.replay()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        for _ in range(steps):
+            ev[0].record(stream)
+            step.fwd()
+            ev[1].record(stream)
+            step.bwd()
+            ev[2].record(stream)
+            torch.cuda.synchronize()
+            t_f.append(ev[0].elapsed_time(ev[1]) * 1e-3)
+            t_b.append(ev[1].elapsed_time(ev[2]) * 1e-3)
+    n = B * h * w
+    mm, last = 2.0 * n * P * C, 2.0 * n * P * K
+    f_fwd = mm + last                # S, logits
+    f_bwd = 3 * mm + 2 * last        # S recomputed, g_act, g_x, g_P, g_W
+    tf, tb = float(np.median(t_f)), float(np.median(t_b))
+    out = {"workload": label + f" (B={B}, C={C}, {h}x{w} map, P={P}, K={K}, f32 products on v_mfma_f32_32x32x2_f32)",
+           "img_per_s": round(B * steps / elapsed, 1), "ms_per_step": round(elapsed / steps * 1e3, 4),
+           "fwd_ms": round(tf * 1e3, 4), "bwd_ms": round(tb * 1e3, 4)}
+    for name, f, t in (("fwd", f_fwd, tf), ("bwd", f_bwd, tb)):
+        ach = f / t / 1e12
+        out[f"roofline_{name}"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_F32_MFMA_TFLOPS,
+                                   "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_MFMA_TFLOPS, 4)}
+    del step
+    return out
+
+
 def time_small_batches(args, device, batches=(2, 4), protos=(361, 190)):
     """The layer step at the reference's per-GPU micro-batches (gin joint_batch_size = 2;
     configs[2]: 32 images over 8 GPUs = 4 per GPU), where launch and tail costs dominate."""
@@ -912,6 +953,7 @@ def main():
     ap.add_argument("--launch", choices=["graph", "eager"], default="graph",
                     help="graph: each step is one HIP graph replay of the three C-ABI calls")
     ap.add_argument("--no-small-batch", action="store_true", help="skip the B=2/4 side lines")
+    ap.add_argument("--no-wide", action="store_true", help="skip the wide-family (C=1024 / C=512, P=2000) side lines")
     ap.add_argument("--no-sigmoid", action="store_true", help="skip the fused add-on sigmoid side line")
     ap.add_argument("--no-train", action="store_true", help="skip the DeepLabV2-R101 DP training-step side line")
     ap.add_argument("--train-accumulations", type=int, default=1,
@@ -993,6 +1035,16 @@ def main():
     small = None
     if not args.no_small_batch and world == 1:
         small = time_small_batches(args, device)
+    wide = None
+    if not args.no_wide and world == 1:
+        # configs[4]: DenseNet-161 add-on depth (BASELINE names a 1024-channel map), 30 prototypes
+        # per class x 19 classes, 513x513 crops at output stride 32 -> 16x16 maps, fp16 feature maps
+        # (widened exactly to f32 at the boundary); the reference's construct_PPNet default
+        # (prototype_shape (2000, 512, 1, 1), 200 classes, 224x224 -> 7x7 maps; model.py:394)
+        wide = {"configs4_densenet_c1024_p570": time_wide(device, args.batch, 1024, 16, 16, 570, 19, torch.float32,
+                                                          label="configs[4] DenseNet depth"),
+                "reference_default_c512_p2000_k200": time_wide(device, args.batch, 512, 7, 7, 2000, 200,
+                                                               torch.float32, label="construct_PPNet default")}
     train = None
     if not args.no_train:
         train = time_train_step(args, device, rank, world, args.train_accumulations)
@@ -1043,6 +1095,8 @@ def main():
             out["push"]["bound_boxes"] = bboxes
         if small is not None:
             out["small_batch"] = small
+        if wide is not None:
+            out["wide_family"] = wide
         if train is not None:
             out["train_step"] = train
         if not args.no_cpu_baseline and world == 1:

@@ -113,8 +113,7 @@ int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, int W,
 
 /*
  * Prototype layer backward: the autograd graph of model.py:203-221, 231-237, 266-278
- * (the reference has no custom backward). Distances are recomputed from x (protoseg_l2_bwd_saved
- * reads the forward's instead).
+ * (the reference has no custom backward). Distances are recomputed from x, never re-read.
  *
  *   g_logits [B, H, W, K] f32 or NULL   upstream grad of logits
  *   g_dist   [B, P, H, W] f32 or NULL   upstream grad of distances (KLD loss, module.py:167-208)
@@ -155,33 +154,6 @@ int protoseg_l2_bwd_kld(const void* x, int x_dtype, int B, int C, int H, int W,
 int protoseg_l2_bwd_kld_supported(int B, int C, int H, int W, int P, int K, int x_dtype, int precision,
                                   int max_per_class);
 
-/*
- * The two backwards above given the forward's distances, as the reference's autograd runs them:
- * torch saves relu's OUTPUT for the relu backward and the distances for the log / division
- * backward (model.py:219, 233), so nothing of S = ||x||^2 - 2 x.p + ||p||^2 is recomputed.
- *   dist [B, P, H, W] f32: protoseg_l2_fwd's dist_out for the same x, protos and eps (unmodified)
- * At BF16X3, C = 64, K <= 32 (P <= 4096, chunks of <= 384 prototypes) with g_x and g_protos /
- * g_w requested, the owner backward (l2_bwd_owner.hip) reads dist instead of recomputing it;
- * every other request runs exactly as protoseg_l2_bwd / protoseg_l2_bwd_kld (dist unused).
- * Same outputs within the precision mode's rounding (the recomputed and the forward's distances
- * differ in summation order only). Replaces model.py:203-283's autograd backward
- * (ThresholdBackward on the saved relu output, then the log / div / conv2d backwards).
- */
-int protoseg_l2_bwd_saved(const void* x, int x_dtype, int B, int C, int H, int W,
-                          const float* protos, int P, const float* w_last, int K,
-                          float eps, int act_kind, int precision, const float* dist,
-                          const float* g_logits, const float* g_dist,
-                          void* g_x, float* g_protos, float* g_w,
-                          void* workspace, size_t workspace_bytes,
-                          protoseg_stream_t stream);
-int protoseg_l2_bwd_kld_saved(const void* x, int x_dtype, int B, int C, int H, int W,
-                              const float* protos, int P, const float* w_last, int K,
-                              float eps, int act_kind, int precision, const float* dist,
-                              const float* g_logits, const float* g_cls, const int32_t* pix_cls,
-                              const int32_t* proto_slot, int max_per_class,
-                              void* g_x, float* g_protos, float* g_w,
-                              void* workspace, size_t workspace_bytes,
-                              protoseg_stream_t stream);
 
 /* 1 if (C, P, K) is inside the compiled kernel family, else 0. */
 int protoseg_l2_supported(int C, int P, int K);

@@ -33,8 +33,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--fmap", type=int, default=65)
     ap.add_argument("--reps", type=int, default=40)
-    ap.add_argument("--call", default="bwd_full", choices=["bwd_full", "bwd_full_xsig", "bwd_saved", "fwd", "fwd_xsig", "push", "mask", "kld", "kldb", "kldc"])
-    ap.add_argument("--also-recompute", action="store_true", help="bwd_saved: also time main's protoseg_l2_bwd")
+    ap.add_argument("--call", default="bwd_full", choices=["bwd_full", "bwd_full_xsig", "fwd", "fwd_xsig", "push", "mask", "kld", "kldb", "kldc"])
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     B, C, h, w, P, K = args.batch, 64, args.fmap, args.fmap, args.protos, 19
@@ -54,11 +53,6 @@ def main():
     P_, s = _lib.ptr, _lib.stream_of(dev)
     act = _lib.X_SIGMOID if args.call.endswith("xsig") else 0
     prec = _lib.PRECISIONS["bf16x3"]
-
-    if args.call == "bwd_saved":  # the forward's distances, as autograd saves them
-        st = libs["main"].protoseg_l2_fwd(P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 0, prec, P_(dist), None,
-                                          P_(logits), s)
-        assert st == 0
 
     if args.call in ("push", "mask"):  # push argmin over 8 Cityscapes-sized maps (bench.py's push leg)
         n_img, ph, pw = 8, 129, 257
@@ -103,12 +97,6 @@ def main():
         elif args.call == "push":
             st = lib.protoseg_push_argmin(P_(xp), n_img, C, ph, pw, P_(protos), P, P_(pcls), P_(mask), P_(keys),
                                           P_(second), s)
-        elif args.call == "bwd_saved" and type(lib).__name__ == "Recompute":
-            st = lib.protoseg_l2_bwd(P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, act, prec, P_(gl), None,
-                                     P_(gx), P_(gp), P_(gw), P_(ws), ws_b, s)
-        elif args.call == "bwd_saved":
-            st = lib.protoseg_l2_bwd_saved(P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, act, prec, P_(dist),
-                                           P_(gl), None, P_(gx), P_(gp), P_(gw), P_(ws), ws_b, s)
         elif args.call.startswith("bwd"):
             st = lib.protoseg_l2_bwd(P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, act, prec, P_(gl), None,
                                      P_(gx), P_(gp), P_(gw), P_(ws), ws_b, s)
@@ -117,11 +105,6 @@ def main():
                                      P_(logits), s)
         assert st == 0, lib.protoseg_last_error()
 
-    if args.also_recompute and args.call == "bwd_saved":
-        class Recompute:  # main's recomputing backward, timed like a variant
-            def __getattr__(self, k):
-                return getattr(libs["main"], k)
-        libs["recompute"] = Recompute()
     ref = None
     for name, lib in libs.items():  # warm-up + the variants agree with main
         call(lib)

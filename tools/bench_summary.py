@@ -18,6 +18,9 @@ if "push" in d:
           "one", json.dumps(p.get("images_per_call_1")))
 if "small_batch" in d:
     print("small", json.dumps({k: v["ms_per_step"] for k, v in d["small_batch"].items()}))
+if "wide_family" in d:
+    for k, v in d["wide_family"].items():
+        print("wide", k, v["ms_per_step"], "fwd", v["fwd_ms"], v["roofline_fwd"]["frac"], "bwd", v["bwd_ms"], v["roofline_bwd"]["frac"])
 for k in ("add_on_sigmoid", "train_step", "cpu_baseline", "eval", "knn_search"):
     if k in d:
         print(k, json.dumps(d[k])[:400])

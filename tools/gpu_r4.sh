@@ -20,22 +20,6 @@ for step in "$@"; do
       tail -30 gpurun_out/${T}_tests_new.log ;;
     diag)
       timeout -k 10 300 python -u tools/debug/kld_compact_diag.py > gpurun_out/${T}_diag.log 2>&1; tail -30 gpurun_out/${T}_diag.log ;;
-    owner)
-      timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
-        tests/test_gpu_owner.py tests/test_gpu_headline_parity.py > gpurun_out/${T}_owner.log 2>&1 || { tail -60 gpurun_out/${T}_owner.log; exit 1; }
-      tail -30 gpurun_out/${T}_owner.log ;;
-    ab-owner)
-      timeout -k 10 300 python -u tools/ab_libs.py --protos 361 --call bwd_saved --reps 30 --also-recompute > gpurun_out/${T}_ab_owner.log 2>&1 \
-        || { tail -20 gpurun_out/${T}_ab_owner.log; exit 1; }
-      cat gpurun_out/${T}_ab_owner.log ;;
-    sq-owner)
-      TAG=owner361_$T DRIVER_ARGS="--P 361 --fwd" bash tools/pmc_bwd.sh > gpurun_out/${T}_pmc_owner.log 2>&1 \
-        || { tail -20 gpurun_out/${T}_pmc_owner.log; exit 1; }
-      tail -25 gpurun_out/${T}_pmc_owner.log ;;
-    kldtest)
-      timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_headline_parity.py tests/test_gpu_kld_compact.py \
-        > gpurun_out/${T}_kldtest.log 2>&1 || { tail -40 gpurun_out/${T}_kldtest.log; exit 1; }
-      tail -3 gpurun_out/${T}_kldtest.log ;;
     smoke)
       timeout -k 10 300 python -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/${T}_smoke.log 2>&1 \
         || { tail -20 gpurun_out/${T}_smoke.log; exit 1; }
@@ -44,9 +28,13 @@ for step in "$@"; do
       timeout -k 10 600 python -u bench.py > gpurun_out/${T}_bench.log 2>&1 || { tail -30 gpurun_out/${T}_bench.log; exit 1; }
       python3 tools/bench_summary.py gpurun_out/${T}_bench.log ;;
     quick)
-      timeout -k 10 300 python -u bench.py --no-kld --no-push --no-knn --no-eval --no-train --no-sigmoid --no-cpu-baseline \
+      timeout -k 10 300 python -u bench.py --no-kld --no-push --no-knn --no-eval --no-train --no-sigmoid --no-cpu-baseline --no-wide \
         > gpurun_out/${T}_quick.log 2>&1 || { tail -30 gpurun_out/${T}_quick.log; exit 1; }
       python3 tools/bench_summary.py gpurun_out/${T}_quick.log ;;
+    wide)
+      timeout -k 10 300 python -u bench.py --no-kld --no-push --no-knn --no-eval --no-train --no-sigmoid --no-cpu-baseline --no-small-batch --side-protos 0 --steps 10 \
+        > gpurun_out/${T}_wide.log 2>&1 || { tail -30 gpurun_out/${T}_wide.log; exit 1; }
+      python3 tools/bench_summary.py gpurun_out/${T}_wide.log ;;
     prof)
       TAG=$T WORKLOADS="p361 p190" bash tools/profile.sh > gpurun_out/${T}_profile.log 2>&1 \
         || { tail -20 gpurun_out/${T}_profile.log; exit 1; }
