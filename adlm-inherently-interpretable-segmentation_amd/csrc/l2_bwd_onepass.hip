@@ -54,6 +54,7 @@ __device__ unsigned long long g_stamps_onepass[1 << 17];
 #include "bf16_split.h"
 #include "l2_bf16_common.h"
 #include "l2_launch.h"
+#include "l2_onepass_layout.h"
 #include "protoseg_host.h"
 
 namespace protoseg {
@@ -63,7 +64,7 @@ namespace {
 using namespace bf16l;
 
 constexpr int kOW = 8;  // waves per workgroup
-constexpr int kOT = 2;  // split terms (bf16x3: 3 MFMAs per product)
+constexpr int kOT = onepass::kT;  // split terms (bf16x3: 3 MFMAs per product)
 constexpr int kOThreads = kOW * 64;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -71,26 +72,11 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-// ---- operand block (l2_prep_onepass_kernel). g = l >> 4, m = l & 15.
-//   wt [ptile Pp/16][term]: g_act B fragment (fragment order, 1 KiB, lane l at 16 l): lane (p =
-//                           16 ptile + m), classes 8 g + e (grad_unit * W)
-//   pi [term][Pp][64 c]:    the (-2P) image, bf16 rows of 128 B, 16-B chunk q (channels 8q ..
-//                           8q+7) at q ^ pi_swz(p); copied to LDS as is. S reads its B fragments
-//                           as rows (lane p, chunk 4 ks + g), phase B its (-2P)^T A fragments
-//                           by transposed reads (4 rows p x 16 channels per 16-lane group):
-//                           both conflict-free under the swizzle (tools/lds_swizzle_check.py pimg)
-//   p2 [Pp]                 ||p||^2 in the family's order (the forward's)
-struct OneOffsets {
-  int wt, pi, p2, total;
-};
-__host__ __device__ constexpr OneOffsets one_offsets(int Pp) {
-  OneOffsets o{};
-  o.wt = 0;
-  o.pi = o.wt + (Pp / 16) * kOT * 1024;
-  o.p2 = o.pi + kOT * Pp * 128;
-  o.total = o.p2 + ((Pp * 4 + 1023) & ~1023);
-  return o;
-}
+// ---- operand block: l2_onepass_layout.h (built by l2_prep_onepass_kernel, or by the forward's
+// prep launch beside its own images)
+using OneOffsets = onepass::Offsets;
+__host__ __device__ constexpr OneOffsets one_offsets(int Pp) { return onepass::offsets(Pp); }
+using onepass::pi_swz;
 
 // LDS regions (bytes)
 struct OneLds {
@@ -124,8 +110,7 @@ __device__ __forceinline__ int ga_off(int n, int chunk) { return n * 32 + (((chu
 __device__ __forceinline__ int gs_off2(int p, int slot) {
   return p * 32 + ((slot ^ (((p >> 2) & 1) | ((p >> 1) & 4))) << 2);
 }
-// (-2P) image: row p (64 channels), 16-B chunk q at q ^ ((p & 2) | ((p >> 1) & 4)).
-__host__ __device__ __forceinline__ int pi_swz(int p) { return (p & 2) | ((p >> 1) & 4); }
+// (-2P) image: row p (64 channels), 16-B chunk q at q ^ pi_swz(p) (l2_onepass_layout.h).
 __device__ __forceinline__ int pi_off(int p, int chunk) { return p * 64 + (((chunk ^ pi_swz(p)) & 7) << 3); }
 
 __device__ __forceinline__ bf16x8 tr_pair(const bf16* lo, const bf16* hi) {
@@ -643,34 +628,13 @@ __global__ __launch_bounds__(256) void l2_prep_onepass_kernel(const float* __res
                                                               float wt_scale, unsigned char* __restrict__ block) {
   const OneOffsets o = one_offsets(Pp);
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
-  float v[8];
-  bf16x8 f[kOT];
   switch (blockIdx.y) {
-    case 0: {  // pi[term][p][chunk q]: channels 8q .. 8q+7 of -2 p
-      if (tid >= Pp * 8) return;
-      const int p = tid >> 3, q = tid & 7;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = p < P ? -2.f * protos[static_cast<size_t>(p) * kC + 8 * q + e] : 0.f;
-      split8<kOT>(v, f);
-      const int off = o.pi + p * 128 + ((q ^ pi_swz(p)) & 7) * 16;
-#pragma unroll
-      for (int t = 0; t < kOT; ++t) *reinterpret_cast<bf16x8*>(block + off + t * Pp * 128) = f[t];
+    case 0:
+      onepass::fill_pi(protos, P, Pp, block, tid);
       break;
-    }
-    case 1: {  // wt[ptile]: lane (p), classes 8 g + e
-      const int lane = tid & 63, frag = tid >> 6, g = lane >> 4, m = lane & 15;
-      if (frag >= Pp / 16) return;
-      const int p = 16 * frag + m;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int k = 8 * g + e;
-        v[e] = (w_last && p < P && k < K) ? wt_scale * w_last[static_cast<size_t>(k) * ldw + p] : 0.f;
-      }
-      split8<kOT>(v, f);
-#pragma unroll
-      for (int t = 0; t < kOT; ++t) *reinterpret_cast<bf16x8*>(block + o.wt + (frag * kOT + t) * 1024 + lane * 16) = f[t];
+    case 1:
+      onepass::fill_wt(w_last, K, ldw, P, Pp, wt_scale, block, tid);
       break;
-    }
     default: {
       float* p2 = reinterpret_cast<float*>(block + o.p2);
       for (int p = tid; p < (o.total - o.p2) / 4; p += gridDim.x * blockDim.x) p2[p] = one_norm2(protos, p, p < P);
@@ -700,6 +664,7 @@ int onepass_t(const Geometry& g, const void* x, const unsigned char* img, float 
 }  // namespace
 
 int bf16_onepass_npt(int P) { return P <= 128 ? 1 : P <= 256 ? 2 : 3; }
+int bf16_onepass_pp(int P) { return kOW * bf16_onepass_npt(P) * 16; }
 
 bool bf16_bwd_onepass_fits(const Geometry& g, int terms) {
   return terms == kOT && g.C == kC && g.P > 0 && g.P <= kOW * 3 * 16 && bf16_sizes_ok(g);

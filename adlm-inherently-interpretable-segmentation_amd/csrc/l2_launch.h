@@ -38,12 +38,16 @@ size_t bf16_bwd_pw_workspace(const Geometry& g);
 // built once per call by launch_prep_bf16 and shared by the kernels of that call.
 size_t bf16_image_bytes(const Geometry& g, int terms);
 // act_kind / eps select the constant factors folded into the W and W^T images (bf16_split.h).
+// fwd_only: only the forward's images. onepass_block (bf16x3, one chunk): also build the one-pass
+// backward's operand block (Pp onepass_Pp) in the same launch.
 int launch_prep_bf16(const Geometry& g, int terms, const float* protos, const float* w_last, int act_kind, float eps,
-                     void* img, hipStream_t stream);
+                     void* img, hipStream_t stream, int fwd_only = 0, void* onepass_block = nullptr,
+                     int onepass_Pp = 0);
 // The images of nchunk prototype chunks of `per` rows (g.P rows in all, W columns at stride
 // g.ldw) in one launch; chunk c's images at c * bf16_image_bytes(Pp(per)).
 int launch_prep_bf16_chunks(const Geometry& g, int per, int nchunk, int terms, const float* protos,
-                            const float* w_last, int act_kind, float eps, void* img, hipStream_t stream);
+                            const float* w_last, int act_kind, float eps, void* img, hipStream_t stream,
+                            int fwd_only = 0, void* onepass_block = nullptr, int onepass_Pp = 0);
 
 // accumulate != 0: logits += this call's (prototype chunks of one forward).
 int launch_fwd_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const void* img, float eps, int act_kind,
@@ -67,6 +71,7 @@ int bf16_bwd_fused_grid(const Geometry& g);
 // (launch_prep_onepass); g_x (+= when accumulate) and a g_P / g_W slab per workgroup for
 // launch_bwd_reduce_bf16_chunks. bf16_onepass_npt: 16-prototype tiles per wave (Pp = 128 npt).
 int bf16_onepass_npt(int P);
+int bf16_onepass_pp(int P);  // the block's padded prototype count (128 npt)
 bool bf16_bwd_onepass_fits(const Geometry& g, int terms);
 int bf16_bwd_onepass_grid(const Geometry& g);
 size_t bf16_onepass_image_bytes(const Geometry& g);

@@ -634,14 +634,16 @@ int stream_block(size_t need, hipStream_t s, int kind, void** out) {
 struct ImageBlock {
   void* ptr = nullptr;
   // per > 0: the images of ceil(g.P / per) prototype chunks of `per` rows, one prep launch.
+  // fwd_only: the forward's images only; onepass_block: the one-pass backward's block too (same launch).
   int build(const Geometry& g, int terms, const float* protos, const float* w_last, int act_kind, float eps,
-            hipStream_t s, int per = 0) {
+            hipStream_t s, int per = 0, int fwd_only = 0, void* onepass_block = nullptr, int onepass_Pp = 0) {
     const int nchunk = per > 0 ? static_cast<int>(ceil_div(g.P, per)) : 1;
     const size_t need = per > 0 ? nchunk * bf16_image_bytes(geometry_of(1, g.C, 1, 1, per, g.K), terms)
                                 : bf16_image_bytes(g, terms);
     if (int st = stream_block(need, s, 0, &ptr)) return st;
-    if (per > 0) return launch_prep_bf16_chunks(g, per, nchunk, terms, protos, w_last, act_kind, eps, ptr, s);
-    return launch_prep_bf16(g, terms, protos, w_last, act_kind, eps, ptr, s);
+    if (per > 0)
+      return launch_prep_bf16_chunks(g, per, nchunk, terms, protos, w_last, act_kind, eps, ptr, s, fwd_only);
+    return launch_prep_bf16(g, terms, protos, w_last, act_kind, eps, ptr, s, fwd_only, onepass_block, onepass_Pp);
   }
   // The fragment-ordered blocks of the one-pass backward (l2_bwd_onepass.hip): nchunk chunks of
   // `per` prototypes (the last may be shorter), chunk c's block at c * chunk_bytes(per).
@@ -660,6 +662,11 @@ struct ImageBlock {
     return PROTOSEG_OK;
   }
 };
+
+// The training backward's operand images built by the forward into a caller buffer
+// (protoseg_l2_fwd_ex / protoseg_l2_bwd_ex): the one-pass block (P in (192, 384] by default) or
+// the fused kernel's images (P <= 192): the layouts the backward's own prep would write.
+enum class TrainOperands { kNone, kOnepass, kFused };
 }  // namespace
 
 // Largest P the bf16 family serves through prototype chunks (C = 64).
@@ -680,6 +687,28 @@ constexpr int kWideMaxC = 4096, kWideMaxP = 65536, kWideMaxK = 4096;
 
 // The C in {32, 64, 128}, K <= 32, P <= 4096 families (bf16 split and f32) vs the wide GEMM family.
 bool use_wide(int C, int K, int P) { return nc_of(C) == 0 || K > 32 || P > kMaxChunkedP; }
+
+namespace {
+// Which operands a bf16x3 training backward of (C, P, K) reads in one launch; kNone when it
+// chunks prototypes or runs another family (the caller's buffer is then not used).
+TrainOperands train_operands_kind(int C, int P, int K, int precision) {
+  if (terms_of(precision) != 2 || C != 64 || P <= 0 || K < 0 || use_wide(C, K, P)) return TrainOperands::kNone;
+  const Geometry g = geometry_of(1, C, 1, 1, P, K);
+  if (use_onepass(P)) return P <= 384 && bf16_bwd_onepass_fits(g, 2) ? TrainOperands::kOnepass : TrainOperands::kNone;
+  return P <= 192 && bf16_bwd_fused_fits(g, 2) ? TrainOperands::kFused : TrainOperands::kNone;
+}
+
+size_t train_operands_bytes(int C, int P, int K, TrainOperands kind) {
+  const Geometry g = geometry_of(1, C, 1, 1, P, K);
+  return kind == TrainOperands::kOnepass ? bf16_onepass_image_bytes(g)
+         : kind == TrainOperands::kFused ? bf16_image_bytes(g, 2)
+                                         : 0;
+}
+}  // namespace
+
+extern "C" size_t protoseg_l2_train_operands_bytes(int C, int P, int K, int precision) {
+  return train_operands_bytes(C, P, K, train_operands_kind(C, P, K, precision));
+}
 
 extern "C" int protoseg_l2_supported(int C, int P, int K) {
   if (C <= 0 || P <= 0 || K < 0) return 0;
@@ -714,17 +743,33 @@ extern "C" int protoseg_l2_x_sigmoid_supported(int B, int C, int H, int W, int P
   return x_sigmoid_path(B, C, H, W, P, K, precision) ? 1 : 0;
 }
 
-extern "C" int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P,
-                               const float* w_last, int K, float eps, int act_kind, int precision, float* dist_out,
-                               float* act_out, float* logits_out, protoseg_stream_t stream) {
+namespace {
+int l2_fwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P, const float* w_last,
+                int K, float eps, int act_kind, int precision, float* dist_out, float* act_out, float* logits_out,
+                void* operands, size_t operands_bytes, protoseg_stream_t stream) {
   const int xsig = split_x_sigmoid(act_kind, B, C, H, W, P, K, precision);
   if (xsig < 0) return -xsig;
   Geometry geo;
   if (int st = validate(x, x_dtype, B, C, H, W, protos, P, K, act_kind, precision, &geo)) return st;
   geo.xsig = xsig;
   if (logits_out && (!w_last || K <= 0)) return fail(PROTOSEG_ERR_INVALID, "logits_out needs w_last and K > 0");
-  if (!dist_out && !act_out && !logits_out) return PROTOSEG_OK;
+  const TrainOperands tk = operands ? train_operands_kind(C, P, K, precision) : TrainOperands::kNone;
+  if (tk != TrainOperands::kNone) {
+    if (operands_bytes < train_operands_bytes(C, P, K, tk))
+      return fail(PROTOSEG_ERR_INVALID, "operands %zu B < %zu B (protoseg_l2_train_operands_bytes)", operands_bytes,
+                  train_operands_bytes(C, P, K, tk));
+    if (K > 0 && !w_last) return fail(PROTOSEG_ERR_INVALID, "operands need w_last");
+  }
+  if (!dist_out && !act_out && !logits_out && tk == TrainOperands::kNone) return PROTOSEG_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const float* w_ops = K > 0 ? w_last : nullptr;  // the backward's W images (g_logits) from the real weights
+  if (tk == TrainOperands::kFused) {  // the forward runs on the backward's full image block
+    if (int st = launch_prep_bf16(geo, 2, protos, w_ops, act_kind, eps, operands, s)) return st;
+    if (!dist_out && !act_out && !logits_out) return PROTOSEG_OK;
+    if (bf16_fwd_fits(geo, 2))
+      return launch_fwd_bf16(geo, x_dtype == PROTOSEG_BF16, 2, x, operands, eps, act_kind, dist_out, act_out,
+                             logits_out, s);
+  }
   if (use_wide(C, K, P)) {  // any C / K: exact f32 GEMMs (l2_wide.hip), every precision request
     if (xsig) return fail(PROTOSEG_ERR_UNSUPPORTED, "PROTOSEG_X_SIGMOID: C = 64, K <= 32 only");
     if (!wide_family_fits(geo)) return fail(PROTOSEG_ERR_UNSUPPORTED, "B*H*W*max(P, C) >= 2^31 elements");
@@ -735,11 +780,18 @@ extern "C" int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, 
   }
   const int terms = terms_of(precision);
   if (terms && bf16_fwd_fits(geo, terms)) {
+    // one prep launch: the forward's images (+ the one-pass backward's block when asked)
+    const bool ob = tk == TrainOperands::kOnepass;
     ImageBlock img;
-    if (int st = img.build(geo, terms, protos, logits_out ? w_last : nullptr, act_kind, eps, s)) return st;
+    if (int st = img.build(geo, terms, protos, ob ? w_ops : logits_out ? w_last : nullptr, act_kind, eps, s, 0, 1,
+                           ob ? operands : nullptr, ob ? bf16_onepass_pp(P) : 0))
+      return st;
+    if (!dist_out && !act_out && !logits_out) return PROTOSEG_OK;
     return launch_fwd_bf16(geo, x_dtype == PROTOSEG_BF16, terms, x, img.ptr, eps, act_kind, dist_out, act_out,
                            logits_out, s);
   }
+  if (tk == TrainOperands::kOnepass)  // (not reached at C = 64, P <= 384: the forward fits one launch)
+    if (int st = launch_prep_onepass(geo, protos, w_ops, act_kind, eps, operands, s)) return st;
   // P beyond the forward's LDS images (Pp > 384, e.g. 30 prototypes/class): prototype chunks of
   // <= 384. Distance / activation rows land at (b * P + p0 + p); the logits are a sum over
   // prototypes, so chunk c > 0 adds to them.
@@ -761,7 +813,7 @@ extern "C" int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, 
         gc.xsig = xsig;
         ImageBlock img;
         if (int st = img.build(gc, terms, protos + static_cast<size_t>(p0) * C, logits_out ? w_last + p0 : nullptr,
-                               act_kind, eps, s))
+                               act_kind, eps, s, 0, 1))
           return st;
         if (int st = launch_fwd_bf16(gc, x_dtype == PROTOSEG_BF16, terms, x, img.ptr, eps, act_kind, dist_out,
                                      act_out, logits_out, s, c > 0))
@@ -795,6 +847,22 @@ extern "C" int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, 
     if (st) return st;
   }
   return PROTOSEG_OK;
+}
+}  // namespace
+
+extern "C" int protoseg_l2_fwd(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P,
+                               const float* w_last, int K, float eps, int act_kind, int precision, float* dist_out,
+                               float* act_out, float* logits_out, protoseg_stream_t stream) {
+  return l2_fwd_impl(x, x_dtype, B, C, H, W, protos, P, w_last, K, eps, act_kind, precision, dist_out, act_out,
+                     logits_out, nullptr, 0, stream);
+}
+
+extern "C" int protoseg_l2_fwd_ex(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P,
+                                  const float* w_last, int K, float eps, int act_kind, int precision, float* dist_out,
+                                  float* act_out, float* logits_out, void* operands, size_t operands_bytes,
+                                  protoseg_stream_t stream) {
+  return l2_fwd_impl(x, x_dtype, B, C, H, W, protos, P, w_last, K, eps, act_kind, precision, dist_out, act_out,
+                     logits_out, operands, operands_bytes, stream);
 }
 
 extern "C" size_t protoseg_l2_bwd_workspace_size(int B, int C, int H, int W, int P, int K) {
@@ -836,7 +904,7 @@ bool kld_compact_path(const Geometry& geo, int x_dtype, int precision, int mpc) 
 int l2_bwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P, const float* w_last,
                 int K, float eps, int act_kind, int precision, const float* g_logits, const float* g_dist,
                 const CompactGd& cgd, void* g_x, float* g_protos, float* g_w, void* workspace, size_t workspace_bytes,
-                protoseg_stream_t stream) {
+                const void* operands, size_t operands_bytes, protoseg_stream_t stream) {
   const int xsig = split_x_sigmoid(act_kind, B, C, H, W, P, K, precision);
   if (xsig < 0) return -xsig;
   Geometry geo;
@@ -866,6 +934,12 @@ int l2_bwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const fl
   const int terms = terms_of(precision);
   const bool xb = x_dtype == PROTOSEG_BF16;
   float* ws = static_cast<float*>(workspace);
+  // the forward's prep wrote this backward's images (protoseg_l2_fwd_ex): used when the
+  // backward runs the kernel they were built for, in one prototype chunk
+  const TrainOperands tk = operands ? train_operands_kind(C, P, K, precision) : TrainOperands::kNone;
+  if (tk != TrainOperands::kNone && operands_bytes < train_operands_bytes(C, P, K, tk))
+    return fail(PROTOSEG_ERR_INVALID, "operands %zu B < %zu B (protoseg_l2_train_operands_bytes)", operands_bytes,
+                train_operands_bytes(C, P, K, tk));
   if (use_wide(C, K, P)) {  // any C / K (l2_wide.hip)
     if (xsig) return fail(PROTOSEG_ERR_UNSUPPORTED, "PROTOSEG_X_SIGMOID: C = 64, K <= 32 only");
     if (cgd.val) return fail(PROTOSEG_ERR_UNSUPPORTED, "compact KLD gradient on the wide family (K > 32 or P > 4096)");
@@ -882,7 +956,9 @@ int l2_bwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const fl
     if (bf16_bwd_onepass_fits(gc, terms)) {
       KernelSpan span(nchunk > 1 ? "l2_bwd_onepass_bf16_kernel" : "", "", s);
       ImageBlock img;
-      if (int st = img.build_onepass(geo, per, nchunk, protos, g_logits ? w_last : nullptr, act_kind, eps, s))
+      if (tk == TrainOperands::kOnepass && nchunk == 1)
+        img.ptr = const_cast<void*>(operands);
+      else if (int st = img.build_onepass(geo, per, nchunk, protos, g_logits ? w_last : nullptr, act_kind, eps, s))
         return st;
       const size_t cb = bf16_onepass_image_bytes(gc);
       const size_t chunk_elems = bf16_bwd_onepass_slab_elems(gc);
@@ -917,7 +993,10 @@ int l2_bwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const fl
       const size_t chunk_elems = static_cast<size_t>(grid) * (static_cast<size_t>(gc.Pp) * C + 32 * gc.Pp + gc.Pp);
       Geometry gall = geometry_of(B, C, H, W, P, K);
       ImageBlock img;
-      if (int st = img.build(gall, terms, protos, g_logits ? w_last : nullptr, act_kind, eps, s, per)) return st;
+      if (tk == TrainOperands::kFused && nchunk == 1)
+        img.ptr = const_cast<void*>(operands);
+      else if (int st = img.build(gall, terms, protos, g_logits ? w_last : nullptr, act_kind, eps, s, per))
+        return st;
       for (int c = 0; c < nchunk; ++c) {
         const int p0 = c * per, pc = P - p0 < per ? P - p0 : per;
         gc = geometry_of(B, C, H, W, pc, K);
@@ -1021,7 +1100,16 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
                                const float* g_logits, const float* g_dist, void* g_x, float* g_protos, float* g_w,
                                void* workspace, size_t workspace_bytes, protoseg_stream_t stream) {
   return l2_bwd_impl(x, x_dtype, B, C, H, W, protos, P, w_last, K, eps, act_kind, precision, g_logits, g_dist,
-                     CompactGd{}, g_x, g_protos, g_w, workspace, workspace_bytes, stream);
+                     CompactGd{}, g_x, g_protos, g_w, workspace, workspace_bytes, nullptr, 0, stream);
+}
+
+extern "C" int protoseg_l2_bwd_ex(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P,
+                                  const float* w_last, int K, float eps, int act_kind, int precision,
+                                  const float* g_logits, const float* g_dist, void* g_x, float* g_protos, float* g_w,
+                                  void* workspace, size_t workspace_bytes, const void* operands,
+                                  size_t operands_bytes, protoseg_stream_t stream) {
+  return l2_bwd_impl(x, x_dtype, B, C, H, W, protos, P, w_last, K, eps, act_kind, precision, g_logits, g_dist,
+                     CompactGd{}, g_x, g_protos, g_w, workspace, workspace_bytes, operands, operands_bytes, stream);
 }
 
 extern "C" int protoseg_l2_bwd_kld_supported(int B, int C, int H, int W, int P, int K, int x_dtype, int precision,
@@ -1036,6 +1124,17 @@ extern "C" int protoseg_l2_bwd_kld(const void* x, int x_dtype, int B, int C, int
                                    const float* g_logits, const float* g_cls, const int32_t* pix_cls,
                                    const int32_t* proto_slot, int max_per_class, void* g_x, float* g_protos,
                                    float* g_w, void* workspace, size_t workspace_bytes, protoseg_stream_t stream) {
+  return protoseg_l2_bwd_kld_ex(x, x_dtype, B, C, H, W, protos, P, w_last, K, eps, act_kind, precision, g_logits,
+                                g_cls, pix_cls, proto_slot, max_per_class, g_x, g_protos, g_w, workspace,
+                                workspace_bytes, nullptr, 0, stream);
+}
+
+extern "C" int protoseg_l2_bwd_kld_ex(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos,
+                                      int P, const float* w_last, int K, float eps, int act_kind, int precision,
+                                      const float* g_logits, const float* g_cls, const int32_t* pix_cls,
+                                      const int32_t* proto_slot, int max_per_class, void* g_x, float* g_protos,
+                                      float* g_w, void* workspace, size_t workspace_bytes, const void* operands,
+                                      size_t operands_bytes, protoseg_stream_t stream) {
   if (!g_cls || !pix_cls || !proto_slot) return fail(PROTOSEG_ERR_INVALID, "g_cls, pix_cls and proto_slot must be non-null");
   CompactGd cgd;
   cgd.val = g_cls;
@@ -1043,5 +1142,5 @@ extern "C" int protoseg_l2_bwd_kld(const void* x, int x_dtype, int B, int C, int
   cgd.slot = proto_slot;
   cgd.mpc = max_per_class;
   return l2_bwd_impl(x, x_dtype, B, C, H, W, protos, P, w_last, K, eps, act_kind, precision, g_logits, nullptr, cgd,
-                     g_x, g_protos, g_w, workspace, workspace_bytes, stream);
+                     g_x, g_protos, g_w, workspace, workspace_bytes, operands, operands_bytes, stream);
 }

@@ -51,16 +51,11 @@ struct WideArgs {
   int accumulate;
   float eps;
   int act_kind;
-  const float* x2;   // kEpiDist: x2[b * x2b + n]
-  long long x2b;
-  const float* p2;   // kEpiDist: p2[m]
   float* act;        // kEpiDist: optional activation output at act[b * ab + m * am + n * an]
   long long am, an, ab;
   const float* D;    // kEpiGs: the distance at the output's address
   const float* gd;   // kEpiGs: dense g_dist at the output's address, or null
   const void* xo;    // kEpiGx: x at the output's address
-  const float* cs;   // kEpiGx: column sums cs[b * csb + n]
-  long long csb;
 };
 
 template <typename T>
@@ -104,10 +99,19 @@ __device__ __forceinline__ void load_tile(const Operand& o, int R, int Kd, int r
   }
 }
 
+// The epilogues' per-column / per-row sums, taken from the LDS stages the GEMM stages anyway
+// (each workgroup contracts over the whole Kd of its batch, so it holds them for its own rows and
+// columns): kEpiDist: x2[n] = sum_c X[c][n]^2 (B columns) and p2[m] = sum_c P[m][c]^2 (A rows);
+// kEpiGx: cs[n] = sum_p G_s[p][n] (B columns). Thread t sums column t & 63 of stage rows
+// 4 (t >> 6) .. + 3; the four partials are added in a fixed order at the end: deterministic, and
+// the same bits in every workgroup of a column (same data, same order). No separate norms pass.
 template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO>
 __global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
   __shared__ float As[kWKs][kWLd];
   __shared__ float Bs[kWKs][kWLd];
+  constexpr bool kSumB = EPI == kEpiDist || EPI == kEpiGx, kSumA = EPI == kEpiDist, kSq = EPI == kEpiDist;
+  __shared__ float red[kSumB ? 2 : 1][4][64];
+  float sum_b = 0.f, sum_a = 0.f;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int j = lane & 31, h = lane >> 5;
   const int wm = wave & 1, wn = wave >> 1;
@@ -143,6 +147,23 @@ __global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
 #pragma unroll
     for (int kk = 0; kk < kWKs / 2; ++kk)
       acc = mfma32(As[2 * kk + h][wm * 32 + j], Bs[2 * kk + h][wn * 32 + j], acc);
+    if constexpr (kSumB) {
+      const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float vb = Bs[4 * q + i][c];
+        sum_b = kSq ? fmaf(vb, vb, sum_b) : sum_b + vb;
+        if constexpr (kSumA) {
+          const float va = As[4 * q + i][c];
+          sum_a = fmaf(va, va, sum_a);
+        }
+      }
+    }
+  }
+  if constexpr (kSumB) {
+    red[0][threadIdx.x >> 6][threadIdx.x & 63] = sum_b;
+    red[1][threadIdx.x >> 6][threadIdx.x & 63] = sum_a;
+    __syncthreads();
   }
 
   // epilogue: lane column n, rows acc_row(r, h)
@@ -156,7 +177,10 @@ __global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
     const long long o = bo * a.ob + m * a.om + static_cast<long long>(n) * a.on;
     float v = acc[r];
     if constexpr (EPI == kEpiDist) {
-      const float d = l2_distance(a.x2[bo * a.x2b + n], a.p2[m], v);
+      const int cn = wn * 32 + j, rm = m - m0;
+      const float x2 = (red[0][0][cn] + red[0][1][cn]) + (red[0][2][cn] + red[0][3][cn]);
+      const float p2 = (red[1][0][rm] + red[1][1][rm]) + (red[1][2][rm] + red[1][3][rm]);
+      const float d = l2_distance(x2, p2, v);
       v = d;
       if (a.act) a.act[bo * a.ab + m * a.am + static_cast<long long>(n) * a.an] = activation(d, a.eps, a.act_kind);
     } else if constexpr (EPI == kEpiGs) {
@@ -166,48 +190,14 @@ __global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
       v = d > 0.f ? g : 0.f;  // relu backward
     } else if constexpr (EPI == kEpiGx) {
       // conv(x^2, ones) backward: 2x sum_p g_s; conv(x, P) backward: -2 P^T g_s
-      v = -2.f * v + 2.f * load_elem<TO>(a.xo, o) * a.cs[bo * a.csb + n];
+      const int cn = wn * 32 + j;
+      const float cs = (red[0][0][cn] + red[0][1][cn]) + (red[0][2][cn] + red[0][3][cn]);
+      v = -2.f * v + 2.f * load_elem<TO>(a.xo, o) * cs;
     }
     TO* out = static_cast<TO*>(a.out);
     if (a.accumulate) v += XIO<TO>::load(out, static_cast<size_t>(o));
     XIO<TO>::store(out, static_cast<size_t>(o), v);
   }
-}
-
-// Sums of squares: x2[b][n] = sum_c x[b][c][n]^2 (threads over (b, n)), p2[p] = sum_c P[p][c]^2.
-template <typename TX>
-__global__ __launch_bounds__(256) void wide_norms_kernel(const TX* __restrict__ x, int C, int HW, int npix,
-                                                         const float* __restrict__ protos, int P,
-                                                         float* __restrict__ x2, float* __restrict__ p2) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < npix) {
-    const int b = i / HW, n = i - b * HW;
-    const TX* xp = x + static_cast<size_t>(b) * C * HW + n;
-    float s = 0.f;
-    for (int c = 0; c < C; ++c) {
-      const float v = XIO<TX>::load(xp, static_cast<size_t>(c) * HW);
-      s = fmaf(v, v, s);
-    }
-    x2[i] = s;
-  } else if (i - npix < P && p2) {
-    const int p = i - npix;
-    const float* pp = protos + static_cast<size_t>(p) * C;
-    float s = 0.f;
-    for (int c = 0; c < C; ++c) s = fmaf(pp[c], pp[c], s);
-    p2[p] = s;
-  }
-}
-
-// cs[b][n] = sum_p G_s[b][p][n] (threads over (b, n): rows read coalesced along n).
-__global__ __launch_bounds__(256) void wide_colsum_kernel(const float* __restrict__ gs, int P, int HW, int npix,
-                                                          float* __restrict__ cs) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= npix) return;
-  const int b = i / HW, n = i - b * HW;
-  const float* g = gs + static_cast<size_t>(b) * P * HW + n;
-  float s = 0.f;
-  for (int p = 0; p < P; ++p) s += g[static_cast<size_t>(p) * HW];
-  cs[i] = s;
 }
 
 // rs[p] = sum_{b, n} G_s[b][p][n]: one workgroup per prototype, fixed-order tree.
@@ -261,7 +251,7 @@ int split_of(int M, int N, long long total) {
 }
 
 struct WideBwdLayout {
-  size_t D, G, x2, p2, cs, rs, part, total;  // float offsets
+  size_t D, G, rs, part, total;  // float offsets
 };
 WideBwdLayout wide_bwd_layout(const Geometry& g) {
   WideBwdLayout l{};
@@ -271,10 +261,7 @@ WideBwdLayout wide_bwd_layout(const Geometry& g) {
   auto al = [](size_t v) { return (v + 63) & ~static_cast<size_t>(63); };
   l.D = 0;
   l.G = al(dp);
-  l.x2 = l.G + al(dp);
-  l.p2 = l.x2 + al(g.npix);
-  l.cs = l.p2 + al(g.P);
-  l.rs = l.cs + al(g.npix);
+  l.rs = l.G + al(dp);
   l.part = l.rs + al(g.P);
   l.total = l.part + al(sp > sw ? sp : sw);
   return l;
@@ -282,21 +269,17 @@ WideBwdLayout wide_bwd_layout(const Geometry& g) {
 
 Operand op(const void* p, long long sr, long long sk, long long sb) { return Operand{p, sr, sk, sb}; }
 
-// D[b][p][n] into `dist` (ld P per image), optional act[g][p]; x2 / p2 scratch given.
+// D[b][p][n] into `dist` (ld P per image), optional act[g][p].
 template <typename TX>
 int wide_distances(const Geometry& g, const TX* x, const float* protos, float eps, int act_kind, float* dist,
-                   float* act, float* x2, float* p2, hipStream_t s) {
+                   float* act, hipStream_t s) {
   const int B = g.npix / g.HW;
-  hipLaunchKernelGGL(wide_norms_kernel<TX>, dim3(static_cast<unsigned>(ceil_div(g.npix + g.P, 256))), dim3(256), 0, s,
-                     x, g.C, g.HW, g.npix, protos, g.P, x2, p2);
-  if (int st = check_launch("wide_norms_kernel")) return st;
   WideArgs a{};
   a.A = op(protos, g.C, 1, 0);                                   // P[p][c]
   a.B = op(x, 1, g.HW, static_cast<long long>(g.C) * g.HW);      // X[b][c][n]: (n, c)
   a.M = g.P, a.N = g.HW, a.Kd = g.C, a.nb = B;
   a.out = dist, a.om = g.HW, a.on = 1, a.ob = static_cast<long long>(g.P) * g.HW;
   a.eps = eps, a.act_kind = act_kind;
-  a.x2 = x2, a.x2b = g.HW, a.p2 = p2;
   a.act = act, a.am = 1, a.an = g.P, a.ab = static_cast<long long>(g.HW) * g.P;  // act[(b HW + n) P + p]
   return gemm<kEpiDist, float, TX, -1, -1, float>(a, B, s);
 }
@@ -309,21 +292,16 @@ bool wide_family_fits(const Geometry& g) {
 }
 
 size_t wide_fwd_scratch_bytes(const Geometry& g, bool need_dist) {
-  size_t f = static_cast<size_t>(g.npix) + g.P + 128;
-  if (need_dist) f += static_cast<size_t>(g.npix) * g.P;
-  return f * sizeof(float);
+  return (need_dist ? static_cast<size_t>(g.npix) * g.P : 0) * sizeof(float) + 256;
 }
 
 size_t wide_bwd_workspace_bytes(const Geometry& g) { return wide_bwd_layout(g).total * sizeof(float); }
 
 int launch_fwd_wide(const Geometry& g, bool x_bf16, const void* x, const float* protos, const float* w_last, float eps,
                     int act_kind, float* dist, float* act, float* logits, void* scratch, hipStream_t s) {
-  float* sc = static_cast<float*>(scratch);
-  float* x2 = sc;
-  float* p2 = x2 + g.npix;
-  float* D = dist ? dist : p2 + g.P + 64;  // the logits read the distances back
-  const int st = x_bf16 ? wide_distances(g, static_cast<const uint16_t*>(x), protos, eps, act_kind, D, act, x2, p2, s)
-                        : wide_distances(g, static_cast<const float*>(x), protos, eps, act_kind, D, act, x2, p2, s);
+  float* D = dist ? dist : static_cast<float*>(scratch);  // the logits read the distances back
+  const int st = x_bf16 ? wide_distances(g, static_cast<const uint16_t*>(x), protos, eps, act_kind, D, act, s)
+                        : wide_distances(g, static_cast<const float*>(x), protos, eps, act_kind, D, act, s);
   if (st || !logits) return st;
   // logits[b][n][k] = sum_p act(D[b][p][n]) W[k][p]
   WideArgs a{};
@@ -341,12 +319,12 @@ int launch_bwd_wide(const Geometry& g, bool x_bf16, const void* x, const float* 
                     void* workspace, hipStream_t s) {
   const WideBwdLayout l = wide_bwd_layout(g);
   float* ws = static_cast<float*>(workspace);
-  float *D = ws + l.D, *G = ws + l.G, *x2 = ws + l.x2, *p2 = ws + l.p2, *cs = ws + l.cs, *rs = ws + l.rs;
+  float *D = ws + l.D, *G = ws + l.G, *rs = ws + l.rs;
   float* part = ws + l.part;
   const int B = g.npix / g.HW;
   const long long img = static_cast<long long>(g.P) * g.HW;
-  int st = x_bf16 ? wide_distances(g, static_cast<const uint16_t*>(x), protos, eps, act_kind, D, nullptr, x2, p2, s)
-                  : wide_distances(g, static_cast<const float*>(x), protos, eps, act_kind, D, nullptr, x2, p2, s);
+  int st = x_bf16 ? wide_distances(g, static_cast<const uint16_t*>(x), protos, eps, act_kind, D, nullptr, s)
+                  : wide_distances(g, static_cast<const float*>(x), protos, eps, act_kind, D, nullptr, s);
   if (st) return st;
   {  // G_s[b][p][n] = (sum_k W[k][p] GL[b][n][k]) act'(D) + g_dist, relu mask (K = 0: g_dist alone)
     WideArgs a{};
@@ -358,15 +336,12 @@ int launch_bwd_wide(const Geometry& g, bool x_bf16, const void* x, const float* 
     if ((st = gemm<kEpiGs, float, float, -1, -1, float>(a, B, s))) return st;
   }
   if (g_x) {  // g_x[b][c][n] = -2 sum_p P[p][c] G_s[b][p][n] + 2 x cs[b][n]
-    hipLaunchKernelGGL(wide_colsum_kernel, dim3(static_cast<unsigned>(ceil_div(g.npix, 256))), dim3(256), 0, s, G, g.P,
-                       g.HW, g.npix, cs);
-    if ((st = check_launch("wide_colsum_kernel"))) return st;
     WideArgs a{};
     a.A = op(protos, 1, g.C, 0);          // (c, p) of P[p][c]
     a.B = op(G, 1, g.HW, img);            // (n, p) of G_s[b][p][n]
     a.M = g.C, a.N = g.HW, a.Kd = g.P, a.nb = B;
     a.out = g_x, a.om = g.HW, a.on = 1, a.ob = static_cast<long long>(g.C) * g.HW;
-    a.xo = x, a.cs = cs, a.csb = g.HW;
+    a.xo = x;
     st = x_bf16 ? gemm<kEpiGx, float, float, -1, -1, uint16_t>(a, B, s) : gemm<kEpiGx, float, float, -1, -1, float>(a, B, s);
     if (st) return st;
   }
@@ -467,19 +442,16 @@ __global__ __launch_bounds__(256) void wide_push_argmin_kernel(const float* __re
 
 }  // namespace
 
-// Distances of n_img images [n_img][P][hw] (the push's wide-C path); x2 / p2 scratch given.
-int wide_push_distances(const float* x, int n_img, int C, int hw, const float* protos, int P, float* dist, float* x2,
-                        float* p2, hipStream_t s) {
+// Distances of n_img images [n_img][P][hw] (the push's wide-C path).
+int wide_push_distances(const float* x, int n_img, int C, int hw, const float* protos, int P, float* dist,
+                        hipStream_t s) {
   Geometry g{};
   g.C = C, g.P = P, g.K = 0, g.HW = hw, g.npix = n_img * hw;
-  return wide_distances(g, x, protos, 1e-4f, PROTOSEG_ACT_LOG, dist, nullptr, x2, p2, s);
+  return wide_distances(g, x, protos, 1e-4f, PROTOSEG_ACT_LOG, dist, nullptr, s);
 }
 
 int wide_push_distances_scratch(const float* x, int C, int hw, const float* protos, int m, float* dist, hipStream_t s) {
-  int st = PROTOSEG_OK;
-  float* sc = static_cast<float*>(wide_scratch((static_cast<size_t>(hw) + m + 128) * sizeof(float), s, &st));
-  if (st) return st;
-  return wide_push_distances(x, 1, C, hw, protos, m, dist, sc, sc + hw, s);
+  return wide_push_distances(x, 1, C, hw, protos, m, dist, s);
 }
 
 int wide_push_argmin(const float* x, int n_img, int C, int hw, const float* protos, int P, const int32_t* proto_class,
@@ -490,15 +462,11 @@ int wide_push_argmin(const float* x, int n_img, int C, int hw, const float* prot
   if (nb < 1) nb = 1;
   if (nb > n_img) nb = n_img;
   int st = PROTOSEG_OK;
-  float* sc = static_cast<float*>(
-      wide_scratch((per_img * nb + static_cast<size_t>(nb) * hw + P + 256) * sizeof(float), s, &st));
+  float* D = static_cast<float*>(wide_scratch((per_img * nb + 256) * sizeof(float), s, &st));
   if (st) return st;
-  float* D = sc;
-  float* x2 = D + per_img * nb;
-  float* p2 = x2 + static_cast<size_t>(nb) * hw;
   for (int i0 = 0; i0 < n_img; i0 += nb) {
     const int ni = n_img - i0 < nb ? n_img - i0 : nb;
-    if ((st = wide_push_distances(x + static_cast<size_t>(i0) * C * hw, ni, C, hw, protos, P, D, x2, p2, s))) return st;
+    if ((st = wide_push_distances(x + static_cast<size_t>(i0) * C * hw, ni, C, hw, protos, P, D, s))) return st;
     // mask planes [words][n_img][hw]: class c in word c >> 5
     hipLaunchKernelGGL(wide_push_argmin_kernel, dim3(static_cast<unsigned>(ceil_div(P, 4)), ni), dim3(256), 0, s, D, P,
                        hw, proto_class, mask + static_cast<size_t>(i0) * hw, static_cast<size_t>(n_img) * hw, words,

@@ -52,6 +52,12 @@ SIGNATURES = {
     "protoseg_l2_bwd_kld": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _i, _vp, _vp, _vp, _vp, _i, _vp,
                                  _vp, _vp, _vp, _sz, _vp]),
     "protoseg_l2_bwd_kld_supported": (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _i]),
+    "protoseg_l2_train_operands_bytes": (_sz, [_i, _i, _i, _i]),
+    "protoseg_l2_fwd_ex": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "protoseg_l2_bwd_ex": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp,
+                                _sz, _vp, _sz, _vp]),
+    "protoseg_l2_bwd_kld_ex": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _i, _vp, _vp, _vp, _vp, _i,
+                                    _vp, _vp, _vp, _vp, _sz, _vp, _sz, _vp]),
     "protoseg_patch_class_mask": (_i, [_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp]),
     "protoseg_push_argmin": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
     "protoseg_push_distances": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _vp]),

@@ -56,11 +56,20 @@ def max_protos(C: int, precision: Optional[str] = None) -> int:
     return int(_lib.load().protoseg_l2_max_protos(C, precision_code(precision)))
 
 
+def train_operands_bytes(C: int, P: int, K: int, precision: int) -> int:
+    """Bytes of the backward's operand images the forward can build (protoseg_l2_train_operands_bytes);
+    0 when the backward at this shape / precision would not read them."""
+    return int(_lib.load().protoseg_l2_train_operands_bytes(C, P, K, int(precision)))
+
+
 @torch.library.custom_op("protoseg::l2_forward", mutates_args=(), device_types="cuda")
 def l2_forward(x: Tensor, protos: Tensor, w_last: Tensor, eps: float, act_kind: int, precision: int,
-               with_dist: bool, with_logits: bool, with_act: bool) -> Tuple[Tensor, Tensor, Tensor]:
-    """Fused prototype-layer forward. Returns (dist [B,P,H,W], logits [B,H,W,K], act [B*H*W,P]);
-    outputs not requested are empty tensors."""
+               with_dist: bool, with_logits: bool, with_act: bool,
+               with_operands: bool = False) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """Fused prototype-layer forward. Returns (dist [B,P,H,W], logits [B,H,W,K], act [B*H*W,P],
+    operands): outputs not requested are empty tensors. with_operands: the training backward's
+    operand images (uint8, protoseg_l2_fwd_ex) built in the forward's prep launch, for
+    l2_backward(..., operands=...); empty when the backward at this shape would not read them."""
     dev = _lib.require_device(x, protos, w_last)
     x = x.contiguous()
     protos = protos.contiguous()
@@ -71,28 +80,39 @@ def l2_forward(x: Tensor, protos: Tensor, w_last: Tensor, eps: float, act_kind: 
     dist = torch.empty((B, P, H, W) if with_dist else (0,), **f32)
     logits = torch.empty((B, H, W, K) if with_logits else (0,), **f32)
     act = torch.empty((B * H * W, P) if with_act else (0,), **f32)
+    nops = train_operands_bytes(C, P, K, precision) if with_operands else 0
+    ops_buf = torch.empty(nops, device=dev, dtype=torch.uint8)
     with torch.cuda.device(dev):
-        _lib.call("protoseg_l2_fwd", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P,
+        _lib.call("protoseg_l2_fwd_ex", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P,
                   _lib.ptr(w_last), K, float(eps), int(act_kind), int(precision), _lib.ptr(dist), _lib.ptr(act),
-                  _lib.ptr(logits), _lib.stream_of(dev))
-    return dist, logits, act
+                  _lib.ptr(logits), _lib.ptr(ops_buf) if nops else None, nops, _lib.stream_of(dev))
+    return dist, logits, act, ops_buf
 
 
 @l2_forward.register_fake
-def _(x, protos, w_last, eps, act_kind, precision, with_dist, with_logits, with_act):
+def _(x, protos, w_last, eps, act_kind, precision, with_dist, with_logits, with_act, with_operands=False):
     B, C, H, W = x.shape
     P, K = protos.shape[0], w_last.shape[0]
     e = lambda *s: x.new_empty(s, dtype=torch.float32)  # noqa: E731
+    nops = train_operands_bytes(C, P, K, precision) if with_operands else 0
     return (e(B, P, H, W) if with_dist else e(0), e(B, H, W, K) if with_logits else e(0),
-            e(B * H * W, P) if with_act else e(0))
+            e(B * H * W, P) if with_act else e(0), x.new_empty(nops, dtype=torch.uint8))
+
+
+def _operands_args(operands: Optional[Tensor]):
+    """(pointer, bytes) of an operands buffer for the _ex calls; (None, 0) without one."""
+    if operands is None or operands.numel() == 0:
+        return None, 0
+    return _lib.ptr(operands), operands.numel()
 
 
 @torch.library.custom_op("protoseg::l2_backward", mutates_args=(), device_types="cuda")
 def l2_backward(x: Tensor, protos: Tensor, w_last: Tensor, g_logits: Optional[Tensor], g_dist: Optional[Tensor],
                 eps: float, act_kind: int, precision: int, need_x: bool, need_protos: bool,
-                need_w: bool) -> Tuple[Tensor, Tensor, Tensor]:
+                need_w: bool, operands: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor]:
     """Backward of l2_forward with respect to (x, protos, w_last); unrequested grads are empty.
-    With X_SIGMOID in act_kind, g_x is the gradient w.r.t. the pre-activation."""
+    With X_SIGMOID in act_kind, g_x is the gradient w.r.t. the pre-activation. operands: the
+    forward's with_operands output (same protos / w_last values), read instead of a prep launch."""
     dev = _lib.require_device(x, protos, w_last, g_logits, g_dist)
     x = x.contiguous()
     protos = protos.contiguous()
@@ -112,15 +132,17 @@ def l2_backward(x: Tensor, protos: Tensor, w_last: Tensor, g_logits: Optional[Te
     # request, g_x alone included): the size query is host-only, torch's allocator caches the block
     ws_bytes = lib.protoseg_l2_bwd_workspace_size(B, C, H, W, P, K)
     ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8) if ws_bytes else None
+    ops_ptr, ops_bytes = _operands_args(operands)
     with torch.cuda.device(dev):
-        _lib.call("protoseg_l2_bwd", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P, _lib.ptr(w_last),
+        _lib.call("protoseg_l2_bwd_ex", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P, _lib.ptr(w_last),
                   K, float(eps), int(act_kind), int(precision), _lib.ptr(g_logits), _lib.ptr(g_dist),
-                  _lib.ptr(g_x), _lib.ptr(g_p), _lib.ptr(g_w), _lib.ptr(ws), ws_bytes, _lib.stream_of(dev))
+                  _lib.ptr(g_x), _lib.ptr(g_p), _lib.ptr(g_w), _lib.ptr(ws), ws_bytes, ops_ptr, ops_bytes,
+                  _lib.stream_of(dev))
     return g_x, g_p, g_w
 
 
 @l2_backward.register_fake
-def _(x, protos, w_last, g_logits, g_dist, eps, act_kind, precision, need_x, need_protos, need_w):
+def _(x, protos, w_last, g_logits, g_dist, eps, act_kind, precision, need_x, need_protos, need_w, operands=None):
     B, C, H, W = x.shape
     P, K = protos.shape[0], w_last.shape[0]
     need_w = need_w and g_logits is not None
@@ -199,7 +221,8 @@ def expand_compact(deposit, B: int, P: int, HW: int, out: Optional[Tensor] = Non
 @torch.library.custom_op("protoseg::l2_backward_kld", mutates_args=(), device_types="cuda")
 def l2_backward_kld(x: Tensor, protos: Tensor, w_last: Tensor, g_logits: Optional[Tensor], g_cls: Tensor,
                     pix_cls: Tensor, proto_slot: Tensor, max_per_class: int, eps: float, act_kind: int, precision: int,
-                    need_x: bool, need_protos: bool, need_w: bool) -> Tuple[Tensor, Tensor, Tensor]:
+                    need_x: bool, need_protos: bool, need_w: bool,
+                    operands: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor]:
     """l2_backward with the KLD loss's compact distance gradient (protoseg_l2_bwd_kld): the
     kernels expand g_dist in registers instead of reading a dense [B, P, H, W] tensor."""
     dev = _lib.require_device(x, protos, w_last, g_logits, g_cls, pix_cls, proto_slot)
@@ -216,17 +239,18 @@ def l2_backward_kld(x: Tensor, protos: Tensor, w_last: Tensor, g_logits: Optiona
     lib = _lib.load()
     ws_bytes = lib.protoseg_l2_bwd_workspace_size(B, C, H, W, P, K)
     ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
+    ops_ptr, ops_bytes = _operands_args(operands)
     with torch.cuda.device(dev):
-        _lib.call("protoseg_l2_bwd_kld", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P,
+        _lib.call("protoseg_l2_bwd_kld_ex", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P,
                   _lib.ptr(w_last), K, float(eps), int(act_kind), int(precision), _lib.ptr(g_logits),
                   _lib.ptr(g_cls), _lib.ptr(pix_cls), _lib.ptr(proto_slot), int(max_per_class), _lib.ptr(g_x),
-                  _lib.ptr(g_p), _lib.ptr(g_w), _lib.ptr(ws), ws_bytes, _lib.stream_of(dev))
+                  _lib.ptr(g_p), _lib.ptr(g_w), _lib.ptr(ws), ws_bytes, ops_ptr, ops_bytes, _lib.stream_of(dev))
     return g_x, g_p, g_w
 
 
 @l2_backward_kld.register_fake
 def _(x, protos, w_last, g_logits, g_cls, pix_cls, proto_slot, max_per_class, eps, act_kind, precision, need_x,
-      need_protos, need_w):
+      need_protos, need_w, operands=None):
     B, C, H, W = x.shape
     P, K = protos.shape[0], w_last.shape[0]
     need_w = need_w and g_logits is not None
@@ -236,8 +260,9 @@ def _(x, protos, w_last, g_logits, g_cls, pix_cls, proto_slot, max_per_class, ep
 
 
 def _setup_context(ctx, inputs, output):
-    x, protos, w_last, eps, act_kind, precision, with_dist, with_logits, with_act = inputs
-    ctx.save_for_backward(x, protos, w_last)
+    x, protos, w_last, eps, act_kind, precision, with_dist, with_logits, with_act = inputs[:9]
+    ctx.save_for_backward(x, protos, w_last)  # (its version check also guards the operands below)
+    ctx.operands = output[3] if output[3].numel() else None
     ctx.eps = eps
     ctx.act_kind = act_kind
     ctx.precision = precision
@@ -266,7 +291,7 @@ def _act_grad_as_dist_grad(x, protos, w_last, g_act, eps, act_kind, precision):
     return ga * ((eps - 1.0) / ((d + 1.0) * (d + eps)))
 
 
-def _backward(ctx, g_dist, g_logits, g_act):
+def _backward(ctx, g_dist, g_logits, g_act, g_operands=None):
     x, protos, w_last = ctx.saved_tensors
     need_x, need_p, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
     sink = ctx.sink
@@ -284,16 +309,18 @@ def _backward(ctx, g_dist, g_logits, g_act):
             dense = expand_compact(dep, B, P, H * W, dense)
         g_dist, compact = dense.reshape(B, P, H, W), []
     if g_dist is None and g_logits is None and not compact:
-        return None, None, None, None, None, None, None, None, None
+        return None, None, None, None, None, None, None, None, None, None
+    ops_buf = ctx.operands
     if compact:
         g_cls, pix_cls, proto_slot, mpc = compact[0]
         g_x, g_p, g_w = l2_backward_kld(x, protos, w_last, g_logits, g_cls, pix_cls, proto_slot, mpc, ctx.eps,
-                                        ctx.act_kind, ctx.precision, need_x, need_p, need_w and g_logits is not None)
+                                        ctx.act_kind, ctx.precision, need_x, need_p, need_w and g_logits is not None,
+                                        ops_buf)
     else:
         g_x, g_p, g_w = l2_backward(x, protos, w_last, g_logits, g_dist, ctx.eps, ctx.act_kind, ctx.precision, need_x,
-                                    need_p, need_w and g_logits is not None)
+                                    need_p, need_w and g_logits is not None, ops_buf)
     return (g_x if need_x else None, g_p if need_p else None, g_w if (need_w and g_w.numel()) else None,
-            None, None, None, None, None, None)
+            None, None, None, None, None, None, None)
 
 
 torch.library.register_autograd("protoseg::l2_forward", _backward, setup_context=_setup_context)
@@ -332,8 +359,13 @@ def prototype_layer(x: Tensor, prototype_vectors: Tensor, last_layer_weight: Ten
             act_kind |= _lib.X_SIGMOID
         else:
             x = torch.sigmoid(x)
-    return torch.ops.protoseg.l2_forward(x, protos, last_layer_weight, float(eps), act_kind,
-                                         precision_code(precision), with_dist, with_logits, with_act)
+    prec = precision_code(precision)
+    # a training forward builds the backward's operand images in its own prep launch (one prep
+    # per step; the saved-tensor version check keeps them tied to these protos / weights)
+    trains = (torch.is_grad_enabled() and x.is_cuda and x.requires_grad
+              and (protos.requires_grad or last_layer_weight.requires_grad))
+    return torch.ops.protoseg.l2_forward(x, protos, last_layer_weight, float(eps), act_kind, prec, with_dist,
+                                         with_logits, with_act, trains)[:3]
 
 
 def l2_distances(x: Tensor, prototype_vectors: Tensor, eps: float = 1e-4, precision: Optional[str] = None) -> Tensor:

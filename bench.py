@@ -99,14 +99,25 @@ class LayerStep:
         # every group but the prototype vectors'; one group here keeps one launch, same cost)
         self.opt = Adam(self.params, lr=2.5e-4, weight_decay=5e-4)
         self.buckets = None
+        # one operand prep per step: the forward's prep launch also writes the backward's
+        # operand images (protoseg_l2_fwd_ex), as the autograd op does in training
+        # (PROTOSEG_FWD_OPERANDS=0: the backward prepares its own, for A/B)
+        nops = lib.protoseg_l2_train_operands_bytes(C, P, K, self.prec)
+        if os.environ.get("PROTOSEG_FWD_OPERANDS", "1") == "0":
+            nops = 0
+        self.ops_bytes = nops
+        self.ops = torch.empty(max(nops, 1), device=device, dtype=torch.uint8)
 
     def _stream(self):
         return _lib.stream_of(self.device)
 
+    def _ops(self):
+        return (_lib.ptr(self.ops) if self.ops_bytes else ctypes.c_void_p(None)), self.ops_bytes
+
     def fwd(self):
-        _lib.call("protoseg_l2_fwd", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w, _lib.ptr(self.protos),
-                  self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec, _lib.ptr(self.dist), ctypes.c_void_p(None),
-                  _lib.ptr(self.logits), self._stream())
+        _lib.call("protoseg_l2_fwd_ex", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w,
+                  _lib.ptr(self.protos), self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec,
+                  _lib.ptr(self.dist), ctypes.c_void_p(None), _lib.ptr(self.logits), *self._ops(), self._stream())
 
     def bwd_x(self):
         _lib.call("protoseg_l2_bwd", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w, _lib.ptr(self.protos),
@@ -122,11 +133,11 @@ class LayerStep:
 
     def bwd(self):
         """One backward call for g_x, g_prototypes and g_last_layer, as the autograd op makes it
-        (ops.l2_backward): one operand-image prep shared by the two backward kernels."""
-        _lib.call("protoseg_l2_bwd", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w, _lib.ptr(self.protos),
-                  self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec, _lib.ptr(self.g_logits),
-                  ctypes.c_void_p(None), _lib.ptr(self.g_x), _lib.ptr(self.g_p), _lib.ptr(self.g_w),
-                  _lib.ptr(self.ws), self.ws_bytes, self._stream())
+        (ops.l2_backward), reading the operand images the forward's prep wrote."""
+        _lib.call("protoseg_l2_bwd_ex", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w,
+                  _lib.ptr(self.protos), self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec,
+                  _lib.ptr(self.g_logits), ctypes.c_void_p(None), _lib.ptr(self.g_x), _lib.ptr(self.g_p),
+                  _lib.ptr(self.g_w), _lib.ptr(self.ws), self.ws_bytes, *self._ops(), self._stream())
 
     # ---- KLD training step (BASELINE configs[2], cityscapes_kld_imnet: loss_weight_kld = 0.25) ----
     def setup_kld(self, seed, weight=0.25):
@@ -167,18 +178,18 @@ class LayerStep:
 
     def bwd_kld(self):
         """Backward with the compact KLD gradient expanded in the kernels (protoseg_l2_bwd_kld)."""
-        _lib.call("protoseg_l2_bwd_kld", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w,
+        _lib.call("protoseg_l2_bwd_kld_ex", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w,
                   _lib.ptr(self.protos), self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec,
                   _lib.ptr(self.g_logits), _lib.ptr(self.g_cls), _lib.ptr(self.pix_cls), _lib.ptr(self.proto_slot),
                   self.mpc, _lib.ptr(self.g_x), _lib.ptr(self.g_p), _lib.ptr(self.g_w), _lib.ptr(self.ws),
-                  self.ws_bytes, self._stream())
+                  self.ws_bytes, *self._ops(), self._stream())
 
     def bwd_gd(self):
         """Backward with the KLD distance gradient (protoseg_l2_bwd g_dist)."""
-        _lib.call("protoseg_l2_bwd", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w, _lib.ptr(self.protos),
-                  self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec, _lib.ptr(self.g_logits),
-                  _lib.ptr(self.g_dist), _lib.ptr(self.g_x), _lib.ptr(self.g_p), _lib.ptr(self.g_w),
-                  _lib.ptr(self.ws), self.ws_bytes, self._stream())
+        _lib.call("protoseg_l2_bwd_ex", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w,
+                  _lib.ptr(self.protos), self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec,
+                  _lib.ptr(self.g_logits), _lib.ptr(self.g_dist), _lib.ptr(self.g_x), _lib.ptr(self.g_p),
+                  _lib.ptr(self.g_w), _lib.ptr(self.ws), self.ws_bytes, *self._ops(), self._stream())
 
     def opt_step(self):
         self.opt.step()
@@ -407,13 +418,13 @@ def time_sigmoid_step(step: LayerStep, steps: int, warmup: int):
     act_f = _lib.ACT_LOG | _lib.X_SIGMOID
 
     def common(x, act, gx):
-        _lib.call("protoseg_l2_fwd", _lib.ptr(x), step.xdt, step.B, step.C, step.h, step.w, _lib.ptr(step.protos),
-                  step.P, _lib.ptr(step.w_last), step.K, 1e-4, act, step.prec, _lib.ptr(step.dist), null,
-                  _lib.ptr(step.logits), step._stream())
-        _lib.call("protoseg_l2_bwd", _lib.ptr(x), step.xdt, step.B, step.C, step.h, step.w, _lib.ptr(step.protos),
-                  step.P, _lib.ptr(step.w_last), step.K, 1e-4, act, step.prec, _lib.ptr(step.g_logits), null,
-                  _lib.ptr(gx), _lib.ptr(step.g_p), _lib.ptr(step.g_w), _lib.ptr(step.ws), step.ws_bytes,
-                  step._stream())
+        _lib.call("protoseg_l2_fwd_ex", _lib.ptr(x), step.xdt, step.B, step.C, step.h, step.w,
+                  _lib.ptr(step.protos), step.P, _lib.ptr(step.w_last), step.K, 1e-4, act, step.prec,
+                  _lib.ptr(step.dist), null, _lib.ptr(step.logits), *step._ops(), step._stream())
+        _lib.call("protoseg_l2_bwd_ex", _lib.ptr(x), step.xdt, step.B, step.C, step.h, step.w,
+                  _lib.ptr(step.protos), step.P, _lib.ptr(step.w_last), step.K, 1e-4, act, step.prec,
+                  _lib.ptr(step.g_logits), null, _lib.ptr(gx), _lib.ptr(step.g_p), _lib.ptr(step.g_w),
+                  _lib.ptr(step.ws), step.ws_bytes, *step._ops(), step._stream())
         step.opt_step()
 
     def fused():

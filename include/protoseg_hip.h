@@ -154,6 +154,43 @@ int protoseg_l2_bwd_kld(const void* x, int x_dtype, int B, int C, int H, int W,
 int protoseg_l2_bwd_kld_supported(int B, int C, int H, int W, int P, int K, int x_dtype, int precision,
                                   int max_per_class);
 
+/*
+ * One operand prep per training step: the forward builds the backward's operand images (the
+ * split P / W^T images and ||p||^2 in the backward kernel's layout) in the same prep launch as its
+ * own, into a caller buffer the backward then reads instead of preparing them again.
+ *   protoseg_l2_train_operands_bytes: the buffer size for (C, P, K, precision); 0 when the
+ *     backward would not read one (it chunks prototypes, another family, not BF16X3): the _ex
+ *     calls then ignore `operands` and behave as the plain calls.
+ *   protoseg_l2_fwd_ex: protoseg_l2_fwd + fills `operands` (w_last non-NULL when K > 0; every
+ *     output may be NULL to fill the operands only).
+ *   protoseg_l2_bwd_ex / protoseg_l2_bwd_kld_ex: protoseg_l2_bwd / _kld reading `operands`
+ *     (NULL: prepared inside the call). The caller guarantees that protos, w_last, P, K, C, eps,
+ *     act_kind (X_SIGMOID aside) and precision are those of the forward that filled it, that its
+ *     values are unchanged since, and that PROTOSEG_BWD (the kernel override) did not change.
+ * Results are bit-identical to the plain calls (the same prep arithmetic, tests/test_gpu_operands.py).
+ */
+size_t protoseg_l2_train_operands_bytes(int C, int P, int K, int precision);
+int protoseg_l2_fwd_ex(const void* x, int x_dtype, int B, int C, int H, int W,
+                       const float* protos, int P, const float* w_last, int K,
+                       float eps, int act_kind, int precision,
+                       float* dist_out, float* act_out, float* logits_out,
+                       void* operands, size_t operands_bytes, protoseg_stream_t stream);
+int protoseg_l2_bwd_ex(const void* x, int x_dtype, int B, int C, int H, int W,
+                       const float* protos, int P, const float* w_last, int K,
+                       float eps, int act_kind, int precision,
+                       const float* g_logits, const float* g_dist,
+                       void* g_x, float* g_protos, float* g_w,
+                       void* workspace, size_t workspace_bytes,
+                       const void* operands, size_t operands_bytes, protoseg_stream_t stream);
+int protoseg_l2_bwd_kld_ex(const void* x, int x_dtype, int B, int C, int H, int W,
+                           const float* protos, int P, const float* w_last, int K,
+                           float eps, int act_kind, int precision,
+                           const float* g_logits, const float* g_cls, const int32_t* pix_cls,
+                           const int32_t* proto_slot, int max_per_class,
+                           void* g_x, float* g_protos, float* g_w,
+                           void* workspace, size_t workspace_bytes,
+                           const void* operands, size_t operands_bytes, protoseg_stream_t stream);
+
 
 /* 1 if (C, P, K) is inside the compiled kernel family, else 0. */
 int protoseg_l2_supported(int C, int P, int K);

@@ -1,0 +1,125 @@
+"""One operand prep per training step (protoseg_l2_fwd_ex / protoseg_l2_bwd_ex / _kld_ex): the
+forward's prep launch also writes the training backward's operand images (the one-pass block for
+P in (192, 384], the fused kernel's images for P <= 192) into a caller buffer, and the backward
+reads them instead of preparing its own. Same prep arithmetic, so every output is bit-identical
+to the plain calls; the autograd path (prototype_layer) passes the buffer through ctx."""
+import pytest
+import torch
+
+from oracle import protoseg_oracle as po
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    from protoseg_amd import _lib, ops
+    return _lib, ops
+
+
+def _inputs(device, B, h, w, P, K, seed):
+    x, protos, w_last = po.synthetic_inputs(B, 64, h, w, P, K, seed=seed)
+    gen = torch.Generator().manual_seed(seed + 1)
+    w_last = w_last + 0.05 * torch.randn(w_last.shape, generator=gen)
+    g_logits = torch.randn(B, h, w, K, generator=gen)
+    g_dist = 0.01 * torch.randn(B, P, h, w, generator=gen)
+    return [t.to(device) for t in (x, protos, w_last, g_logits, g_dist)]
+
+
+@pytest.mark.parametrize("P,K,bwd,kind", [
+    (361, 19, None, "onepass"),      # the metric's 19 prototypes/class
+    (190, 19, None, "fused"),        # 10 prototypes/class
+    (96, 32, None, "fused"),
+    (190, 19, "onepass", "onepass"),  # PROTOSEG_BWD override: the one-pass block at Pp 256
+    (570, 19, None, "none"),         # two prototype chunks: no operands, plain calls
+])
+@pytest.mark.parametrize("activation", ["log", "linear"])
+def test_fwd_bwd_with_operands_bit_identical(device, monkeypatch, P, K, bwd, kind, activation):
+    _lib, ops = _ops()
+    if bwd:
+        monkeypatch.setenv("PROTOSEG_BWD", bwd)
+    B, h, w = 2, 33, 31
+    x, protos, w_last, g_logits, g_dist = _inputs(device, B, h, w, P, K, seed=P + K)
+    act, prec = ops.ACT_KINDS[activation], ops.PRECISIONS["bf16x3"]
+    nbytes = ops.train_operands_bytes(64, P, K, prec)
+    assert (nbytes > 0) == (kind != "none")
+    d0, l0, a0, o0 = ops.l2_forward(x, protos, w_last, 1e-4, act, prec, True, True, True)
+    d1, l1, a1, o1 = ops.l2_forward(x, protos, w_last, 1e-4, act, prec, True, True, True, True)
+    assert o0.numel() == 0 and o1.numel() == nbytes
+    for a, b in ((d0, d1), (l0, l1), (a0, a1)):
+        assert torch.equal(a, b)
+    ref = ops.l2_backward(x, protos, w_last, g_logits, g_dist, 1e-4, act, prec, True, True, True)
+    got = ops.l2_backward(x, protos, w_last, g_logits, g_dist, 1e-4, act, prec, True, True, True, o1)
+    torch.cuda.synchronize()
+    for name, a, b in zip(("g_x", "g_protos", "g_w"), ref, got):
+        assert torch.equal(a, b), name
+
+
+def test_operands_only_forward_and_x_sigmoid(device):
+    """Every output NULL fills the operands only; the X_SIGMOID backward reads them too."""
+    _lib, ops = _ops()
+    B, h, w, P, K = 1, 29, 37, 361, 19
+    x, protos, w_last, g_logits, _ = _inputs(device, B, h, w, P, K, seed=5)
+    prec = ops.PRECISIONS["bf16x3"]
+    act = _lib.ACT_LOG | _lib.X_SIGMOID
+    _, _, _, ob = ops.l2_forward(x, protos, w_last, 1e-4, act, prec, False, False, False, True)
+    assert ob.numel() == ops.train_operands_bytes(64, P, K, prec)
+    ref = ops.l2_backward(x, protos, w_last, g_logits, None, 1e-4, act, prec, True, True, True)
+    got = ops.l2_backward(x, protos, w_last, g_logits, None, 1e-4, act, prec, True, True, True, ob)
+    torch.cuda.synchronize()
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+
+
+def test_kld_backward_reads_operands(device):
+    _lib, ops = _ops()
+    B, h, w, P, K, mpc = 2, 17, 19, 361, 19, 19
+    x, protos, w_last, g_logits, _ = _inputs(device, B, h, w, P, K, seed=9)
+    prec = ops.PRECISIONS["bf16x3"]
+    gen = torch.Generator().manual_seed(4)
+    npix = B * h * w
+    g_cls = torch.randn(npix, mpc, generator=gen).to(device)
+    pix_cls = torch.randint(-1, K, (npix,), generator=gen, dtype=torch.int32).to(device)
+    proto_slot = torch.tensor([(p // mpc) * 256 + p % mpc for p in range(P)], dtype=torch.int32, device=device)
+    _, _, _, ob = ops.l2_forward(x, protos, w_last, 1e-4, 0, prec, True, True, False, True)
+    ref = ops.l2_backward_kld(x, protos, w_last, g_logits, g_cls, pix_cls, proto_slot, mpc, 1e-4, 0, prec,
+                              True, True, True)
+    got = ops.l2_backward_kld(x, protos, w_last, g_logits, g_cls, pix_cls, proto_slot, mpc, 1e-4, 0, prec,
+                              True, True, True, ob)
+    torch.cuda.synchronize()
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+
+
+def test_short_operands_buffer_fails_loudly(device):
+    _lib, ops = _ops()
+    x, protos, w_last, g_logits, _ = _inputs(device, 1, 9, 9, 361, 19, seed=2)
+    prec = ops.PRECISIONS["bf16x3"]
+    n = ops.train_operands_bytes(64, 361, 19, prec)
+    short = torch.empty(n - 256, device=device, dtype=torch.uint8)
+    d = torch.empty(1, 361, 9, 9, device=device)
+    with pytest.raises(_lib.ProtosegError, match="operands"):
+        _lib.call("protoseg_l2_fwd_ex", _lib.ptr(x), _lib.F32, 1, 64, 9, 9, _lib.ptr(protos), 361, _lib.ptr(w_last),
+                  19, 1e-4, 0, prec, _lib.ptr(d), None, None, _lib.ptr(short), short.numel(), _lib.stream_of(device))
+
+
+@pytest.mark.parametrize("P", [190, 361])
+def test_autograd_layer_uses_forward_operands(device, P):
+    """prototype_layer in a training graph: gradients equal l2_backward's without operands."""
+    _lib, ops = _ops()
+    B, h, w, K = 2, 21, 23, 19
+    x, protos, w_last, g_logits, g_dist = _inputs(device, B, h, w, P, K, seed=P)
+    xr, pr, wr = (t.clone().requires_grad_(True) for t in (x, protos, w_last))
+    dist, logits, _ = ops.prototype_layer(xr, pr[:, :, None, None], wr)
+    (logits * g_logits).sum().backward(retain_graph=True)
+    ref = ops.l2_backward(x, protos, w_last, g_logits, None, 1e-4, 0, ops.PRECISIONS["bf16x3"], True, True, True)
+    torch.cuda.synchronize()
+    assert torch.equal(xr.grad, ref[0]) and torch.equal(pr.grad.reshape(P, 64), ref[1])
+    assert torch.equal(wr.grad, ref[2])
+    # a second backward over the retained graph reads the same operands again
+    for t in (xr, pr, wr):
+        t.grad = None
+    ((logits * g_logits).sum() + (dist * g_dist).sum()).backward()
+    ref2 = ops.l2_backward(x, protos, w_last, g_logits, g_dist, 1e-4, 0, ops.PRECISIONS["bf16x3"], True, True, True)
+    torch.cuda.synchronize()
+    assert torch.equal(xr.grad, ref2[0]) and torch.equal(pr.grad.reshape(P, 64), ref2[1])
+    assert torch.equal(wr.grad, ref2[2])

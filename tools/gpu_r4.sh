@@ -18,6 +18,14 @@ for step in "$@"; do
         tests/test_gpu_headline_parity.py tests/test_gpu_kld_compact.py tests/test_checkpoint.py tests/test_gpu_dp_capture.py \
         > gpurun_out/${T}_tests_new.log 2>&1 || { tail -60 gpurun_out/${T}_tests_new.log; exit 1; }
       tail -30 gpurun_out/${T}_tests_new.log ;;
+    ptest)  # PT_FILES="tests/a.py tests/b.py"
+      timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu ${PT_FILES} \
+        > gpurun_out/${T}_ptest.log 2>&1 || { tail -60 gpurun_out/${T}_ptest.log; exit 1; }
+      tail -3 gpurun_out/${T}_ptest.log ;;
+    quick-noops)
+      PROTOSEG_FWD_OPERANDS=0 timeout -k 10 300 python -u bench.py --no-kld --no-push --no-knn --no-eval --no-train --no-sigmoid --no-cpu-baseline --no-wide \
+        > gpurun_out/${T}_quick_noops.log 2>&1 || { tail -30 gpurun_out/${T}_quick_noops.log; exit 1; }
+      python3 tools/bench_summary.py gpurun_out/${T}_quick_noops.log ;;
     diag)
       timeout -k 10 300 python -u tools/debug/kld_compact_diag.py > gpurun_out/${T}_diag.log 2>&1; tail -30 gpurun_out/${T}_diag.log ;;
     smoke)
