@@ -84,12 +84,11 @@ __global__ __launch_bounds__(kAdamBlock) void adam_kernel(AdamTensors ts, float 
       p[i] = pi[r] - step_size * mr / (sqrtf(vr) / bc2_sqrt + eps);
     }
   }
-  // Step count: the last workgroup to arrive publishes t (all reads of state[0] are done by then).
+  // Step count: the last workgroup to arrive publishes t (all reads of state[0] are done by then:
+  // each workgroup's read returned before its ticket, so no fence is needed — a device-scope
+  // release here wrote back the XCD's L2 once per workgroup, ~30 ns each, serialised).
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(state + 1, 1) == nblk - 1;
-  }
+  if (threadIdx.x == 0) last = atomicAdd(state + 1, 1) == nblk - 1;
   __syncthreads();
   if (last && threadIdx.x == 0) {
     atomicExch(state, t);

@@ -35,7 +35,10 @@ namespace {
 constexpr int kKldMaxPerClass = 32;  // prototypes of one class held per workgroup
 constexpr int kKldMaxClasses = 63;   // K + 1 buckets handled by one wave
 constexpr int kKldThreads = 256;     // = pixels per staged chunk
-constexpr int kKldRange = 1024;      // pixels per kld_partial_kernel workgroup
+#ifndef KLD_RANGE
+#define KLD_RANGE 1024
+#endif
+constexpr int kKldRange = KLD_RANGE;  // pixels per kld_partial_kernel workgroup (a multiple of 256)
 constexpr int kKldPair = kKldMaxPerClass * kKldMaxPerClass;
 constexpr int kKldLdsStride = kKldThreads + 1;  // padded rows: conflict-free task reads
 constexpr size_t kKldMaxDynLds = 2 * kKldMaxPerClass * kKldLdsStride * sizeof(float);

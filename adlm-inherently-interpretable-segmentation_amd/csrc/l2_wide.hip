@@ -20,6 +20,7 @@
 #include "l2_launch.h"
 
 #include <map>
+#include <type_traits>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -28,25 +29,28 @@ namespace protoseg {
 
 namespace {
 
-constexpr int kWT = 64;    // workgroup output tile (rows and columns)
-constexpr int kWKs = 16;   // contraction per LDS stage
+constexpr int kWT = 64;        // workgroup output tile (rows and columns)
+constexpr int kWKs = 32;       // contraction per LDS stage
 constexpr int kWThreads = 256;
-constexpr int kWLd = kWT + 4;  // LDS row pitch (floats)
+constexpr int kWLd = kWT + 1;  // LDS row pitch (floats), odd: a k-fast store (32 k rows of one column) hits 32 banks
 
 enum WideEpi { kEpiStore = 0, kEpiDist = 1, kEpiGs = 2, kEpiGx = 3 };
 
 // Element (r, k) of batch b at p[b * sb + r * sr + k * sk]; r is the output row (A) or column (B).
+// Every operand of the layer's GEMMs is a row- or column-major view of an NCHW / [P, C] / [K, P]
+// tensor, so sr == 1 ("rows fast") or sk == 1 ("k fast"); element offsets are below 2^31
+// (wide_family_fits), so addresses are 32-bit offsets from the operand's base.
 struct Operand {
   const void* p;
-  long long sr, sk, sb;
+  unsigned sr, sk, sb;
 };
 
 struct WideArgs {
   Operand A, B;
   int M, N, Kd, nb;  // per-batch contraction Kd; nb batches
-  int bk;            // 1: the contraction runs over (batch, k) and splits over blockIdx.z; 0: one output per batch
-  int ksplit;        // bk: workgroups along the contraction
-  void* out;         // element (m, n) of batch (or split) z at out[z * ob + m * om + n * on]
+  int bk;            // 1: the contraction runs over (batch, k) flattened, split over blockIdx.z
+  int ksplit;        // workgroups along the contraction (bk: z = split; else z = b * ksplit + split)
+  void* out;         // element (m, n) of output slab z at out[z * ob + m * om + n * on]
   long long om, on, ob;
   int accumulate;
   float eps;
@@ -70,45 +74,98 @@ __device__ __forceinline__ float on_load(float v, float eps) {
   else return activation(v, eps, ACT);
 }
 
-// Stages rows [r0, r0 + 64) x contraction [k0, k0 + 16) of an operand into registers: four
-// elements per thread, the thread map coalesced along whichever index has stride 1.
-template <typename T, int ACT>
-__device__ __forceinline__ void load_tile(const Operand& o, int R, int Kd, int r0, int k0, int b, int bk, float eps,
-                                          float (&v)[4], int (&lr)[4], int (&lk)[4]) {
-  const int t = threadIdx.x;
-  const bool rows_fast = o.sr == 1;
+// One operand's share of a 64-row x 32-k stage: eight elements per thread.
+//   MODE 0 (rows fast): row t & 63, k = (t >> 6) + 4i — 64 consecutive rows per k, coalesced;
+//   MODE 1 (k fast):    k = t & 31, row (t >> 5) + 8i — 32 consecutive k per row, coalesced.
+// The element's row (and, MODE 0, k) offset is fixed for the whole contraction; the stage moves
+// a uniform base (non-bk) or, for a k-fast operand over the flattened (batch, pixel) contraction,
+// one per-thread (batch, k) position advanced by 32 per stage (no division in the loop).
+template <typename T, int ACT, int MODE>
+struct Stager {
+  const T* p;
+  unsigned fix[8];
+  unsigned rok;  // bit i: element i's row is inside the operand
+  int kt;        // MODE 1: this thread's k in the stage
+  int bb, kin;   // MODE 1, bk: batch and in-batch k of this thread's current contraction index
+  unsigned sb;
+
+  __device__ __forceinline__ void init(const Operand& o, int R, int r0, int kbeg, int Kd, int bk) {
+    p = static_cast<const T*>(o.p);
+    const int t = threadIdx.x;
+    rok = 0;
+    sb = o.sb;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = rows_fast ? (t & 63) : (t >> 4) + 16 * i;
-    const int k = rows_fast ? (t >> 6) + 4 * i : (t & 15);
-    lr[i] = r;
-    lk[i] = k;
-    const int rr = r0 + r;
-    int kk = k0 + k, bb = b;
-    bool ok = rr < R;
-    if (bk) {  // flattened (batch, k) contraction
-      bb = kk / Kd;
-      kk -= bb * Kd;
-      ok = ok && bb < b;  // b = the batch count here
-    } else {
-      ok = ok && kk < Kd;
+    for (int i = 0; i < 8; ++i) {
+      const int r = MODE == 0 ? (t & 63) : (t >> 5) + 8 * i;
+      const int k = MODE == 0 ? (t >> 6) + 4 * i : (t & 31);
+      const bool ok = r0 + r < R;
+      rok |= ok ? (1u << i) : 0u;
+      fix[i] = ok ? (MODE == 0 ? static_cast<unsigned>(r0 + r) + static_cast<unsigned>(k) * o.sk
+                               : static_cast<unsigned>(r0 + r) * o.sr)
+                  : 0u;
     }
-    float x = 0.f;
-    if (ok) x = on_load<ACT>(load_elem<T>(o.p, bb * o.sb + rr * o.sr + kk * o.sk), eps);
-    v[i] = x;
+    kt = t & 31;
+    if (MODE == 1 && bk) {
+      const int kk = kbeg + kt;  // flattened index of this thread's first element
+      bb = kk / Kd;
+      kin = kk - bb * Kd;
+    }
   }
+  // Stage at contraction base kb (flattened for bk); lim = kend - kb; base = the stage's uniform
+  // offset. Raw values: the zeroing of elements outside the operand (okm) and the activation
+  // happen in store(), after the MFMAs the loads are in flight under.
+  __device__ __forceinline__ void load(unsigned base, int lim, int bk, float (&v)[8], unsigned& okm) const {
+    const unsigned kofs = MODE == 1 ? (bk ? static_cast<unsigned>(bb) * sb + static_cast<unsigned>(kin)
+                                          : static_cast<unsigned>(kt))
+                                    : 0u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int k = MODE == 0 ? (static_cast<int>(threadIdx.x) >> 6) + 4 * i : kt;
+      const bool ok = ((rok >> i) & 1u) && k < lim;
+      if (i == 0) okm = 0;
+      okm |= ok ? (1u << i) : 0u;
+      // branch-free: an element outside the operand loads element 0 (zeroed in store())
+      v[i] = XIO<T>::load(p, static_cast<size_t>(ok ? base + fix[i] + kofs : 0u));
+    }
+  }
+  __device__ __forceinline__ void advance(int Kd) {  // MODE 1, bk: the next stage's (batch, k)
+    kin += kWKs;
+    while (kin >= Kd) {
+      kin -= Kd;
+      ++bb;
+    }
+  }
+  __device__ __forceinline__ void store(float (*S)[kWLd], const float (&v)[8], unsigned okm, float eps) const {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float x = ((okm >> i) & 1u) ? on_load<ACT>(v[i], eps) : 0.f;
+      if (MODE == 0) S[(t >> 6) + 4 * i][t & 63] = x;
+      else S[t & 31][(t >> 5) + 8 * i] = x;
+    }
+  }
+};
+
+// Uniform offset of a stage at contraction base kb: batch b (non-bk) or flattened (bk, MODE 0:
+// affine, sb == Kd * sk); MODE 1 bk carries its position per thread.
+template <int MODE>
+__device__ __forceinline__ unsigned stage_base(const Operand& o, int b, int kb, int bk) {
+  if (bk) return MODE == 0 ? static_cast<unsigned>(kb) * o.sk : 0u;
+  return static_cast<unsigned>(b) * o.sb + static_cast<unsigned>(kb) * (MODE == 0 ? o.sk : 1u);
 }
 
-// The epilogues' per-column / per-row sums, taken from the LDS stages the GEMM stages anyway
-// (each workgroup contracts over the whole Kd of its batch, so it holds them for its own rows and
-// columns): kEpiDist: x2[n] = sum_c X[c][n]^2 (B columns) and p2[m] = sum_c P[m][c]^2 (A rows);
-// kEpiGx: cs[n] = sum_p G_s[p][n] (B columns). Thread t sums column t & 63 of stage rows
-// 4 (t >> 6) .. + 3; the four partials are added in a fixed order at the end: deterministic, and
-// the same bits in every workgroup of a column (same data, same order). No separate norms pass.
-template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO>
-__global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
-  __shared__ float As[kWKs][kWLd];
-  __shared__ float Bs[kWKs][kWLd];
+// C[z] (64 x 64 tile) = A (M x Kd) B^T (N x Kd) over 32-k stages, double-buffered in LDS (one
+// barrier per stage, the next stage's global loads in flight under this stage's 16 MFMAs per
+// wave), v_mfma_f32_32x32x2_f32: exact f32 fma chains in k order.
+// The epilogues' per-column / per-row sums come from the same LDS stages (a non-split workgroup
+// contracts over the whole Kd of its batch): kEpiDist: x2[n] = sum_c X[c][n]^2 (B columns) and
+// p2[m] = sum_c P[m][c]^2 (A rows); kEpiGx: cs[n] = sum_p G_s[p][n] (B columns). Thread t sums
+// column t & 63 of stage rows 8 (t >> 6) .. + 7; the four partials are added in a fixed order:
+// deterministic, the same bits in every workgroup of a column, and no separate norms pass.
+template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO, int MA, int MB>
+__global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(4))) void wide_gemm_kernel(WideArgs a) {
+  __shared__ float As[2][kWKs][kWLd];
+  __shared__ float Bs[2][kWKs][kWLd];
   constexpr bool kSumB = EPI == kEpiDist || EPI == kEpiGx, kSumA = EPI == kEpiDist, kSq = EPI == kEpiDist;
   __shared__ float red[kSumB ? 2 : 1][4][64];
   float sum_b = 0.f, sum_a = 0.f;
@@ -116,49 +173,65 @@ __global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
   const int j = lane & 31, h = lane >> 5;
   const int wm = wave & 1, wn = wave >> 1;
   const int m0 = blockIdx.y * kWT, n0 = blockIdx.x * kWT, z = blockIdx.z;
-  // contraction range of this workgroup, in flattened (batch, k) units for bk
-  long long kbeg = 0, kend = a.Kd;
-  int bsel = z;
-  if (a.bk) {
-    const long long total = static_cast<long long>(a.nb) * a.Kd;
-    const long long chunks = (total + kWKs - 1) / kWKs;
-    kbeg = (chunks * z / a.ksplit) * kWKs;
-    kend = (chunks * (z + 1) / a.ksplit) * kWKs;
-    if (kend > total) kend = total;
-    bsel = a.nb;  // load_tile's batch bound
-  }
+  // contraction range of this workgroup (flattened (batch, k) units for bk), whole stages
+  const int split = a.bk ? z : z % a.ksplit, bsel = a.bk ? 0 : z / a.ksplit;
+  const long long total = a.bk ? static_cast<long long>(a.nb) * a.Kd : a.Kd;
+  const long long chunks = (total + kWKs - 1) / kWKs;
+  const int kbeg = static_cast<int>((chunks * split / a.ksplit) * kWKs);
+  int kend = static_cast<int>((chunks * (split + 1) / a.ksplit) * kWKs);
+  if (kend > total) kend = static_cast<int>(total);
+  Stager<TA, AACT, MA> sa;
+  Stager<TB, BACT, MB> sb;
+  sa.init(a.A, a.M, m0, kbeg, a.Kd, a.bk);
+  sb.init(a.B, a.N, n0, kbeg, a.Kd, a.bk);
   f32x16 acc = zero16();
-  float va[4], vb[4];
-  int ra[4], ka[4], rb[4], kb[4];
-  auto fetch = [&](long long k0) {
-    load_tile<TA, AACT>(a.A, a.M, a.Kd, m0, static_cast<int>(k0), bsel, a.bk, a.eps, va, ra, ka);
-    load_tile<TB, BACT>(a.B, a.N, a.Kd, n0, static_cast<int>(k0), bsel, a.bk, a.eps, vb, rb, kb);
-  };
-  if (kbeg < kend) fetch(kbeg);
-  for (long long k0 = kbeg; k0 < kend; k0 += kWKs) {
-    __syncthreads();  // the previous stage's MFMA reads are done
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      As[ka[i]][ra[i]] = va[i];
-      Bs[kb[i]][rb[i]] = vb[i];
+  // two stages of loads in flight: register slot s & 1 holds stage s until it is stored to LDS
+  float va[2][8], vb[2][8];
+  unsigned oka[2] = {0, 0}, okb[2] = {0, 0};
+  const int nst = kend > kbeg ? (kend - kbeg + kWKs - 1) / kWKs : 0;
+  auto issue = [&](int stg, float (&ra)[8], float (&rb)[8], unsigned& ka, unsigned& kb_) {
+    const int kb = kbeg + stg * kWKs;
+    if (stg > 0) {  // stages are issued in order: the k-fast bk positions advance one stage
+      if (MA == 1 && a.bk) sa.advance(a.Kd);
+      if (MB == 1 && a.bk) sb.advance(a.Kd);
     }
+    sa.load(stage_base<MA>(a.A, bsel, kb, a.bk), kend - kb, a.bk, ra, ka);
+    sb.load(stage_base<MB>(a.B, bsel, kb, a.bk), kend - kb, a.bk, rb, kb_);
+  };
+  if (nst > 0) {
+    issue(0, va[0], vb[0], oka[0], okb[0]);
+    if (nst > 1) issue(1, va[1], vb[1], oka[1], okb[1]);
+    sa.store(As[0], va[0], oka[0], a.eps);
+    sb.store(Bs[0], vb[0], okb[0], a.eps);
     __syncthreads();
-    if (k0 + kWKs < kend) fetch(k0 + kWKs);  // next stage's loads in flight under the MFMAs
+  }
+  auto body = [&](int st, auto par) __attribute__((always_inline)) {
+    constexpr int P = decltype(par)::value;  // st & 1: LDS buffer and register slot of stage st
+    if (st + 2 < nst) issue(st + 2, va[P], vb[P], oka[P], okb[P]);  // slot P was stored last stage
 #pragma unroll
     for (int kk = 0; kk < kWKs / 2; ++kk)
-      acc = mfma32(As[2 * kk + h][wm * 32 + j], Bs[2 * kk + h][wn * 32 + j], acc);
+      acc = mfma32(As[P][2 * kk + h][wm * 32 + j], Bs[P][2 * kk + h][wn * 32 + j], acc);
     if constexpr (kSumB) {
       const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float vb = Bs[4 * q + i][c];
-        sum_b = kSq ? fmaf(vb, vb, sum_b) : sum_b + vb;
+      for (int i = 0; i < 8; ++i) {
+        const float vbv = Bs[P][8 * q + i][c];
+        sum_b = kSq ? fmaf(vbv, vbv, sum_b) : sum_b + vbv;
         if constexpr (kSumA) {
-          const float va = As[4 * q + i][c];
-          sum_a = fmaf(va, va, sum_a);
+          const float vav = As[P][8 * q + i][c];
+          sum_a = fmaf(vav, vav, sum_a);
         }
       }
     }
+    if (st + 1 < nst) {
+      sa.store(As[P ^ 1], va[P ^ 1], oka[P ^ 1], a.eps);
+      sb.store(Bs[P ^ 1], vb[P ^ 1], okb[P ^ 1], a.eps);
+    }
+    __syncthreads();
+  };
+  for (int st = 0; st < nst; st += 2) {
+    body(st, std::integral_constant<int, 0>());
+    if (st + 1 < nst) body(st + 1, std::integral_constant<int, 1>());
   }
   if constexpr (kSumB) {
     red[0][threadIdx.x >> 6][threadIdx.x & 63] = sum_b;
@@ -169,7 +242,7 @@ __global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
   // epilogue: lane column n, rows acc_row(r, h)
   const int n = n0 + wn * 32 + j;
   if (n >= a.N) return;
-  const int bo = a.bk ? z : bsel;  // output batch (or split) index
+  const int bo = a.bk ? z : (a.ksplit > 1 ? z : bsel);  // output batch (or split slab) index
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int m = m0 + wm * 32 + acc_row(r, h);
@@ -219,35 +292,66 @@ __global__ __launch_bounds__(256) void wide_rowsum_kernel(const float* __restric
   if (threadIdx.x == 0) rs[p] = red[0];
 }
 
-// Split-K partial slabs [S][M][N] -> out[m][n] in slab order; kind 1 (g_P): -2 sum + 2 p rs[m].
-__global__ __launch_bounds__(256) void wide_finish_kernel(const float* __restrict__ part, int S, int M, int N, int kind,
-                                                          const float* __restrict__ protos, const float* __restrict__ rs,
-                                                          float* __restrict__ out, long long ldo) {
+// Split-K partial slabs [nbatch][S][M][N] -> out[b * obatch + m * ldo + n] in slab order;
+// kind 1 (g_P): -2 sum + 2 p rs[m].
+__global__ __launch_bounds__(256) void wide_finish_kernel(const float* __restrict__ part, int S, int nbatch, int M,
+                                                          int N, int kind, const float* __restrict__ protos,
+                                                          const float* __restrict__ rs, float* __restrict__ out,
+                                                          long long ldo, long long obatch) {
   const long long e = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
-  if (e >= static_cast<long long>(M) * N) return;
-  const int m = static_cast<int>(e / N), n = static_cast<int>(e - static_cast<long long>(m) * N);
+  const long long mn = static_cast<long long>(M) * N;
+  if (e >= mn * nbatch) return;
+  const long long b = e / mn, r = e - b * mn;
+  const int m = static_cast<int>(r / N), n = static_cast<int>(r - static_cast<long long>(m) * N);
+  const float* pp = part + static_cast<size_t>(b) * S * mn + r;
   float s = 0.f;
-  for (int i = 0; i < S; ++i) s += part[static_cast<size_t>(i) * M * N + e];
-  if (kind == 1) s = -2.f * s + 2.f * protos[e] * rs[m];
-  out[m * ldo + n] = s;
+  for (int i = 0; i < S; ++i) s += pp[static_cast<size_t>(i) * mn];
+  if (kind == 1) s = -2.f * s + 2.f * protos[r] * rs[m];
+  out[b * obatch + m * ldo + n] = s;
 }
 
+// Stager mode of an operand: k fast (1) when a flattened contraction is not affine in its
+// index (the (batch, pixel) runs of NCHW tensors), else rows fast (0) where sr == 1.
+int stager_mode(const Operand& o, const WideArgs& a) {
+  if (a.bk && a.nb > 1 && o.sb != static_cast<unsigned>(a.Kd) * o.sk) return o.sk == 1 ? 1 : -1;
+  if (o.sr == 1) return 0;
+  return o.sk == 1 ? 1 : -1;
+}
+
+// grid_z: batches x splits (or the bk splits); a.ksplit 0 means 1.
 template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO>
-int gemm(const WideArgs& a, int grid_z, hipStream_t s) {
+int gemm(WideArgs a, int grid_z, hipStream_t s) {
+  if (a.ksplit < 1) a.ksplit = 1;
   const dim3 grid(static_cast<unsigned>(ceil_div(a.N, kWT)), static_cast<unsigned>(ceil_div(a.M, kWT)),
                   static_cast<unsigned>(grid_z));
-  hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO>), grid, dim3(kWThreads), 0, s, a);
+  const int ma = stager_mode(a.A, a), mb = stager_mode(a.B, a);
+  if (ma < 0 || mb < 0) return fail(PROTOSEG_ERR_UNSUPPORTED, "wide GEMM operand with no unit stride");
+  if (ma == 0 && mb == 0)
+    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 0, 0>), grid, dim3(kWThreads), 0, s, a);
+  else if (ma == 0)
+    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 0, 1>), grid, dim3(kWThreads), 0, s, a);
+  else if (mb == 0)
+    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 1, 0>), grid, dim3(kWThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 1, 1>), grid, dim3(kWThreads), 0, s, a);
   return check_launch("wide_gemm_kernel");
 }
 
-// Workgroups along a pixel contraction: ~512 workgroups in all, at least 1, at most 64.
-int split_of(int M, int N, long long total) {
-  const long long tiles = ceil_div(M, kWT) * ceil_div(N, kWT);
-  long long s = 512 / (tiles > 0 ? tiles : 1);
-  const long long chunks = ceil_div(total, kWKs);
-  if (s > chunks) s = chunks;
+// Workgroups along a contraction of `total` for `groups` output tiles (x batches): about 1024
+// workgroups in all (four per CU at the kernel's 35 KB of LDS), each at least 4 stages, at most 64.
+int split_of(long long groups, long long total) {
+  long long s = 1024 / (groups > 0 ? groups : 1);
+  const long long cap = ceil_div(total, 4 * kWKs);
+  if (s > cap) s = cap;
   if (s > 64) s = 64;
   return static_cast<int>(s < 1 ? 1 : s);
+}
+int split_of(int M, int N, long long total) { return split_of(ceil_div(M, kWT) * ceil_div(N, kWT), total); }
+// The logits GEMM (M = HW, N = K per image): split over the prototypes when the images' tiles
+// alone leave the CUs idle.
+int logits_split(const Geometry& g) {
+  const long long groups = ceil_div(g.HW, kWT) * ceil_div(g.K, kWT) * (g.npix / g.HW);
+  return groups >= 512 ? 1 : split_of(groups, g.P);
 }
 
 struct WideBwdLayout {
@@ -267,7 +371,9 @@ WideBwdLayout wide_bwd_layout(const Geometry& g) {
   return l;
 }
 
-Operand op(const void* p, long long sr, long long sk, long long sb) { return Operand{p, sr, sk, sb}; }
+Operand op(const void* p, long long sr, long long sk, long long sb) {
+  return Operand{p, static_cast<unsigned>(sr), static_cast<unsigned>(sk), static_cast<unsigned>(sb)};
+}
 
 // D[b][p][n] into `dist` (ld P per image), optional act[g][p].
 template <typename TX>
@@ -287,31 +393,47 @@ int wide_distances(const Geometry& g, const TX* x, const float* protos, float ep
 }  // namespace
 
 bool wide_family_fits(const Geometry& g) {
-  return g.C >= 1 && g.P >= 1 && g.K >= 0 && static_cast<long long>(g.npix) * g.P < (1LL << 31) &&
-         static_cast<long long>(g.npix) * g.C < (1LL << 31);
+  const long long lim = 1LL << 31;
+  return g.C >= 1 && g.P >= 1 && g.K >= 0 && static_cast<long long>(g.npix) * g.P < lim &&
+         static_cast<long long>(g.npix) * g.C < lim && static_cast<long long>(g.npix) * g.K < lim &&
+         static_cast<long long>(g.P) * g.C < lim && static_cast<long long>(g.P) * g.K < lim;
 }
 
+// The distances (when the caller wants logits only) and the logits' split-K slabs.
 size_t wide_fwd_scratch_bytes(const Geometry& g, bool need_dist) {
-  return (need_dist ? static_cast<size_t>(g.npix) * g.P : 0) * sizeof(float) + 256;
+  const size_t d = need_dist ? static_cast<size_t>(g.npix) * g.P : 0;
+  const int S = logits_split(g);
+  const size_t part = S > 1 ? static_cast<size_t>(S) * g.npix * g.K : 0;
+  return (((d + 63) & ~static_cast<size_t>(63)) + part) * sizeof(float) + 256;
 }
 
 size_t wide_bwd_workspace_bytes(const Geometry& g) { return wide_bwd_layout(g).total * sizeof(float); }
 
 int launch_fwd_wide(const Geometry& g, bool x_bf16, const void* x, const float* protos, const float* w_last, float eps,
                     int act_kind, float* dist, float* act, float* logits, void* scratch, hipStream_t s) {
-  float* D = dist ? dist : static_cast<float*>(scratch);  // the logits read the distances back
-  const int st = x_bf16 ? wide_distances(g, static_cast<const uint16_t*>(x), protos, eps, act_kind, D, act, s)
-                        : wide_distances(g, static_cast<const float*>(x), protos, eps, act_kind, D, act, s);
+  float* sc = static_cast<float*>(scratch);
+  float* D = dist ? dist : sc;  // the logits read the distances back
+  float* part = sc + (dist ? 0 : ((static_cast<size_t>(g.npix) * g.P + 63) & ~static_cast<size_t>(63)));
+  int st = x_bf16 ? wide_distances(g, static_cast<const uint16_t*>(x), protos, eps, act_kind, D, act, s)
+                  : wide_distances(g, static_cast<const float*>(x), protos, eps, act_kind, D, act, s);
   if (st || !logits) return st;
-  // logits[b][n][k] = sum_p act(D[b][p][n]) W[k][p]
+  // logits[b][n][k] = sum_p act(D[b][p][n]) W[k][p]; split over p into slabs [b][S][HW][K] when
+  // the images' tiles are too few for the CUs
+  const int S = logits_split(g), B = g.npix / g.HW;
   WideArgs a{};
   a.A = op(D, 1, g.HW, static_cast<long long>(g.P) * g.HW);   // (n, p) of D[b][p][n]
   a.B = op(w_last, g.ldw, 1, 0);                              // (k, p) of W[k][p]
-  a.M = g.HW, a.N = g.K, a.Kd = g.P, a.nb = g.npix / g.HW;
-  a.out = logits, a.om = g.K, a.on = 1, a.ob = static_cast<long long>(g.HW) * g.K;
+  a.M = g.HW, a.N = g.K, a.Kd = g.P, a.nb = B, a.ksplit = S;
+  a.out = S > 1 ? static_cast<void*>(part) : logits, a.om = g.K, a.on = 1, a.ob = static_cast<long long>(g.HW) * g.K;
   a.eps = eps;
-  return act_kind == PROTOSEG_ACT_LOG ? gemm<kEpiStore, float, float, 0, -1, float>(a, a.nb, s)
-                                      : gemm<kEpiStore, float, float, 1, -1, float>(a, a.nb, s);
+  st = act_kind == PROTOSEG_ACT_LOG ? gemm<kEpiStore, float, float, 0, -1, float>(a, B * S, s)
+                                    : gemm<kEpiStore, float, float, 1, -1, float>(a, B * S, s);
+  if (st || S == 1) return st;
+  const long long e = static_cast<long long>(g.npix) * g.K;
+  hipLaunchKernelGGL(wide_finish_kernel, dim3(static_cast<unsigned>(ceil_div(e, 256))), dim3(256), 0, s, part, S, B,
+                     g.HW, g.K, 0, nullptr, nullptr, logits, static_cast<long long>(g.K),
+                     static_cast<long long>(g.HW) * g.K);
+  return check_launch("wide_finish_kernel");
 }
 
 int launch_bwd_wide(const Geometry& g, bool x_bf16, const void* x, const float* protos, const float* w_last, float eps,
@@ -358,8 +480,8 @@ int launch_bwd_wide(const Geometry& g, bool x_bf16, const void* x, const float* 
                 : gemm<kEpiStore, float, float, -1, -1, float>(a, S, s);
     if (st) return st;
     const long long e = static_cast<long long>(g.P) * g.C;
-    hipLaunchKernelGGL(wide_finish_kernel, dim3(static_cast<unsigned>(ceil_div(e, 256))), dim3(256), 0, s, part, S,
-                       g.P, g.C, 1, protos, rs, g_protos, static_cast<long long>(g.C));
+    hipLaunchKernelGGL(wide_finish_kernel, dim3(static_cast<unsigned>(ceil_div(e, 256))), dim3(256), 0, s, part, S, 1,
+                       g.P, g.C, 1, protos, rs, g_protos, static_cast<long long>(g.C), 0LL);
     if ((st = check_launch("wide_finish_kernel"))) return st;
   }
   if (g_w && g_logits) {  // g_W[k][p] = sum_{b,n} GL[b][n][k] act(D[b][p][n])
@@ -374,8 +496,8 @@ int launch_bwd_wide(const Geometry& g, bool x_bf16, const void* x, const float* 
                                       : gemm<kEpiStore, float, float, -1, 1, float>(a, S, s);
     if (st) return st;
     const long long e = static_cast<long long>(g.K) * g.P;
-    hipLaunchKernelGGL(wide_finish_kernel, dim3(static_cast<unsigned>(ceil_div(e, 256))), dim3(256), 0, s, part, S,
-                       g.K, g.P, 0, nullptr, nullptr, g_w, static_cast<long long>(g.ldw));
+    hipLaunchKernelGGL(wide_finish_kernel, dim3(static_cast<unsigned>(ceil_div(e, 256))), dim3(256), 0, s, part, S, 1,
+                       g.K, g.P, 0, nullptr, nullptr, g_w, static_cast<long long>(g.ldw), 0LL);
     if ((st = check_launch("wide_finish_kernel"))) return st;
   }
   return PROTOSEG_OK;

@@ -508,6 +508,18 @@ def push_prototypes(dataset, prototype_network_parallel, prototype_layer_stride=
         img_tensor, labels = load_raw(push_iter)
         return ppnet.conv_features(img_tensor), labels
 
+    scan_runs = {}  # image index -> the image indices of the backbone batch the scan ran it in
+
+    def load_as_scanned(push_iter):
+        """The image's features as the scan computed them: its whole scan batch through the
+        backbone again (a batch-of-1 convolution need not equal the batched one bit for bit,
+        and the exact-tie resolution compares distances exactly)."""
+        ids = scan_runs.get(push_iter, [push_iter])
+        raw = [load_raw(i) for i in ids]
+        feats = ppnet.conv_features(torch.cat([r[0] for r in raw], 0))
+        k = ids.index(push_iter)
+        return feats[k:k + 1], raw[k][1]
+
     log("Updating prototypes...")
     per = max(1, int(images_per_batch))
     with torch.no_grad():
@@ -522,6 +534,9 @@ def push_prototypes(dataset, prototype_network_parallel, prototype_layer_stride=
                 labels = torch.stack([r[1] for r in run], 0)
                 push_update(state, ppnet.conv_features(imgs), labels, ppnet.prototype_vectors, proto_class_t,
                             run[0][2], lut, words)
+                ids = [r[2] for r in run]
+                for i in ids:
+                    scan_runs[i] = ids
                 run.clear()
 
         for push_iter in range(lo, hi):
@@ -535,7 +550,7 @@ def push_prototypes(dataset, prototype_network_parallel, prototype_layer_stride=
     # exact ties inside a winning image, in the reference's set order (this rank's winners,
     # before the shards merge: the owner's patch travels with its key)
     with torch.no_grad():
-        moved = resolve_exact_ties(state, load, ppnet.prototype_vectors, proto_class_t, lut, log=log)
+        moved = resolve_exact_ties(state, load_as_scanned, ppnet.prototype_vectors, proto_class_t, lut, log=log)
     if moved:
         log(f"\t{len(moved)} exact tie(s) resolved in the reference's patch order: {moved[:20]}")
     if world > 1:

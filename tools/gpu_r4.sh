@@ -26,6 +26,37 @@ for step in "$@"; do
       PROTOSEG_FWD_OPERANDS=0 timeout -k 10 300 python -u bench.py --no-kld --no-push --no-knn --no-eval --no-train --no-sigmoid --no-cpu-baseline --no-wide \
         > gpurun_out/${T}_quick_noops.log 2>&1 || { tail -30 gpurun_out/${T}_quick_noops.log; exit 1; }
       python3 tools/bench_summary.py gpurun_out/${T}_quick_noops.log ;;
+    widetrace)  # rocprofv3 kernel trace of each wide configuration alone (per-launch table)
+      for cfg in c4 ref; do
+        ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/wt_${T}_$cfg" \
+            -o wt --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/wide_run.py" $cfg 10 \
+            > "$GRAFT_REPO_ROOT/gpurun_out/${T}_wt_$cfg.log" 2>&1 ) || { tail -20 gpurun_out/${T}_wt_$cfg.log; exit 1; }
+        tail -1 gpurun_out/${T}_wt_$cfg.log
+        python3 tools/ktrace_grid.py $(find gpurun_out/wt_${T}_$cfg -name '*kernel_trace.csv')
+      done ;;
+    steptrace)  # kernel trace of the KLD step and the small-batch layer steps, each alone
+      for spec in "kld --protos 361" "kld --protos 190" "layer --protos 361 --batch 2" "layer --protos 361 --batch 4" "layer --protos 361"; do
+        tag=$(echo "$spec" | tr -d ' -' )
+        ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/st_${T}_$tag" \
+            -o st --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/step_trace.py" $spec \
+            > "$GRAFT_REPO_ROOT/gpurun_out/${T}_st_$tag.log" 2>&1 ) || { tail -20 gpurun_out/${T}_st_$tag.log; exit 1; }
+        grep "ms/step" gpurun_out/${T}_st_$tag.log
+        python3 tools/ktrace_grid.py $(find gpurun_out/st_${T}_$tag -name '*kernel_trace.csv')
+      done ;;
+    abkld)  # interleaved A/B of the build_var/* KLD variants against the main build
+      for P in 361 190; do
+        for c in kld kldc; do
+          timeout -k 10 300 python -u tools/ab_libs.py --protos $P --call $c --reps 40 > gpurun_out/${T}_ab_${c}_$P.log 2>&1 \
+            || { tail -20 gpurun_out/${T}_ab_${c}_$P.log; exit 1; }
+          tail -6 gpurun_out/${T}_ab_${c}_$P.log
+        done
+      done ;;
+    pushtrace)  # kernel trace of the push inner step alone
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/pt_${T}" \
+          -o pt --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/push_trace.py" 8 20 \
+          > "$GRAFT_REPO_ROOT/gpurun_out/${T}_pt.log" 2>&1 ) || { tail -20 gpurun_out/${T}_pt.log; exit 1; }
+      tail -1 gpurun_out/${T}_pt.log
+      python3 tools/ktrace_grid.py $(find gpurun_out/pt_${T} -name '*kernel_trace.csv') ;;
     diag)
       timeout -k 10 300 python -u tools/debug/kld_compact_diag.py > gpurun_out/${T}_diag.log 2>&1; tail -30 gpurun_out/${T}_diag.log ;;
     smoke)

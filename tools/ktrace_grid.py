@@ -11,8 +11,8 @@ for path in sys.argv[1:]:
     groups = collections.OrderedDict()
     with open(path) as f:
         for row in csv.DictReader(f):
-            name = re.sub(r"\(.*", "", row["Kernel_Name"].replace("void ", ""))
-            name = name.replace("protoseg::(anonymous namespace)::", "")
+            name = row["Kernel_Name"].replace("void ", "").replace("protoseg::(anonymous namespace)::", "")
+            name = re.sub(r"\(.*", "", name.replace("protoseg::", ""))
             grid = tuple(int(row[k]) // max(int(row[k.replace("Grid", "Workgroup")]), 1)
                          for k in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z"))
             key = (name[:60], grid, row["VGPR_Count"], row["Accum_VGPR_Count"], row["LDS_Block_Size"])
