@@ -603,3 +603,33 @@ extern "C" int protoseg_push_merge(const uint64_t* img_keys, const uint64_t* img
                      reinterpret_cast<long long*>(global_img), global_patch, global_fmap);
   return check_launch("push_merge_kernel");
 }
+
+// push.py:184-281 for one batch of equal-geometry images in ONE host call: class masks, the
+// masked top-2 argmin and the strict-'<' merge into the running state, with the mask and the
+// per-image keys in this stream's scratch (kPushUpdate) instead of caller tensors. The result
+// is the three-call sequence's (same kernels, same order).
+extern "C" int protoseg_push_update(const void* label, int label_dtype, int n_img, int H_img, int W_img,
+                                    const int32_t* lut, int lut_size, int words, const float* x, int C, int h, int w,
+                                    const float* protos, int P, const int32_t* proto_class, int64_t first_img,
+                                    float* global_dist, float* global_second, int64_t* global_img,
+                                    int32_t* global_patch, float* global_fmap, protoseg_stream_t stream) {
+  if (words < 1 || words > 64) return fail(PROTOSEG_ERR_INVALID, "words=%d outside [1, 64]", words);
+  if (n_img <= 0 || h <= 0 || w <= 0 || P <= 0) return fail(PROTOSEG_ERR_INVALID, "bad shape");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const size_t hw = static_cast<size_t>(h) * w;
+  const size_t mask_bytes = (static_cast<size_t>(words) * n_img * hw * 4 + 255) & ~static_cast<size_t>(255);
+  const size_t key_bytes = static_cast<size_t>(n_img) * P * 8;
+  void* sc = nullptr;
+  if (int st = stream_scratch(ScratchKind::kPushUpdate, mask_bytes + 2 * key_bytes, 1u << 20, s, &sc)) return st;
+  auto* mask = static_cast<uint32_t*>(sc);
+  auto* keys = reinterpret_cast<uint64_t*>(static_cast<unsigned char*>(sc) + mask_bytes);
+  uint64_t* second = global_second ? keys + static_cast<size_t>(n_img) * P : nullptr;
+  if (int st = protoseg_patch_class_mask_words(label, label_dtype, n_img, H_img, W_img, h, w, lut, lut_size, words,
+                                               mask, stream))
+    return st;
+  if (int st = protoseg_push_argmin_words(x, n_img, C, h, w, protos, P, proto_class, mask, words, keys, second,
+                                          stream))
+    return st;
+  return protoseg_push_merge(keys, second, n_img, first_img, x, C, static_cast<int>(hw), P, global_dist,
+                             global_second, global_img, global_patch, global_fmap, stream);
+}

@@ -65,6 +65,8 @@ SIGNATURES = {
     "protoseg_push_argmin_words": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _i, _vp, _vp, _vp]),
     "protoseg_push_distances_words": (_i, [_vp, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
     "protoseg_push_merge": (_i, [_vp, _vp, _i, _i64, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "protoseg_push_update": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _i, _i, _i, _vp, _i, _vp, _i64, _vp, _vp,
+                                  _vp, _vp, _vp, _vp]),
     "protoseg_kld_workspace_size": (_sz, [_i, _i, _i, _i]),
     "protoseg_kld_forward": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _vp, _sz, _vp]),
     "protoseg_kld_backward": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _sz, _vp, _vp]),

@@ -152,19 +152,27 @@ def push_update(state: PushState, x: Tensor, labels: Tensor, protos: Tensor, pro
     n, C, h, w = x.shape
     if labels.dim() == 2:
         labels = labels.unsqueeze(0)
+    labels = labels.contiguous()
+    dt = _label_dtype(labels)
+    if dt < 0:
+        raise _lib.ProtosegError(f"label dtype {labels.dtype} unsupported (int64, int32, uint8)")
     if words is None:  # class-mask planes (one below 33 classes); callers in a loop pass it
         words = _class_words(proto_class)
-    mask = patch_class_mask(labels, h, w, lut, words=words)
-    keys, second = push_argmin(x, protos, proto_class, mask, with_second=True)
-    dev = x.device
-    P = keys.shape[1]
+    dev = _lib.require_device(x, labels, protos, proto_class, lut)
+    protos = protos.reshape(protos.shape[0], -1).float().contiguous()
+    P = protos.shape[0]
     if state.second is None:
         state.second = torch.full((P,), math.inf, device=dev, dtype=torch.float32)
-    with torch.cuda.device(dev):
-        _lib.call("protoseg_push_merge", _lib.ptr(keys), _lib.ptr(second), n, int(first_img), _lib.ptr(x), C, h * w,
-                  P, _lib.ptr(state.dist), _lib.ptr(state.second), _lib.ptr(state.img), _lib.ptr(state.patch),
-                  _lib.ptr(state.fmap), _lib.stream_of(dev))
+    pc = proto_class if proto_class.dtype == torch.int32 and proto_class.is_contiguous() \
+        else proto_class.to(torch.int32).contiguous()
+    lut_c = lut.to(torch.int32).contiguous() if lut is not None else None
     H, W = labels.shape[-2:]
+    # mask -> top-2 argmin -> merge in one library call (masks and keys in its stream scratch)
+    with torch.cuda.device(dev):
+        _lib.call("protoseg_push_update", _lib.ptr(labels), dt, n, int(H), int(W), _lib.ptr(lut_c),
+                  0 if lut_c is None else lut_c.numel(), int(words), _lib.ptr(x), C, h, w, _lib.ptr(protos), P,
+                  _lib.ptr(pc), int(first_img), _lib.ptr(state.dist), _lib.ptr(state.second), _lib.ptr(state.img),
+                  _lib.ptr(state.patch), _lib.ptr(state.fmap), _lib.stream_of(dev))
     for i in range(n):
         state.geometry[first_img + i] = (int(H), int(W), int(h), int(w))
 

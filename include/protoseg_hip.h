@@ -9,9 +9,11 @@
  * Conventions (all entry points):
  *  - device pointers, plain integer shapes, a stream; no torch types;
  *  - tensors are dense, row-major, in the layouts stated per argument;
- *  - outputs are caller-allocated; the only temporary memory is the caller-owned workspace
- *    sized by the matching *_workspace_size() call; no hidden hipMalloc / sync, so every
- *    call can be captured into a hipGraph;
+ *  - outputs are caller-allocated; temporary memory is the caller-owned workspace sized by the
+ *    matching *_workspace_size() call, or the library's grow-only per-stream scratch (operand
+ *    images, push masks / keys): allocated on a call's first use of a size and reused, never
+ *    freed while the process runs, so once warm every call is kernel launches only (no sync,
+ *    no allocation) and can be captured into a hipGraph;
  *  - return PROTOSEG_OK (0) or a protoseg_status code; protoseg_last_error() gives text;
  *  - reentrant: the only global state is a once-initialised per-kernel LDS attribute table.
  */
@@ -299,6 +301,19 @@ int protoseg_push_merge(const uint64_t* img_keys, const uint64_t* img_second, in
                         const float* x, int C, int hw, int P,
                         float* global_dist, float* global_second, int64_t* global_img, int32_t* global_patch,
                         float* global_fmap, protoseg_stream_t stream);
+
+/*
+ * Steps 1-3 in one host call for one batch of equal-geometry images (push_prototypes' inner
+ * step, push.py:184-281): protoseg_patch_class_mask_words -> protoseg_push_argmin_words ->
+ * protoseg_push_merge, with the masks and per-image keys in library scratch on `stream`
+ * (grow-only, one block per stream: capturable once it exists). Same results as the three calls;
+ * global_second may be NULL (no runner-up tracking).
+ */
+int protoseg_push_update(const void* label, int label_dtype, int n_img, int H_img, int W_img,
+                         const int32_t* lut, int lut_size, int words, const float* x, int C, int h, int w,
+                         const float* protos, int P, const int32_t* proto_class, int64_t first_img,
+                         float* global_dist, float* global_second, int64_t* global_img,
+                         int32_t* global_patch, float* global_fmap, protoseg_stream_t stream);
 
 /*
  * KLD similarity loss. Replaces segmentation/module.py:167-208 (the Python loop over images x

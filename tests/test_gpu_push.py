@@ -356,6 +356,8 @@ def test_push_prototypes_batched_scan_resolves_planted_ties(device, tmp_path):
     for img_id in ds.img_ids:
         Image.fromarray(rng.integers(0, 256, size=(72, 104, 3), dtype=np.uint8)).save(ds.get_img_path(img_id))
         np.save(ann_dir / f"{img_id}.npy", rng.integers(0, K + 1, size=(64, 96)).astype(np.int64))
+    protos0 = net.prototype_vectors.detach().reshape(P, C).clone()  # the push projects and prunes them
+    pc = push.prototype_classes(net).cpu().numpy()
     logs = []
     state = push_prototypes(ds, net, images_per_batch=8, log=lambda *a: logs.append(" ".join(map(str, a))))
     assert not any("not reproduced" in line for line in logs), logs
@@ -367,10 +369,9 @@ def test_push_prototypes_batched_scan_resolves_planted_ties(device, tmp_path):
         imgs = torch.cat([to_normalized_tensor(Image.open(ds.get_img_path(i)).convert("RGB").crop((4, 4, 100, 68)))
                           .unsqueeze(0) for i in ds.img_ids]).to(device)
         feats = fake_features(imgs)
-    pc = push.prototype_classes(net).cpu().numpy()
     ref = pu.PushOracleState(P, C)
     for i, img_id in enumerate(ds.img_ids):
-        d = push.push_distances(feats[i:i + 1], net.prototype_vectors.reshape(P, C)).cpu().numpy()  # [P, h*w]
+        d = push.push_distances(feats[i:i + 1], protos0).cpu().numpy()  # [P, h*w]
         h, w = feats.shape[2:]
         y = np.load(ann_dir / f"{img_id}.npy")
         pu.update_prototypes_on_image_core(ref, feats[i].cpu().numpy(), d.reshape(P, h, w).transpose(1, 2, 0), y, pc,
@@ -379,3 +380,30 @@ def test_push_prototypes_batched_scan_resolves_planted_ties(device, tmp_path):
     assert found.sum() > 10
     assert np.array_equal(state.img.cpu().numpy(), ref.proto_rf_boxes[:, 0])
     assert np.array_equal(state.patch.cpu().numpy()[found], ref.winner_patch[found])
+
+
+def test_push_update_one_call_equals_three_calls(device):
+    """protoseg_push_update (one host call, masks / keys in library scratch) leaves the state the
+    mask -> argmin -> merge sequence leaves, bit for bit, over two batches."""
+    from protoseg_amd import _lib
+    push = _push()
+    C, h, w, P, K, n = 64, 17, 23, 40, 19, 3
+    gen = torch.Generator().manual_seed(21)
+    pc = torch.argmax(po.class_identity(P, K), dim=1).to(torch.int32).to(device)
+    protos = torch.rand(P, C, generator=gen).to(device)
+    a, b = push.PushState.create(P, C, device), push.PushState.create(P, C, device)
+    for first in (0, n):
+        x = torch.sigmoid(2 * torch.randn(n, C, h, w, generator=gen)).to(device)
+        lab = torch.from_numpy(np.random.default_rng(first).integers(0, K + 1, size=(n, 4 * h, 4 * w))).to(device)
+        push.push_update(a, x, lab, protos, pc, first)
+        mask = push.patch_class_mask(lab, h, w)
+        keys, second = push.push_argmin(x, protos, pc, mask, with_second=True)
+        if b.second is None:
+            b.second = torch.full((P,), float("inf"), device=device)
+        with torch.cuda.device(device):
+            _lib.call("protoseg_push_merge", _lib.ptr(keys), _lib.ptr(second), n, first, _lib.ptr(x), C, h * w, P,
+                      _lib.ptr(b.dist), _lib.ptr(b.second), _lib.ptr(b.img), _lib.ptr(b.patch), _lib.ptr(b.fmap),
+                      _lib.stream_of(device))
+    torch.cuda.synchronize()
+    for f in ("dist", "second", "img", "patch", "fmap"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f

@@ -57,6 +57,12 @@ for step in "$@"; do
           > "$GRAFT_REPO_ROOT/gpurun_out/${T}_pt.log" 2>&1 ) || { tail -20 gpurun_out/${T}_pt.log; exit 1; }
       tail -1 gpurun_out/${T}_pt.log
       python3 tools/ktrace_grid.py $(find gpurun_out/pt_${T} -name '*kernel_trace.csv') ;;
+    abfwd)  # interleaved A/B of the build_var/* variants on the forward call
+      for P in 361 190; do
+        timeout -k 10 300 python -u tools/ab_libs.py --protos $P --call fwd --reps 40 > gpurun_out/${T}_ab_fwd_$P.log 2>&1 \
+          || { tail -20 gpurun_out/${T}_ab_fwd_$P.log; exit 1; }
+        tail -4 gpurun_out/${T}_ab_fwd_$P.log
+      done ;;
     diag)
       timeout -k 10 300 python -u tools/debug/kld_compact_diag.py > gpurun_out/${T}_diag.log 2>&1; tail -30 gpurun_out/${T}_diag.log ;;
     smoke)
