@@ -3,19 +3,24 @@
 // The reference loops in Python over images x classes present x prototype pairs, with a
 // masked_select, a log_softmax and two kl_div per pair and host syncs per class (module.py:170,
 // 174). Here the same quantities come from these launches:
-//   kld_lists_kernel     prototype -> class buckets (ascending prototype ids), module.py:173
-//   kld_partial_kernel   one workgroup per (class c, image b, pixel range s), one pass over the
-//                        range's class pixels (running max): the local max m_i and
-//                        sum_n exp(z_i - m_i) of each class prototype (z = distance), and
-//                        T_ij = sum_n exp(z_i - m_i) (z_i - z_j)
+//   forward (protoseg_kld_forward):
+//   kld_partial_kernel   one workgroup per (class c, image b, pixel range s): the class's prototype
+//                        list (ascending ids, module.py:173; published once for the later
+//                        kernels), the range's class pixels, their class distances gathered once
+//                        (kept per pixel in zc for the backward), one pass with a running max:
+//                        the local max m_i and sum_n exp(z_i - m_i) of each class prototype
+//                        (z = distance) and T_ij = sum_n exp(z_i - m_i) (z_i - z_j)
 //   kld_merge_kernel     per (c, b): L_i = log-sum-exp over the ranges (module.py:183) and
 //                        KL(p_i || p_j) = sum_s exp(m_i^s - L_i) T_ij^s - (L_i - L_j), which is
 //                        sum_n p_i (lp_i - lp_j) regrouped (module.py:190-198)
 //   kld_finalize_kernel  mean of exp(-(KL_ij + KL_ji) / 2) over all pairs (module.py:199-206)
-//   kld_grad_kernel      d(g_loss * loss) / d distances, dense [B, P, HW]: what autograd of the
-//                        reference ops produces; zero outside each prototype's class pixels
+//   backward, compact layout (protoseg_kld_backward_compact), ONE launch:
+//   kld_grad_compact_kernel  per (c, b, s): proto_slot, pix_cls of the range's pixels, the
+//                        group's coefficients and the gradient at its class pixels from zc
+//   backward, dense layout (protoseg_kld_backward): kld_coef_kernel + kld_grad_kernel, the
+//                        [B, P, HW] gradient autograd of the reference ops produces
 // Only the class's own prototype rows are read at the class's pixels (about 1/K of the distance
-// tensor); the dense gradient write is the dominant traffic.
+// tensor); the dense gradient write is the dominant traffic of the dense layout.
 //
 // Reference semantics kept (oracle/kld_oracle.py): the label value c selects prototype column
 // c (module.py:170-178: void = 0 pairs with class-0 prototypes, value K is skipped); a class
@@ -38,7 +43,10 @@ constexpr int kKldThreads = 256;     // = pixels per staged chunk
 #ifndef KLD_RANGE
 #define KLD_RANGE 1024
 #endif
-constexpr int kKldRange = KLD_RANGE;  // pixels per kld_partial_kernel workgroup (a multiple of 256)
+constexpr int kKldRange = KLD_RANGE;
+#ifndef KLD_ZC
+#define KLD_ZC 1  // the forward keeps the gathered class distances per pixel for the compact backward
+#endif  // pixels per kld_partial_kernel workgroup (a multiple of 256)
 constexpr int kKldPair = kKldMaxPerClass * kKldMaxPerClass;
 constexpr int kKldLdsStride = kKldThreads + 1;  // padded rows: conflict-free task reads
 constexpr size_t kKldMaxDynLds = 2 * kKldMaxPerClass * kKldLdsStride * sizeof(float);
@@ -61,6 +69,7 @@ struct KldLayout {
   size_t slot;   // int [P]: bucket * 256 + position in the bucket (the compact gradient's column)
   size_t rcnt;   // int [B * K * S]: class pixels in each 1024-pixel range
   size_t plist;  // int [B * K * HW]: per (image, class) the class pixels of range s at s * 1024 + q
+  size_t zc;     // float [B * HW * 32]: each pixel's own-class distances by class slot (row stride mpc)
   size_t total;
 };
 
@@ -90,6 +99,8 @@ KldLayout kld_layout(int B, int P, int HW, int K) {
   o = align256(o + static_cast<size_t>(B) * K * kld_ranges(HW) * 4);
   l.plist = o;
   o = align256(o + static_cast<size_t>(B) * K * HW * 4);
+  l.zc = o;
+  o = align256(o + static_cast<size_t>(B) * HW * kKldMaxPerClass * 4);
   l.total = o;
   return l;
 }
@@ -98,6 +109,7 @@ struct KldPtrs {
   int *off, *idx, *cnt, *stat;
   float *lse, *kl, *part, *group;
   int *slot, *rcnt, *plist;
+  float* zc;
 };
 
 KldPtrs kld_ptrs(void* ws, const KldLayout& l) {
@@ -107,48 +119,58 @@ KldPtrs kld_ptrs(void* ws, const KldLayout& l) {
           reinterpret_cast<float*>(b + l.lse),  reinterpret_cast<float*>(b + l.kl),
           reinterpret_cast<float*>(b + l.part), reinterpret_cast<float*>(b + l.group),
           reinterpret_cast<int*>(b + l.slot),   reinterpret_cast<int*>(b + l.rcnt),
-          reinterpret_cast<int*>(b + l.plist)};
+          reinterpret_cast<int*>(b + l.plist),  reinterpret_cast<float*>(b + l.zc)};
 }
 
 __device__ __forceinline__ int bucket_of(int pc, int K) { return (pc >= 0 && pc < K) ? pc : K; }
 
 constexpr int kKldListMaxP = 1 << 20;
 
-// One wave per bucket c (grid K + 1): prototypes scanned 64 at a time (lane = prototype), a
-// ballot per chunk for the bucket's members (module.py:173: nonzero of the identity column = the
-// prototypes whose class is c, ascending) and for the prototypes of lower buckets (the bucket's
-// start). Bucket K collects prototypes with no class in [0, K). Two sweeps: counts, then places.
-__global__ __launch_bounds__(64) void kld_lists_kernel(const int32_t* __restrict__ proto_class, int P, int K,
-                                                       int* __restrict__ off, int* __restrict__ idx,
-                                                       int* __restrict__ slot) {
-  const int lane = threadIdx.x, c = blockIdx.x;
-  int start = 0, cnt = 0;
+__device__ __forceinline__ int lane_rank(unsigned long long m) {  // set bits of m below this lane
+  return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0));
+}
+
+// One wave scans proto_class (64 prototypes per step) for bucket c (module.py:173: nonzero of the
+// identity column = the prototypes whose class is c, ascending; bucket K: no class in [0, K)):
+// its start in the bucket order and count, the first kKldMaxPerClass members into `first`, and
+// with `publish` every member into idx / slot and the start into off[c] (the lists later
+// kernels read: the owner workgroup of each bucket writes them in the forward's first launch).
+__device__ __forceinline__ void class_list_scan(const int32_t* __restrict__ proto_class, int P, int K, int c,
+                                                bool publish, int* first, int* start_out, int* cnt_out,
+                                                int* __restrict__ off, int* __restrict__ idx, int* __restrict__ slot) {
+  const int lane = threadIdx.x & 63;
+  int start = 0;
   for (int p0 = 0; p0 < P; p0 += 64) {
     const int p = p0 + lane;
-    const int bk = p < P ? bucket_of(proto_class[p], K) : K + 1;
+    const int pc = p < P ? proto_class[p] : -1;
+    const int bk = p < P ? ((pc >= 0 && pc < K) ? pc : K) : K + 1;
     start += __popcll(__ballot(bk < c));
-    cnt += __popcll(__ballot(bk == c));
   }
-  if (lane == 0) {
+  int cnt = 0;
+  for (int p0 = 0; p0 < P; p0 += 64) {
+    const int p = p0 + lane;
+    const int pc = p < P ? proto_class[p] : -1;
+    const bool in = p < P && ((pc >= 0 && pc < K) ? pc : K) == c;
+    const unsigned long long m = __ballot(in);
+    if (in) {
+      const int r = cnt + lane_rank(m);
+      if (r < kKldMaxPerClass) first[r] = p;
+      if (publish) {
+        idx[start + r] = p;
+        // the compact gradient's column: class * 256 + rank; a rank past 255 would wrap into the
+        // next class's code, and such a class holds more prototypes than any max_per_class (its
+        // groups add no pairs), so its prototypes get class -2, which no pixel carries
+        slot[p] = r < 256 ? c * 256 + r : -2 * 256;
+      }
+    }
+    cnt += __popcll(m);
+  }
+  if (publish && lane == 0) {
     off[c] = start;
     if (c == K) off[K + 1] = start + cnt;
   }
-  int pos = start;
-  for (int p0 = 0; p0 < P; p0 += 64) {
-    const int p = p0 + lane;
-    const bool in = p < P && bucket_of(proto_class[p], K) == c;
-    const unsigned long long m = __ballot(in);
-    if (in) {
-      const int r = pos + __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0));
-      idx[r] = p;
-      // the prototype's column of the compact gradient: class * 256 + rank. A rank past 255 would
-      // wrap into the next class's code; such a class holds more prototypes than any max_per_class
-      // (its groups add no pairs), so its prototypes get class -2, which no pixel carries.
-      slot[p] = r - start < 256 ? c * 256 + (r - start) : -2 * 256;
-    }
-    pos += __popcll(m);
-  }
+  *start_out = start;
+  *cnt_out = cnt;
 }
 
 template <typename TL>
@@ -156,9 +178,6 @@ __device__ __forceinline__ long long label_at(const TL* lab, int n) {
   return static_cast<long long>(lab[n]);
 }
 
-__device__ __forceinline__ int lane_rank(unsigned long long m) {  // set bits of m below this lane
-  return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0));
-}
 
 // n / d for 0 <= n < 2^23, d >= 1 with r = 1/d (v_rcp_f32, 1 ulp): the quotient estimate is
 // within 1 of n / d, one correction step makes it exact; replaces the ~25-instruction integer
@@ -213,21 +232,51 @@ __device__ __forceinline__ void lse_merge(float& m, float& s, float mo, float so
 template <typename TL>
 __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* __restrict__ dist, int P, int HW,
                                                                   const TL* __restrict__ label, int K, int mpc,
-                                                                  const int* __restrict__ off,
-                                                                  const int* __restrict__ idx,
+                                                                  const int32_t* __restrict__ proto_class,
+                                                                  int* __restrict__ off, int* __restrict__ idx,
+                                                                  int* __restrict__ slot,
                                                                   float* __restrict__ part, int* __restrict__ rcnt,
-                                                                  int* __restrict__ plist) {
+                                                                  int* __restrict__ plist, float* __restrict__ zc) {
   extern __shared__ __attribute__((aligned(16))) float kld_smem[];
   __shared__ int s_proto[kKldMaxPerClass];
   __shared__ float s_m[kKldMaxPerClass];
   __shared__ float s_scale[kKldMaxPerClass];
   __shared__ int s_wc[kKldRange / 64];
   __shared__ int s_list[kKldRange];
+  __shared__ int s_cnt;
   constexpr int kRows = kKldRange / kKldThreads;
   const int c = blockIdx.x, b = blockIdx.y, rs = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int o0 = off[c];
-  const int npc_all = off[c + 1] - o0;
+  const TL* lab = label + static_cast<size_t>(b) * HW;
+  const int n0 = rs * kKldRange, n1 = min(HW, n0 + kKldRange);
+  bool in[kRows];
+  int below[kRows];
+#pragma unroll
+  for (int r = 0; r < kRows; ++r) {  // all label loads in flight together (under the list scan)
+    const int n = n0 + r * kKldThreads + tid;
+    in[r] = n < n1 && label_at(lab, n) == c;
+  }
+  // the class's prototype list (was a launch of its own): wave 0 of every workgroup scans
+  // proto_class; the (image 0, range 0) workgroup of bucket c publishes it, the one of bucket
+  // K - 1 also bucket K's (the prototypes without a class)
+  const bool publish = b == 0 && rs == 0;
+  if (wave == 0) {
+    int st, cnt;
+    class_list_scan(proto_class, P, K, c, publish, s_proto, &st, &cnt, off, idx, slot);
+    if (lane == 0) s_cnt = cnt;
+  } else if (wave == 1 && publish && c == K - 1) {  // bucket K: published only (its first
+    int st, cnt;                                      // members land in s_list, rewritten below)
+    class_list_scan(proto_class, P, K, K, true, s_list, &st, &cnt, off, idx, slot);
+  }
+#pragma unroll
+  for (int r = 0; r < kRows; ++r) {
+    const unsigned long long bal = __ballot(in[r]);
+    below[r] = lane_rank(bal);
+    if (lane == 0) s_wc[r * (kKldThreads / 64) + wave] = __popcll(bal);
+  }
+  if (tid < kKldMaxPerClass) s_m[tid] = -INFINITY;
+  __syncthreads();
+  const int npc_all = s_cnt;
   const int npc = npc_all < mpc ? npc_all : mpc;
   const size_t bc = static_cast<size_t>(b) * K + c;
   float* out = part + (bc * gridDim.z + rs) * kKldPartFloats;
@@ -239,26 +288,6 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
     }
     return;
   }
-  const TL* lab = label + static_cast<size_t>(b) * HW;
-  const int n0 = rs * kKldRange, n1 = min(HW, n0 + kKldRange);
-  bool in[kRows];
-  int below[kRows];
-#pragma unroll
-  for (int r = 0; r < kRows; ++r) {  // all label loads in flight together
-    const int n = n0 + r * kKldThreads + tid;
-    in[r] = n < n1 && label_at(lab, n) == c;
-  }
-#pragma unroll
-  for (int r = 0; r < kRows; ++r) {
-    const unsigned long long bal = __ballot(in[r]);
-    below[r] = lane_rank(bal);
-    if (lane == 0) s_wc[r * (kKldThreads / 64) + wave] = __popcll(bal);
-  }
-  if (tid < npc) {
-    s_proto[tid] = idx[o0 + tid];
-    s_m[tid] = -INFINITY;
-  }
-  __syncthreads();
   int total = 0;
   int* pl = plist + bc * HW + n0;
 #pragma unroll
@@ -313,6 +342,14 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
     const int kq = min(kKldThreads, total - base);
     gather_tasks(db, HW, s_list + base, kq, s_proto, npc, sz, kKldLdsStride);
     __syncthreads();
+    if (KLD_ZC) {  // the chunk's class distances, row per pixel (slot fastest: coalesced rows)
+      const float rn = qrcp(npc);
+      float* zb = zc + static_cast<size_t>(b) * HW * mpc;
+      for (int t = tid; t < npc * kq; t += kKldThreads) {
+        const int q = qdiv(t, npc, rn), i = t - q * npc;
+        zb[static_cast<size_t>(s_list[base + q]) * mpc + i] = sz[i * kKldLdsStride + q];
+      }
+    }
     {  // chunk max per prototype (8 threads per row) -> running max and the rescale factor
       const int i = tid >> 3, l8 = tid & 7;
       float mx = -INFINITY;
@@ -386,63 +423,94 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
   }
 }
 
-// One wave per (class c, image b): merges the range partials in range order.
-__global__ __launch_bounds__(64) void kld_merge_kernel(int P, int K, int S, int mpc, const int* __restrict__ off,
-                                                       const int* __restrict__ idx, const float* __restrict__ part,
-                                                       int* __restrict__ cnt_out, float* __restrict__ lse_out,
-                                                       float* __restrict__ kl_out, float* __restrict__ group_out) {
+// One workgroup per (class c, image b): merges the range partials in range order. L_i per
+// slot (thread i), the per-(range, slot) factors exp(m_i^s - L_i) once each (was once per entry
+// and range), then KL_ij over the workgroup's 256 threads, and this group's sum of
+// exp(-kld_ij) over its pairs i < j (per-thread partials added in a fixed order).
+constexpr int kKldMergeMaxS = 64;  // ranges whose factors are staged in LDS (beyond: inline)
+__global__ __launch_bounds__(256) void kld_merge_kernel(int P, int K, int S, int mpc, const int* __restrict__ off,
+                                                        const int* __restrict__ idx, const float* __restrict__ part,
+                                                        int* __restrict__ cnt_out, float* __restrict__ lse_out,
+                                                        float* __restrict__ kl_out, float* __restrict__ group_out) {
   __shared__ float s_L[kKldMaxPerClass];
-  const int c = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
+  __shared__ float s_sc[kKldMergeMaxS][kKldMaxPerClass];
+  __shared__ int s_ok[kKldMergeMaxS];
+  __shared__ float s_kl[kKldPair];
+  __shared__ float s_sum[256];
+  __shared__ int s_cnt;
+  const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int npc_all = off[c + 1] - off[c];
   const int npc = npc_all < mpc ? npc_all : mpc;
   const float* pb = part + (static_cast<size_t>(b) * K + c) * S * kKldPartFloats;
-  int cnt = 0;
-  if (npc >= 1 && npc_all <= mpc)
-    for (int s = 0; s < S; ++s) cnt += static_cast<int>(pb[s * kKldPartFloats + 2 * kKldMaxPerClass]);
-  if (lane == 0) cnt_out[static_cast<size_t>(b) * K + c] = cnt;
+  const bool valid = npc >= 1 && npc_all <= mpc;
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
+  for (int s = tid; s < S && valid; s += 256) {
+    const int n = static_cast<int>(pb[s * kKldPartFloats + 2 * kKldMaxPerClass]);
+    if (s < kKldMergeMaxS) s_ok[s] = n > 0;
+    atomicAdd(&s_cnt, n);  // integer sum: order-free
+  }
+  __syncthreads();
+  const int cnt = s_cnt;
+  float* gsum = group_out + (static_cast<size_t>(b) * K + c) * 2;  // (sum of exp(-kld), pairs)
+  if (tid == 0) cnt_out[static_cast<size_t>(b) * K + c] = cnt;
   if (cnt == 0) {
-    if (lane == 0) group_out[(static_cast<size_t>(b) * K + c) * 2] = group_out[(static_cast<size_t>(b) * K + c) * 2 + 1] = 0.f;
+    if (tid == 0) gsum[0] = gsum[1] = 0.f;
     return;
   }
-  if (lane < npc) {  // L_i = log sum_s S_i^s exp(m_i^s)  (log-sum-exp of d over the class pixels)
+  if (tid < npc) {  // L_i = log sum_s S_i^s exp(m_i^s)  (log-sum-exp of d over the class pixels)
     float M = -INFINITY, Ssum = 0.f;
     for (int s = 0; s < S; ++s) {
       const float* q = pb + s * kKldPartFloats;
-      if (q[2 * kKldMaxPerClass] > 0.f) lse_merge(M, Ssum, q[lane], q[kKldMaxPerClass + lane]);
+      if (q[2 * kKldMaxPerClass] > 0.f) lse_merge(M, Ssum, q[tid], q[kKldMaxPerClass + tid]);
     }
     const float L = M + logf(Ssum);
-    s_L[lane] = L;
-    lse_out[static_cast<size_t>(b) * P + idx[off[c] + lane]] = L;
+    s_L[tid] = L;
+    lse_out[static_cast<size_t>(b) * P + idx[off[c] + tid]] = L;
   }
   __syncthreads();
-  float* gsum = group_out + (static_cast<size_t>(b) * K + c) * 2;  // (sum of exp(-kld), pairs)
   if (npc < 2 || cnt < 2) {
-    if (lane == 0) gsum[0] = gsum[1] = 0.f;
+    if (tid == 0) gsum[0] = gsum[1] = 0.f;
     return;
   }
+  const int Ss = S < kKldMergeMaxS ? S : kKldMergeMaxS;
+  for (int t = tid; t < Ss * npc; t += 256) {
+    const int s = t / npc, i = t - s * npc;
+    s_sc[s][i] = expf(pb[s * kKldPartFloats + i] - s_L[i]);
+  }
+  __syncthreads();
   float* klb = kl_out + (static_cast<size_t>(b) * K + c) * kKldPair;
-  for (int e = lane; e < npc * npc; e += 64) {
+  for (int e = tid; e < npc * npc; e += 256) {
     const int i = e / npc, j = e - i * npc;
     if (i == j) continue;
     float t = 0.f;
     for (int s = 0; s < S; ++s) {
       const float* q = pb + s * kKldPartFloats;
-      if (q[2 * kKldMaxPerClass] > 0.f)
-        t = fmaf(expf(q[i] - s_L[i]), q[2 * kKldMaxPerClass + 1 + i * kKldMaxPerClass + j], t);
+      const bool ok = s < kKldMergeMaxS ? s_ok[s] != 0 : q[2 * kKldMaxPerClass] > 0.f;
+      if (ok) {
+        const float sc = s < kKldMergeMaxS ? s_sc[s][i] : expf(q[i] - s_L[i]);
+        t = fmaf(sc, q[2 * kKldMaxPerClass + 1 + i * kKldMaxPerClass + j], t);
+      }
     }
-    klb[i * kKldMaxPerClass + j] = t - (s_L[i] - s_L[j]);
+    const float kl = t - (s_L[i] - s_L[j]);
+    klb[i * kKldMaxPerClass + j] = kl;
+    s_kl[i * kKldMaxPerClass + j] = kl;
   }
   __syncthreads();
   // this group's pairs i < j: kld = (KL(p_j||p_i) + KL(p_i||p_j)) / 2 (module.py:195-199)
   float sum = 0.f;
-  for (int e = lane; e < npc * npc; e += 64) {
+  for (int e = tid; e < npc * npc; e += 256) {
     const int i = e / npc, j = e - i * npc;
-    if (i < j) sum += expf(-((klb[j * kKldMaxPerClass + i] + klb[i * kKldMaxPerClass + j]) / 2.f));
+    if (i < j) sum += expf(-((s_kl[j * kKldMaxPerClass + i] + s_kl[i * kKldMaxPerClass + j]) / 2.f));
   }
-#pragma unroll
-  for (int sh = 32; sh >= 1; sh >>= 1) sum += __shfl_xor(sum, sh);
-  if (lane == 0) {
-    gsum[0] = sum;
+  s_sum[tid] = sum;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (tid < w) s_sum[tid] += s_sum[tid + w];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    gsum[0] = s_sum[0];
     gsum[1] = static_cast<float>(npc * (npc - 1) / 2);
   }
 }
@@ -482,26 +550,119 @@ __global__ __launch_bounds__(256) void kld_finalize_kernel(int groups, const flo
   }
 }
 
-// Backward coefficients per (class c, image b): w_ij = -g_loss exp(-kld_ij) / n_pairs
-// (mean, exp(-x) and the /2 of module.py:199-206 differentiated), stored as (w_ij, KL_ij) pairs.
+// Backward coefficients per (class c, image b): w_ij = -g_loss exp(-kld_ij) / n_pairs (mean,
+// exp(-x) and the /2 of module.py:199-206 differentiated; w_ii = 0), and per slot i the group
+// constants R_i = sum_j w_ij and WK_i = sum_j w_ij KL_ij of the regrouped gradient (kld_slot_grad).
+// Layout per group (kKldCoefFloats): w [npc][npc] | (R_i, WK_i) [npc] at kKldPair.
+constexpr int kKldCoefFloats = kKldPair + 2 * kKldMaxPerClass;
 __global__ __launch_bounds__(64) void kld_coef_kernel(int K, int mpc, const int* __restrict__ off,
                                                       const int* __restrict__ cnt, const float* __restrict__ kl,
                                                       const int* __restrict__ stat, const float* __restrict__ g_loss,
-                                                      float2* __restrict__ coef) {
+                                                      float* __restrict__ coef) {
+  __shared__ float s_w[kKldPair];
   const int c = blockIdx.x, b = blockIdx.y;
   const int npc = off[c + 1] - off[c];
   const int np = stat[0];
   if (npc < 2 || npc > mpc || np == 0 || cnt[static_cast<size_t>(b) * K + c] < 2) return;
   const float gl = g_loss ? g_loss[0] : 1.f;
   const float* klb = kl + (static_cast<size_t>(b) * K + c) * kKldPair;
-  float2* cb = coef + (static_cast<size_t>(b) * K + c) * kKldPair;
+  float* cb = coef + (static_cast<size_t>(b) * K + c) * kKldCoefFloats;
   for (int e = threadIdx.x; e < npc * npc; e += 64) {
     const int i = e / npc, j = e - i * npc;
-    // the merge kernel leaves KL's diagonal unwritten (workspace garbage, possibly NaN): the
-    // pair (w_ii, KL_ii) = (0, 0) keeps 0 * KL_ii out of the gradient sums
+    // the merge kernel leaves KL's diagonal unwritten (workspace garbage, possibly NaN): w_ii = 0
+    // and KL_ii = 0 keep it out of every sum
     const float kij = i == j ? 0.f : klb[i * kKldMaxPerClass + j], kji = i == j ? 0.f : klb[j * kKldMaxPerClass + i];
     const float w = i == j ? 0.f : -(gl / static_cast<float>(np)) * expf(-((kji + kij) / 2.f));
-    cb[i * npc + j] = make_float2(w, kij);
+    s_w[e] = w;
+    cb[e] = w;
+  }
+  __syncthreads();
+  const int i = threadIdx.x;
+  if (i < npc) {
+    float r = 0.f, wk = 0.f;
+    for (int j = 0; j < npc; ++j) {
+      const float w = s_w[i * npc + j];
+      r += w;
+      wk = fmaf(w, i == j ? 0.f : klb[i * kKldMaxPerClass + j], wk);
+    }
+    cb[kKldPair + 2 * i] = r;
+    cb[kKldPair + 2 * i + 1] = wk;
+  }
+}
+
+// d(g_loss * loss) / d z_i at one pixel of a contributing (image, class) group, regrouped from
+// the autograd of log_softmax + the two kl_div per pair (module.py:183-206):
+//   g_i = sum_j w_ij (p_i (lp_i - lp_j - KL_ij + 1) - p_j) / 2
+//       = (p_i ((lp_i + 1) R_i - WK_i - sum_j w_ij lp_j) - sum_j w_ij p_j) / 2
+// Two dot products per slot (four chains over j, fixed-order sum); `lp(j)` / `p(j)` read the
+// pixel's log-probabilities / probabilities, `w(j)` row i of the group's w. Both gradient layouts
+// (dense kld_grad_kernel, compact kld_grad_compact_kernel) call this: compact == dense bit for bit.
+template <typename LP, typename PJ, typename WJ>
+__device__ __forceinline__ float kld_slot_grad(int npc, float pi, float li, float ri, float wki, LP lp, PJ pj, WJ w) {
+  float a[4] = {0.f, 0.f, 0.f, 0.f}, q[4] = {0.f, 0.f, 0.f, 0.f};
+  int j = 0;
+  for (; j + 3 < npc; j += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float wj = w(j + u);
+      a[u] = fmaf(wj, lp(j + u), a[u]);
+      q[u] = fmaf(wj, pj(j + u), q[u]);
+    }
+  }
+  for (; j < npc; ++j) {
+    const float wj = w(j);
+    a[0] = fmaf(wj, lp(j), a[0]);
+    q[0] = fmaf(wj, pj(j), q[0]);
+  }
+  const float A = (a[0] + a[1]) + (a[2] + a[3]), Q = (q[0] + q[1]) + (q[2] + q[3]);
+  return 0.5f * (pi * ((li + 1.f) * ri - wki - A) - Q);
+}
+
+// kld_slot_grad for the four slots i0 .. i0 + 3 at once (the pixel's lp_j / p_j read once for
+// the four): each slot's operations and order are kld_slot_grad's, so the results are its bits.
+// Slots past npc repeat slot npc - 1 (their results are not stored).
+template <typename LP, typename PJ, typename WIJ>
+__device__ __forceinline__ void kld_block_grad(int npc, int i0, const float (&pi)[4], const float (&li)[4],
+                                               const float (&ri)[4], const float (&wki)[4], LP lp, PJ pj, WIJ w,
+                                               float (&g)[4]) {
+  float a[4][4], q[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[r][u] = q[r][u] = 0.f;
+  int ii[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) ii[r] = min(i0 + r, npc - 1);
+  int j = 0;
+  for (; j + 3 < npc; j += 4) {
+    float lj[4], pjv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      lj[u] = lp(j + u);
+      pjv[u] = pj(j + u);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float wj = w(ii[r], j + u);
+        a[r][u] = fmaf(wj, lj[u], a[r][u]);
+        q[r][u] = fmaf(wj, pjv[u], q[r][u]);
+      }
+  }
+  for (; j < npc; ++j) {
+    const float lj = lp(j), pjv = pj(j);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float wj = w(ii[r], j);
+      a[r][0] = fmaf(wj, lj, a[r][0]);
+      q[r][0] = fmaf(wj, pjv, q[r][0]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float A = (a[r][0] + a[r][1]) + (a[r][2] + a[r][3]), Q = (q[r][0] + q[r][1]) + (q[r][2] + q[r][3]);
+    g[r] = 0.5f * (pi[r] * ((li[r] + 1.f) * ri[r] - wki[r] - A) - Q);
   }
 }
 
@@ -515,7 +676,7 @@ template <typename TL>
 __global__ __launch_bounds__(kKldThreads) void kld_grad_kernel(
     const float* __restrict__ dist, int P, int HW, const TL* __restrict__ label, int K, int mpc,
     const int* __restrict__ off, const int* __restrict__ idx, const int* __restrict__ cnt,
-    const float* __restrict__ lse, const float2* __restrict__ coef, const int* __restrict__ stat,
+    const float* __restrict__ lse, const float* __restrict__ coef, const int* __restrict__ stat,
     float* __restrict__ g_dist) {
   extern __shared__ __attribute__((aligned(16))) float kld_smem[];
   const int b = blockIdx.y, tid = threadIdx.x;
@@ -540,26 +701,12 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_kernel(
       slp[i * kKldLdsStride + tid] = lp;
       sp[i * kKldLdsStride + tid] = expf(lp);
     }
-    const float2* cb = coef + (static_cast<size_t>(b) * K + c) * kKldPair;
+    const float* cb = coef + (static_cast<size_t>(b) * K + c) * kKldCoefFloats;
     for (int i = 0; i < npc; ++i) {
-      const float pi = sp[i * kKldLdsStride + tid], li = slp[i * kKldLdsStride + tid];
-      // the compact kernel's order (four chains over j, fixed-order sum): both layouts hold the
-      // same f32 values
-      float gj[4] = {0.f, 0.f, 0.f, 0.f};
-      int j = 0;
-      for (; j + 3 < npc; j += 4) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float2 wk = cb[i * npc + j + u];  // (w_ij, KL_ij); w_ii = 0
-          gj[u] = fmaf(wk.x, pi * (li - slp[(j + u) * kKldLdsStride + tid] - wk.y + 1.f) - sp[(j + u) * kKldLdsStride + tid],
-                       gj[u]);
-        }
-      }
-      for (; j < npc; ++j) {
-        const float2 wk = cb[i * npc + j];
-        gj[0] = fmaf(wk.x, pi * (li - slp[j * kKldLdsStride + tid] - wk.y + 1.f) - sp[j * kKldLdsStride + tid], gj[0]);
-      }
-      sg[i * kKldLdsStride + tid] = 0.5f * ((gj[0] + gj[1]) + (gj[2] + gj[3]));
+      sg[i * kKldLdsStride + tid] = kld_slot_grad(
+          npc, sp[i * kKldLdsStride + tid], slp[i * kKldLdsStride + tid], cb[kKldPair + 2 * i], cb[kKldPair + 2 * i + 1],
+          [&](int j) { return slp[j * kKldLdsStride + tid]; }, [&](int j) { return sp[j * kKldLdsStride + tid]; },
+          [&](int j) { return cb[i * npc + j]; });
     }
   }
   float* gb = g_dist + static_cast<size_t>(b) * P * HW + n;
@@ -579,28 +726,71 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_kernel(
 // b, pixel range s) of a contributing group then walks the range's class-pixel list the forward
 // left in plist, thread = pixel. LDS (dynamic): [mpc][257] p | [mpc][257] log p (each thread its
 // own column) | the group's (w_ij, KL_ij) pairs.
+//
+// The same launch also writes what used to take three more: proto_slot (workgroups (c, 0, 0)
+// copy their bucket's columns; the one of bucket K - 1 also bucket K's), pix_cls for every pixel
+// (the workgroup of the pixel's label, class 0's for labels outside [0, K), writes c or -1: each
+// pixel exactly once, no memset), and the group's coefficients (kld_coef_kernel's arithmetic, in
+// LDS).
+template <typename TL>
 __global__ __launch_bounds__(kKldThreads) void kld_grad_compact_kernel(
-    const float* __restrict__ dist, int P, int HW, int K, int mpc, const int* __restrict__ off,
-    const int* __restrict__ idx, const int* __restrict__ cnt, const float* __restrict__ lse,
-    const float2* __restrict__ coef, const int* __restrict__ stat, const int* __restrict__ rcnt,
-    const int* __restrict__ plist, float* __restrict__ g_cls, int32_t* __restrict__ pix_cls) {
+    const float* __restrict__ dist, int P, int HW, const TL* __restrict__ label, int K, int mpc,
+    const int* __restrict__ off, const int* __restrict__ idx, const int* __restrict__ slot,
+    const int* __restrict__ cnt, const float* __restrict__ lse, const float* __restrict__ kl,
+    const int* __restrict__ stat, const float* __restrict__ g_loss, const int* __restrict__ rcnt,
+    const int* __restrict__ plist, const float* __restrict__ zc, float* __restrict__ g_cls,
+    int32_t* __restrict__ pix_cls, int32_t* __restrict__ proto_slot) {
   extern __shared__ __attribute__((aligned(16))) float kld_smem[];
   __shared__ int s_proto[kKldMaxPerClass];
   __shared__ float s_lse[kKldMaxPerClass];
   const int c = blockIdx.x, b = blockIdx.y, rs = blockIdx.z, tid = threadIdx.x;
   const size_t bc = static_cast<size_t>(b) * K + c;
-  const int q1 = rcnt[bc * gridDim.z + rs];
-  if (q1 == 0) return;
   const int o0 = off[c];
   const int npc = off[c + 1] - o0;
-  if (npc < 2 || npc > mpc || stat[0] == 0 || cnt[bc] < 2) return;  // uniform: the group adds no pair
+  if (b == 0 && rs == 0) {
+    for (int r = tid; r < npc; r += kKldThreads) proto_slot[idx[o0 + r]] = slot[idx[o0 + r]];
+    if (c == K - 1)
+      for (int r = off[K] + tid; r < off[K + 1]; r += kKldThreads) proto_slot[idx[r]] = slot[idx[r]];
+  }
+  const bool contributes = npc >= 2 && npc <= mpc && stat[0] != 0 && cnt[bc] >= 2;
+  {
+    const TL* lab = label + static_cast<size_t>(b) * HW;
+    int32_t* pcb = pix_cls + static_cast<size_t>(b) * HW;
+    const int n1 = min(HW, (rs + 1) * kKldRange);
+    for (int n = rs * kKldRange + tid; n < n1; n += kKldThreads) {
+      const long long l = label_at(lab, n);
+      const int owner = (l >= 0 && l < K) ? static_cast<int>(l) : 0;
+      if (owner == c) pcb[n] = (l == c && contributes) ? c : -1;
+    }
+  }
+  if (!contributes) return;  // uniform: the group adds no pair
+  const int q1 = rcnt[bc * gridDim.z + rs];
+  if (q1 == 0) return;
   const int* pl = plist + bc * HW + rs * kKldRange;
-  int32_t* pc = pix_cls + static_cast<size_t>(b) * HW;
   float* sp = kld_smem;
   float* slp = sp + mpc * kKldLdsStride;
-  float2* scoef = reinterpret_cast<float2*>(slp + mpc * kKldLdsStride);
-  const float2* cb = coef + (static_cast<size_t>(b) * K + c) * kKldPair;
-  for (int e = tid; e < npc * npc; e += kKldThreads) scoef[e] = cb[e];
+  float* scoef = slp + mpc * kKldLdsStride;  // w [npc][npc] | (R_i, WK_i) at kKldPair
+  {  // kld_coef_kernel's coefficients, same operations
+    const int np = stat[0];
+    const float gl = g_loss ? g_loss[0] : 1.f;
+    const float* klb = kl + bc * kKldPair;
+    for (int e = tid; e < npc * npc; e += kKldThreads) {
+      const int i = e / npc, j = e - i * npc;
+      const float kij = i == j ? 0.f : klb[i * kKldMaxPerClass + j], kji = i == j ? 0.f : klb[j * kKldMaxPerClass + i];
+      scoef[e] = i == j ? 0.f : -(gl / static_cast<float>(np)) * expf(-((kji + kij) / 2.f));
+    }
+    __syncthreads();
+    if (tid < npc) {
+      float r = 0.f, wk = 0.f;
+      for (int j = 0; j < npc; ++j) {
+        const float w = scoef[tid * npc + j];
+        r += w;
+        wk = fmaf(w, tid == j ? 0.f : klb[tid * kKldMaxPerClass + j], wk);
+      }
+      scoef[kKldPair + 2 * tid] = r;
+      scoef[kKldPair + 2 * tid + 1] = wk;
+    }
+  }
   if (tid < npc) {
     s_proto[tid] = idx[o0 + tid];
     s_lse[tid] = lse[static_cast<size_t>(b) * P + idx[o0 + tid]];
@@ -610,8 +800,16 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_compact_kernel(
   for (int base = 0; base < q1; base += kKldThreads) {  // chunks of 256 class pixels
     const int kq = min(kKldThreads, q1 - base);
     const int* lq = pl + base;
-    gather_tasks(db, HW, lq, kq, s_proto, npc, slp, kKldLdsStride);
-    for (int q = tid; q < kq; q += kKldThreads) pc[lq[q]] = c;
+    if (KLD_ZC) {  // the forward's per-pixel rows of the class distances (no gather from dist)
+      const float rn = qrcp(npc);
+      const float* zb = zc + static_cast<size_t>(b) * HW * mpc;
+      for (int t = tid; t < npc * kq; t += kKldThreads) {
+        const int q = qdiv(t, npc, rn), i = t - q * npc;
+        slp[i * kKldLdsStride + q] = zb[static_cast<size_t>(lq[q]) * mpc + i];
+      }
+    } else {
+      gather_tasks(db, HW, lq, kq, s_proto, npc, slp, kKldLdsStride);
+    }
     __syncthreads();
     const float rk = qrcp(kq);
     for (int t = tid; t < npc * kq; t += kKldThreads) {
@@ -622,50 +820,27 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_compact_kernel(
     }
     __syncthreads();
     // one task per (pixel, block of 4 class slots), pixel fastest: a wave's lanes share the slot
-    // block, so the (w_ij, KL_ij) reads are broadcasts, and a pixel's lp_j / p_j are read once
-    // for its 4 slots (the LDS reads bounded the chunk). Each slot's sum is kld_grad_kernel's
-    // sequence (four chains over j, the same expression), so compact == dense bit for bit.
+    // block, so the w reads are broadcasts, and a pixel's lp_j / p_j are read once for its 4
+    // slots; each slot is kld_slot_grad's sequence, so compact == dense bit for bit
     const int nib = (npc + 3) >> 2;
     for (int t = tid; t < nib * kq; t += kKldThreads) {
       const int ib = qdiv(t, kq, rk), q = t - ib * kq;
-      int ii[4];
-      float pi[4], li[4], gj[4][4];
+      float pi[4], li[4], ri[4], wki[4], g[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        ii[r] = min(4 * ib + r, npc - 1);  // slots past npc repeat the last one (not stored)
-        pi[r] = sp[ii[r] * kKldLdsStride + q];
-        li[r] = slp[ii[r] * kKldLdsStride + q];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) gj[r][u] = 0.f;
+        const int i = min(4 * ib + r, npc - 1);
+        pi[r] = sp[i * kKldLdsStride + q];
+        li[r] = slp[i * kKldLdsStride + q];
+        ri[r] = scoef[kKldPair + 2 * i];
+        wki[r] = scoef[kKldPair + 2 * i + 1];
       }
-      int j = 0;
-      for (; j + 3 < npc; j += 4) {
-        float lj[4], pj[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          lj[u] = slp[(j + u) * kKldLdsStride + q];
-          pj[u] = sp[(j + u) * kKldLdsStride + q];
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const float2 wk = scoef[ii[r] * npc + j + u];  // (w_ij, KL_ij); w_ii = 0
-            gj[r][u] = fmaf(wk.x, pi[r] * (li[r] - lj[u] - wk.y + 1.f) - pj[u], gj[r][u]);
-          }
-      }
-      for (; j < npc; ++j) {
-        const float lj = slp[j * kKldLdsStride + q], pj = sp[j * kKldLdsStride + q];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float2 wk = scoef[ii[r] * npc + j];
-          gj[r][0] = fmaf(wk.x, pi[r] * (li[r] - lj - wk.y + 1.f) - pj, gj[r][0]);
-        }
-      }
+      kld_block_grad(
+          npc, 4 * ib, pi, li, ri, wki, [&](int j) { return slp[j * kKldLdsStride + q]; },
+          [&](int j) { return sp[j * kKldLdsStride + q]; }, [&](int i, int j) { return scoef[i * npc + j]; }, g);
       float* row = g_cls + (static_cast<size_t>(b) * HW + lq[q]) * mpc;
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (4 * ib + r < npc) row[4 * ib + r] = 0.5f * ((gj[r][0] + gj[r][1]) + (gj[r][2] + gj[r][3]));
+        if (4 * ib + r < npc) row[4 * ib + r] = g[r];
     }
     __syncthreads();
   }
@@ -738,19 +913,18 @@ extern "C" int protoseg_kld_forward(const float* dist, int B, int P, int HW, con
   const KldLayout l = kld_layout(B, P, HW, K);
   const KldPtrs w = kld_ptrs(workspace, l);
   const int S = kld_ranges(HW);
-  hipLaunchKernelGGL(kld_lists_kernel, dim3(K + 1), dim3(64), 0, s, proto_class, P, K, w.off, w.idx, w.slot);
-  if (int st = check_launch("kld_lists_kernel")) return st;
   const size_t lds = std::max(static_cast<size_t>(2) * max_per_class * kKldLdsStride * sizeof(float),
                               static_cast<size_t>(kKldThreads) * 16 * sizeof(float));
   const int st = by_label(label_dtype, [&](auto tl) {
     using TL = std::remove_pointer_t<decltype(tl)>;
     if (int e = ensure_lds<kld_partial_kernel<TL>, kKldMaxDynLds>()) return e;
     hipLaunchKernelGGL(kld_partial_kernel<TL>, dim3(K, B, S), dim3(kKldThreads), lds, s, dist, P, HW,
-                       static_cast<const TL*>(label), K, max_per_class, w.off, w.idx, w.part, w.rcnt, w.plist);
+                       static_cast<const TL*>(label), K, max_per_class, proto_class, w.off, w.idx, w.slot, w.part,
+                       w.rcnt, w.plist, w.zc);
     return check_launch("kld_partial_kernel");
   });
   if (st) return st;
-  hipLaunchKernelGGL(kld_merge_kernel, dim3(K, B), dim3(64), 0, s, P, K, S, max_per_class, w.off, w.idx, w.part, w.cnt,
+  hipLaunchKernelGGL(kld_merge_kernel, dim3(K, B), dim3(256), 0, s, P, K, S, max_per_class, w.off, w.idx, w.part, w.cnt,
                      w.lse, w.kl, w.group);
   if (int e = check_launch("kld_merge_kernel")) return e;
   hipLaunchKernelGGL(kld_finalize_kernel, dim3(1), dim3(256), 0, s, B * K, w.group, w.off, K, max_per_class, w.stat,
@@ -769,7 +943,7 @@ extern "C" int protoseg_kld_backward(const float* dist, int B, int P, int HW, co
   const KldLayout l = kld_layout(B, P, HW, K);
   const KldPtrs w = kld_ptrs(workspace, l);
   // the range partials are dead after the forward: their space holds the backward coefficients
-  float2* coef = reinterpret_cast<float2*>(w.part);
+  float* coef = w.part;
   hipLaunchKernelGGL(kld_coef_kernel, dim3(K, B), dim3(64), 0, s, K, max_per_class, w.off, w.cnt, w.kl, w.stat, g_loss,
                      coef);
   if (int st = check_launch("kld_coef_kernel")) return st;
@@ -796,20 +970,16 @@ extern "C" int protoseg_kld_backward_compact(const float* dist, int B, int P, in
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const KldLayout l = kld_layout(B, P, HW, K);
   const KldPtrs w = kld_ptrs(workspace, l);
-  if (hipMemcpyAsync(proto_slot, w.slot, static_cast<size_t>(P) * 4, hipMemcpyDeviceToDevice, s) != hipSuccess)
-    return check_launch("proto_slot copy");
-  float2* coef = reinterpret_cast<float2*>(w.part);
-  hipLaunchKernelGGL(kld_coef_kernel, dim3(K, B), dim3(64), 0, s, K, max_per_class, w.off, w.cnt, w.kl, w.stat, g_loss,
-                     coef);
-  if (int st = check_launch("kld_coef_kernel")) return st;
-  const size_t lds = static_cast<size_t>(2) * max_per_class * kKldLdsStride * sizeof(float) +
-                     static_cast<size_t>(max_per_class) * max_per_class * sizeof(float2);
-  if (int e = ensure_lds<kld_grad_compact_kernel, kKldMaxDynLds + kKldPair * sizeof(float2)>()) return e;
-  if (hipMemsetAsync(pix_cls, 0xFF, static_cast<size_t>(B) * HW * 4, s) != hipSuccess)  // -1: no gradient
-    return check_launch("pix_cls memset");
-  hipLaunchKernelGGL(kld_grad_compact_kernel, dim3(K, B, kld_ranges(HW)), dim3(kKldThreads), lds, s, dist, P, HW, K,
-                     max_per_class, w.off, w.idx, w.cnt, w.lse, coef, w.stat, w.rcnt, w.plist, g_cls, pix_cls);
-  return check_launch("kld_grad_compact_kernel");
+  // one launch: proto_slot, pix_cls, the coefficients and the gradient (kld_grad_compact_kernel)
+  const size_t lds = (static_cast<size_t>(2) * max_per_class * kKldLdsStride + kKldCoefFloats) * sizeof(float);
+  return by_label(label_dtype, [&](auto tl) {
+    using TL = std::remove_pointer_t<decltype(tl)>;
+    if (int e = ensure_lds<kld_grad_compact_kernel<TL>, kKldMaxDynLds + kKldCoefFloats * sizeof(float)>()) return e;
+    hipLaunchKernelGGL(kld_grad_compact_kernel<TL>, dim3(K, B, kld_ranges(HW)), dim3(kKldThreads), lds, s, dist, P,
+                       HW, static_cast<const TL*>(label), K, max_per_class, w.off, w.idx, w.slot, w.cnt, w.lse, w.kl,
+                       w.stat, g_loss, w.rcnt, w.plist, w.zc, g_cls, pix_cls, proto_slot);
+    return check_launch("kld_grad_compact_kernel");
+  });
 }
 
 extern "C" int protoseg_kld_expand(const float* g_cls, const int32_t* pix_cls, const int32_t* proto_slot, int B, int P,

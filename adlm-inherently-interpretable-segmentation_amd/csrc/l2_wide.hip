@@ -163,7 +163,7 @@ __device__ __forceinline__ unsigned stage_base(const Operand& o, int b, int kb, 
 // column t & 63 of stage rows 8 (t >> 6) .. + 7; the four partials are added in a fixed order:
 // deterministic, the same bits in every workgroup of a column, and no separate norms pass.
 template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO, int MA, int MB>
-__global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(4))) void wide_gemm_kernel(WideArgs a) {
+__global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
   __shared__ float As[2][kWKs][kWLd];
   __shared__ float Bs[2][kWKs][kWLd];
   constexpr bool kSumB = EPI == kEpiDist || EPI == kEpiGx, kSumA = EPI == kEpiDist, kSq = EPI == kEpiDist;
@@ -185,53 +185,48 @@ __global__ __launch_bounds__(kWThreads) __attribute__((amdgpu_waves_per_eu(4))) 
   sa.init(a.A, a.M, m0, kbeg, a.Kd, a.bk);
   sb.init(a.B, a.N, n0, kbeg, a.Kd, a.bk);
   f32x16 acc = zero16();
-  // two stages of loads in flight: register slot s & 1 holds stage s until it is stored to LDS
-  float va[2][8], vb[2][8];
-  unsigned oka[2] = {0, 0}, okb[2] = {0, 0};
+  float va[8], vb[8];
+  unsigned oka = 0, okb = 0;
   const int nst = kend > kbeg ? (kend - kbeg + kWKs - 1) / kWKs : 0;
-  auto issue = [&](int stg, float (&ra)[8], float (&rb)[8], unsigned& ka, unsigned& kb_) {
-    const int kb = kbeg + stg * kWKs;
-    if (stg > 0) {  // stages are issued in order: the k-fast bk positions advance one stage
-      if (MA == 1 && a.bk) sa.advance(a.Kd);
-      if (MB == 1 && a.bk) sb.advance(a.Kd);
-    }
-    sa.load(stage_base<MA>(a.A, bsel, kb, a.bk), kend - kb, a.bk, ra, ka);
-    sb.load(stage_base<MB>(a.B, bsel, kb, a.bk), kend - kb, a.bk, rb, kb_);
-  };
   if (nst > 0) {
-    issue(0, va[0], vb[0], oka[0], okb[0]);
-    if (nst > 1) issue(1, va[1], vb[1], oka[1], okb[1]);
-    sa.store(As[0], va[0], oka[0], a.eps);
-    sb.store(Bs[0], vb[0], okb[0], a.eps);
+    sa.load(stage_base<MA>(a.A, bsel, kbeg, a.bk), kend - kbeg, a.bk, va, oka);
+    sb.load(stage_base<MB>(a.B, bsel, kbeg, a.bk), kend - kbeg, a.bk, vb, okb);
+    sa.store(As[0], va, oka, a.eps);
+    sb.store(Bs[0], vb, okb, a.eps);
     __syncthreads();
   }
-  auto body = [&](int st, auto par) __attribute__((always_inline)) {
-    constexpr int P = decltype(par)::value;  // st & 1: LDS buffer and register slot of stage st
-    if (st + 2 < nst) issue(st + 2, va[P], vb[P], oka[P], okb[P]);  // slot P was stored last stage
+  // (two stages of loads in flight measured 1-3 % slower at the 4-waves-per-SIMD register cap
+  // they need: DESIGN 5.4)
+  for (int st = 0; st < nst; ++st) {
+    const int cur = st & 1;
+    const bool more = st + 1 < nst;
+    if (more) {  // the next stage's loads, in flight under this stage's MFMAs
+      const int kb = kbeg + (st + 1) * kWKs;
+      if (MA == 1 && a.bk) sa.advance(a.Kd);
+      if (MB == 1 && a.bk) sb.advance(a.Kd);
+      sa.load(stage_base<MA>(a.A, bsel, kb, a.bk), kend - kb, a.bk, va, oka);
+      sb.load(stage_base<MB>(a.B, bsel, kb, a.bk), kend - kb, a.bk, vb, okb);
+    }
 #pragma unroll
     for (int kk = 0; kk < kWKs / 2; ++kk)
-      acc = mfma32(As[P][2 * kk + h][wm * 32 + j], Bs[P][2 * kk + h][wn * 32 + j], acc);
+      acc = mfma32(As[cur][2 * kk + h][wm * 32 + j], Bs[cur][2 * kk + h][wn * 32 + j], acc);
     if constexpr (kSumB) {
       const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const float vbv = Bs[P][8 * q + i][c];
+        const float vbv = Bs[cur][8 * q + i][c];
         sum_b = kSq ? fmaf(vbv, vbv, sum_b) : sum_b + vbv;
         if constexpr (kSumA) {
-          const float vav = As[P][8 * q + i][c];
+          const float vav = As[cur][8 * q + i][c];
           sum_a = fmaf(vav, vav, sum_a);
         }
       }
     }
-    if (st + 1 < nst) {
-      sa.store(As[P ^ 1], va[P ^ 1], oka[P ^ 1], a.eps);
-      sb.store(Bs[P ^ 1], vb[P ^ 1], okb[P ^ 1], a.eps);
+    if (more) {
+      sa.store(As[cur ^ 1], va, oka, a.eps);
+      sb.store(Bs[cur ^ 1], vb, okb, a.eps);
     }
     __syncthreads();
-  };
-  for (int st = 0; st < nst; st += 2) {
-    body(st, std::integral_constant<int, 0>());
-    if (st + 1 < nst) body(st + 1, std::integral_constant<int, 1>());
   }
   if constexpr (kSumB) {
     red[0][threadIdx.x >> 6][threadIdx.x & 63] = sum_b;

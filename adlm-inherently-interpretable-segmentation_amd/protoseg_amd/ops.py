@@ -330,11 +330,12 @@ def prototype_layer(x: Tensor, prototype_vectors: Tensor, last_layer_weight: Ten
                     activation: str = "log", with_dist: bool = True, with_logits: bool = True,
                     with_act: bool = False, precision: Optional[str] = None,
                     x_sigmoid: bool = False) -> Tuple[Tensor, Tensor, Tensor]:
-    """Distances, logits and activations of the PPNet prototype layer (1x1 prototypes).
+    """Distances, logits and activations of the PPNet prototype layer.
 
-    x: [B, C, H, W] add-on-layer output (float32, bfloat16, or float16 widened to f32); prototype_vectors: [P, C, 1, 1]
-    or [P, C]; last_layer_weight: [K, P]. Returns (distances [B,P,H,W], logits [B,H,W,K],
-    activations [B*H*W, P]) with unrequested outputs empty.
+    x: [B, C, H, W] add-on-layer output (float32, bfloat16, or float16 widened to f32); prototype_vectors: [P, C, kh, kw]
+    or [P, C]; last_layer_weight: [K, P]. Returns (distances [B,P,H',W'], logits [B,H',W',K],
+    activations [B*H'*W', P]) with unrequested outputs empty; H' = H - kh + 1, W' = W - kw + 1
+    (k x k prototypes run on the unfolded map, C k k deep).
 
     x_sigmoid=True: x is the add-on layers' pre-activation and the layer input is sigmoid(x)
     (model.py:124-128's final nn.Sigmoid). The kernels apply it on load where
@@ -345,10 +346,24 @@ def prototype_layer(x: Tensor, prototype_vectors: Tensor, last_layer_weight: Ten
     if activation not in ACT_KINDS:
         raise _lib.ProtosegError(f"activation {activation!r} has no HIP kernel ('log' or 'linear')")
     protos = prototype_vectors.reshape(prototype_vectors.shape[0], -1)
+    kernel = tuple(prototype_vectors.shape[2:]) if prototype_vectors.dim() == 4 else (1, 1)
+    if kernel != (1, 1):
+        # k x k prototypes (model.py:203-221 is a general F.conv2d, no padding): the k x k
+        # windows as columns (unfold, in prototype_vectors.reshape(P, -1)'s (c, dy, dx) order),
+        # then the same kernels on 1x1 prototypes of depth C k k; autograd folds g_x back
+        if prototype_vectors.shape[1] != x.shape[1]:
+            raise _lib.ProtosegError(f"prototype depth {prototype_vectors.shape[1]} != feature channels {x.shape[1]}")
+        B, C, H, W = x.shape
+        kh, kw = kernel
+        if kh > H or kw > W:
+            raise _lib.ProtosegError(f"{kh}x{kw} prototypes on a {H}x{W} map")
+        if x.dtype == torch.float16:
+            x = x.float()
+        if x_sigmoid:
+            x, x_sigmoid = torch.sigmoid(x), False
+        x = torch.nn.functional.unfold(x, (kh, kw)).reshape(B, C * kh * kw, H - kh + 1, W - kw + 1)
     if protos.shape[1] != x.shape[1]:
         raise _lib.ProtosegError(f"prototype depth {protos.shape[1]} != feature channels {x.shape[1]}")
-    if tuple(prototype_vectors.shape[2:]) not in ((), (1, 1)):
-        raise _lib.ProtosegError(f"only 1x1 prototypes are supported, got {tuple(prototype_vectors.shape)}")
     if x.dtype == torch.float16:
         # fp16 feature maps (BASELINE config 5, DenseNet-161 fp16): widened exactly to f32 at the
         # boundary; the layer computes as for f32 input and autograd narrows g_x back to fp16.

@@ -87,6 +87,8 @@ def push_argmin(x: Tensor, protos: Tensor, proto_class: Tensor, mask: Tensor, wi
     protos = protos.reshape(protos.shape[0], -1).float().contiguous()
     n, C, h, w = x.shape
     P = protos.shape[0]
+    if protos.shape[1] != C:
+        raise _lib.ProtosegError(f"push_argmin: prototypes hold {protos.shape[1]} values, the map {C} channels")
     keys = torch.empty((n, P), device=dev, dtype=torch.int64)
     second = torch.empty_like(keys) if with_second else None
     with torch.cuda.device(dev):
@@ -161,6 +163,9 @@ def push_update(state: PushState, x: Tensor, labels: Tensor, protos: Tensor, pro
     dev = _lib.require_device(x, labels, protos, proto_class, lut)
     protos = protos.reshape(protos.shape[0], -1).float().contiguous()
     P = protos.shape[0]
+    if protos.shape[1] != C:
+        raise _lib.ProtosegError(f"push projects 1x1 prototypes (depth {C}); got {protos.shape[1]} values per "
+                                 "prototype (k x k prototypes: push.py's patch windows are not built here)")
     if state.second is None:
         state.second = torch.full((P,), math.inf, device=dev, dtype=torch.float32)
     pc = proto_class if proto_class.dtype == torch.int32 and proto_class.is_contiguous() \
@@ -364,7 +369,7 @@ def batch_bound_boxes(items, protos: Tensor, proto_class: np.ndarray, rf_boxes_a
         g["ids"].extend(int(j) for j in ids)
         g["dist"].append(dist)
         g["labels"].append(labels.reshape(labels.shape[-2:]))
-    max_dist = float(protos.shape[1])  # push.py:229 prototype_shape[1] * [2] * [3]
+    max_dist = float(np.prod(protos.shape[1:]))  # push.py:229 prototype_shape[1] * [2] * [3]
     out: Dict[int, tuple] = {}
     for (_, (H, W), _), g in groups.items():
         dist = torch.cat(g["dist"], 0)
@@ -476,7 +481,19 @@ def push_prototypes(dataset, prototype_network_parallel, prototype_layer_stride=
     log("\tpush")
     start = time.time()
     device = ppnet.prototype_vectors.device
-    P, C = ppnet.num_prototypes, ppnet.prototype_shape[1]
+    P = ppnet.num_prototypes
+    shape = tuple(ppnet.prototype_shape)
+    kh, kw = (shape[2], shape[3]) if len(shape) == 4 else (1, 1)
+    C = int(np.prod(shape[1:]))  # values per prototype: the k x k window, C k k deep
+
+    def scan_features(f):
+        """The push's view of a feature map: each k x k window as one column (push.py:276-280
+        takes protoL_input_[:, i:i+h, j:j+w]), the 1 x 1 kernels on a C k k deep map."""
+        if (kh, kw) == (1, 1):
+            return f
+        n, c, H, W = f.shape
+        return torch.nn.functional.unfold(f, (kh, kw)).reshape(n, c * kh * kw, H - kh + 1, W - kw + 1)
+
     proto_class_t = prototype_classes(ppnet).to(device)
     proto_class = proto_class_t.cpu().numpy()
     words = mask_words(int(proto_class.max()) + 1)
@@ -524,7 +541,7 @@ def push_prototypes(dataset, prototype_network_parallel, prototype_layer_stride=
         and the exact-tie resolution compares distances exactly)."""
         ids = scan_runs.get(push_iter, [push_iter])
         raw = [load_raw(i) for i in ids]
-        feats = ppnet.conv_features(torch.cat([r[0] for r in raw], 0))
+        feats = scan_features(ppnet.conv_features(torch.cat([r[0] for r in raw], 0)))
         k = ids.index(push_iter)
         return feats[k:k + 1], raw[k][1]
 
@@ -540,7 +557,7 @@ def push_prototypes(dataset, prototype_network_parallel, prototype_layer_stride=
             if run:
                 imgs = torch.cat([r[0] for r in run], 0)
                 labels = torch.stack([r[1] for r in run], 0)
-                push_update(state, ppnet.conv_features(imgs), labels, ppnet.prototype_vectors, proto_class_t,
+                push_update(state, scan_features(ppnet.conv_features(imgs)), labels, ppnet.prototype_vectors, proto_class_t,
                             run[0][2], lut, words)
                 ids = [r[2] for r in run]
                 for i in ids:

@@ -521,3 +521,31 @@ def test_ppnet_forward_image_fuses_add_on_sigmoid(device):
     g_ref = [p.grad for p in net.features.parameters() if p.grad is not None]
     for a, b in zip(g_head, g_ref):
         assert_scaled_close(a, b, 1e-3, "backbone grad")
+
+
+@pytest.mark.parametrize("kh,kw,C", [(3, 3, 64), (2, 3, 32)])
+def test_kxk_prototypes_vs_oracle(device, kh, kw, C):
+    """k x k prototypes (model.py:203-221 with prototype_shape[2:] > 1): the layer runs on the
+    unfolded map (wide family at C k k); distances, logits and every gradient against the oracle's
+    F.conv2d formulation and its autograd."""
+    ops = _ops()
+    B, h, w, P, K = 2, 13, 17, 38, 19
+    gen = torch.Generator().manual_seed(kh * 10 + kw)
+    x = torch.sigmoid(2 * torch.randn(B, C, h, w, generator=gen))
+    protos = torch.rand(P, C, kh, kw, generator=gen)
+    w_last = po.last_layer_init(po.class_identity(P, K))
+    g_logits = torch.randn(B, h - kh + 1, w - kw + 1, K, generator=gen)
+    xr, pr, wr = (t.clone().requires_grad_(True) for t in (x, protos, w_last))
+    ref_logits, ref_dist = po.forward_from_conv_features(xr, pr, wr)
+    (ref_logits * g_logits).sum().backward()
+    xd, pd, wd = (t.to(device).requires_grad_(True) for t in (x, protos, w_last))
+    dist, logits, _ = ops.prototype_layer(xd, pd, wd)
+    (logits * g_logits.to(device)).sum().backward()
+    torch.cuda.synchronize()
+    assert dist.shape == (B, P, h - kh + 1, w - kw + 1)
+    xu = torch.nn.functional.unfold(x, (kh, kw)).reshape(B, C * kh * kw, h - kh + 1, w - kw + 1)
+    assert_dist_close(dist, ref_dist.detach(), xu, protos.reshape(P, -1))
+    assert_scaled_close(logits, ref_logits.detach(), 1e-4, "logits")
+    assert_scaled_close(xd.grad, xr.grad, 1e-4, "g_x")
+    assert_scaled_close(pd.grad, pr.grad, 1e-4, "g_protos")
+    assert_scaled_close(wd.grad, wr.grad, 1e-4, "g_w")

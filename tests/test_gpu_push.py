@@ -407,3 +407,64 @@ def test_push_update_one_call_equals_three_calls(device):
     torch.cuda.synchronize()
     for f in ("dist", "second", "img", "patch", "fmap"):
         assert torch.equal(getattr(a, f), getattr(b, f)), f
+
+
+def test_push_prototypes_kxk_prototypes(device, tmp_path):
+    """push_prototypes with 2 x 2 prototypes (push.py:276-280 keeps the k x k window
+    protoL_input_[:, i:i+h, j:j+w]): the scan runs on the unfolded map; winners, patches and the
+    pushed windows equal the reference loop (oracle push.py:195-307) on the same windows."""
+    from PIL import Image
+
+    from oracle import push_oracle as pu
+    from protoseg_amd.deeplab import deeplabv2_resnet101_features
+    from protoseg_amd.model import PPNet
+    from protoseg_amd.push import push_prototypes, to_normalized_tensor
+
+    push = _push()
+    torch.manual_seed(1)
+    P, K, C, k = 38, 19, 64, 2
+    net = PPNet(deeplabv2_resnet101_features(n_blocks=(1, 1, 1, 1), scales=[]), 513, (P, C, k, k), None, K,
+                add_on_layers_type="deeplab_simple").to(device).eval()
+    proj = torch.randn(C, 3, generator=torch.Generator().manual_seed(4)).to(device)
+    # an elementwise stand-in backbone: bit-reproducible across calls and batch compositions
+    net.conv_features = lambda imgs: torch.sigmoid(torch.einsum("oc,nchw->nohw", proj,
+                                                                torch.nn.functional.avg_pool2d(imgs, 8)))
+    rng = np.random.default_rng(3)
+    img_dir, ann_dir = tmp_path / "img", tmp_path / "ann"
+    img_dir.mkdir()
+    ann_dir.mkdir()
+
+    class DS:
+        img_ids = [f"im{i}" for i in range(3)]
+        image_margin_size = 4
+        annotations_dir = str(ann_dir)
+
+        def get_img_path(self, img_id):
+            return str(img_dir / f"{img_id}.png")
+
+    ds = DS()
+    for img_id in ds.img_ids:
+        Image.fromarray(rng.integers(0, 256, size=(72, 104, 3), dtype=np.uint8)).save(ds.get_img_path(img_id))
+        np.save(ann_dir / f"{img_id}.npy", rng.integers(0, K + 1, size=(64, 96)).astype(np.int64))
+    protos0 = net.prototype_vectors.detach().reshape(P, -1).clone()
+    pc = push.prototype_classes(net).cpu().numpy()
+    with torch.no_grad():
+        imgs = torch.cat([to_normalized_tensor(Image.open(ds.get_img_path(i)).convert("RGB").crop((4, 4, 100, 68)))
+                          .unsqueeze(0) for i in ds.img_ids]).to(device)
+        f = net.conv_features(imgs)
+        n, c, H, W = f.shape
+        feats = torch.nn.functional.unfold(f, (k, k)).reshape(n, c * k * k, H - k + 1, W - k + 1)
+    state = push_prototypes(ds, net, images_per_batch=8, log=lambda *_: None)
+    ref = pu.PushOracleState(P, C * k * k)
+    h, w = feats.shape[2:]
+    for i, img_id in enumerate(ds.img_ids):
+        d = push.push_distances(feats[i:i + 1], protos0).cpu().numpy()
+        pu.update_prototypes_on_image_core(ref, feats[i].cpu().numpy(), d.reshape(P, h, w).transpose(1, 2, 0),
+                                           np.load(ann_dir / f"{img_id}.npy"), pc, K, i)
+    found = ref.proto_rf_boxes[:, 0] >= 0
+    assert found.sum() > 10
+    assert np.array_equal(state.img.cpu().numpy(), ref.proto_rf_boxes[:, 0])
+    assert np.array_equal(state.patch.cpu().numpy()[found], ref.winner_patch[found])
+    assert np.array_equal(state.fmap.cpu().numpy()[found],
+                          ref.global_min_fmap_patches.reshape(P, -1)[found].astype(np.float32))
+    assert tuple(net.prototype_vectors.shape[1:]) == (C, k, k)  # pushed windows keep the k x k shape
