@@ -32,7 +32,6 @@ namespace {
 constexpr int kWT = 64;        // workgroup output tile (rows and columns)
 constexpr int kWKs = 32;       // contraction per LDS stage
 constexpr int kWThreads = 256;
-constexpr int kWLd = kWT + 1;  // LDS row pitch (floats), odd: a k-fast store (32 k rows of one column) hits 32 banks
 
 enum WideEpi { kEpiStore = 0, kEpiDist = 1, kEpiGs = 2, kEpiGx = 3 };
 
@@ -74,20 +73,26 @@ __device__ __forceinline__ float on_load(float v, float eps) {
   else return activation(v, eps, ACT);
 }
 
-// One operand's share of a 64-row x 32-k stage: eight elements per thread.
-//   MODE 0 (rows fast): row t & 63, k = (t >> 6) + 4i — 64 consecutive rows per k, coalesced;
+// One operand's share of a ROWS-row x 32-k stage (ROWS = 64 or 128): ROWS / 8 elements per thread.
+//   MODE 0 (rows fast): row t % ROWS, k = t / ROWS + (256 / ROWS) i — ROWS consecutive rows per
+//                       k, coalesced;
 //   MODE 1 (k fast):    k = t & 31, row (t >> 5) + 8i — 32 consecutive k per row, coalesced.
 // The element's row (and, MODE 0, k) offset is fixed for the whole contraction; the stage moves
 // a uniform base (non-bk) or, for a k-fast operand over the flattened (batch, pixel) contraction,
 // one per-thread (batch, k) position advanced by 32 per stage (no division in the loop).
-template <typename T, int ACT, int MODE>
+template <typename T, int ACT, int MODE, int ROWS>
 struct Stager {
+  static constexpr int kE = ROWS / 8;
+  static constexpr int kLd = ROWS + 1;  // LDS row pitch (odd: k-fast stores spread over the banks)
   const T* p;
-  unsigned fix[8];
+  unsigned fix[kE];
   unsigned rok;  // bit i: element i's row is inside the operand
   int kt;        // MODE 1: this thread's k in the stage
   int bb, kin;   // MODE 1, bk: batch and in-batch k of this thread's current contraction index
   unsigned sb;
+
+  __device__ __forceinline__ static int row_of_e(int t, int i) { return MODE == 0 ? (t % ROWS) : (t >> 5) + 8 * i; }
+  __device__ __forceinline__ static int k_of_e(int t, int i) { return MODE == 0 ? t / ROWS + (256 / ROWS) * i : (t & 31); }
 
   __device__ __forceinline__ void init(const Operand& o, int R, int r0, int kbeg, int Kd, int bk) {
     p = static_cast<const T*>(o.p);
@@ -95,9 +100,8 @@ struct Stager {
     rok = 0;
     sb = o.sb;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int r = MODE == 0 ? (t & 63) : (t >> 5) + 8 * i;
-      const int k = MODE == 0 ? (t >> 6) + 4 * i : (t & 31);
+    for (int i = 0; i < kE; ++i) {
+      const int r = row_of_e(t, i), k = k_of_e(t, i);
       const bool ok = r0 + r < R;
       rok |= ok ? (1u << i) : 0u;
       fix[i] = ok ? (MODE == 0 ? static_cast<unsigned>(r0 + r) + static_cast<unsigned>(k) * o.sk
@@ -114,15 +118,15 @@ struct Stager {
   // Stage at contraction base kb (flattened for bk); lim = kend - kb; base = the stage's uniform
   // offset. Raw values: the zeroing of elements outside the operand (okm) and the activation
   // happen in store(), after the MFMAs the loads are in flight under.
-  __device__ __forceinline__ void load(unsigned base, int lim, int bk, float (&v)[8], unsigned& okm) const {
+  __device__ __forceinline__ void load(unsigned base, int lim, int bk, float (&v)[kE], unsigned& okm) const {
     const unsigned kofs = MODE == 1 ? (bk ? static_cast<unsigned>(bb) * sb + static_cast<unsigned>(kin)
                                           : static_cast<unsigned>(kt))
                                     : 0u;
+    okm = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int k = MODE == 0 ? (static_cast<int>(threadIdx.x) >> 6) + 4 * i : kt;
+    for (int i = 0; i < kE; ++i) {
+      const int k = k_of_e(static_cast<int>(threadIdx.x), i);
       const bool ok = ((rok >> i) & 1u) && k < lim;
-      if (i == 0) okm = 0;
       okm |= ok ? (1u << i) : 0u;
       // branch-free: an element outside the operand loads element 0 (zeroed in store())
       v[i] = XIO<T>::load(p, static_cast<size_t>(ok ? base + fix[i] + kofs : 0u));
@@ -135,13 +139,12 @@ struct Stager {
       ++bb;
     }
   }
-  __device__ __forceinline__ void store(float (*S)[kWLd], const float (&v)[8], unsigned okm, float eps) const {
+  __device__ __forceinline__ void store(float* S, const float (&v)[kE], unsigned okm, float eps) const {
     const int t = threadIdx.x;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < kE; ++i) {
       const float x = ((okm >> i) & 1u) ? on_load<ACT>(v[i], eps) : 0.f;
-      if (MODE == 0) S[(t >> 6) + 4 * i][t & 63] = x;
-      else S[t & 31][(t >> 5) + 8 * i] = x;
+      S[k_of_e(t, i) * kLd + row_of_e(t, i)] = x;
     }
   }
 };
@@ -154,25 +157,31 @@ __device__ __forceinline__ unsigned stage_base(const Operand& o, int b, int kb, 
   return static_cast<unsigned>(b) * o.sb + static_cast<unsigned>(kb) * (MODE == 0 ? o.sk : 1u);
 }
 
-// C[z] (64 x 64 tile) = A (M x Kd) B^T (N x Kd) over 32-k stages, double-buffered in LDS (one
-// barrier per stage, the next stage's global loads in flight under this stage's 16 MFMAs per
-// wave), v_mfma_f32_32x32x2_f32: exact f32 fma chains in k order.
+// C[z] (TM x 64 tile, TM = 64 or 128 rows) = A (M x Kd) B^T (N x Kd) over 32-k stages,
+// double-buffered in LDS (one barrier per stage, the next stage's global loads in flight under
+// this stage's MFMAs), v_mfma_f32_32x32x2_f32: exact f32 fma chains in k order. TM = 64: each of
+// the 4 waves one 32 x 32 block; TM = 128 (M >= 256): each wave a 32-row strip of two blocks,
+// which halves the B-operand traffic per product and reads each A fragment once for two MFMAs.
 // The epilogues' per-column / per-row sums come from the same LDS stages (a non-split workgroup
 // contracts over the whole Kd of its batch): kEpiDist: x2[n] = sum_c X[c][n]^2 (B columns) and
-// p2[m] = sum_c P[m][c]^2 (A rows); kEpiGx: cs[n] = sum_p G_s[p][n] (B columns). Thread t sums
-// column t & 63 of stage rows 8 (t >> 6) .. + 7; the four partials are added in a fixed order:
-// deterministic, the same bits in every workgroup of a column, and no separate norms pass.
-template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO, int MA, int MB>
+// p2[m] = sum_c P[m][c]^2 (A rows); kEpiGx: cs[n] = sum_p G_s[p][n] (B columns). Thread t sums one
+// column (row) over a fixed slice of the stage's k rows; the slices' partials are added in a fixed
+// order: deterministic, the same bits in every workgroup of a column, no separate norms pass.
+template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO, int MA, int MB, int TM>
 __global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
-  __shared__ float As[2][kWKs][kWLd];
-  __shared__ float Bs[2][kWKs][kWLd];
+  constexpr int kLdA = TM + 1, kLdB = kWT + 1;
+  constexpr int kNC = TM == 128 ? 2 : 1;  // 32-column blocks per wave
+  constexpr int kQA = kWThreads / TM;     // k slices of the A-row sums
+  __shared__ float As[2][kWKs * kLdA];
+  __shared__ float Bs[2][kWKs * kLdB];
   constexpr bool kSumB = EPI == kEpiDist || EPI == kEpiGx, kSumA = EPI == kEpiDist, kSq = EPI == kEpiDist;
-  __shared__ float red[kSumB ? 2 : 1][4][64];
+  __shared__ float redB[kSumB ? 4 : 1][64];
+  __shared__ float redA[kSumA ? kQA : 1][kSumA ? TM : 1];
   float sum_b = 0.f, sum_a = 0.f;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int j = lane & 31, h = lane >> 5;
-  const int wm = wave & 1, wn = wave >> 1;
-  const int m0 = blockIdx.y * kWT, n0 = blockIdx.x * kWT, z = blockIdx.z;
+  const int wm = TM == 128 ? wave : (wave & 1), wn0 = TM == 128 ? 0 : (wave >> 1);
+  const int m0 = blockIdx.y * TM, n0 = blockIdx.x * kWT, z = blockIdx.z;
   // contraction range of this workgroup (flattened (batch, k) units for bk), whole stages
   const int split = a.bk ? z : z % a.ksplit, bsel = a.bk ? 0 : z / a.ksplit;
   const long long total = a.bk ? static_cast<long long>(a.nb) * a.Kd : a.Kd;
@@ -180,12 +189,14 @@ __global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
   const int kbeg = static_cast<int>((chunks * split / a.ksplit) * kWKs);
   int kend = static_cast<int>((chunks * (split + 1) / a.ksplit) * kWKs);
   if (kend > total) kend = static_cast<int>(total);
-  Stager<TA, AACT, MA> sa;
-  Stager<TB, BACT, MB> sb;
+  Stager<TA, AACT, MA, TM> sa;
+  Stager<TB, BACT, MB, kWT> sb;
   sa.init(a.A, a.M, m0, kbeg, a.Kd, a.bk);
   sb.init(a.B, a.N, n0, kbeg, a.Kd, a.bk);
-  f32x16 acc = zero16();
-  float va[8], vb[8];
+  f32x16 acc[kNC];
+#pragma unroll
+  for (int c = 0; c < kNC; ++c) acc[c] = zero16();
+  float va[TM / 8], vb[kWT / 8];
   unsigned oka = 0, okb = 0;
   const int nst = kend > kbeg ? (kend - kbeg + kWKs - 1) / kWKs : 0;
   if (nst > 0) {
@@ -207,19 +218,28 @@ __global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
       sa.load(stage_base<MA>(a.A, bsel, kb, a.bk), kend - kb, a.bk, va, oka);
       sb.load(stage_base<MB>(a.B, bsel, kb, a.bk), kend - kb, a.bk, vb, okb);
     }
+    const float* Ac = As[cur];
+    const float* Bc = Bs[cur];
 #pragma unroll
-    for (int kk = 0; kk < kWKs / 2; ++kk)
-      acc = mfma32(As[cur][2 * kk + h][wm * 32 + j], Bs[cur][2 * kk + h][wn * 32 + j], acc);
+    for (int kk = 0; kk < kWKs / 2; ++kk) {
+      const float av = Ac[(2 * kk + h) * kLdA + wm * 32 + j];
+#pragma unroll
+      for (int c = 0; c < kNC; ++c) acc[c] = mfma32(av, Bc[(2 * kk + h) * kLdB + (wn0 + c) * 32 + j], acc[c]);
+    }
     if constexpr (kSumB) {
       const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const float vbv = Bs[cur][8 * q + i][c];
+        const float vbv = Bc[(8 * q + i) * kLdB + c];
         sum_b = kSq ? fmaf(vbv, vbv, sum_b) : sum_b + vbv;
-        if constexpr (kSumA) {
-          const float vav = As[cur][8 * q + i][c];
-          sum_a = fmaf(vav, vav, sum_a);
-        }
+      }
+    }
+    if constexpr (kSumA) {
+      const int r = threadIdx.x % TM, q = threadIdx.x / TM;
+#pragma unroll
+      for (int i = 0; i < kWKs / kQA; ++i) {
+        const float vav = Ac[((kWKs / kQA) * q + i) * kLdA + r];
+        sum_a = fmaf(vav, vav, sum_a);
       }
     }
     if (more) {
@@ -228,43 +248,46 @@ __global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
     }
     __syncthreads();
   }
-  if constexpr (kSumB) {
-    red[0][threadIdx.x >> 6][threadIdx.x & 63] = sum_b;
-    red[1][threadIdx.x >> 6][threadIdx.x & 63] = sum_a;
-    __syncthreads();
-  }
+  if constexpr (kSumB) redB[threadIdx.x >> 6][threadIdx.x & 63] = sum_b;
+  if constexpr (kSumA) redA[threadIdx.x / TM][threadIdx.x % TM] = sum_a;
+  if constexpr (kSumB) __syncthreads();
 
   // epilogue: lane column n, rows acc_row(r, h)
-  const int n = n0 + wn * 32 + j;
-  if (n >= a.N) return;
   const int bo = a.bk ? z : (a.ksplit > 1 ? z : bsel);  // output batch (or split slab) index
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int m = m0 + wm * 32 + acc_row(r, h);
-    if (m >= a.M) continue;
-    const long long o = bo * a.ob + m * a.om + static_cast<long long>(n) * a.on;
-    float v = acc[r];
-    if constexpr (EPI == kEpiDist) {
-      const int cn = wn * 32 + j, rm = m - m0;
-      const float x2 = (red[0][0][cn] + red[0][1][cn]) + (red[0][2][cn] + red[0][3][cn]);
-      const float p2 = (red[1][0][rm] + red[1][1][rm]) + (red[1][2][rm] + red[1][3][rm]);
-      const float d = l2_distance(x2, p2, v);
-      v = d;
-      if (a.act) a.act[bo * a.ab + m * a.am + static_cast<long long>(n) * a.an] = activation(d, a.eps, a.act_kind);
-    } else if constexpr (EPI == kEpiGs) {
-      const float d = a.D[o];
-      float g = v * activation_grad(d, a.eps, a.act_kind);
-      if (a.gd) g += a.gd[o];
-      v = d > 0.f ? g : 0.f;  // relu backward
-    } else if constexpr (EPI == kEpiGx) {
-      // conv(x^2, ones) backward: 2x sum_p g_s; conv(x, P) backward: -2 P^T g_s
-      const int cn = wn * 32 + j;
-      const float cs = (red[0][0][cn] + red[0][1][cn]) + (red[0][2][cn] + red[0][3][cn]);
-      v = -2.f * v + 2.f * load_elem<TO>(a.xo, o) * cs;
+  for (int c = 0; c < kNC; ++c) {
+    const int cn = (wn0 + c) * 32 + j;
+    const int n = n0 + cn;
+    if (n >= a.N) continue;
+    float colsum = 0.f;
+    if constexpr (kSumB) colsum = (redB[0][cn] + redB[1][cn]) + (redB[2][cn] + redB[3][cn]);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rm = wm * 32 + acc_row(r, h);
+      const int m = m0 + rm;
+      if (m >= a.M) continue;
+      const long long o = bo * a.ob + m * a.om + static_cast<long long>(n) * a.on;
+      float v = acc[c][r];
+      if constexpr (EPI == kEpiDist) {
+        float p2;
+        if constexpr (kQA == 4) p2 = (redA[0][rm] + redA[1][rm]) + (redA[2][rm] + redA[3][rm]);
+        else p2 = redA[0][rm] + redA[1][rm];
+        const float d = l2_distance(colsum, p2, v);
+        v = d;
+        if (a.act) a.act[bo * a.ab + m * a.am + static_cast<long long>(n) * a.an] = activation(d, a.eps, a.act_kind);
+      } else if constexpr (EPI == kEpiGs) {
+        const float d = a.D[o];
+        float g = v * activation_grad(d, a.eps, a.act_kind);
+        if (a.gd) g += a.gd[o];
+        v = d > 0.f ? g : 0.f;  // relu backward
+      } else if constexpr (EPI == kEpiGx) {
+        // conv(x^2, ones) backward: 2x sum_p g_s; conv(x, P) backward: -2 P^T g_s
+        v = -2.f * v + 2.f * load_elem<TO>(a.xo, o) * colsum;
+      }
+      TO* out = static_cast<TO*>(a.out);
+      if (a.accumulate) v += XIO<TO>::load(out, static_cast<size_t>(o));
+      XIO<TO>::store(out, static_cast<size_t>(o), v);
     }
-    TO* out = static_cast<TO*>(a.out);
-    if (a.accumulate) v += XIO<TO>::load(out, static_cast<size_t>(o));
-    XIO<TO>::store(out, static_cast<size_t>(o), v);
   }
 }
 
@@ -313,23 +336,32 @@ int stager_mode(const Operand& o, const WideArgs& a) {
   return o.sk == 1 ? 1 : -1;
 }
 
+#ifndef WIDE_TM128
+#define WIDE_TM128 1  // 128-row tiles for M >= 256
+#endif
+template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO, int TM>
+int gemm_tm(const WideArgs& a, int grid_z, int ma, int mb, hipStream_t s) {
+  const dim3 grid(static_cast<unsigned>(ceil_div(a.N, kWT)), static_cast<unsigned>(ceil_div(a.M, TM)),
+                  static_cast<unsigned>(grid_z));
+  if (ma == 0 && mb == 0)
+    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 0, 0, TM>), grid, dim3(kWThreads), 0, s, a);
+  else if (ma == 0)
+    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 0, 1, TM>), grid, dim3(kWThreads), 0, s, a);
+  else if (mb == 0)
+    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 1, 0, TM>), grid, dim3(kWThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 1, 1, TM>), grid, dim3(kWThreads), 0, s, a);
+  return check_launch("wide_gemm_kernel");
+}
+
 // grid_z: batches x splits (or the bk splits); a.ksplit 0 means 1.
 template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO>
 int gemm(WideArgs a, int grid_z, hipStream_t s) {
   if (a.ksplit < 1) a.ksplit = 1;
-  const dim3 grid(static_cast<unsigned>(ceil_div(a.N, kWT)), static_cast<unsigned>(ceil_div(a.M, kWT)),
-                  static_cast<unsigned>(grid_z));
   const int ma = stager_mode(a.A, a), mb = stager_mode(a.B, a);
   if (ma < 0 || mb < 0) return fail(PROTOSEG_ERR_UNSUPPORTED, "wide GEMM operand with no unit stride");
-  if (ma == 0 && mb == 0)
-    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 0, 0>), grid, dim3(kWThreads), 0, s, a);
-  else if (ma == 0)
-    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 0, 1>), grid, dim3(kWThreads), 0, s, a);
-  else if (mb == 0)
-    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 1, 0>), grid, dim3(kWThreads), 0, s, a);
-  else
-    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 1, 1>), grid, dim3(kWThreads), 0, s, a);
-  return check_launch("wide_gemm_kernel");
+  if (WIDE_TM128 && a.M >= 256) return gemm_tm<EPI, TA, TB, AACT, BACT, TO, 128>(a, grid_z, ma, mb, s);
+  return gemm_tm<EPI, TA, TB, AACT, BACT, TO, 64>(a, grid_z, ma, mb, s);
 }
 
 // Workgroups along a contraction of `total` for `groups` output tiles (x batches): about 1024
@@ -341,11 +373,12 @@ int split_of(long long groups, long long total) {
   if (s > 64) s = 64;
   return static_cast<int>(s < 1 ? 1 : s);
 }
-int split_of(int M, int N, long long total) { return split_of(ceil_div(M, kWT) * ceil_div(N, kWT), total); }
+int tile_rows(int M) { return WIDE_TM128 && M >= 256 ? 128 : 64; }  // gemm()'s choice
+int split_of(int M, int N, long long total) { return split_of(ceil_div(M, tile_rows(M)) * ceil_div(N, kWT), total); }
 // The logits GEMM (M = HW, N = K per image): split over the prototypes when the images' tiles
 // alone leave the CUs idle.
 int logits_split(const Geometry& g) {
-  const long long groups = ceil_div(g.HW, kWT) * ceil_div(g.K, kWT) * (g.npix / g.HW);
+  const long long groups = ceil_div(g.HW, tile_rows(g.HW)) * ceil_div(g.K, kWT) * (g.npix / g.HW);
   return groups >= 512 ? 1 : split_of(groups, g.P);
 }
 

@@ -63,6 +63,14 @@ for step in "$@"; do
           || { tail -20 gpurun_out/${T}_ab_fwd_$P.log; exit 1; }
         tail -4 gpurun_out/${T}_ab_fwd_$P.log
       done ;;
+    sqwide)  # SQ counters over the configs[4] wide step alone
+      TAG=wide_c4_$T DRIVER=tools/wide_run.py DRIVER_ARGS="c4 3" bash tools/pmc_bwd.sh > gpurun_out/${T}_sqwide.log 2>&1 \
+        || { tail -20 gpurun_out/${T}_sqwide.log; exit 1; }
+      grep -E "wide_gemm|derived" gpurun_out/${T}_sqwide.log | head -20 ;;
+    sqpush)  # SQ counters over the push inner step alone
+      TAG=push_$T DRIVER=tools/push_trace.py DRIVER_ARGS="8 5" bash tools/pmc_bwd.sh > gpurun_out/${T}_sqpush.log 2>&1 \
+        || { tail -20 gpurun_out/${T}_sqpush.log; exit 1; }
+      grep -E "push_argmin|patch_mask|derived" gpurun_out/${T}_sqpush.log | head -20 ;;
     diag)
       timeout -k 10 300 python -u tools/debug/kld_compact_diag.py > gpurun_out/${T}_diag.log 2>&1; tail -30 gpurun_out/${T}_diag.log ;;
     smoke)

@@ -1,5 +1,6 @@
 #!/bin/bash
-# SQ counter passes over tools/bwd_driver.py (one counter group per pass; kernel trace only).
+# SQ counter passes over tools/bwd_driver.py, or the script DRIVER names (one counter group per
+# pass; kernel trace only).
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${TAG:-bwd}
@@ -13,7 +14,7 @@ for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WA
   i=$((i+1))
   echo "== pass $i: $grp"
   timeout -k 10 120 rocprofv3 --kernel-trace --pmc $grp -d "$OUT/p$i" -o p$i --output-format csv -- \
-    python3 "$R/tools/bwd_driver.py" ${DRIVER_ARGS:-} > "$OUT/p$i.log" 2>&1
+    python3 "$R/${DRIVER:-tools/bwd_driver.py}" ${DRIVER_ARGS:-} > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "rc=$rc"; tail -n 1 "$OUT/p$i.log"
   if [ $rc -ne 0 ]; then exit $rc; fi
