@@ -20,7 +20,7 @@ namespace {
 
 constexpr int kAdamMaxTensors = 8;
 constexpr int kAdamBlock = 256;
-constexpr int kAdamPerThread = 16;  // elements per thread: fewer workgroups, fewer step-count tickets
+constexpr int kAdamPerThread = 4;
 
 struct AdamTensors {
   float* p[kAdamMaxTensors];

@@ -6,8 +6,7 @@
 //   forward (protoseg_kld_forward):
 //   kld_partial_kernel   one workgroup per (class c, image b, pixel range s): the class's prototype
 //                        list (ascending ids, module.py:173; published once for the later
-//                        kernels), the range's class pixels, their class distances gathered once
-//                        (kept per pixel in zc for the backward), one pass with a running max:
+//                        kernels), the range's class pixels, one pass with a running max:
 //                        the local max m_i and sum_n exp(z_i - m_i) of each class prototype
 //                        (z = distance) and T_ij = sum_n exp(z_i - m_i) (z_i - z_j)
 //   kld_merge_kernel     per (c, b): L_i = log-sum-exp over the ranges (module.py:183) and
@@ -16,7 +15,7 @@
 //   kld_finalize_kernel  mean of exp(-(KL_ij + KL_ji) / 2) over all pairs (module.py:199-206)
 //   backward, compact layout (protoseg_kld_backward_compact), ONE launch:
 //   kld_grad_compact_kernel  per (c, b, s): proto_slot, pix_cls of the range's pixels, the
-//                        group's coefficients and the gradient at its class pixels from zc
+//                        group's coefficients and the gradient at its class pixels
 //   backward, dense layout (protoseg_kld_backward): kld_coef_kernel + kld_grad_kernel, the
 //                        [B, P, HW] gradient autograd of the reference ops produces
 // Only the class's own prototype rows are read at the class's pixels (about 1/K of the distance
@@ -44,9 +43,7 @@ constexpr int kKldThreads = 256;     // = pixels per staged chunk
 #define KLD_RANGE 1024
 #endif
 constexpr int kKldRange = KLD_RANGE;
-#ifndef KLD_ZC
-#define KLD_ZC 1  // the forward keeps the gathered class distances per pixel for the compact backward
-#endif  // pixels per kld_partial_kernel workgroup (a multiple of 256)
+  // pixels per kld_partial_kernel workgroup (a multiple of 256)
 constexpr int kKldPair = kKldMaxPerClass * kKldMaxPerClass;
 constexpr int kKldLdsStride = kKldThreads + 1;  // padded rows: conflict-free task reads
 constexpr size_t kKldMaxDynLds = 2 * kKldMaxPerClass * kKldLdsStride * sizeof(float);
@@ -69,7 +66,6 @@ struct KldLayout {
   size_t slot;   // int [P]: bucket * 256 + position in the bucket (the compact gradient's column)
   size_t rcnt;   // int [B * K * S]: class pixels in each 1024-pixel range
   size_t plist;  // int [B * K * HW]: per (image, class) the class pixels of range s at s * 1024 + q
-  size_t zc;     // float [B * HW * 32]: each pixel's own-class distances by class slot (row stride mpc)
   size_t total;
 };
 
@@ -99,8 +95,6 @@ KldLayout kld_layout(int B, int P, int HW, int K) {
   o = align256(o + static_cast<size_t>(B) * K * kld_ranges(HW) * 4);
   l.plist = o;
   o = align256(o + static_cast<size_t>(B) * K * HW * 4);
-  l.zc = o;
-  o = align256(o + static_cast<size_t>(B) * HW * kKldMaxPerClass * 4);
   l.total = o;
   return l;
 }
@@ -109,7 +103,6 @@ struct KldPtrs {
   int *off, *idx, *cnt, *stat;
   float *lse, *kl, *part, *group;
   int *slot, *rcnt, *plist;
-  float* zc;
 };
 
 KldPtrs kld_ptrs(void* ws, const KldLayout& l) {
@@ -119,7 +112,7 @@ KldPtrs kld_ptrs(void* ws, const KldLayout& l) {
           reinterpret_cast<float*>(b + l.lse),  reinterpret_cast<float*>(b + l.kl),
           reinterpret_cast<float*>(b + l.part), reinterpret_cast<float*>(b + l.group),
           reinterpret_cast<int*>(b + l.slot),   reinterpret_cast<int*>(b + l.rcnt),
-          reinterpret_cast<int*>(b + l.plist),  reinterpret_cast<float*>(b + l.zc)};
+          reinterpret_cast<int*>(b + l.plist)};
 }
 
 __device__ __forceinline__ int bucket_of(int pc, int K) { return (pc >= 0 && pc < K) ? pc : K; }
@@ -139,35 +132,48 @@ __device__ __forceinline__ void class_list_scan(const int32_t* __restrict__ prot
                                                 bool publish, int* first, int* start_out, int* cnt_out,
                                                 int* __restrict__ off, int* __restrict__ idx, int* __restrict__ slot) {
   const int lane = threadIdx.x & 63;
-  int start = 0;
-  for (int p0 = 0; p0 < P; p0 += 64) {
-    const int p = p0 + lane;
-    const int pc = p < P ? proto_class[p] : -1;
-    const int bk = p < P ? ((pc >= 0 && pc < K) ? pc : K) : K + 1;
-    start += __popcll(__ballot(bk < c));
+  // one pass: the bucket start (prototypes of lower buckets) and the members in ascending order;
+  // eight chunks' loads in flight at a time (the scan is on the workgroup's critical path)
+  int start = 0, cnt = 0;
+  for (int p0 = 0; p0 < P; p0 += 8 * 64) {
+    int bk[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int p = p0 + 64 * u + lane;
+      const int pc = p < P ? proto_class[p] : -1;
+      bk[u] = p < P ? ((pc >= 0 && pc < K) ? pc : K) : K + 1;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int p = p0 + 64 * u + lane;
+      start += __popcll(__ballot(bk[u] < c));
+      const bool in = bk[u] == c;
+      const unsigned long long m = __ballot(in);
+      if (in && cnt + lane_rank(m) < kKldMaxPerClass) first[cnt + lane_rank(m)] = p;
+      cnt += __popcll(m);
+    }
   }
-  int cnt = 0;
-  for (int p0 = 0; p0 < P; p0 += 64) {
-    const int p = p0 + lane;
-    const int pc = p < P ? proto_class[p] : -1;
-    const bool in = p < P && ((pc >= 0 && pc < K) ? pc : K) == c;
-    const unsigned long long m = __ballot(in);
-    if (in) {
-      const int r = cnt + lane_rank(m);
-      if (r < kKldMaxPerClass) first[r] = p;
-      if (publish) {
+  if (publish) {  // the bucket's published list (a second pass: members past the first 32 too)
+    int r0 = 0;
+    for (int p0 = 0; p0 < P; p0 += 64) {
+      const int p = p0 + lane;
+      const int pc = p < P ? proto_class[p] : -1;
+      const bool in = p < P && ((pc >= 0 && pc < K) ? pc : K) == c;
+      const unsigned long long m = __ballot(in);
+      if (in) {
+        const int r = r0 + lane_rank(m);
         idx[start + r] = p;
         // the compact gradient's column: class * 256 + rank; a rank past 255 would wrap into the
         // next class's code, and such a class holds more prototypes than any max_per_class (its
         // groups add no pairs), so its prototypes get class -2, which no pixel carries
         slot[p] = r < 256 ? c * 256 + r : -2 * 256;
       }
+      r0 += __popcll(m);
     }
-    cnt += __popcll(m);
-  }
-  if (publish && lane == 0) {
-    off[c] = start;
-    if (c == K) off[K + 1] = start + cnt;
+    if (lane == 0) {
+      off[c] = start;
+      if (c == K) off[K + 1] = start + cnt;
+    }
   }
   *start_out = start;
   *cnt_out = cnt;
@@ -236,7 +242,7 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
                                                                   int* __restrict__ off, int* __restrict__ idx,
                                                                   int* __restrict__ slot,
                                                                   float* __restrict__ part, int* __restrict__ rcnt,
-                                                                  int* __restrict__ plist, float* __restrict__ zc) {
+                                                                  int* __restrict__ plist) {
   extern __shared__ __attribute__((aligned(16))) float kld_smem[];
   __shared__ int s_proto[kKldMaxPerClass];
   __shared__ float s_m[kKldMaxPerClass];
@@ -342,14 +348,6 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
     const int kq = min(kKldThreads, total - base);
     gather_tasks(db, HW, s_list + base, kq, s_proto, npc, sz, kKldLdsStride);
     __syncthreads();
-    if (KLD_ZC) {  // the chunk's class distances, row per pixel (slot fastest: coalesced rows)
-      const float rn = qrcp(npc);
-      float* zb = zc + static_cast<size_t>(b) * HW * mpc;
-      for (int t = tid; t < npc * kq; t += kKldThreads) {
-        const int q = qdiv(t, npc, rn), i = t - q * npc;
-        zb[static_cast<size_t>(s_list[base + q]) * mpc + i] = sz[i * kKldLdsStride + q];
-      }
-    }
     {  // chunk max per prototype (8 threads per row) -> running max and the rescale factor
       const int i = tid >> 3, l8 = tid & 7;
       float mx = -INFINITY;
@@ -738,78 +736,79 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_compact_kernel(
     const int* __restrict__ off, const int* __restrict__ idx, const int* __restrict__ slot,
     const int* __restrict__ cnt, const float* __restrict__ lse, const float* __restrict__ kl,
     const int* __restrict__ stat, const float* __restrict__ g_loss, const int* __restrict__ rcnt,
-    const int* __restrict__ plist, const float* __restrict__ zc, float* __restrict__ g_cls,
-    int32_t* __restrict__ pix_cls, int32_t* __restrict__ proto_slot) {
+    const int* __restrict__ plist, float* __restrict__ g_cls, int32_t* __restrict__ pix_cls,
+    int32_t* __restrict__ proto_slot) {
   extern __shared__ __attribute__((aligned(16))) float kld_smem[];
   __shared__ int s_proto[kKldMaxPerClass];
   __shared__ float s_lse[kKldMaxPerClass];
+  constexpr int kRows = kKldRange / kKldThreads;
   const int c = blockIdx.x, b = blockIdx.y, rs = blockIdx.z, tid = threadIdx.x;
   const size_t bc = static_cast<size_t>(b) * K + c;
-  const int o0 = off[c];
-  const int npc = off[c + 1] - o0;
+  // The prologue's global reads in three round trips: (1) the group's scalars and the range's
+  // labels, (2) what depends on them (this thread's prototype id, its KL entries, the class-pixel
+  // list), (3) the log-sum-exps and the first chunk's distances.
+  const int o0 = off[c], o1 = off[c + 1];
+  const int np = stat[0], ncls = cnt[bc], q1 = rcnt[bc * gridDim.z + rs];
+  const TL* lab = label + static_cast<size_t>(b) * HW;
+  const int n0 = rs * kKldRange, n1 = min(HW, n0 + kKldRange);
+  long long lv[kRows];
+#pragma unroll
+  for (int r = 0; r < kRows; ++r) {
+    const int n = n0 + r * kKldThreads + tid;
+    lv[r] = n < n1 ? label_at(lab, n) : -1;
+  }
+  const int npc = o1 - o0;
+  const bool contributes = npc >= 2 && npc <= mpc && np != 0 && ncls >= 2;
+  {  // pix_cls: the pixels whose label is c (c = 0 also takes labels outside [0, K))
+    int32_t* pcb = pix_cls + static_cast<size_t>(b) * HW;
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      const int n = n0 + r * kKldThreads + tid;
+      const long long l = lv[r];
+      const int owner = (l >= 0 && l < K) ? static_cast<int>(l) : 0;
+      if (n < n1 && owner == c) pcb[n] = (l == c && contributes) ? c : -1;
+    }
+  }
   if (b == 0 && rs == 0) {
     for (int r = tid; r < npc; r += kKldThreads) proto_slot[idx[o0 + r]] = slot[idx[o0 + r]];
     if (c == K - 1)
       for (int r = off[K] + tid; r < off[K + 1]; r += kKldThreads) proto_slot[idx[r]] = slot[idx[r]];
   }
-  const bool contributes = npc >= 2 && npc <= mpc && stat[0] != 0 && cnt[bc] >= 2;
-  {
-    const TL* lab = label + static_cast<size_t>(b) * HW;
-    int32_t* pcb = pix_cls + static_cast<size_t>(b) * HW;
-    const int n1 = min(HW, (rs + 1) * kKldRange);
-    for (int n = rs * kKldRange + tid; n < n1; n += kKldThreads) {
-      const long long l = label_at(lab, n);
-      const int owner = (l >= 0 && l < K) ? static_cast<int>(l) : 0;
-      if (owner == c) pcb[n] = (l == c && contributes) ? c : -1;
-    }
-  }
-  if (!contributes) return;  // uniform: the group adds no pair
-  const int q1 = rcnt[bc * gridDim.z + rs];
-  if (q1 == 0) return;
+  if (!contributes || q1 == 0) return;  // uniform: the group adds no pair here
   const int* pl = plist + bc * HW + rs * kKldRange;
   float* sp = kld_smem;
   float* slp = sp + mpc * kKldLdsStride;
   float* scoef = slp + mpc * kKldLdsStride;  // w [npc][npc] | (R_i, WK_i) at kKldPair
+  const float* klb = kl + bc * kKldPair;
+  const int my_p = tid < npc ? idx[o0 + tid] : 0;
   {  // kld_coef_kernel's coefficients, same operations
-    const int np = stat[0];
     const float gl = g_loss ? g_loss[0] : 1.f;
-    const float* klb = kl + bc * kKldPair;
     for (int e = tid; e < npc * npc; e += kKldThreads) {
       const int i = e / npc, j = e - i * npc;
       const float kij = i == j ? 0.f : klb[i * kKldMaxPerClass + j], kji = i == j ? 0.f : klb[j * kKldMaxPerClass + i];
       scoef[e] = i == j ? 0.f : -(gl / static_cast<float>(np)) * expf(-((kji + kij) / 2.f));
     }
-    __syncthreads();
-    if (tid < npc) {
-      float r = 0.f, wk = 0.f;
-      for (int j = 0; j < npc; ++j) {
-        const float w = scoef[tid * npc + j];
-        r += w;
-        wk = fmaf(w, tid == j ? 0.f : klb[tid * kKldMaxPerClass + j], wk);
-      }
-      scoef[kKldPair + 2 * tid] = r;
-      scoef[kKldPair + 2 * tid + 1] = wk;
-    }
   }
   if (tid < npc) {
-    s_proto[tid] = idx[o0 + tid];
-    s_lse[tid] = lse[static_cast<size_t>(b) * P + idx[o0 + tid]];
+    s_proto[tid] = my_p;
+    s_lse[tid] = lse[static_cast<size_t>(b) * P + my_p];
   }
   __syncthreads();
+  if (tid < npc) {
+    float r = 0.f, wk = 0.f;
+    for (int j = 0; j < npc; ++j) {
+      const float w = scoef[tid * npc + j];
+      r += w;
+      wk = fmaf(w, tid == j ? 0.f : klb[tid * kKldMaxPerClass + j], wk);
+    }
+    scoef[kKldPair + 2 * tid] = r;
+    scoef[kKldPair + 2 * tid + 1] = wk;
+  }
   const float* db = dist + static_cast<size_t>(b) * P * HW;
   for (int base = 0; base < q1; base += kKldThreads) {  // chunks of 256 class pixels
     const int kq = min(kKldThreads, q1 - base);
     const int* lq = pl + base;
-    if (KLD_ZC) {  // the forward's per-pixel rows of the class distances (no gather from dist)
-      const float rn = qrcp(npc);
-      const float* zb = zc + static_cast<size_t>(b) * HW * mpc;
-      for (int t = tid; t < npc * kq; t += kKldThreads) {
-        const int q = qdiv(t, npc, rn), i = t - q * npc;
-        slp[i * kKldLdsStride + q] = zb[static_cast<size_t>(lq[q]) * mpc + i];
-      }
-    } else {
-      gather_tasks(db, HW, lq, kq, s_proto, npc, slp, kKldLdsStride);
-    }
+    gather_tasks(db, HW, lq, kq, s_proto, npc, slp, kKldLdsStride);
     __syncthreads();
     const float rk = qrcp(kq);
     for (int t = tid; t < npc * kq; t += kKldThreads) {
@@ -920,7 +919,7 @@ extern "C" int protoseg_kld_forward(const float* dist, int B, int P, int HW, con
     if (int e = ensure_lds<kld_partial_kernel<TL>, kKldMaxDynLds>()) return e;
     hipLaunchKernelGGL(kld_partial_kernel<TL>, dim3(K, B, S), dim3(kKldThreads), lds, s, dist, P, HW,
                        static_cast<const TL*>(label), K, max_per_class, proto_class, w.off, w.idx, w.slot, w.part,
-                       w.rcnt, w.plist, w.zc);
+                       w.rcnt, w.plist);
     return check_launch("kld_partial_kernel");
   });
   if (st) return st;
@@ -977,7 +976,7 @@ extern "C" int protoseg_kld_backward_compact(const float* dist, int B, int P, in
     if (int e = ensure_lds<kld_grad_compact_kernel<TL>, kKldMaxDynLds + kKldCoefFloats * sizeof(float)>()) return e;
     hipLaunchKernelGGL(kld_grad_compact_kernel<TL>, dim3(K, B, kld_ranges(HW)), dim3(kKldThreads), lds, s, dist, P,
                        HW, static_cast<const TL*>(label), K, max_per_class, w.off, w.idx, w.slot, w.cnt, w.lse, w.kl,
-                       w.stat, g_loss, w.rcnt, w.plist, w.zc, g_cls, pix_cls, proto_slot);
+                       w.stat, g_loss, w.rcnt, w.plist, g_cls, pix_cls, proto_slot);
     return check_launch("kld_grad_compact_kernel");
   });
 }

@@ -337,7 +337,7 @@ int stager_mode(const Operand& o, const WideArgs& a) {
 }
 
 #ifndef WIDE_TM128
-#define WIDE_TM128 1  // 128-row tiles for M >= 256
+#define WIDE_TM128 0  // 128-row tiles for M >= 256 (measured slower: DESIGN 5.4)
 #endif
 template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO, int TM>
 int gemm_tm(const WideArgs& a, int grid_z, int ma, int mb, hipStream_t s) {
