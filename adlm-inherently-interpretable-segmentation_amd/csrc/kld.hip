@@ -115,8 +115,6 @@ KldPtrs kld_ptrs(void* ws, const KldLayout& l) {
           reinterpret_cast<int*>(b + l.plist)};
 }
 
-__device__ __forceinline__ int bucket_of(int pc, int K) { return (pc >= 0 && pc < K) ? pc : K; }
-
 constexpr int kKldListMaxP = 1 << 20;
 
 __device__ __forceinline__ int lane_rank(unsigned long long m) {  // set bits of m below this lane
@@ -426,6 +424,100 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
 // and range), then KL_ij over the workgroup's 256 threads, and this group's sum of
 // exp(-kld_ij) over its pairs i < j (per-thread partials added in a fixed order).
 constexpr int kKldMergeMaxS = 64;  // ranges whose factors are staged in LDS (beyond: inline)
+constexpr int kKldMergeRegS = 8;   // ranges held in registers by kld_merge_regs
+
+// kld_merge_kernel for S <= kKldMergeRegS ranges: the range partials are read into registers
+// first (counts, m_i^s and S_i^s with the group's scalars; then the workgroup's T_ij^s entries),
+// so the merge waits on two global round trips instead of four; operations and order are the
+// general path's (bit-identical results).
+__device__ __forceinline__ void kld_merge_regs(const float* __restrict__ pb, int P, int K, int S, int npc, bool valid,
+                                               int c, int b, const int* __restrict__ off,
+                                               const int* __restrict__ idx, int* __restrict__ cnt_out,
+                                               float* __restrict__ lse_out, float* __restrict__ kl_out,
+                                               float* __restrict__ group_out, float* s_L, float* s_fac,
+                                               float* s_kl, float* s_sum) {
+  static_assert(kKldPair % 256 == 0 && kKldMergeRegS <= kKldMergeMaxS, "merge fast path layout");
+  __shared__ int s_n[kKldMergeRegS];
+  const int tid = threadIdx.x;
+  float mi[kKldMergeRegS], si[kKldMergeRegS];
+  int nr = 0;
+  if (tid < kKldMergeRegS && tid < S && valid) nr = static_cast<int>(pb[tid * kKldPartFloats + 2 * kKldMaxPerClass]);
+#pragma unroll
+  for (int s = 0; s < kKldMergeRegS; ++s) {
+    const bool ld = s < S && tid < npc;
+    mi[s] = ld ? pb[s * kKldPartFloats + tid] : 0.f;
+    si[s] = ld ? pb[s * kKldPartFloats + kKldMaxPerClass + tid] : 0.f;
+  }
+  // the entries this thread merges (e = tid + 256 u of the npc x npc grid), all ranges
+  constexpr int kU = kKldPair / 256;
+  float tv[kU][kKldMergeRegS];
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const int e = tid + 256 * u, i = e / (npc > 0 ? npc : 1), j = e - i * npc;
+#pragma unroll
+    for (int s = 0; s < kKldMergeRegS; ++s)
+      tv[u][s] = (e < npc * npc && s < S) ? pb[s * kKldPartFloats + 2 * kKldMaxPerClass + 1 + i * kKldMaxPerClass + j]
+                                          : 0.f;
+  }
+  if (tid < kKldMergeRegS) s_n[tid] = tid < S ? nr : 0;
+  __syncthreads();
+  int cnt = 0;
+  for (int s = 0; s < S; ++s) cnt += s_n[s];
+  float* gsum = group_out + (static_cast<size_t>(b) * K + c) * 2;  // (sum of exp(-kld), pairs)
+  if (tid == 0) cnt_out[static_cast<size_t>(b) * K + c] = cnt;
+  if (cnt == 0) {
+    if (tid == 0) gsum[0] = gsum[1] = 0.f;
+    return;
+  }
+  if (tid < npc) {  // L_i, then this slot's factors exp(m_i^s - L_i)
+    float M = -INFINITY, Ssum = 0.f;
+#pragma unroll
+    for (int s = 0; s < kKldMergeRegS; ++s)
+      if (s < S && s_n[s] > 0) lse_merge(M, Ssum, mi[s], si[s]);
+    const float L = M + logf(Ssum);
+    s_L[tid] = L;
+    lse_out[static_cast<size_t>(b) * P + idx[off[c] + tid]] = L;
+#pragma unroll
+    for (int s = 0; s < kKldMergeRegS; ++s) s_fac[s * kKldMaxPerClass + tid] = expf(mi[s] - L);
+  }
+  __syncthreads();
+  if (npc < 2 || cnt < 2) {
+    if (tid == 0) gsum[0] = gsum[1] = 0.f;
+    return;
+  }
+  float* klb = kl_out + (static_cast<size_t>(b) * K + c) * kKldPair;
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const int e = tid + 256 * u;
+    if (e >= npc * npc) continue;
+    const int i = e / npc, j = e - i * npc;
+    if (i == j) continue;
+    float t = 0.f;
+#pragma unroll
+    for (int s = 0; s < kKldMergeRegS; ++s)
+      if (s < S && s_n[s] > 0) t = fmaf(s_fac[s * kKldMaxPerClass + i], tv[u][s], t);
+    const float kl = t - (s_L[i] - s_L[j]);
+    klb[i * kKldMaxPerClass + j] = kl;
+    s_kl[i * kKldMaxPerClass + j] = kl;
+  }
+  __syncthreads();
+  // this group's pairs i < j: kld = (KL(p_j||p_i) + KL(p_i||p_j)) / 2 (module.py:195-199)
+  float sum = 0.f;
+  for (int e = tid; e < npc * npc; e += 256) {
+    const int i = e / npc, j = e - i * npc;
+    if (i < j) sum += expf(-((s_kl[j * kKldMaxPerClass + i] + s_kl[i * kKldMaxPerClass + j]) / 2.f));
+  }
+  s_sum[tid] = sum;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (tid < w) s_sum[tid] += s_sum[tid + w];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    gsum[0] = s_sum[0];
+    gsum[1] = static_cast<float>(npc * (npc - 1) / 2);
+  }
+}
 __global__ __launch_bounds__(256) void kld_merge_kernel(int P, int K, int S, int mpc, const int* __restrict__ off,
                                                         const int* __restrict__ idx, const float* __restrict__ part,
                                                         int* __restrict__ cnt_out, float* __restrict__ lse_out,
@@ -441,6 +533,11 @@ __global__ __launch_bounds__(256) void kld_merge_kernel(int P, int K, int S, int
   const int npc = npc_all < mpc ? npc_all : mpc;
   const float* pb = part + (static_cast<size_t>(b) * K + c) * S * kKldPartFloats;
   const bool valid = npc >= 1 && npc_all <= mpc;
+  if (S <= kKldMergeRegS) {  // the same sums with every global read in two round trips
+    kld_merge_regs(pb, P, K, S, npc, valid, c, b, off, idx, cnt_out, lse_out, kl_out, group_out, s_L, &s_sc[0][0], s_kl,
+                   s_sum);
+    return;
+  }
   if (tid == 0) s_cnt = 0;
   __syncthreads();
   for (int s = tid; s < S && valid; s += 256) {
@@ -525,9 +622,13 @@ __global__ __launch_bounds__(256) void kld_finalize_kernel(int groups, const flo
     sum += group_sums[2 * gi];
     n += group_sums[2 * gi + 1];
   }
+  // a class holding more than max_per_class prototypes: the loss is NaN (one class per thread,
+  // loads in parallel rather than a chain of dependent ones)
+  int over_c = 0;
+  for (int c = threadIdx.x; c < K; c += 256) over_c |= off[c + 1] - off[c] > mpc;
   s_sum[threadIdx.x] = sum;
   s_n[threadIdx.x] = n;
-  __syncthreads();
+  const bool over = __syncthreads_or(over_c) != 0;
   for (int w = 128; w >= 1; w >>= 1) {
     if (static_cast<int>(threadIdx.x) < w) {
       s_sum[threadIdx.x] += s_sum[threadIdx.x + w];
@@ -538,8 +639,6 @@ __global__ __launch_bounds__(256) void kld_finalize_kernel(int groups, const flo
   if (threadIdx.x == 0) {
     const int np = static_cast<int>(s_n[0]);
     float loss = np > 0 ? s_sum[0] / static_cast<float>(np) : 0.f;
-    bool over = false;  // a class holding more than max_per_class prototypes: the loss is NaN
-    for (int c = 0; c < K; ++c) over = over || off[c + 1] - off[c] > mpc;
     if (over) loss = __builtin_nanf("");
     stat[0] = np;
     stat[1] = over ? 1 : 0;

@@ -51,6 +51,12 @@ for step in "$@"; do
           tail -6 gpurun_out/${T}_ab_${c}_$P.log
         done
       done ;;
+    abpush)  # interleaved A/B of the build_var/* push variants on the argmin call (8 maps)
+      for P in 190 361; do
+        timeout -k 10 300 python -u tools/ab_libs.py --protos $P --call push --reps 40 > gpurun_out/${T}_ab_push_$P.log 2>&1 \
+          || { tail -20 gpurun_out/${T}_ab_push_$P.log; exit 1; }
+        tail -4 gpurun_out/${T}_ab_push_$P.log
+      done ;;
     pushtrace)  # kernel trace of the push inner step alone
       ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/pt_${T}" \
           -o pt --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/push_trace.py" 8 20 \
@@ -71,6 +77,10 @@ for step in "$@"; do
       TAG=push_$T DRIVER=tools/push_trace.py DRIVER_ARGS="8 5" bash tools/pmc_bwd.sh > gpurun_out/${T}_sqpush.log 2>&1 \
         || { tail -20 gpurun_out/${T}_sqpush.log; exit 1; }
       grep -E "push_argmin|patch_mask|derived" gpurun_out/${T}_sqpush.log | head -20 ;;
+    profall)  # the three profile workloads (trace + FETCH_SIZE + WRITE_SIZE passes each)
+      TAG=$T WORKLOADS="p361 p190 rest" bash tools/profile.sh > gpurun_out/${T}_profile.log 2>&1 \
+        || { tail -20 gpurun_out/${T}_profile.log; exit 1; }
+      for wl in p361 p190 rest; do python3 tools/kstats.py gpurun_out/prof_$T/$wl/trace/trace_kernel_stats.csv; done ;;
     diag)
       timeout -k 10 300 python -u tools/debug/kld_compact_diag.py > gpurun_out/${T}_diag.log 2>&1; tail -30 gpurun_out/${T}_diag.log ;;
     smoke)
