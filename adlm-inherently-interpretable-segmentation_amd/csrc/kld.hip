@@ -232,8 +232,10 @@ __device__ __forceinline__ void lse_merge(float& m, float& s, float mo, float so
 // max per prototype updates the running max m_i, the accumulators S_i = sum e_i and T_ij = sum
 // e_i (z_i - z_j) (e_i = exp(z_i - m_i)) are rescaled by exp(m_old - m_new), and the chunk is
 // added. The range partial (m_i, S_i, T_ij, count) is the one a separate max pass would give, up
-// to rounding. LDS (dynamic): [mpc][257] e | [mpc][257] z.
-template <typename TL>
+// to rounding. LDS (dynamic): [mpc][257] e | [mpc][257] z, or with RC (recompute) [mpc][257] z
+// only: e_i = exp(z_i - m_i) is recomputed where used (the same expression: same bits), half the
+// LDS and more workgroups per CU for many prototypes per class, but more VGPRs (kld_recompute).
+template <typename TL, bool RC>
 __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* __restrict__ dist, int P, int HW,
                                                                   const TL* __restrict__ label, int K, int mpc,
                                                                   const int32_t* __restrict__ proto_class,
@@ -316,8 +318,8 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
   __syncthreads();
   const float* db = dist + static_cast<size_t>(b) * P * HW;
 
-  float* se = kld_smem;                          // [npc][257]
-  float* sz = kld_smem + npc * kKldLdsStride;    // [npc][257]
+  float* se = kld_smem;                                      // [npc][257] (stored e)
+  float* sz = RC ? kld_smem : kld_smem + npc * kKldLdsStride;  // [npc][257]
   const int E = npc * npc;
   // T_ij in 4 x 4 register blocks: thread = (block (bi, bj), pixel group g); per pixel it reads
   // e and z of its 4 rows and z of its 4 columns (12 LDS values for 16 fma, where one thread per
@@ -361,29 +363,31 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
       }
     }
     __syncthreads();
+    float mr[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float sc = s_scale[min(i0 + r, npc - 1)];
+      mr[r] = s_m[min(i0 + r, npc - 1)];
       ssum[r] *= sc;
 #pragma unroll
       for (int cc = 0; cc < 4; ++cc) acc[r][cc] *= sc;
     }
-    {
+    if constexpr (!RC) {
       const float rk = qrcp(kq);
       for (int t = tid; t < npc * kq; t += kKldThreads) {
         const int i = qdiv(t, kq, rk), q = t - i * kq;
         se[i * kKldLdsStride + q] = expf(sz[i * kKldLdsStride + q] - s_m[i]);
       }
+      __syncthreads();
     }
-    __syncthreads();
     if (worker) {
       for (int q = g; q < kq; q += G) {
         float e[4], zi[4], zj[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          e[r] = se[ri[r] + q];
           zi[r] = sz[ri[r] + q];
           zj[r] = sz[rj[r] + q];
+          e[r] = RC ? expf(zi[r] - mr[r]) : se[ri[r] + q];
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -821,15 +825,15 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_kernel(
 // position in its class) at each pixel of a contributing (image, class) group, pix_cls[g] = that
 // class. pix_cls is set to -1 everywhere first (one memset); one workgroup per (class c, image
 // b, pixel range s) of a contributing group then walks the range's class-pixel list the forward
-// left in plist, thread = pixel. LDS (dynamic): [mpc][257] p | [mpc][257] log p (each thread its
-// own column) | the group's (w_ij, KL_ij) pairs.
+// left in plist. LDS (dynamic): [mpc][257] p | [mpc][257] log p | the group's coefficients; with
+// RC the p rows are not stored: p = exp(lp) is recomputed where used (same bits, kld_recompute).
 //
 // The same launch also writes what used to take three more: proto_slot (workgroups (c, 0, 0)
 // copy their bucket's columns; the one of bucket K - 1 also bucket K's), pix_cls for every pixel
 // (the workgroup of the pixel's label, class 0's for labels outside [0, K), writes c or -1: each
 // pixel exactly once, no memset), and the group's coefficients (kld_coef_kernel's arithmetic, in
 // LDS).
-template <typename TL>
+template <typename TL, bool RC>
 __global__ __launch_bounds__(kKldThreads) void kld_grad_compact_kernel(
     const float* __restrict__ dist, int P, int HW, const TL* __restrict__ label, int K, int mpc,
     const int* __restrict__ off, const int* __restrict__ idx, const int* __restrict__ slot,
@@ -875,8 +879,8 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_compact_kernel(
   }
   if (!contributes || q1 == 0) return;  // uniform: the group adds no pair here
   const int* pl = plist + bc * HW + rs * kKldRange;
-  float* sp = kld_smem;
-  float* slp = sp + mpc * kKldLdsStride;
+  float* sp = kld_smem;  // (stored p)
+  float* slp = RC ? kld_smem : kld_smem + mpc * kKldLdsStride;
   float* scoef = slp + mpc * kKldLdsStride;  // w [npc][npc] | (R_i, WK_i) at kKldPair
   const float* klb = kl + bc * kKldPair;
   const int my_p = tid < npc ? idx[o0 + tid] : 0;
@@ -914,7 +918,7 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_compact_kernel(
       const int i = qdiv(t, kq, rk), q = t - i * kq;
       const float lp = slp[i * kKldLdsStride + q] - s_lse[i];
       slp[i * kKldLdsStride + q] = lp;
-      sp[i * kKldLdsStride + q] = expf(lp);
+      if constexpr (!RC) sp[i * kKldLdsStride + q] = expf(lp);
     }
     __syncthreads();
     // one task per (pixel, block of 4 class slots), pixel fastest: a wave's lanes share the slot
@@ -927,14 +931,15 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_compact_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = min(4 * ib + r, npc - 1);
-        pi[r] = sp[i * kKldLdsStride + q];
         li[r] = slp[i * kKldLdsStride + q];
+        pi[r] = RC ? expf(li[r]) : sp[i * kKldLdsStride + q];
         ri[r] = scoef[kKldPair + 2 * i];
         wki[r] = scoef[kKldPair + 2 * i + 1];
       }
       kld_block_grad(
           npc, 4 * ib, pi, li, ri, wki, [&](int j) { return slp[j * kKldLdsStride + q]; },
-          [&](int j) { return sp[j * kKldLdsStride + q]; }, [&](int i, int j) { return scoef[i * npc + j]; }, g);
+          [&](int j) { return RC ? expf(slp[j * kKldLdsStride + q]) : sp[j * kKldLdsStride + q]; },
+          [&](int i, int j) { return scoef[i * npc + j]; }, g);
       float* row = g_cls + (static_cast<size_t>(b) * HW + lq[q]) * mpc;
 #pragma unroll
       for (int r = 0; r < 4; ++r)
@@ -977,6 +982,16 @@ int kld_check(const float* dist, int B, int P, int HW, const void* label, int la
   return PROTOSEG_OK;
 }
 
+template <auto K>
+struct KernelTag {
+  static constexpr auto value = K;
+};
+
+// Recompute e / p instead of storing their rows (the RC kernels) when the stored rows would hold
+// the partial / compact kernels to fewer workgroups per CU than their extra VGPRs do: measured
+// (profiles/r04/r4t_ab_kld*.log) faster at 19 prototypes per class, slower at 10.
+bool kld_recompute(int mpc) { return mpc > 12; }
+
 template <typename Fn>
 int by_label(int label_dtype, Fn&& fn) {
   switch (label_dtype) {
@@ -1011,15 +1026,19 @@ extern "C" int protoseg_kld_forward(const float* dist, int B, int P, int HW, con
   const KldLayout l = kld_layout(B, P, HW, K);
   const KldPtrs w = kld_ptrs(workspace, l);
   const int S = kld_ranges(HW);
-  const size_t lds = std::max(static_cast<size_t>(2) * max_per_class * kKldLdsStride * sizeof(float),
+  const bool rc = kld_recompute(max_per_class);
+  const size_t lds = std::max(static_cast<size_t>(rc ? 1 : 2) * max_per_class * kKldLdsStride * sizeof(float),
                               static_cast<size_t>(kKldThreads) * 16 * sizeof(float));
   const int st = by_label(label_dtype, [&](auto tl) {
     using TL = std::remove_pointer_t<decltype(tl)>;
-    if (int e = ensure_lds<kld_partial_kernel<TL>, kKldMaxDynLds>()) return e;
-    hipLaunchKernelGGL(kld_partial_kernel<TL>, dim3(K, B, S), dim3(kKldThreads), lds, s, dist, P, HW,
-                       static_cast<const TL*>(label), K, max_per_class, proto_class, w.off, w.idx, w.slot, w.part,
-                       w.rcnt, w.plist);
-    return check_launch("kld_partial_kernel");
+    auto go = [&](auto kern) {
+      if (int e = ensure_lds<decltype(kern)::value, kKldMaxDynLds>()) return e;
+      hipLaunchKernelGGL(decltype(kern)::value, dim3(K, B, S), dim3(kKldThreads), lds, s, dist, P, HW,
+                         static_cast<const TL*>(label), K, max_per_class, proto_class, w.off, w.idx, w.slot, w.part,
+                         w.rcnt, w.plist);
+      return check_launch("kld_partial_kernel");
+    };
+    return rc ? go(KernelTag<kld_partial_kernel<TL, true>>()) : go(KernelTag<kld_partial_kernel<TL, false>>());
   });
   if (st) return st;
   hipLaunchKernelGGL(kld_merge_kernel, dim3(K, B), dim3(256), 0, s, P, K, S, max_per_class, w.off, w.idx, w.part, w.cnt,
@@ -1069,14 +1088,19 @@ extern "C" int protoseg_kld_backward_compact(const float* dist, int B, int P, in
   const KldLayout l = kld_layout(B, P, HW, K);
   const KldPtrs w = kld_ptrs(workspace, l);
   // one launch: proto_slot, pix_cls, the coefficients and the gradient (kld_grad_compact_kernel)
-  const size_t lds = (static_cast<size_t>(2) * max_per_class * kKldLdsStride + kKldCoefFloats) * sizeof(float);
+  const bool rc = kld_recompute(max_per_class);
+  const size_t lds =
+      (static_cast<size_t>(rc ? 1 : 2) * max_per_class * kKldLdsStride + kKldCoefFloats) * sizeof(float);
   return by_label(label_dtype, [&](auto tl) {
     using TL = std::remove_pointer_t<decltype(tl)>;
-    if (int e = ensure_lds<kld_grad_compact_kernel<TL>, kKldMaxDynLds + kKldCoefFloats * sizeof(float)>()) return e;
-    hipLaunchKernelGGL(kld_grad_compact_kernel<TL>, dim3(K, B, kld_ranges(HW)), dim3(kKldThreads), lds, s, dist, P,
-                       HW, static_cast<const TL*>(label), K, max_per_class, w.off, w.idx, w.slot, w.cnt, w.lse, w.kl,
-                       w.stat, g_loss, w.rcnt, w.plist, g_cls, pix_cls, proto_slot);
-    return check_launch("kld_grad_compact_kernel");
+    auto go = [&](auto kern) {
+      if (int e = ensure_lds<decltype(kern)::value, kKldMaxDynLds + kKldCoefFloats * sizeof(float)>()) return e;
+      hipLaunchKernelGGL(decltype(kern)::value, dim3(K, B, kld_ranges(HW)), dim3(kKldThreads), lds, s, dist, P, HW,
+                         static_cast<const TL*>(label), K, max_per_class, w.off, w.idx, w.slot, w.cnt, w.lse, w.kl,
+                         w.stat, g_loss, w.rcnt, w.plist, g_cls, pix_cls, proto_slot);
+      return check_launch("kld_grad_compact_kernel");
+    };
+    return rc ? go(KernelTag<kld_grad_compact_kernel<TL, true>>()) : go(KernelTag<kld_grad_compact_kernel<TL, false>>());
   });
 }
 
