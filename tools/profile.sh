@@ -14,8 +14,8 @@ cd /tmp && export TMPDIR=/tmp
 # one configuration per workload: no side lines that launch the same kernels at other shapes
 B=(python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-small-batch --no-train --no-sigmoid)
 declare -A ARGS
-ARGS[p361]="--protos 361 --side-protos 0 --no-kld --no-push --no-knn --no-eval"
-ARGS[p190]="--protos 190 --side-protos 0 --no-kld --no-push --no-knn --no-eval"
+ARGS[p361]="--protos 361 --side-protos 0 --no-kld --no-push --no-knn --no-eval --no-wide"
+ARGS[p190]="--protos 190 --side-protos 0 --no-kld --no-push --no-knn --no-eval --no-wide"
 ARGS[rest]="--protos 190 --side-protos 0"
 run() {  # run <workload> <pass> <seconds> <rocprof args...>
   local wl=$1 name=$2 secs=$3; shift 3
