@@ -927,23 +927,24 @@ __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __
   const int gs_e = Pp * kC + 32 * Pp + p_of_e;
   float s = 0.f, gs = 0.f;
   if (active) {
-    int si = grp;
-    for (; si + 28 < S; si += 32) {  // 8 slabs per step for this group
-      float v[8], u[8];
+    // this group's slabs grp, grp + 4, ... added in order, kReduceBatch loads in flight per step;
+    // the last step's loads are predicated, not issued one round trip at a time
+    constexpr int kReduceBatch = 16;
+    for (int si = grp; si < S; si += 4 * kReduceBatch) {
+      float v[kReduceBatch], u[kReduceBatch];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        v[k] = slab[static_cast<size_t>(si + 4 * k) * E + e];
-        u[k] = is_gp ? slab[static_cast<size_t>(si + 4 * k) * E + gs_e] : 0.f;
+      for (int k = 0; k < kReduceBatch; ++k) {
+        const bool ok = si + 4 * k < S;
+        v[k] = ok ? slab[static_cast<size_t>(si + 4 * k) * E + e] : 0.f;
+        u[k] = ok && is_gp ? slab[static_cast<size_t>(si + 4 * k) * E + gs_e] : 0.f;
       }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        s += v[k];
-        gs += u[k];
+      for (int k = 0; k < kReduceBatch; ++k) {
+        if (si + 4 * k < S) {
+          s += v[k];
+          gs += u[k];
+        }
       }
-    }
-    for (; si < S; si += 4) {
-      s += slab[static_cast<size_t>(si) * E + e];
-      if (is_gp) gs += slab[static_cast<size_t>(si) * E + gs_e];
     }
   }
   part[grp][threadIdx.x & 63] = s;

@@ -33,7 +33,8 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--fmap", type=int, default=65)
     ap.add_argument("--reps", type=int, default=40)
-    ap.add_argument("--call", default="bwd_full", choices=["bwd_full", "bwd_full_xsig", "fwd", "fwd_xsig", "push", "mask", "kld", "kldb", "kldc"])
+    ap.add_argument("--call", default="bwd_full", choices=["bwd_full", "bwd_full_xsig", "fwd", "fwd_xsig", "push", "mask", "kld", "kldb", "kldc",
+                                                       "bwdk"])
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     B, C, h, w, P, K = args.batch, 64, args.fmap, args.fmap, args.protos, 19
@@ -65,7 +66,7 @@ def main():
         st = libs["main"].protoseg_patch_class_mask(P_(lab), _lib.U8, n_img, 1024, 2048, ph, pw, None, 0, P_(mask), s)
         assert st == 0
 
-    if args.call in ("kld", "kldb", "kldc"):  # KLD forward (kldb: + backward, kldc: + compact backward) on the layer's distances (bench.py setup_kld: 8x8 label blocks)
+    if args.call in ("kld", "kldb", "kldc", "bwdk"):  # KLD forward (kldb: + backward, kldc: + compact backward) on the layer's distances (bench.py setup_kld: 8x8 label blocks)
         blocks = torch.randint(0, K + 1, (B, (h + 7) // 8, (w + 7) // 8), generator=gen)
         tgt = blocks.repeat_interleave(8, 1).repeat_interleave(8, 2)[:, :h, :w].reshape(B, -1).contiguous().to(dev)
         pcls = torch.clamp(torch.arange(P) // (P // K), max=K - 1).to(torch.int32).to(dev)
@@ -81,6 +82,13 @@ def main():
         st = libs["main"].protoseg_l2_fwd(P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 0,
                                           _lib.PRECISIONS["bf16x3"], P_(dist), None, P_(logits), s)
         assert st == 0
+        if args.call == "bwdk":  # the layer backward with the compact KLD gradient (protoseg_l2_bwd_kld)
+            st = libs["main"].protoseg_kld_forward(P_(dist), B, P, h * w, P_(tgt), _lib.I64, P_(pcls), K, mpc,
+                                                   P_(kloss), None, P_(kws), kws_b, s)
+            st = st or libs["main"].protoseg_kld_backward_compact(P_(dist), B, P, h * w, P_(tgt), _lib.I64, P_(pcls),
+                                                                  K, mpc, P_(kg), P_(kws), kws_b, P_(gcls), P_(pixc),
+                                                                  P_(pslot), s)
+            assert st == 0
 
     def call(lib):
         if args.call == "mask":
@@ -94,6 +102,9 @@ def main():
             if args.call == "kldc" and st == 0:
                 st = lib.protoseg_kld_backward_compact(P_(dist), B, P, h * w, P_(tgt), _lib.I64, P_(pcls), K, mpc,
                                                        P_(kg), P_(kws), kws_b, P_(gcls), P_(pixc), P_(pslot), s)
+        elif args.call == "bwdk":
+            st = lib.protoseg_l2_bwd_kld(P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 0, prec, P_(gl),
+                                         P_(gcls), P_(pixc), P_(pslot), mpc, P_(gx), P_(gp), P_(gw), P_(ws), ws_b, s)
         elif args.call == "push":
             st = lib.protoseg_push_argmin(P_(xp), n_img, C, ph, pw, P_(protos), P, P_(pcls), P_(mask), P_(keys),
                                           P_(second), s)
@@ -111,7 +122,7 @@ def main():
         torch.cuda.synchronize()
         out = (gdist if args.call == "kldb" else gcls if args.call == "kldc" else mask.float() if args.call == "mask" else
                kloss.reshape(1) if args.call == "kld" else keys.float() if args.call == "push" else
-               gx if args.call.startswith("bwd") else logits).clone()
+               torch.cat([gx.flatten(), gp.flatten(), gw.flatten()]) if args.call.startswith("bwd") else logits).clone()
         if ref is None:
             ref = out
         else:

@@ -51,6 +51,18 @@ for step in "$@"; do
           tail -6 gpurun_out/${T}_ab_${c}_$P.log
         done
       done ;;
+    abbwdk)  # interleaved A/B of the build_var/* variants on the layer backward with the compact KLD gradient
+      for P in 361 190; do
+        timeout -k 10 300 python -u tools/ab_libs.py --protos $P --call bwdk --reps 40 > gpurun_out/${T}_ab_bwdk_$P.log 2>&1 \
+          || { tail -20 gpurun_out/${T}_ab_bwdk_$P.log; exit 1; }
+        tail -4 gpurun_out/${T}_ab_bwdk_$P.log
+      done ;;
+    abbwd)  # interleaved A/B of the build_var/* variants on the plain layer backward
+      for P in 361 190; do
+        timeout -k 10 300 python -u tools/ab_libs.py --protos $P --call bwd_full --reps 40 > gpurun_out/${T}_ab_bwd_$P.log 2>&1 \
+          || { tail -20 gpurun_out/${T}_ab_bwd_$P.log; exit 1; }
+        tail -6 gpurun_out/${T}_ab_bwd_$P.log
+      done ;;
     abpush)  # interleaved A/B of the build_var/* push variants on the argmin call (8 maps)
       for P in 190 361; do
         timeout -k 10 300 python -u tools/ab_libs.py --protos $P --call push --reps 40 > gpurun_out/${T}_ab_push_$P.log 2>&1 \
