@@ -8,6 +8,7 @@
 //   push_argmin_kernel  fused distance + masked per-prototype top-2 keys (push.py:249-263)
 //   push_top2_kernel    folds the pixel stripes' partial top-2
 //   push_merge_kernel   strict-'<' fold in image order + winner gather (push.py:265-281)
+//   push_top2_merge_kernel  the two above in one launch (protoseg_push_update, native path)
 #include <map>
 #include <mutex>
 #include <vector>
@@ -66,13 +67,22 @@ __global__ __launch_bounds__(256) void patch_mask_kernel(const TL* __restrict__ 
   for (int c0 = 4 * static_cast<int>(threadIdx.x); c0 < W; c0 += 4 * static_cast<int>(blockDim.x)) {
     uint32_t b4[4] = {0u, 0u, 0u, 0u};
     const int nc = W - c0 < 4 ? W - c0 : 4;
-    for (int i = r0; i < r1; ++i) {
-      const TL* row = L + static_cast<size_t>(i) * W + c0;
-      if (vec4) {
-        const uint32_t q = *reinterpret_cast<const uint32_t*>(row);
+    if (vec4) {  // the patch row's label rows 8 at a time: 8 loads in flight, not one per round trip
+      for (int i = r0; i < r1; i += 8) {
+        uint32_t q[8];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) b4[k] |= cls_bit(static_cast<long long>((q >> (8 * k)) & 0xffu));
-      } else {
+        for (int u = 0; u < 8; ++u)
+          q[u] = i + u < r1 ? *reinterpret_cast<const uint32_t*>(L + static_cast<size_t>(i + u) * W + c0) : 0u;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (i + u < r1)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) b4[k] |= cls_bit(static_cast<long long>((q[u] >> (8 * k)) & 0xffu));
+      }
+    }
+    for (int i = vec4 ? r1 : r0; i < r1; ++i) {
+      const TL* row = L + static_cast<size_t>(i) * W + c0;
+      {
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           if (k < nc) b4[k] |= cls_bit(static_cast<long long>(row[k]));
@@ -364,6 +374,68 @@ __global__ __launch_bounds__(256) void push_merge_kernel(const unsigned long lon
     gfmap[static_cast<size_t>(p) * C + c] = x[(static_cast<size_t>(win) * C + c) * hw + patch];
 }
 
+// push_top2_kernel + push_merge_kernel in one launch (protoseg_push_update): one wave per
+// prototype folds each image's stripe partials across its lanes (a butterfly of top2_merge: the
+// keys are unique per patch, so the fold's result does not depend on its order and equals
+// push_top2_kernel's sequential one), then merges the images in order exactly as
+// push_merge_kernel does. The images' partials are loaded 8 images at a time (all in flight).
+__global__ __launch_bounds__(256) void push_top2_merge_kernel(const unsigned long long* __restrict__ part, int parts,
+                                                              int n_img, long long first_img,
+                                                              const float* __restrict__ x, int C, int hw, int P,
+                                                              float* __restrict__ gdist, float* __restrict__ gsecond,
+                                                              long long* __restrict__ gimg, int* __restrict__ gpatch,
+                                                              float* __restrict__ gfmap) {
+  const int p = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (p >= P) return;  // wave-uniform
+  float best = gdist[p];
+  float sec = gsecond ? gsecond[p] : 0.f;
+  int win = -1;
+  uint32_t patch = 0;
+  for (int i0 = 0; i0 < n_img; i0 += 8) {
+    unsigned long long kb[8], ks[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      kb[u] = ks[u] = ~0ull;
+      if (i0 + u < n_img)
+        for (int pt = lane; pt < parts; pt += 64) {
+          const unsigned long long* o = part + ((static_cast<size_t>(i0 + u) * parts + pt) * P + p) * 2;
+          top2_merge(kb[u], ks[u], o[0], o[1]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) top2_merge(kb[u], ks[u], shfl_xor_u64(kb[u], m), shfl_xor_u64(ks[u], m));
+      const unsigned long long key = kb[u];
+      if (i0 + u >= n_img || key == ~0ull) continue;  // no patch of the prototype's class (push.py:255-256)
+      const float d = __uint_as_float(static_cast<uint32_t>(key >> 32));
+      if (gsecond) {
+        const unsigned long long k2 = ks[u];
+        const float d2 = k2 == ~0ull ? __builtin_inff() : __uint_as_float(static_cast<uint32_t>(k2 >> 32));
+        if (d < best)
+          sec = best < d2 ? best : d2;
+        else
+          sec = d < sec ? d : sec;
+      }
+      if (d < best) {
+        best = d;
+        win = i0 + u;
+        patch = static_cast<uint32_t>(key);
+      }
+    }
+  }
+  if (lane == 0 && gsecond) gsecond[p] = sec;
+  if (win < 0) return;
+  if (lane == 0) {
+    gdist[p] = best;
+    gimg[p] = first_img + win;
+    gpatch[p] = static_cast<int>(patch);
+  }
+  for (int c = lane; c < C; c += 64)
+    gfmap[static_cast<size_t>(p) * C + c] = x[(static_cast<size_t>(win) * C + c) * hw + patch];
+}
+
 // push_dist_kernel: the distances of m (gathered) prototypes at every pixel of one image in
 // push_argmin_kernel's arithmetic, operation for operation: the same layout-B MFMA chain
 // (A = x channel 32 ct + 16 h + r of pixel j, B = the same channel of prototype j, in the same
@@ -487,12 +559,16 @@ extern "C" int protoseg_push_argmin(const float* x, int n_img, int C, int h, int
   return protoseg_push_argmin_words(x, n_img, C, h, w, protos, P, proto_class, mask, 1, img_keys, img_second, stream);
 }
 
-extern "C" int protoseg_push_argmin_words(const float* x, int n_img, int C, int h, int w, const float* protos, int P,
-                                          const int32_t* proto_class, const uint32_t* mask, int words,
-                                          uint64_t* img_keys, uint64_t* img_second, protoseg_stream_t stream) {
+// The argmin of protoseg_push_argmin_words. With parts_out, the native path stops after the
+// partial top-2 kernels and returns their scratch and count (the caller folds them:
+// push_top2_merge_kernel); *parts_out = 0 when the wide path ran and wrote img_keys itself.
+int push_argmin_impl(const float* x, int n_img, int C, int h, int w, const float* protos, int P,
+                     const int32_t* proto_class, const uint32_t* mask, int words, uint64_t* img_keys,
+                     uint64_t* img_second, hipStream_t s, const unsigned long long** part_out, int* parts_out) {
   if (words < 1 || words > 64) return fail(PROTOSEG_ERR_INVALID, "words=%d outside [1, 64]", words);
   if (!x || !protos || !proto_class || !mask || !img_keys)
     return fail(PROTOSEG_ERR_INVALID, "null pointer argument");
+  if (parts_out) *parts_out = 0;
   if (n_img <= 0 || h <= 0 || w <= 0 || P <= 0) return fail(PROTOSEG_ERR_INVALID, "bad shape");
   const int nc = nc_of_push(C);
   if (n_img > 65535) return fail(PROTOSEG_ERR_UNSUPPORTED, "n_img=%d per call", n_img);
@@ -502,12 +578,11 @@ extern "C" int protoseg_push_argmin_words(const float* x, int n_img, int C, int 
     if (hwc * C * n_img >= (1LL << 31) || hwc * P >= (1LL << 31))
       return fail(PROTOSEG_ERR_UNSUPPORTED, "n_img*h*w*C or h*w*P >= 2^31");
     return wide_push_argmin(x, n_img, C, static_cast<int>(hwc), protos, P, proto_class, mask, words, img_keys,
-                            img_second, reinterpret_cast<hipStream_t>(stream));
+                            img_second, s);
   }
   if (reinterpret_cast<uintptr_t>(protos) % 16 != 0) return fail(PROTOSEG_ERR_INVALID, "protos must be 16-B aligned");
   const long long HW = static_cast<long long>(h) * w;
   if (HW >= (1LL << 31) / 2) return fail(PROTOSEG_ERR_UNSUPPORTED, "h*w=%lld", HW);
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int npt = static_cast<int>(ceil_div(P, 32));
   // prototype chunks of equal width (P = 361: 6 + 6 tiles, not 8 + 4, so both launches keep 3
   // waves per SIMD): `per` tiles in `full` chunks, then the remainder chunk
@@ -548,11 +623,23 @@ extern "C" int protoseg_push_argmin_words(const float* x, int n_img, int C, int 
     launch(push_argmin_kernel<4>, rem ? 1 : 0, full * per, rem);
   }
   if (int e = check_launch("push_argmin_kernel")) return e;
+  if (parts_out) {
+    *part_out = part;
+    *parts_out = static_cast<int>(stripes) * kPushSplit;
+    return PROTOSEG_OK;
+  }
   const long long n = static_cast<long long>(n_img) * P;
   hipLaunchKernelGGL(push_top2_kernel, dim3(static_cast<unsigned>(ceil_div(n, 256))), dim3(256), 0, s, part, n_img,
                      static_cast<int>(stripes) * kPushSplit, P, reinterpret_cast<unsigned long long*>(img_keys),
                      reinterpret_cast<unsigned long long*>(img_second));
   return check_launch("push_top2_kernel");
+}
+
+extern "C" int protoseg_push_argmin_words(const float* x, int n_img, int C, int h, int w, const float* protos, int P,
+                                          const int32_t* proto_class, const uint32_t* mask, int words,
+                                          uint64_t* img_keys, uint64_t* img_second, protoseg_stream_t stream) {
+  return push_argmin_impl(x, n_img, C, h, w, protos, P, proto_class, mask, words, img_keys, img_second,
+                          reinterpret_cast<hipStream_t>(stream), nullptr, nullptr);
 }
 
 extern "C" int protoseg_push_distances(const float* x, int C, int h, int w, const float* protos, int m, float* dist,
@@ -627,9 +714,19 @@ extern "C" int protoseg_push_update(const void* label, int label_dtype, int n_im
   if (int st = protoseg_patch_class_mask_words(label, label_dtype, n_img, H_img, W_img, h, w, lut, lut_size, words,
                                                mask, stream))
     return st;
-  if (int st = protoseg_push_argmin_words(x, n_img, C, h, w, protos, P, proto_class, mask, words, keys, second,
-                                          stream))
+  const unsigned long long* part = nullptr;
+  int parts = 0;
+  if (int st = push_argmin_impl(x, n_img, C, h, w, protos, P, proto_class, mask, words, keys, second, s, &part, &parts))
     return st;
-  return protoseg_push_merge(keys, second, n_img, first_img, x, C, static_cast<int>(hw), P, global_dist,
-                             global_second, global_img, global_patch, global_fmap, stream);
+  if (parts == 0)  // the wide path wrote the per-image keys
+    return protoseg_push_merge(keys, second, n_img, first_img, x, C, static_cast<int>(hw), P, global_dist,
+                               global_second, global_img, global_patch, global_fmap, stream);
+  if (!global_dist || !global_img || !global_patch || !global_fmap)
+    return fail(PROTOSEG_ERR_INVALID, "null pointer argument");
+  const int waves_per_block = 4;
+  hipLaunchKernelGGL(push_top2_merge_kernel, dim3(static_cast<unsigned>(ceil_div(P, waves_per_block))),
+                     dim3(waves_per_block * 64), 0, s, part, parts, n_img, static_cast<long long>(first_img), x, C,
+                     static_cast<int>(hw), P, global_dist, global_second, reinterpret_cast<long long*>(global_img),
+                     global_patch, global_fmap);
+  return check_launch("push_top2_merge_kernel");
 }

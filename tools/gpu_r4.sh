@@ -63,6 +63,10 @@ for step in "$@"; do
           || { tail -20 gpurun_out/${T}_ab_bwd_$P.log; exit 1; }
         tail -6 gpurun_out/${T}_ab_bwd_$P.log
       done ;;
+    abmask)  # interleaved A/B of the build_var/* variants on the patch class mask (8 Cityscapes labels)
+      timeout -k 10 300 python -u tools/ab_libs.py --protos 190 --call mask --reps 40 > gpurun_out/${T}_ab_mask.log 2>&1 \
+        || { tail -20 gpurun_out/${T}_ab_mask.log; exit 1; }
+      tail -4 gpurun_out/${T}_ab_mask.log ;;
     abpush)  # interleaved A/B of the build_var/* push variants on the argmin call (8 maps)
       for P in 190 361; do
         timeout -k 10 300 python -u tools/ab_libs.py --protos $P --call push --reps 40 > gpurun_out/${T}_ab_push_$P.log 2>&1 \
