@@ -67,6 +67,12 @@ for step in "$@"; do
       timeout -k 10 300 python -u tools/ab_libs.py --protos 190 --call mask --reps 40 > gpurun_out/${T}_ab_mask.log 2>&1 \
         || { tail -20 gpurun_out/${T}_ab_mask.log; exit 1; }
       tail -4 gpurun_out/${T}_ab_mask.log ;;
+    abfwdsb)  # interleaved A/B of the build_var/* variants on the small-batch forward
+      for B in 2 4 8; do
+        timeout -k 10 300 python -u tools/ab_libs.py --protos 361 --batch $B --call fwd --reps 40 > gpurun_out/${T}_ab_fwd_B$B.log 2>&1 \
+          || { tail -20 gpurun_out/${T}_ab_fwd_B$B.log; exit 1; }
+        tail -3 gpurun_out/${T}_ab_fwd_B$B.log
+      done ;;
     abpush)  # interleaved A/B of the build_var/* push variants on the argmin call (8 maps)
       for P in 190 361; do
         timeout -k 10 300 python -u tools/ab_libs.py --protos $P --call push --reps 40 > gpurun_out/${T}_ab_push_$P.log 2>&1 \
