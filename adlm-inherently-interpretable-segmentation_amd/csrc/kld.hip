@@ -50,6 +50,21 @@ constexpr size_t kKldMaxDynLds = 2 * kKldMaxPerClass * kKldLdsStride * sizeof(fl
 // one range partial: m[32] | s[32] | count | T[32][32]
 constexpr int kKldPartFloats = 2 * kKldMaxPerClass + 1 + kKldPair;
 
+// Per-wave phase stamps of the partial kernel (debug builds only: make stamps, tools/stamps_kld.py).
+#ifdef PROTOSEG_STAMPS
+__device__ unsigned long long g_stamps_kld[1 << 17];
+#define KSTAMP(slot, clk)                                                                                 \
+  do {                                                                                                  \
+    const unsigned _g = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;                \
+    const unsigned _i = (_g * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (slot);                    \
+    if ((threadIdx.x & 63) == 0 && _i < (1u << 17)) g_stamps_kld[_i] = clk;                           \
+  } while (0)
+#else
+#define KSTAMP(slot, clk) \
+  do {                    \
+  } while (0)
+#endif
+
 size_t align256(size_t v) { return (v + 255) & ~static_cast<size_t>(255); }
 int kld_ranges(int HW) { return static_cast<int>(ceil_div(HW, kKldRange)); }
 
@@ -134,11 +149,19 @@ __device__ __forceinline__ void class_list_scan(const int32_t* __restrict__ prot
   // eight chunks' loads in flight at a time (the scan is on the workgroup's critical path)
   int start = 0, cnt = 0;
   for (int p0 = 0; p0 < P; p0 += 8 * 64) {
-    int bk[8];
+    int bk[8], pcv[8];
+    // clamped, unconditional loads, pinned before any use: otherwise the compiler sinks each load
+    // into its `p < P` branch with a wait of its own, eight round trips instead of one
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int p = p0 + 64 * u + lane;
-      const int pc = p < P ? proto_class[p] : -1;
+      pcv[u] = proto_class[p < P ? p : P - 1];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) asm volatile("" : "+v"(pcv[u]));
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int p = p0 + 64 * u + lane, pc = pcv[u];
       bk[u] = p < P ? ((pc >= 0 && pc < K) ? pc : K) : K + 1;
     }
 #pragma unroll
@@ -208,9 +231,10 @@ __device__ __forceinline__ void gather_tasks(const float* __restrict__ db, int H
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int t = t0 + u * kKldThreads;
-      const int i = qdiv(t, kq, rk), q = t - i * kq;
+      const int i = qdiv(t, kq, rk), q = t - i * kq;  // q < kq for every t: a valid list entry
       ro[u] = i * stride + q;
-      v[u] = t < T ? db[static_cast<size_t>(s_proto[i < npc ? i : 0]) * HW + list[q]] : 0.f;
+      const float ld = db[static_cast<size_t>(s_proto[i < npc ? i : 0]) * HW + list[q]];  // unconditional
+      v[u] = t < T ? ld : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
@@ -253,14 +277,17 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
   constexpr int kRows = kKldRange / kKldThreads;
   const int c = blockIdx.x, b = blockIdx.y, rs = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  KSTAMP(7, __builtin_amdgcn_s_memrealtime());
+  KSTAMP(0, __builtin_amdgcn_s_memtime());
   const TL* lab = label + static_cast<size_t>(b) * HW;
   const int n0 = rs * kKldRange, n1 = min(HW, n0 + kKldRange);
   bool in[kRows];
   int below[kRows];
 #pragma unroll
-  for (int r = 0; r < kRows; ++r) {  // all label loads in flight together (under the list scan)
-    const int n = n0 + r * kKldThreads + tid;
-    in[r] = n < n1 && label_at(lab, n) == c;
+  for (int r = 0; r < kRows; ++r) {  // all label loads in flight together (under the list scan);
+    const int n = n0 + r * kKldThreads + tid;  // clamped, unconditional (see class_list_scan)
+    const long long l = label_at(lab, n < n1 ? n : n0);
+    in[r] = n < n1 && l == c;
   }
   // the class's prototype list (was a launch of its own): wave 0 of every workgroup scans
   // proto_class; the (image 0, range 0) workgroup of bucket c publishes it, the one of bucket
@@ -282,6 +309,7 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
   }
   if (tid < kKldMaxPerClass) s_m[tid] = -INFINITY;
   __syncthreads();
+  KSTAMP(1, __builtin_amdgcn_s_memtime());
   const int npc_all = s_cnt;
   const int npc = npc_all < mpc ? npc_all : mpc;
   const size_t bc = static_cast<size_t>(b) * K + c;
@@ -313,9 +341,11 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
   if (tid == 0) *rc = total;
   if (total == 0) {  // uniform
     if (tid == 0) out[2 * kKldMaxPerClass] = 0.f;
+    KSTAMP(6, __builtin_amdgcn_s_memtime());
     return;
   }
   __syncthreads();
+  KSTAMP(2, __builtin_amdgcn_s_memtime());
   const float* db = dist + static_cast<size_t>(b) * P * HW;
 
   float* se = kld_smem;                                      // [npc][257] (stored e)
@@ -348,6 +378,7 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
     const int kq = min(kKldThreads, total - base);
     gather_tasks(db, HW, s_list + base, kq, s_proto, npc, sz, kKldLdsStride);
     __syncthreads();
+    if (base == 0) KSTAMP(3, __builtin_amdgcn_s_memtime());
     {  // chunk max per prototype (8 threads per row) -> running max and the rescale factor
       const int i = tid >> 3, l8 = tid & 7;
       float mx = -INFINITY;
@@ -399,6 +430,7 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
     }
     __syncthreads();
   }
+  KSTAMP(4, __builtin_amdgcn_s_memtime());
   if (tid == 0) out[2 * kKldMaxPerClass] = static_cast<float>(total);
   // the pixel groups' blocks -> LDS [block][g][16], then a fixed-order sum over g per entry
   float* red = kld_smem;
@@ -421,6 +453,7 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
       out[2 * kKldMaxPerClass + 1 + i * kKldMaxPerClass + j] = v;
     }
   }
+  KSTAMP(5, __builtin_amdgcn_s_memtime());
 }
 
 // One workgroup per (class c, image b): merges the range partials in range order. L_i per
@@ -844,6 +877,7 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_compact_kernel(
   extern __shared__ __attribute__((aligned(16))) float kld_smem[];
   __shared__ int s_proto[kKldMaxPerClass];
   __shared__ float s_lse[kKldMaxPerClass];
+  __shared__ int s_lq[kKldThreads];  // the chunk's class pixels (the gather's addresses from LDS)
   constexpr int kRows = kKldRange / kKldThreads;
   const int c = blockIdx.x, b = blockIdx.y, rs = blockIdx.z, tid = threadIdx.x;
   const size_t bc = static_cast<size_t>(b) * K + c;
@@ -858,7 +892,8 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_compact_kernel(
 #pragma unroll
   for (int r = 0; r < kRows; ++r) {
     const int n = n0 + r * kKldThreads + tid;
-    lv[r] = n < n1 ? label_at(lab, n) : -1;
+    const long long l = label_at(lab, n < n1 ? n : n0);  // clamped, unconditional
+    lv[r] = n < n1 ? l : -1;
   }
   const int npc = o1 - o0;
   const bool contributes = npc >= 2 && npc <= mpc && np != 0 && ncls >= 2;
@@ -896,6 +931,7 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_compact_kernel(
     s_proto[tid] = my_p;
     s_lse[tid] = lse[static_cast<size_t>(b) * P + my_p];
   }
+  if (tid < q1) s_lq[tid] = pl[tid];  // the first chunk's list, in the same round trip
   __syncthreads();
   if (tid < npc) {
     float r = 0.f, wk = 0.f;
@@ -910,7 +946,11 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_compact_kernel(
   const float* db = dist + static_cast<size_t>(b) * P * HW;
   for (int base = 0; base < q1; base += kKldThreads) {  // chunks of 256 class pixels
     const int kq = min(kKldThreads, q1 - base);
-    const int* lq = pl + base;
+    const int* lq = s_lq;
+    if (base > 0) {  // the previous chunk's loop-end barrier has passed: every s_lq read is done
+      if (tid < kq) s_lq[tid] = pl[base + tid];
+      __syncthreads();
+    }
     gather_tasks(db, HW, lq, kq, s_proto, npc, slp, kKldLdsStride);
     __syncthreads();
     const float rk = qrcp(kq);
@@ -1115,3 +1155,15 @@ extern "C" int protoseg_kld_expand(const float* g_cls, const int32_t* pix_cls, c
                      pix_cls, proto_slot, P, HW, max_per_class, accumulate, g_dist);
   return check_launch("kld_expand_kernel");
 }
+
+#ifdef PROTOSEG_STAMPS
+// Debug builds: copy (and with dst = null, clear) the KLD partial kernel's stamps.
+extern "C" int protoseg_debug_stamps_kld(void* dst, size_t bytes) {
+  using protoseg::g_stamps_kld;
+  const size_t n = bytes < sizeof(g_stamps_kld) ? bytes : sizeof(g_stamps_kld);
+  if (dst) return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_stamps_kld), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 3;
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamps_kld)) != hipSuccess) return 3;
+  return hipMemset(p, 0, sizeof(g_stamps_kld)) == hipSuccess ? 0 : 3;
+}
+#endif

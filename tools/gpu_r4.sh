@@ -73,6 +73,13 @@ for step in "$@"; do
           || { tail -20 gpurun_out/${T}_ab_fwd_B$B.log; exit 1; }
         tail -3 gpurun_out/${T}_ab_fwd_B$B.log
       done ;;
+    stampskld)  # per-wave phase stamps of the KLD partial kernel (make stamps build)
+      for P in 361 190; do
+        PROTOSEG_HIP_LIB=$PWD/adlm-inherently-interpretable-segmentation_amd/csrc/build_stamps/libprotoseg_hip.so \
+          timeout -k 10 300 python -u tools/stamps_kld.py $P > gpurun_out/${T}_stamps_kld_$P.log 2>&1 \
+          || { tail -20 gpurun_out/${T}_stamps_kld_$P.log; exit 1; }
+        grep -v "^W20" gpurun_out/${T}_stamps_kld_$P.log | tail -10
+      done ;;
     abpush)  # interleaved A/B of the build_var/* push variants on the argmin call (8 maps)
       for P in 190 361; do
         timeout -k 10 300 python -u tools/ab_libs.py --protos $P --call push --reps 40 > gpurun_out/${T}_ab_push_$P.log 2>&1 \
