@@ -479,11 +479,21 @@ __device__ __forceinline__ void kld_merge_regs(const float* __restrict__ pb, int
   float mi[kKldMergeRegS], si[kKldMergeRegS];
   int nr = 0;
   if (tid < kKldMergeRegS && tid < S && valid) nr = static_cast<int>(pb[tid * kKldPartFloats + 2 * kKldMaxPerClass]);
+  {  // clamped loads, pinned before the guards select (pin_batch)
+    const int sc = S - 1, tc = tid < kKldMaxPerClass ? tid : 0;
 #pragma unroll
-  for (int s = 0; s < kKldMergeRegS; ++s) {
-    const bool ld = s < S && tid < npc;
-    mi[s] = ld ? pb[s * kKldPartFloats + tid] : 0.f;
-    si[s] = ld ? pb[s * kKldPartFloats + kKldMaxPerClass + tid] : 0.f;
+    for (int s = 0; s < kKldMergeRegS; ++s) {
+      mi[s] = pb[(s < S ? s : sc) * kKldPartFloats + tc];
+      si[s] = pb[(s < S ? s : sc) * kKldPartFloats + kKldMaxPerClass + tc];
+    }
+    pin_batch(mi);
+    pin_batch(si);
+#pragma unroll
+    for (int s = 0; s < kKldMergeRegS; ++s) {
+      const bool ld = s < S && tid < npc;
+      mi[s] = ld ? mi[s] : 0.f;
+      si[s] = ld ? si[s] : 0.f;
+    }
   }
   // the entries this thread merges (e = tid + 256 u of the npc x npc grid), all ranges
   constexpr int kU = kKldPair / 256;
@@ -491,10 +501,18 @@ __device__ __forceinline__ void kld_merge_regs(const float* __restrict__ pb, int
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
     const int e = tid + 256 * u, i = e / (npc > 0 ? npc : 1), j = e - i * npc;
+    const int ec = e < npc * npc ? i * kKldMaxPerClass + j : 0;  // clamped, pinned below
 #pragma unroll
     for (int s = 0; s < kKldMergeRegS; ++s)
-      tv[u][s] = (e < npc * npc && s < S) ? pb[s * kKldPartFloats + 2 * kKldMaxPerClass + 1 + i * kKldMaxPerClass + j]
-                                          : 0.f;
+      tv[u][s] = pb[(s < S ? s : S - 1) * kKldPartFloats + 2 * kKldMaxPerClass + 1 + ec];
+  }
+#pragma unroll
+  for (int u = 0; u < kU; ++u) pin_batch(tv[u]);
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const int e = tid + 256 * u;
+#pragma unroll
+    for (int s = 0; s < kKldMergeRegS; ++s) tv[u][s] = (e < npc * npc && s < S) ? tv[u][s] : 0.f;
   }
   if (tid < kKldMergeRegS) s_n[tid] = tid < S ? nr : 0;
   __syncthreads();
@@ -878,6 +896,7 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_compact_kernel(
   __shared__ int s_proto[kKldMaxPerClass];
   __shared__ float s_lse[kKldMaxPerClass];
   __shared__ int s_lq[kKldThreads];  // the chunk's class pixels (the gather's addresses from LDS)
+  __shared__ float s_klg[kKldPair];  // the group's KL_ij (0 on the diagonal)
   constexpr int kRows = kKldRange / kKldThreads;
   const int c = blockIdx.x, b = blockIdx.y, rs = blockIdx.z, tid = threadIdx.x;
   const size_t bc = static_cast<size_t>(b) * K + c;
@@ -919,11 +938,15 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_compact_kernel(
   float* scoef = slp + mpc * kKldLdsStride;  // w [npc][npc] | (R_i, WK_i) at kKldPair
   const float* klb = kl + bc * kKldPair;
   const int my_p = tid < npc ? idx[o0 + tid] : 0;
-  {  // kld_coef_kernel's coefficients, same operations
+  {  // kld_coef_kernel's coefficients, same operations; KL_ij also into s_klg for the R / WK sums
+    // (their guarded global reads compiled to a branch and a wait per j: a round trip each)
     const float gl = g_loss ? g_loss[0] : 1.f;
     for (int e = tid; e < npc * npc; e += kKldThreads) {
       const int i = e / npc, j = e - i * npc;
-      const float kij = i == j ? 0.f : klb[i * kKldMaxPerClass + j], kji = i == j ? 0.f : klb[j * kKldMaxPerClass + i];
+      float kk[2] = {klb[i * kKldMaxPerClass + j], klb[j * kKldMaxPerClass + i]};  // diagonal read, unused
+      pin_batch(kk);
+      const float kij = i == j ? 0.f : kk[0], kji = i == j ? 0.f : kk[1];
+      s_klg[e] = kij;
       scoef[e] = i == j ? 0.f : -(gl / static_cast<float>(np)) * expf(-((kji + kij) / 2.f));
     }
   }
@@ -938,7 +961,7 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_compact_kernel(
     for (int j = 0; j < npc; ++j) {
       const float w = scoef[tid * npc + j];
       r += w;
-      wk = fmaf(w, tid == j ? 0.f : klb[tid * kKldMaxPerClass + j], wk);
+      wk = fmaf(w, s_klg[tid * npc + j], wk);  // 0 on the diagonal
     }
     scoef[kKldPair + 2 * tid] = r;
     scoef[kKldPair + 2 * tid + 1] = wk;

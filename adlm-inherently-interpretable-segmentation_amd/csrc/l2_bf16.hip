@@ -47,15 +47,14 @@ __device__ void stage_p_rows(bf16* img, const float* __restrict__ protos, int P,
   const int plane = Pp * kC;
   for (int idx = tid; idx < Pp * 8; idx += nth) {
     const int p = idx >> 3, e8 = idx & 7, q = e8 >> 1, h = e8 & 1;
-    const int pc = p < P ? p : P - 1;  // clamped: every load is issued unconditionally
+    const int pc = p < P ? p : P - 1;  // clamped: every load is issued unconditionally (pin_batch)
     float v[8];
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj)
-      v[jj] = -2.f * protos[static_cast<size_t>(pc) * kC + chan_of(q, h, jj)];
-    bf16x8 f[T];
-    if (p >= P)
+    for (int jj = 0; jj < 8; ++jj) v[jj] = protos[static_cast<size_t>(pc) * kC + chan_of(q, h, jj)];
+    pin_batch(v);
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) v[jj] = 0.f;
+    for (int jj = 0; jj < 8; ++jj) v[jj] = p < P ? -2.f * v[jj] : 0.f;
+    bf16x8 f[T];
     split8<T>(v, f);
     store_frag<T>(img, plane, img_off<8>(p, e8), f);
   }
@@ -71,8 +70,13 @@ __device__ void stage_pt_perm(bf16* img, const float* __restrict__ protos, int P
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
       const int p = pt * 32 + perm_of(e8 * 8 + jj);
-      const float t = -2.f * protos[static_cast<size_t>(p < P ? p : P - 1) * kC + c];  // -2 folded in (exact)
-      v[jj] = p < P ? t : 0.f;
+      v[jj] = protos[static_cast<size_t>(p < P ? p : P - 1) * kC + c];
+    }
+    pin_batch(v);
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int p = pt * 32 + perm_of(e8 * 8 + jj);
+      v[jj] = p < P ? -2.f * v[jj] : 0.f;  // -2 folded in (exact)
     }
     bf16x8 f[T];
     split8<T>(v, f);
@@ -89,13 +93,19 @@ __device__ void stage_w_perm(bf16* img, const float* __restrict__ w, int K, int 
     const int row = idx >> 2, e8 = idx & 3;  // row = pt*32 + k
     const int pt = row >> 5, k = row & 31;
     float v[8] = {};
-    if (K > 0)  // w is null iff K = 0 (uniform)
+    if (K > 0) {  // w is null iff K = 0 (uniform)
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
         const int p = pt * 32 + perm_of(e8 * 8 + jj);
-        const float t = w[static_cast<size_t>(k < K ? k : 0) * ldw + (p < P ? p : P - 1)];
-        v[jj] = (k < K && p < P) ? scale * t : 0.f;
+        v[jj] = w[static_cast<size_t>(k < K ? k : 0) * ldw + (p < P ? p : P - 1)];
       }
+      pin_batch(v);
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int p = pt * 32 + perm_of(e8 * 8 + jj);
+        v[jj] = (k < K && p < P) ? scale * v[jj] : 0.f;
+      }
+    }
     bf16x8 f[T];
     split8<T>(v, f);
     store_frag<T>(img, plane, img_off<4>(row, e8), f);
@@ -111,13 +121,19 @@ __device__ void stage_wt_rows(bf16* img, const float* __restrict__ w, int K, int
   for (int idx = tid; idx < Pp * 4; idx += nth) {
     const int p = idx >> 2, e8 = idx & 3;
     float v[8] = {};
-    if (K > 0)  // w is null iff K = 0 (uniform)
+    if (K > 0) {  // w is null iff K = 0 (uniform)
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
         const int k = e8 * 8 + jj;
-        const float t = w[static_cast<size_t>(k < K ? k : 0) * ldw + (p < P ? p : P - 1)];
-        v[jj] = (k < K && p < P) ? scale * t : 0.f;
+        v[jj] = w[static_cast<size_t>(k < K ? k : 0) * ldw + (p < P ? p : P - 1)];
       }
+      pin_batch(v);
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int k = e8 * 8 + jj;
+        v[jj] = (k < K && p < P) ? scale * v[jj] : 0.f;
+      }
+    }
     bf16x8 f[T];
     split8<T>(v, f);
     store_frag<T>(img, plane, img_off<4>(p, e8), f);

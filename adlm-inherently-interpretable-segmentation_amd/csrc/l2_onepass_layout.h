@@ -39,8 +39,12 @@ __device__ __forceinline__ void fill_pi(const float* __restrict__ protos, int P,
   const int p = tid >> 3, q = tid & 7;
   float v[8];
   bf16x8 f[kT];
+  const int pc = p < P ? p : P - 1;  // clamped loads, pinned (pin_batch)
 #pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = p < P ? -2.f * protos[static_cast<size_t>(p) * kC + 8 * q + e] : 0.f;
+  for (int e = 0; e < 8; ++e) v[e] = protos[static_cast<size_t>(pc) * kC + 8 * q + e];
+  pin_batch(v);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = p < P ? -2.f * v[e] : 0.f;
   split8<kT>(v, f);
   const int off = o.pi + p * 128 + ((q ^ pi_swz(p)) & 7) * 16;
 #pragma unroll
@@ -55,12 +59,15 @@ __device__ __forceinline__ void fill_wt(const float* __restrict__ w_last, int K,
   const int lane = tid & 63, frag = tid >> 6, g = lane >> 4, m = lane & 15;
   if (frag >= Pp / 16) return;
   const int p = 16 * frag + m;
-  float v[8];
+  float v[8] = {};
   bf16x8 f[kT];
+  if (w_last && K > 0) {  // clamped loads, pinned (pin_batch)
+    const int pc = p < P ? p : P - 1;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int k = 8 * g + e;
-    v[e] = (w_last && p < P && k < K) ? wt_scale * w_last[static_cast<size_t>(k) * ldw + p] : 0.f;
+    for (int e = 0; e < 8; ++e) v[e] = w_last[static_cast<size_t>(8 * g + e < K ? 8 * g + e : K - 1) * ldw + pc];
+    pin_batch(v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (p < P && 8 * g + e < K) ? wt_scale * v[e] : 0.f;
   }
   split8<kT>(v, f);
 #pragma unroll

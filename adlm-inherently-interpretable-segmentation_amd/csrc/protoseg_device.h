@@ -79,6 +79,15 @@ __device__ __forceinline__ float activation_grad(float d, float eps, int act_kin
 
 // Orders this wave's preceding LDS accesses before its following ones, for data that
 // crosses lanes of the same wave (the compiler cannot see that dependency).
+// A batch of guarded loads: every element is loaded through a clamped (always valid) address,
+// then the batch is pinned in VGPRs before the guards select. Left alone, the compiler sinks each
+// load into its guard's branch with a wait of its own: one round trip per load, not per batch.
+template <int N, typename T>
+__device__ __forceinline__ void pin_batch(T (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
+}
+
 __device__ __forceinline__ void wave_lds_fence() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }

@@ -71,8 +71,9 @@ __global__ __launch_bounds__(256) void patch_mask_kernel(const TL* __restrict__ 
       for (int i = r0; i < r1; i += 8) {
         uint32_t q[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-          q[u] = i + u < r1 ? *reinterpret_cast<const uint32_t*>(L + static_cast<size_t>(i + u) * W + c0) : 0u;
+        for (int u = 0; u < 8; ++u)  // clamped rows, pinned (pin_batch); rows past r1 are not OR-ed
+          q[u] = *reinterpret_cast<const uint32_t*>(L + static_cast<size_t>(i + u < r1 ? i + u : r1 - 1) * W + c0);
+        pin_batch(q);
 #pragma unroll
         for (int u = 0; u < 8; ++u)
           if (i + u < r1)
