@@ -139,6 +139,7 @@ __global__ __launch_bounds__(kEvalThreads) void eval_seg_kernel(const float* __r
 // kEvalRows output rows at once: 4 loads per class serve kEvalRows pixels instead of one.
 // Grid: (column tiles, source rows h, images); a group with more rows runs in chunks.
 constexpr int kEvalRows = 8;
+constexpr int kEvalBatch = 4;  // classes / prototypes whose loads are in flight together
 
 template <typename TL>
 __global__ __launch_bounds__(kEvalThreads) void eval_rows_kernel(const float* __restrict__ logits,
@@ -193,28 +194,32 @@ __global__ __launch_bounds__(kEvalThreads) void eval_rows_kernel(const float* __
           pred[r] = 0;
         }
       }
-      if (K > 1) {
-        u00 = lb[q00 + 1];
-        u01 = lb[q01 + 1];
-        u10 = lb[q10 + 1];
-        u11 = lb[q11 + 1];
-      }
-      for (int k = 1; k < K; ++k) {
-        const float a = lx.l0 * u00 + lx.l1 * u01;
-        const float bb = lx.l0 * u10 + lx.l1 * u11;
-        if (k + 1 < K) {
-          const float* ln = lb + k + 1;
-          u00 = ln[q00];
-          u01 = ln[q01];
-          u10 = ln[q10];
-          u11 = ln[q11];
+      // the other classes kEvalBatch at a time: the batch's loads (clamped, pinned) in flight
+      // together, then evaluated in class order (one round trip per batch, not per class)
+      for (int k0 = 1; k0 < K; k0 += kEvalBatch) {
+        float uu[kEvalBatch][4];
+#pragma unroll
+        for (int j = 0; j < kEvalBatch; ++j) {
+          const float* ln = lb + (k0 + j < K ? k0 + j : K - 1);
+          uu[j][0] = ln[q00];
+          uu[j][1] = ln[q01];
+          uu[j][2] = ln[q10];
+          uu[j][3] = ln[q11];
         }
 #pragma unroll
-        for (int r = 0; r < kEvalRows; ++r) {
-          const float v = l0[r] * a + l1[r] * bb;
-          if (v > best[r]) {  // torch.argmax: first maximal index
-            best[r] = v;
-            pred[r] = k;
+        for (int j = 0; j < kEvalBatch; ++j) pin_batch(uu[j]);
+#pragma unroll
+        for (int j = 0; j < kEvalBatch; ++j) {
+          if (k0 + j >= K) break;  // uniform
+          const float a = lx.l0 * uu[j][0] + lx.l1 * uu[j][1];
+          const float bb = lx.l0 * uu[j][2] + lx.l1 * uu[j][3];
+#pragma unroll
+          for (int r = 0; r < kEvalRows; ++r) {
+            const float v = l0[r] * a + l1[r] * bb;
+            if (v > best[r]) {  // torch.argmax: first maximal index
+              best[r] = v;
+              pred[r] = k0 + j;
+            }
           }
         }
       }
@@ -238,29 +243,30 @@ __global__ __launch_bounds__(kEvalThreads) void eval_rows_kernel(const float* __
           near[r] = 0;
         }
       }
-      if (P > 1) {
-        const float* dp = db + plane;
-        v00 = dp[o00];
-        v01 = dp[o01];
-        v10 = dp[o10];
-        v11 = dp[o11];
-      }
-      for (int p = 1; p < P; ++p) {
-        const float a = lx.l0 * v00 + lx.l1 * v01;
-        const float bb = lx.l0 * v10 + lx.l1 * v11;
-        if (p + 1 < P) {
-          const float* dn = db + static_cast<size_t>(p + 1) * plane;
-          v00 = dn[o00];
-          v01 = dn[o01];
-          v10 = dn[o10];
-          v11 = dn[o11];
+      for (int p0 = 1; p0 < P; p0 += kEvalBatch) {  // batched as the classes
+        float vv[kEvalBatch][4];
+#pragma unroll
+        for (int j = 0; j < kEvalBatch; ++j) {
+          const float* dn = db + static_cast<size_t>(p0 + j < P ? p0 + j : P - 1) * plane;
+          vv[j][0] = dn[o00];
+          vv[j][1] = dn[o01];
+          vv[j][2] = dn[o10];
+          vv[j][3] = dn[o11];
         }
 #pragma unroll
-        for (int r = 0; r < kEvalRows; ++r) {
-          const float v = l0[r] * a + l1[r] * bb;
-          if (v < best[r]) {  // torch.argmin: first minimal index
-            best[r] = v;
-            near[r] = p;
+        for (int j = 0; j < kEvalBatch; ++j) pin_batch(vv[j]);
+#pragma unroll
+        for (int j = 0; j < kEvalBatch; ++j) {
+          if (p0 + j >= P) break;  // uniform
+          const float a = lx.l0 * vv[j][0] + lx.l1 * vv[j][1];
+          const float bb = lx.l0 * vv[j][2] + lx.l1 * vv[j][3];
+#pragma unroll
+          for (int r = 0; r < kEvalRows; ++r) {
+            const float v = l0[r] * a + l1[r] * bb;
+            if (v < best[r]) {  // torch.argmin: first minimal index
+              best[r] = v;
+              near[r] = p0 + j;
+            }
           }
         }
       }

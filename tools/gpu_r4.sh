@@ -80,6 +80,16 @@ for step in "$@"; do
           || { tail -20 gpurun_out/${T}_stamps_kld_$P.log; exit 1; }
         grep -v "^W20" gpurun_out/${T}_stamps_kld_$P.log | tail -10
       done ;;
+    evalb)  # the bench's eval line alone (plus the headline step it always runs)
+      timeout -k 10 300 python -u bench.py --no-kld --no-push --no-knn --no-train --no-sigmoid --no-cpu-baseline --no-wide \
+        --no-small-batch --side-protos 0 > gpurun_out/${T}_evalb.log 2>&1 || { tail -30 gpurun_out/${T}_evalb.log; exit 1; }
+      python3 tools/bench_summary.py gpurun_out/${T}_evalb.log ;;
+    abchunk)  # interleaved A/B of the build_var/* variants at P = 570 (two prototype chunks)
+      for c in fwd bwd_full; do
+        timeout -k 10 300 python -u tools/ab_libs.py --protos 570 --call $c --reps 30 > gpurun_out/${T}_ab_${c}_570.log 2>&1 \
+          || { tail -20 gpurun_out/${T}_ab_${c}_570.log; exit 1; }
+        tail -3 gpurun_out/${T}_ab_${c}_570.log
+      done ;;
     abpush)  # interleaved A/B of the build_var/* push variants on the argmin call (8 maps)
       for P in 190 361; do
         timeout -k 10 300 python -u tools/ab_libs.py --protos $P --call push --reps 40 > gpurun_out/${T}_ab_push_$P.log 2>&1 \
