@@ -425,11 +425,18 @@ __global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
     const int g = t * 32 + j;
     const unsigned lbase = g < npix ? static_cast<unsigned>((g * K + 4 * h) * 4) : kOOB;
     const int krem = K - 4 * h;
+    float old[16];
+    if (accumulate) {  // chunk c > 0: the earlier chunks' logits, loaded as one batch (pin_batch)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        old[r] = BufIO<float>::load(rl, row_of(r) < krem ? lbase : kOOB, static_cast<unsigned>(row_of(r) * 4));
+      pin_batch(old);
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const unsigned off = row_of(r) < krem ? lbase : kOOB;
       float v = lacc[r];
-      if (accumulate) v = BufIO<float>::load(rl, off, static_cast<unsigned>(row_of(r) * 4)) + v;  // chunk c > 0
+      if (accumulate) v = old[r] + v;
       BufIO<float>::store(rl, v, off, static_cast<unsigned>(row_of(r) * 4));
     }
   };
@@ -587,6 +594,14 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
   // gx[ct] register 8s+jj is channel chan_of(2ct+s, h, jj) — the channel of raw[(2ct+s)*8+jj].
   // conv(x^2, ones) backward then pow backward: gsum * (2x); plus the xp branch in gx.
   auto store_gx = [&](unsigned xoff, const float (&raw)[kNQ * 8], const f32x16 (&gx)[2], float gsum_all) {
+    float old[kNQ * 8];
+    if (accumulate) {  // prototype chunks: the earlier chunks' g_x, loaded as one batch (pin_batch)
+#pragma unroll
+      for (int q = 0; q < kNQ; ++q)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) old[q * 8 + jj] = BufIO<TX>::load(rgx, xoff, chan_base(q, jj) * cs);
+      pin_batch(old);
+    }
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
@@ -595,7 +610,7 @@ __global__ __launch_bounds__(kWavesA * 64) void l2_bwd_x_bf16_kernel(
         for (int jj = 0; jj < 8; ++jj) {
           const int q = 2 * ct + s;
           float v = gx[ct][8 * s + jj] + gsum_all * (2.f * raw[q * 8 + jj]);
-          if (accumulate) v = BufIO<TX>::load(rgx, xoff, chan_base(q, jj) * cs) + v;  // prototype chunks
+          if (accumulate) v = old[q * 8 + jj] + v;
           BufIO<TX>::store(rgx, v, xoff, chan_base(q, jj) * cs);
         }
   };
