@@ -260,7 +260,7 @@ __device__ __forceinline__ void lse_merge(float& m, float& s, float mo, float so
 // only: e_i = exp(z_i - m_i) is recomputed where used (the same expression: same bits), half the
 // LDS and more workgroups per CU for many prototypes per class, but more VGPRs (kld_recompute).
 template <typename TL, bool RC>
-__global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* __restrict__ dist, int P, int HW,
+__global__ __launch_bounds__(kKldThreads) __attribute__((amdgpu_waves_per_eu(5))) void kld_partial_kernel(const float* __restrict__ dist, int P, int HW,
                                                                   const TL* __restrict__ label, int K, int mpc,
                                                                   const int32_t* __restrict__ proto_class,
                                                                   int* __restrict__ off, int* __restrict__ idx,
@@ -383,7 +383,14 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
       const int i = tid >> 3, l8 = tid & 7;
       float mx = -INFINITY;
       if (i < npc)
-        for (int q = l8; q < kq; q += 8) mx = fmaxf(mx, sz[i * kKldLdsStride + q]);
+        for (int q = l8; q < kq; q += 32) {  // 4 LDS reads in flight (clamped: a repeat changes no max)
+          float t[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) t[u] = sz[i * kKldLdsStride + (q + 8 * u < kq ? q + 8 * u : q)];
+          pin_batch(t);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) mx = fmaxf(mx, t[u]);
+        }
       mx = fmaxf(mx, __shfl_xor(mx, 1));
       mx = fmaxf(mx, __shfl_xor(mx, 2));
       mx = fmaxf(mx, __shfl_xor(mx, 4));
@@ -445,7 +452,15 @@ __global__ __launch_bounds__(kKldThreads) void kld_partial_kernel(const float* _
     const int i = e / npc, j = e - i * npc;
     const int b2 = (i >> 2) * nbi + (j >> 2), sl = (i & 3) * 4 + (j & 3);
     float v = 0.f;
-    for (int gg = 0; gg < G; ++gg) v += red[(b2 * G + gg) * 16 + sl];
+    for (int g0 = 0; g0 < G; g0 += 8) {  // 8 LDS reads in flight (clamped, pinned), added in order
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = red[(b2 * G + (g0 + u < G ? g0 + u : G - 1)) * 16 + sl];
+      pin_batch(t);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (g0 + u < G) v += t[u];
+    }
     if (i == j) {
       out[i] = s_m[i];
       out[kKldMaxPerClass + i] = v;
@@ -885,7 +900,7 @@ __global__ __launch_bounds__(kKldThreads) void kld_grad_kernel(
 // pixel exactly once, no memset), and the group's coefficients (kld_coef_kernel's arithmetic, in
 // LDS).
 template <typename TL, bool RC>
-__global__ __launch_bounds__(kKldThreads) void kld_grad_compact_kernel(
+__global__ __launch_bounds__(kKldThreads) __attribute__((amdgpu_waves_per_eu(5))) void kld_grad_compact_kernel(
     const float* __restrict__ dist, int P, int HW, const TL* __restrict__ label, int K, int mpc,
     const int* __restrict__ off, const int* __restrict__ idx, const int* __restrict__ slot,
     const int* __restrict__ cnt, const float* __restrict__ lse, const float* __restrict__ kl,
