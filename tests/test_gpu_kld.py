@@ -77,6 +77,21 @@ def test_kld_vs_oracle(device, ldtype, B, h, w, P, K, block):
     assert n > 0 and 0.0 < loss <= 1.0
 
 
+@pytest.mark.parametrize("B,h,w,P,K,block", [
+    (1, 65, 65, 361, 19, 8),    # 5 pixel ranges (<= 8: the merge's register path), 19 per class
+                                # (the partial / compact kernels' recomputed-exp form)
+    (1, 97, 97, 38, 19, 6),     # 10 ranges: the merge's general path
+    (1, 129, 67, 190, 19, 8),   # 9 ranges at 10 per class (stored-exp form)
+])
+def test_kld_vs_oracle_many_ranges(device, B, h, w, P, K, block):
+    x, protos, _ = po.synthetic_inputs(B, 64, h, w, P, K, seed=h + P)
+    dist = po.l2_convolution(x, protos[:, :, None, None], torch.ones(P, 64, 1, 1))
+    target = ko.synthetic_targets(B, h, w, K, seed=w, block=block)
+    ident = po.class_identity(P, K)
+    loss, n = _check(dist, target, ident, device, g_loss=0.5)
+    assert n > 0 and 0.0 < loss <= 1.0
+
+
 def test_kld_no_pairs_and_skip_rules(device):
     P, K, h, w = 6, 3, 4, 4
     dist = torch.rand(1, P, h, w)
