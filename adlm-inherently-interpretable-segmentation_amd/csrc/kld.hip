@@ -219,25 +219,32 @@ __device__ __forceinline__ int qdiv(int n, int d, float r) {
 __device__ __forceinline__ float qrcp(int d) { return __builtin_amdgcn_rcpf(static_cast<float>(d)); }
 
 // Gathers rows[i][q] = d[s_proto[i]][list[q]] for i < npc, q < kq over the workgroup's threads
-// (q fastest: consecutive lanes read consecutive class pixels of one prototype row), four loads
-// in flight per thread.
+// (q fastest: consecutive lanes read consecutive class pixels of one prototype row), kG loads in
+// flight per thread (pinned batches: the LDS address reads together, then the loads).
+template <int kG>
 __device__ __forceinline__ void gather_tasks(const float* __restrict__ db, int HW, const int* list, int kq,
                                              const int* s_proto, int npc, float* rows, int stride) {
   const int T = npc * kq;
   const float rk = qrcp(kq);
-  for (int t0 = threadIdx.x; t0 < T; t0 += 4 * kKldThreads) {
-    float v[4];
-    int ro[4];
+  // kG tasks per thread in flight: their LDS address reads, then their loads
+  for (int t0 = threadIdx.x; t0 < T; t0 += kG * kKldThreads) {
+    int pr[kG], lq[kG], ro[kG];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kG; ++u) {
       const int t = t0 + u * kKldThreads;
       const int i = qdiv(t, kq, rk), q = t - i * kq;  // q < kq for every t: a valid list entry
       ro[u] = i * stride + q;
-      const float ld = db[static_cast<size_t>(s_proto[i < npc ? i : 0]) * HW + list[q]];  // unconditional
-      v[u] = t < T ? ld : 0.f;
+      pr[u] = s_proto[i < npc ? i : 0];
+      lq[u] = list[q];
     }
+    pin_batch(pr);
+    pin_batch(lq);
+    float v[kG];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < kG; ++u) v[u] = db[static_cast<size_t>(pr[u]) * HW + lq[u]];  // clamped: valid
+    pin_batch(v);
+#pragma unroll
+    for (int u = 0; u < kG; ++u)
       if (t0 + u * kKldThreads < T) rows[ro[u]] = v[u];
   }
 }
@@ -376,7 +383,7 @@ __global__ __launch_bounds__(kKldThreads) __attribute__((amdgpu_waves_per_eu(5))
   }
   for (int base = 0; base < total; base += kKldThreads) {
     const int kq = min(kKldThreads, total - base);
-    gather_tasks(db, HW, s_list + base, kq, s_proto, npc, sz, kKldLdsStride);
+    gather_tasks<4>(db, HW, s_list + base, kq, s_proto, npc, sz, kKldLdsStride);
     __syncthreads();
     if (base == 0) KSTAMP(3, __builtin_amdgcn_s_memtime());
     {  // chunk max per prototype (8 threads per row) -> running max and the rescale factor
@@ -989,7 +996,7 @@ __global__ __launch_bounds__(kKldThreads) __attribute__((amdgpu_waves_per_eu(5))
       if (tid < kq) s_lq[tid] = pl[base + tid];
       __syncthreads();
     }
-    gather_tasks(db, HW, lq, kq, s_proto, npc, slp, kKldLdsStride);
+    gather_tasks<8>(db, HW, lq, kq, s_proto, npc, slp, kKldLdsStride);
     __syncthreads();
     const float rk = qrcp(kq);
     for (int t = tid; t < npc * kq; t += kKldThreads) {
