@@ -81,6 +81,17 @@ int launch_prep_onepass(const Geometry& g, const float* protos, const float* w_l
 int launch_bwd_onepass_bf16(const Geometry& g, bool x_bf16, const void* x, const void* img, float eps, int act_kind,
                             const float* g_logits, const float* g_dist, void* g_x, float* ws, hipStream_t stream,
                             int accumulate = 0);
+// Wave-owned backward (l2_bwd_wave.hip): bf16x3, P <= 384 per launch, 4 waves (one per SIMD)
+// each owning a quarter of the prototypes for every product; reads the standard bf16 operand
+// image block (launch_prep_bf16, bf16_image_bytes(P)); g_x (+= when accumulate) and a g_P / g_W
+// slab per workgroup in the reduce kernel's layout (launch_bwd_reduce_bf16_chunks).
+int bf16_wave_nb(int P);
+bool bf16_bwd_wave_fits(const Geometry& g, int terms);
+int bf16_bwd_wave_grid(const Geometry& g);
+size_t bf16_bwd_wave_slab_elems(const Geometry& g);
+int launch_bwd_wave_bf16(const Geometry& g, bool x_bf16, const void* x, const void* img, float eps, int act_kind,
+                         const float* g_logits, const float* g_dist, void* g_x, float* ws, hipStream_t stream,
+                         int accumulate = 0);
 // Fixed-order sum of `slabs` partial slabs in ws (+ 2p sum g_s) into g_protos / g_w.
 int launch_bwd_reduce_bf16(const Geometry& g, const float* ws, int slabs, const float* protos, int act_kind,
                            float* g_protos, float* g_w, hipStream_t stream);

@@ -617,15 +617,22 @@ namespace {
 // kernel launches and can be captured in a HIP graph once the block exists.
 constexpr size_t kImageBlockMin = 512 * 1024;
 
-// Backward kernel choice for the bf16x3 training backward: the one-pass kernel for P > 192 (one
-// pass over X instead of 192-prototype chunks), the fused kernel below; PROTOSEG_BWD=onepass /
-// fused forces one (read per call: tests and measurement A/B switch it in one process).
-bool use_onepass(int P) {
+// Backward kernel choice for the bf16x3 training backward (C = 64):
+//   wave    l2_bwd_wave.hip: 4 waves, one per SIMD, each owning a quarter of the prototypes for
+//           every product (P <= 384 per launch, prototype chunks beyond);
+//   onepass l2_bwd_onepass.hip: 8 waves, owner phase + g_x phase (P <= 384 per launch);
+//   fused   l2_bwd_fused.hip: 6 owner + 2 g_x waves (P <= 192 per launch).
+// PROTOSEG_BWD=wave / onepass / fused forces one (read per call: tests and measurement A/B
+// switch it in one process).
+enum class BwdKernel { kWave, kOnepass, kFused };
+BwdKernel bwd_kernel(int P) {
   const char* e = getenv("PROTOSEG_BWD");
-  if (e && !strcmp(e, "onepass")) return true;
-  if (e && !strcmp(e, "fused")) return false;
-  return P > 192;
+  if (e && !strcmp(e, "wave")) return BwdKernel::kWave;
+  if (e && !strcmp(e, "onepass")) return BwdKernel::kOnepass;
+  if (e && !strcmp(e, "fused")) return BwdKernel::kFused;
+  return P > 192 ? BwdKernel::kOnepass : BwdKernel::kFused;
 }
+bool use_onepass(int P) { return bwd_kernel(P) == BwdKernel::kOnepass; }
 
 int stream_block(size_t need, hipStream_t s, int kind, void** out) {
   return stream_scratch(static_cast<ScratchKind>(kind), need, kImageBlockMin, s, out);
@@ -694,8 +701,14 @@ namespace {
 TrainOperands train_operands_kind(int C, int P, int K, int precision) {
   if (terms_of(precision) != 2 || C != 64 || P <= 0 || K < 0 || use_wide(C, K, P)) return TrainOperands::kNone;
   const Geometry g = geometry_of(1, C, 1, 1, P, K);
-  if (use_onepass(P)) return P <= 384 && bf16_bwd_onepass_fits(g, 2) ? TrainOperands::kOnepass : TrainOperands::kNone;
-  return P <= 192 && bf16_bwd_fused_fits(g, 2) ? TrainOperands::kFused : TrainOperands::kNone;
+  switch (bwd_kernel(P)) {
+    case BwdKernel::kWave:  // the standard image block (launch_prep_bf16), one chunk
+      return P <= 384 && bf16_bwd_wave_fits(g, 2) ? TrainOperands::kFused : TrainOperands::kNone;
+    case BwdKernel::kOnepass:
+      return P <= 384 && bf16_bwd_onepass_fits(g, 2) ? TrainOperands::kOnepass : TrainOperands::kNone;
+    default:
+      return P <= 192 && bf16_bwd_fused_fits(g, 2) ? TrainOperands::kFused : TrainOperands::kNone;
+  }
 }
 
 size_t train_operands_bytes(int C, int P, int K, TrainOperands kind) {
@@ -881,6 +894,14 @@ extern "C" size_t protoseg_l2_bwd_workspace_size(int B, int C, int H, int W, int
       if (q > need) need = q;
     }
   }
+  if (C == 64) {  // wave backward: one slab per workgroup and prototype chunk of <= 384
+    const int nchunk = static_cast<int>(ceil_div(P, 384)), per = static_cast<int>(ceil_div(P, nchunk));
+    const Geometry gc = geometry_of(B, C, H, W, per, K);
+    if (bf16_bwd_wave_fits(gc, 2)) {
+      const size_t q = static_cast<size_t>(nchunk) * bf16_bwd_wave_slab_elems(gc) * sizeof(float);
+      if (q > need) need = q;
+    }
+  }
   if (C == 64) {  // fused backward: one slab per workgroup and prototype chunk (fused_chunks)
     const int nchunk = static_cast<int>(ceil_div(P, 192)), per = static_cast<int>(ceil_div(P, nchunk));
     const Geometry gc = geometry_of(B, C, H, W, per, K);
@@ -946,6 +967,37 @@ int l2_bwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const fl
     if (!wide_family_fits(geo)) return fail(PROTOSEG_ERR_UNSUPPORTED, "B*H*W*max(P, C) >= 2^31 elements");
     return launch_bwd_wide(geo, xb, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_x, g_protos,
                            g_logits ? g_w : nullptr, workspace, s);
+  }
+  // Training backward at bf16x3, wave-owned prototypes (l2_bwd_wave.hip): up to 384 prototypes
+  // per launch over the standard operand images, prototype chunks beyond (chunk c > 0 adds its
+  // g_x), one slab reduce.
+  if (terms == 2 && (xsig || (g_x && (g_protos || g_w))) && bwd_kernel(P) == BwdKernel::kWave) {
+    const int nchunk = static_cast<int>(ceil_div(P, 384)), per = static_cast<int>(ceil_div(P, nchunk));
+    Geometry gc = geometry_of(B, C, H, W, per, K);
+    if (bf16_bwd_wave_fits(gc, terms)) {
+      KernelSpan span(nchunk > 1 ? "l2_bwd_wave_bf16_kernel" : "", "", s);
+      const size_t cb = bf16_image_bytes(gc, terms);
+      const size_t chunk_elems = bf16_bwd_wave_slab_elems(gc);
+      const int grid = bf16_bwd_wave_grid(gc);
+      ImageBlock img;
+      if (tk == TrainOperands::kFused && nchunk == 1)
+        img.ptr = const_cast<void*>(operands);
+      else if (int st = img.build(geo, terms, protos, g_logits ? w_last : nullptr, act_kind, eps, s, per))
+        return st;
+      for (int c = 0; c < nchunk; ++c) {
+        const int p0 = c * per, pc = P - p0 < per ? P - p0 : per;
+        Geometry gq = geometry_of(B, C, H, W, pc, K);
+        gq.ldw = gq.ldd = P;
+        gq.p0 = p0;
+        gq.xsig = xsig;
+        gq.cgd = cgd;
+        if (int st = launch_bwd_wave_bf16(gq, xb, x, static_cast<unsigned char*>(img.ptr) + c * cb, eps, act_kind,
+                                          g_logits, g_dist, g_x, ws + c * chunk_elems, s, c > 0))
+          return st;
+      }
+      return launch_bwd_reduce_bf16_chunks(geo, per, nchunk, ws, grid, chunk_elems, protos, act_kind, g_protos,
+                                           g_logits ? g_w : nullptr, s);
+    }
   }
   // Training backward at bf16x3: ONE pass over X for up to 384 prototypes (19 prototypes/class;
   // l2_bwd_onepass.hip), prototype chunks of <= 384 beyond (chunk c > 0 adds its g_x), one slab

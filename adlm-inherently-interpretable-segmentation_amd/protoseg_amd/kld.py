@@ -63,11 +63,12 @@ def _(distances, target_img, proto_class, num_classes, max_per_class):
             distances.new_empty((n,), dtype=torch.uint8))
 
 
-# The backward writes its per-pair coefficients into the workspace's range-partial region, which
-# the forward leaves dead; every value the forward produced for the backward (lists, counts,
-# log-sum-exps, KL matrices, pair count) is only read. So the op does not count as mutating the
-# workspace: a second backward over a retained graph (retain_graph=True) recomputes the same
-# coefficients from the same forward results.
+# protoseg_kld_backward writes its per-pair coefficients into the workspace's range-partial
+# region (dead after the forward). The op runs it on a private copy of the workspace, so it really
+# mutates none of its inputs (mutates_args=() holds for torch.library.opcheck and
+# functionalization). This is the dense fallback path (hooks, explicit-input passes, the wide
+# family); the training path's compact backward computes its coefficients in LDS and writes nothing
+# into the workspace.
 @torch.library.custom_op("protoseg::kld_backward", mutates_args=(), device_types="cuda")
 def kld_backward(distances: Tensor, target_img: Tensor, proto_class: Tensor, num_classes: int, max_per_class: int,
                  workspace: Tensor, g_loss: Tensor) -> Tensor:
@@ -80,9 +81,10 @@ def kld_backward(distances: Tensor, target_img: Tensor, proto_class: Tensor, num
     pc = proto_class.to(torch.int32).contiguous()
     g = g_loss.to(torch.float32).contiguous()
     g_dist = torch.empty_like(d)
+    ws = workspace.clone()  # the coefficients go into the copy's range-partial region
     with torch.cuda.device(dev):
         _lib.call("protoseg_kld_backward", _lib.ptr(d), B, P, HW, _lib.ptr(t), ldt, _lib.ptr(pc), int(num_classes),
-                  int(max_per_class), _lib.ptr(g), _lib.ptr(workspace), workspace.numel(), _lib.ptr(g_dist),
+                  int(max_per_class), _lib.ptr(g), _lib.ptr(ws), ws.numel(), _lib.ptr(g_dist),
                   _lib.stream_of(dev))
     return g_dist
 
@@ -133,11 +135,35 @@ def kld_backward_compact(distances: Tensor, target_img: Tensor, proto_class: Ten
     return g_cls, pix_cls, proto_slot
 
 
+# A private leaf that every _KldToLayer node takes as an input (and never sends a gradient to):
+# its AccumulateGrad node is in each KLD graph. In a plain backward() the engine runs every node
+# of the graph, so it reports that node as executing; when the pass has explicit inputs
+# (autograd.grad, backward(inputs=...)) it runs only the nodes that lead to them, and the probe is
+# never one of them. That tells the two kinds of pass apart from inside the backward.
+_probe_state: dict = {}
+
+
+def _graph_probe(device) -> Tuple[Tensor, object]:
+    hit = _probe_state.get(str(device))
+    if hit is None:
+        probe = torch.zeros((), device=device, requires_grad=True)
+        node = torch.autograd.graph.get_gradient_edge(probe).node  # its AccumulateGrad
+        hit = _probe_state[str(device)] = (probe, node)
+    return hit
+
+
+def _pass_runs_every_node(probe_node) -> bool:
+    """True in a backward pass without explicit inputs (every node of the graph executes)."""
+    try:
+        return bool(torch._C._will_engine_execute_node(probe_node))
+    except (AttributeError, RuntimeError):  # no engine introspection: treat as explicit inputs
+        return False
+
+
 def _layer_backward_runs(layer_node) -> bool:
     """Whether the current backward pass will run the prototype layer's backward past its own
     node, i.e. consume a deposit: some node behind it (x's producer, the prototypes' or the last
-    layer's AccumulateGrad) executes. ``autograd.grad(loss, distances)`` and
-    ``backward(inputs=[distances])`` stop at the distances: the layer never runs."""
+    layer's AccumulateGrad) executes."""
     if layer_node is None:
         return False
     try:
@@ -150,20 +176,23 @@ class _KldToLayer(torch.autograd.Function):
     """kld_forward whose backward hands the compact gradient to the prototype layer that produced
     ``distances`` (ops.DistGradSink) instead of returning a dense [B, P, H, W] tensor.
 
-    The hand-off is taken only when the layer's backward consumes it in the same backward pass
-    and nothing observes the gradient at ``distances`` itself (``retain_grad`` or a tensor hook):
-    otherwise this returns the dense gradient, so ``autograd.grad(kld, distances)``, hooks and
-    ``backward(inputs=[distances])`` see the real values. Deposits carry the backward pass's
-    graph-task id and the layer takes only its own pass's, so a ``retain_graph`` replay never
-    sums a stale deposit."""
+    The hand-off is taken only in a plain ``backward()`` (no explicit inputs) that runs the
+    layer's backward, with nothing observing the gradient at ``distances`` itself (``retain_grad``
+    or a tensor hook). Any pass with explicit inputs (``autograd.grad``, ``backward(inputs=...)``)
+    gets the dense gradient: ``distances`` may be one of its capture targets, and the engine does
+    not say which tensors those are. So captures, hooks and ``retain_grad`` see the real values.
+    Deposits carry the backward pass's graph-task id and the layer takes only its own pass's, so a
+    ``retain_graph`` replay never sums a stale deposit."""
 
     @staticmethod
-    def forward(ctx, distances, target_img, proto_class, num_classes, max_per_class, sink, layer_node):
+    def forward(ctx, distances, target_img, proto_class, num_classes, max_per_class, sink, layer_node, probe,
+                probe_node):
         loss, npairs, ws = torch.ops.protoseg.kld_forward(distances, target_img, proto_class, num_classes,
                                                           max_per_class)
         ctx.save_for_backward(distances, target_img, proto_class, ws)
         ctx.num_classes, ctx.max_per_class, ctx.sink = num_classes, max_per_class, sink
         ctx.layer_node = layer_node
+        ctx.probe_node = probe_node
         ctx.dist_ref = sink.dist_ref
         ctx.mark_non_differentiable(npairs)
         return loss, npairs
@@ -171,12 +200,12 @@ class _KldToLayer(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_loss, g_npairs):
         distances, target_img, proto_class, ws = ctx.saved_tensors
-        none = (None,) * 6
+        none = (None,) * 8
         if g_loss is None or not ctx.needs_input_grad[0]:
             return (None,) + none
         d = ctx.dist_ref() if ctx.dist_ref is not None else None
         observed = d is not None and (d.retains_grad or bool(getattr(d, "_backward_hooks", None)))
-        if observed or not _layer_backward_runs(ctx.layer_node):
+        if observed or not _pass_runs_every_node(ctx.probe_node) or not _layer_backward_runs(ctx.layer_node):
             g = kld_backward(distances, target_img, proto_class, ctx.num_classes, ctx.max_per_class, ws, g_loss)
             return (g.to(distances.dtype),) + none
         g_cls, pix_cls, proto_slot = kld_backward_compact(distances, target_img, proto_class, ctx.num_classes,
@@ -191,8 +220,9 @@ def kld_with_pairs(distances: Tensor, target_img: Tensor, proto_class: Tensor, n
     layer in that form (no [B, P, H, W] tensor); otherwise autograd gets the dense one."""
     sink = getattr(distances, "_protoseg_sink", None)
     if sink is not None and distances.requires_grad and torch.is_grad_enabled() and sink.accepts(max_per_class):
+        probe, probe_node = _graph_probe(distances.device)
         return _KldToLayer.apply(distances, target_img, proto_class, int(num_classes), int(max_per_class), sink,
-                                 distances.grad_fn)
+                                 distances.grad_fn, probe, probe_node)
     loss, npairs, _ = torch.ops.protoseg.kld_forward(distances, target_img, proto_class, int(num_classes),
                                                      int(max_per_class))
     return loss, npairs

@@ -261,8 +261,9 @@ def _(x, protos, w_last, g_logits, g_cls, pix_cls, proto_slot, max_per_class, ep
 
 def _setup_context(ctx, inputs, output):
     x, protos, w_last, eps, act_kind, precision, with_dist, with_logits, with_act = inputs[:9]
-    ctx.save_for_backward(x, protos, w_last)  # (its version check also guards the operands below)
-    ctx.operands = output[3] if output[3].numel() else None
+    # the forward-built operand images are saved like the inputs, so saved-tensor hooks see them
+    # and the version check guards them (an empty tensor when the forward built none)
+    ctx.save_for_backward(x, protos, w_last, output[3])
     ctx.eps = eps
     ctx.act_kind = act_kind
     ctx.precision = precision
@@ -292,7 +293,7 @@ def _act_grad_as_dist_grad(x, protos, w_last, g_act, eps, act_kind, precision):
 
 
 def _backward(ctx, g_dist, g_logits, g_act, g_operands=None):
-    x, protos, w_last = ctx.saved_tensors
+    x, protos, w_last, operands = ctx.saved_tensors
     need_x, need_p, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
     sink = ctx.sink
     compact = sink.take() if sink is not None else []
@@ -310,7 +311,7 @@ def _backward(ctx, g_dist, g_logits, g_act, g_operands=None):
         g_dist, compact = dense.reshape(B, P, H, W), []
     if g_dist is None and g_logits is None and not compact:
         return None, None, None, None, None, None, None, None, None, None
-    ops_buf = ctx.operands
+    ops_buf = operands if operands.numel() else None
     if compact:
         g_cls, pix_cls, proto_slot, mpc = compact[0]
         g_x, g_p, g_w = l2_backward_kld(x, protos, w_last, g_logits, g_cls, pix_cls, proto_slot, mpc, ctx.eps,

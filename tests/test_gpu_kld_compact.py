@@ -64,7 +64,8 @@ def _layer_inputs(B, h, w, P, K, seed):
 
 
 @pytest.mark.parametrize("P,bwd", [(190, "fused"), (190, "onepass"), (361, "onepass"), (570, "onepass"),
-                                   (570, "fused"), (38, "fused")])
+                                   (570, "fused"), (38, "fused"), (38, "wave"), (190, "wave"), (361, "wave"),
+                                   (570, "wave")])
 def test_l2_bwd_kld_equals_dense(device, monkeypatch, P, bwd):
     """protoseg_l2_bwd_kld == protoseg_l2_bwd on the expanded g_dist, bit for bit, for the fused
     (P <= 192 per chunk) and one-pass (P <= 384 per chunk) kernels, chunked P included."""
@@ -248,6 +249,57 @@ def test_hand_off_retain_graph_and_partial_passes(device):
     for a, b, f in zip(leaves, leaves2, first):
         assert torch.equal(f, b.grad)
         assert torch.equal(a.grad, b.grad + b.grad)
+
+
+def test_hand_off_explicit_inputs_with_the_layer_behind(device):
+    """a pass with explicit inputs that captures the distances AND runs the layer's
+    backward (backward(inputs=[dist, protos]); autograd.grad over [dist, a non-leaf upstream of x])
+    must see the dense KLD gradient at the distances, and the layer's gradients must equal the
+    dense path's: the hand-off is only taken in plain backward() passes."""
+    _, kld, ops = _mods()
+    P, K = 190, 19
+
+    def run(mode, dense_only):
+        leaves, dist, logits, gl, target, ident = _layer_and_kld(device, P, K)
+        d_in = dist * 1.0 if dense_only else dist
+        loss = 0.25 * kld.kld_loss(d_in, target, ident) + (logits * gl).sum()
+        if mode == "inputs":
+            loss.backward(inputs=[dist, leaves[1]])
+            out = [dist.grad, leaves[1].grad]
+        else:
+            out = list(torch.autograd.grad(loss, [dist, leaves[1], leaves[2]]))
+        torch.cuda.synchronize()
+        return [t.detach().clone() for t in out], dist, target, ident
+
+    for mode in ("inputs", "grad"):
+        got, dist, target, ident = run(mode, False)
+        ref, _, _, _ = run(mode, True)
+        assert torch.equal(got[0], _dense_kld_grad(dist, target, ident)), mode
+        for a, b in zip(got, ref):
+            assert torch.equal(a, b), mode
+        assert dist._protoseg_sink.deposits == []
+
+    # autograd.grad over the distances and a non-leaf tensor upstream of x
+    _lib, kld, ops = _mods()
+    B, h, w = 2, 33, 35
+    x, protos, w_last, g_logits = _layer_inputs(B, h, w, P, K, seed=31)
+    target = ko.synthetic_targets(B, h, w, K, seed=32, block=5).to(device)
+    ident = po.class_identity(P, K)
+
+    def grads(dense_only):
+        x0 = x.to(device).requires_grad_(True)
+        feats = x0 * 1.0  # a non-leaf before the layer's x
+        dist, logits, _ = ops.prototype_layer(feats, protos.to(device), w_last.to(device))
+        d_in = dist * 1.0 if dense_only else dist
+        loss = 0.25 * kld.kld_loss(d_in, target, ident) + (logits * g_logits.to(device)).sum()
+        gd, gf = torch.autograd.grad(loss, [dist, feats])
+        torch.cuda.synchronize()
+        return gd, gf, dist
+
+    gd, gf, dist = grads(False)
+    rd, rf, _ = grads(True)
+    assert torch.equal(gd, _dense_kld_grad(dist, target, ident)) and torch.equal(gd, rd)
+    assert torch.equal(gf, rf)
 
 
 def test_kld_gradient_ignores_stale_workspace(device):

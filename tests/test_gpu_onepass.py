@@ -1,8 +1,12 @@
-"""The one-pass training backward (l2_bwd_onepass.hip: up to 384 prototypes per launch, 8 waves
-with equal roles, 16x16x32 bf16 MFMA, bf16x3 products) against the oracle's autograd of
-model.py:203-283, and against the 192-prototype fused kernel it replaces for P > 192.
-PROTOSEG_BWD selects the kernel per call (onepass / fused). Tolerance: rtol 1e-4 of each
-gradient's own scale, as tests/test_gpu_l2.py."""
+"""The training backwards that serve up to 384 prototypes per launch, against the oracle's autograd
+of model.py:203-283 and against the 192-prototype fused kernel:
+  onepass  l2_bwd_onepass.hip: 8 waves with equal roles, 16x16x32 bf16 MFMA;
+  wave     l2_bwd_wave.hip: 4 waves, one per SIMD, each owning a quarter of the prototypes for
+           every product, 32x32x16 bf16 MFMA.
+Both bf16x3 products. PROTOSEG_BWD selects the kernel per call (wave / onepass / fused).
+Tolerance: rtol 1e-4 of each gradient's own scale, as tests/test_gpu_l2.py."""
+
+KERNELS = ["onepass", "wave"]
 import pytest
 import torch
 
@@ -33,8 +37,9 @@ def assert_scaled_close(a, ref, rtol=1e-4, name=""):
     (1, 16, 16, 570, 19),    # two chunks of 285 (g_x accumulated by the second)
 ])
 @pytest.mark.parametrize("activation", ["log", "linear"])
-def test_onepass_backward_vs_oracle(device, monkeypatch, B, h, w, P, K, activation):
-    monkeypatch.setenv("PROTOSEG_BWD", "onepass")
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_onepass_backward_vs_oracle(device, monkeypatch, B, h, w, P, K, activation, kernel):
+    monkeypatch.setenv("PROTOSEG_BWD", kernel)
     ops = _ops()
     x, protos, w_last = po.synthetic_inputs(B, 64, h, w, P, K, seed=B * 100 + h + P)
     gen = torch.Generator().manual_seed(11)
@@ -50,8 +55,9 @@ def test_onepass_backward_vs_oracle(device, monkeypatch, B, h, w, P, K, activati
 
 
 @pytest.mark.parametrize("P", [190, 361])
-def test_onepass_backward_with_g_dist(device, monkeypatch, P):
-    monkeypatch.setenv("PROTOSEG_BWD", "onepass")
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_onepass_backward_with_g_dist(device, monkeypatch, P, kernel):
+    monkeypatch.setenv("PROTOSEG_BWD", kernel)
     ops = _ops()
     B, h, w, K = 2, 33, 31, 19
     x, protos, w_last = po.synthetic_inputs(B, 64, h, w, P, K, seed=P)
@@ -68,7 +74,8 @@ def test_onepass_backward_with_g_dist(device, monkeypatch, P):
 
 
 @pytest.mark.parametrize("P", [190, 361])
-def test_onepass_equals_fused_within_rounding(device, monkeypatch, P):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_onepass_equals_fused_within_rounding(device, monkeypatch, P, kernel):
     """The same gradients from both kernels (different MFMA shapes and summation orders)."""
     ops = _ops()
     B, h, w, K = 4, 65, 65, 19
@@ -78,15 +85,16 @@ def test_onepass_equals_fused_within_rounding(device, monkeypatch, P):
             ops.PRECISIONS["bf16x3"], True, True, True)
     monkeypatch.setenv("PROTOSEG_BWD", "fused")
     a = ops.l2_backward(*args)
-    monkeypatch.setenv("PROTOSEG_BWD", "onepass")
+    monkeypatch.setenv("PROTOSEG_BWD", kernel)
     b = ops.l2_backward(*args)
     torch.cuda.synchronize()
     for u, v, name in zip(a, b, ("g_x", "g_protos", "g_w")):
         assert_scaled_close(v, u, 2e-5, name)
 
 
-def test_onepass_deterministic(device, monkeypatch):
-    monkeypatch.setenv("PROTOSEG_BWD", "onepass")
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_onepass_deterministic(device, monkeypatch, kernel):
+    monkeypatch.setenv("PROTOSEG_BWD", kernel)
     ops = _ops()
     B, h, w, P, K = 8, 65, 65, 361, 19
     x, protos, w_last = po.synthetic_inputs(B, 64, h, w, P, K, seed=1)
@@ -100,7 +108,8 @@ def test_onepass_deterministic(device, monkeypatch):
 
 
 @pytest.mark.parametrize("xdtype", [torch.float32, torch.bfloat16])
-def test_onepass_x_sigmoid_and_bf16_features(device, monkeypatch, xdtype):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_onepass_x_sigmoid_and_bf16_features(device, monkeypatch, xdtype, kernel):
     from protoseg_amd import _lib
     """PROTOSEG_X_SIGMOID (the add-on nn.Sigmoid on the x load) and bf16 feature maps at P = 361:
     against the oracle on sigmoid(pre-activation), gradient taken w.r.t. the pre-activation."""

@@ -30,6 +30,8 @@ def _inputs(device, B, h, w, P, K, seed):
     (190, 19, None, "fused"),        # 10 prototypes/class
     (96, 32, None, "fused"),
     (190, 19, "onepass", "onepass"),  # PROTOSEG_BWD override: the one-pass block at Pp 256
+    (361, 19, "wave", "fused"),      # the wave-owned backward reads the standard image block
+    (190, 19, "wave", "fused"),
     (570, 19, None, "none"),         # two prototype chunks: no operands, plain calls
 ])
 @pytest.mark.parametrize("activation", ["log", "linear"])

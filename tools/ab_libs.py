@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--fmap", type=int, default=65)
     ap.add_argument("--reps", type=int, default=40)
+    ap.add_argument("--main-bwd", default="", help="PROTOSEG_BWD values to run the main library with")
     ap.add_argument("--call", default="bwd_full", choices=["bwd_full", "bwd_full_xsig", "fwd", "fwd_xsig", "push", "mask", "kld", "kldb", "kldc",
                                                        "bwdk"])
     args = ap.parse_args()
@@ -47,9 +48,22 @@ def main():
     logits = torch.empty(B, h, w, K, device=dev)
     gx, gp, gw = torch.empty_like(x), torch.empty(P, C, device=dev), torch.empty(K, P, device=dev)
     libs = {"main": load(os.path.join(CSRC, "libprotoseg_hip.so"))}
+    # PROTOSEG_BWD per library: --main-bwd for main (several: main@k1, main@k2 entries), a BWD file
+    # in a variant's directory for that variant (else the process environment)
+    bwd_of = {}
+    if args.main_bwd:
+        main = libs.pop("main")
+        for k in args.main_bwd.split(","):
+            libs[f"main@{k}"] = main
+            bwd_of[f"main@{k}"] = k
     for d in sorted(glob.glob(os.path.join(CSRC, "build_var", "*", "libprotoseg_hip.so"))):
-        libs[os.path.basename(os.path.dirname(d))] = load(d)
-    ws_b = libs["main"].protoseg_l2_bwd_workspace_size(B, C, h, w, P, K)
+        name = os.path.basename(os.path.dirname(d))
+        libs[name] = load(d)
+        f = os.path.join(os.path.dirname(d), "BWD")
+        if os.path.exists(f):
+            bwd_of[name] = open(f).read().strip()
+    first = next(iter(libs.values()))
+    ws_b = max(lb.protoseg_l2_bwd_workspace_size(B, C, h, w, P, K) for lb in libs.values())
     ws = torch.empty(ws_b, device=dev, dtype=torch.uint8)
     P_, s = _lib.ptr, _lib.stream_of(dev)
     act = _lib.X_SIGMOID if args.call.endswith("xsig") else 0
@@ -63,7 +77,7 @@ def main():
         pcls = torch.clamp(torch.arange(P) // max(1, P // K), max=K - 1).to(torch.int32).to(dev)
         keys = torch.empty((n_img, P), device=dev, dtype=torch.int64)
         second = torch.empty_like(keys)
-        st = libs["main"].protoseg_patch_class_mask(P_(lab), _lib.U8, n_img, 1024, 2048, ph, pw, None, 0, P_(mask), s)
+        st = first.protoseg_patch_class_mask(P_(lab), _lib.U8, n_img, 1024, 2048, ph, pw, None, 0, P_(mask), s)
         assert st == 0
 
     if args.call in ("kld", "kldb", "kldc", "bwdk"):  # KLD forward (kldb: + backward, kldc: + compact backward) on the layer's distances (bench.py setup_kld: 8x8 label blocks)
@@ -79,18 +93,20 @@ def main():
         gcls = torch.empty(B * h * w, mpc, device=dev)
         pixc = torch.empty(B * h * w, device=dev, dtype=torch.int32)
         pslot = torch.empty(P, device=dev, dtype=torch.int32)
-        st = libs["main"].protoseg_l2_fwd(P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 0,
+        st = first.protoseg_l2_fwd(P_(x), 0, B, C, h, w, P_(protos), P, P_(wl), K, 1e-4, 0,
                                           _lib.PRECISIONS["bf16x3"], P_(dist), None, P_(logits), s)
         assert st == 0
         if args.call == "bwdk":  # the layer backward with the compact KLD gradient (protoseg_l2_bwd_kld)
-            st = libs["main"].protoseg_kld_forward(P_(dist), B, P, h * w, P_(tgt), _lib.I64, P_(pcls), K, mpc,
+            st = first.protoseg_kld_forward(P_(dist), B, P, h * w, P_(tgt), _lib.I64, P_(pcls), K, mpc,
                                                    P_(kloss), None, P_(kws), kws_b, s)
-            st = st or libs["main"].protoseg_kld_backward_compact(P_(dist), B, P, h * w, P_(tgt), _lib.I64, P_(pcls),
+            st = st or first.protoseg_kld_backward_compact(P_(dist), B, P, h * w, P_(tgt), _lib.I64, P_(pcls),
                                                                   K, mpc, P_(kg), P_(kws), kws_b, P_(gcls), P_(pixc),
                                                                   P_(pslot), s)
             assert st == 0
 
-    def call(lib):
+    def call(lib, name=None):
+        if name in bwd_of:
+            os.environ["PROTOSEG_BWD"] = bwd_of[name]
         if args.call == "mask":
             st = lib.protoseg_patch_class_mask(P_(lab), _lib.U8, n_img, 1024, 2048, ph, pw, None, 0, P_(mask), s)
         elif args.call in ("kld", "kldb", "kldc"):
@@ -118,7 +134,7 @@ def main():
 
     ref = None
     for name, lib in libs.items():  # warm-up + the variants agree with main
-        call(lib)
+        call(lib, name)
         torch.cuda.synchronize()
         out = (gdist if args.call == "kldb" else gcls if args.call == "kldc" else mask.float() if args.call == "mask" else
                kloss.reshape(1) if args.call == "kld" else keys.float() if args.call == "push" else
@@ -133,7 +149,7 @@ def main():
         for name, lib in libs.items():
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
-            call(lib)
+            call(lib, name)
             b.record()
             times[name].append((a, b))
     torch.cuda.synchronize()

@@ -14,7 +14,7 @@ mkdir -p "$d"
 cp "$src" "$d/$obj.hip"
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $extra "$@" -I"$C/../../include" -I"$C" -c "$d/$obj.hip" -o "$d/$obj.o"
 objs=""
-for o in capi l2_layer l2_wide l2_bf16 l2_bwd_fused l2_bwd_onepass push kld eval knn bbox adam; do
+for o in capi l2_layer l2_wide l2_bf16 l2_bwd_fused l2_bwd_onepass l2_bwd_wave push kld eval knn bbox adam; do
   [ "$o" = "$obj" ] || objs="$objs $C/$o.o"
 done
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fPIC $objs "$d/$obj.o" -o "$d/libprotoseg_hip.so"
