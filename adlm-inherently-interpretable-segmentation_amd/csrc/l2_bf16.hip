@@ -939,7 +939,8 @@ __global__ __launch_bounds__(MAXT) void l2_bwd_pw_bf16_kernel(
 __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __restrict__ slab, int S, int P,
                                                                   int per, int K, int ldw, const float* __restrict__ protos,
                                                                   float w_unit, float* __restrict__ g_protos,
-                                                                  float* __restrict__ g_w, size_t chunk_elems) {
+                                                                  float* __restrict__ g_w, size_t chunk_elems,
+                                                                  int gp_t) {
   __shared__ float part[4][64];
   __shared__ float gpart[4][64];
   const int p0 = static_cast<int>(blockIdx.y) * per;
@@ -954,7 +955,8 @@ __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __
   const int grp = threadIdx.x >> 6;
   const bool active = e < Pp * kC + 32 * Pp;
   const bool is_gp = e < Pp * kC;
-  const int p_of_e = is_gp ? e / kC : 0;
+  // gp_t: the slab's g_P block is [c][Pp] (element c * Pp + p), else [Pp][c]
+  const int p_of_e = is_gp ? (gp_t ? e % Pp : e / kC) : 0;
   const int gs_e = Pp * kC + 32 * Pp + p_of_e;
   float s = 0.f, gs = 0.f;
   if (active) {
@@ -985,7 +987,7 @@ __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __
   const int l = threadIdx.x;
   const float tot = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
   if (is_gp) {
-    const int c = e - p_of_e * kC;
+    const int c = gp_t ? e / Pp : e - p_of_e * kC;
     if (p_of_e < P && g_protos) {
       const float gst = ((gpart[0][l] + gpart[1][l]) + gpart[2][l]) + gpart[3][l];
       g_protos[static_cast<size_t>(p_of_e) * kC + c] = tot + gst * (2.f * protos[static_cast<size_t>(p_of_e) * kC + c]);
@@ -1191,12 +1193,12 @@ int launch_prep_bf16(const Geometry& g, int terms, const float* protos, const fl
 
 int launch_bwd_reduce_bf16_chunks(const Geometry& g, int per, int nchunk, const float* ws, int slabs,
                                   size_t chunk_elems, const float* protos, int act_kind, float* g_protos, float* g_w,
-                                  hipStream_t stream) {
+                                  hipStream_t stream, int gp_t) {
   const int Pp = static_cast<int>(ceil_div(per, 32) * 32);
   const int elems = Pp * kC + 32 * Pp;
   hipLaunchKernelGGL(l2_bwd_reduce_bf16_kernel, dim3(static_cast<unsigned>(ceil_div(elems, 64)), nchunk), dim3(256),
                      0, stream, ws, slabs, g.P, per, g.K, g.ldw, protos, act_unit(act_kind), g_protos, g_w,
-                     chunk_elems);
+                     chunk_elems, gp_t);
   return check_launch("l2_bwd_reduce_bf16_kernel");
 }
 

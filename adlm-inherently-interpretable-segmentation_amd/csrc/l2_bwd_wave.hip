@@ -111,6 +111,22 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 
 #define WSCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 
+// WAVE_STAMP (diagnostic builds only): per-wave s_memtime deltas per phase, summed over the
+// tiles, into a buffer of their own (read by protoseg_dev_wave_stamps); nothing else reads it.
+#ifdef WAVE_STAMP
+__device__ unsigned long long g_wave_stamp[1024 * 16];
+#define WSTAMP(k)                                                  \
+  do {                                                             \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    st_acc[k] += now_ - st_last;                                   \
+    st_last = now_;                                                \
+  } while (0)
+#else
+#define WSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
 __device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
   return static_cast<uint32_t>(__builtin_bit_cast(uint16_t, static_cast<bf16>(lo))) |
          (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, static_cast<bf16>(hi))) << 16);
@@ -133,6 +149,9 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
 
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = wave_id();
   const int ntiles = (npix + 31) / 32;
+#ifdef WAVE_STAMP
+  unsigned long long st_acc[16] = {}, st_last = __builtin_amdgcn_s_memtime();
+#endif
   const int G = static_cast<int>(gridDim.x);
   const int iters = (ntiles - static_cast<int>(blockIdx.x) + G - 1) / G;
   const unsigned sz = sizeof(TX);
@@ -159,7 +178,7 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
   // image, registers for the launch), ||p||^2 as a bf16 pair (the B operand of the k-step that
   // adds ||x||^2 + ||p||^2, below) and (GD = 2) the class / compact column
   bf16x8 wreg[NB][2][kWT];
-  uint32_t p2pk[NB];
+  uint32_t p2pk[NB][2];
   int pcls[NB], pslot[NB];
 #pragma unroll
   for (int jb = 0; jb < NB; ++jb) {
@@ -174,8 +193,11 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
                         rimg, wb + static_cast<unsigned>((t * Pi * 32 + img_off<4>(p, 2 * s + h)) * 2), 0, 0));
     const float p2 = __uint_as_float(
         __builtin_amdgcn_raw_buffer_load_b32(rimg, p < Pi ? static_cast<unsigned>(io.p2 + 4 * p) : kOOB, 0, 0));
+    // three bf16 terms hold the f32 exactly (hi, mid, lo: 8 + 8 + 8 significant bits)
     const float p2h = static_cast<float>(static_cast<bf16>(p2));
-    p2pk[jb] = pack_bf16(p2h, p2 - p2h);
+    const float p2m = static_cast<float>(static_cast<bf16>(p2 - p2h));
+    p2pk[jb][0] = h == 0 ? pack_bf16(1.f, p2h) : 0u;
+    p2pk[jb][1] = h == 0 ? pack_bf16(p2m, (p2 - p2h) - p2m) : 0u;
     pcls[jb] = -2;  // never a pixel class (those are >= -1)
     pslot[jb] = 0;
     if constexpr (GD == 2) {
@@ -191,33 +213,42 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
   // (buffer_load ... lds: no registers; out-of-range lanes land as 0). x piece k (channels 2k,
   // 2k + 1: [c][n] rows, lane = pixel) for k = 8 wave .. 8 wave + 7; g_logits pieces of the
   // tile's contiguous 32 K floats m = wave, wave + 4, ...
-  auto stage_dma = [&](int t) __attribute__((always_inline)) {
+  struct Stage {
+    unsigned off;  // the lane's x offset (kOOB past the map)
+    int lim;       // valid floats of the tile's g_logits run
+  };
+  auto stage_of = [&](int t) __attribute__((always_inline)) -> Stage {
     const int n = lane & 31, gp = t * 32 + n;
-    unsigned off = kOOB;
+    Stage st{kOOB, t < ntiles ? min(32, npix - t * 32) * K : 0};
     if (t < ntiles && gp < npix) {
       const int b = div_pix(gp, HW);
-      off = static_cast<unsigned>((b * kC + (lane >> 5)) * HW + (gp - b * HW)) * sz;
+      st.off = static_cast<unsigned>((b * kC + (lane >> 5)) * HW + (gp - b * HW)) * sz;
     }
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
+    return st;
+  };
+  // piece m of tile t: m = 0..7 x pieces, 8..11 g_logits pieces (16 pieces of 64 floats cover
+  // 32 K <= 1024; pieces past the run land zeros), 12 the pixel classes (GD = 2, wave 3)
+  auto stage_piece = [&](int t, const Stage& st, int m) __attribute__((always_inline)) {
+    if (m < 8) {
       const int k = 8 * wave + m;
-      dma<TX>(rx, smem_raw + L.raw + k * 256, off, static_cast<unsigned>(2 * k) * chs);
-    }
-    // g_logits: 16 pieces of 64 floats cover 32 K <= 1024 (pieces past the run land zeros)
-    const int lim = t < ntiles ? min(32, npix - t * 32) * K : 0;  // valid floats of the tile's run
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      const int m = wave + kWW * mi;
-      dma<float>(rg, smem_raw + L.raw_gl + m * 256, m * 64 + lane < lim ? static_cast<unsigned>(lane * 4) : kOOB,
-                 static_cast<unsigned>((t * 32 * K + m * 64) * 4));
-    }
-    if constexpr (GD == 2) {
+      dma<TX>(rx, smem_raw + L.raw + k * 256, st.off, static_cast<unsigned>(2 * k) * chs);
+    } else if (m < 12) {
+      const int mg = wave + kWW * (m - 8);
+      dma<float>(rg, smem_raw + L.raw_gl + mg * 256, mg * 64 + lane < st.lim ? static_cast<unsigned>(lane * 4) : kOOB,
+                 static_cast<unsigned>((t * 32 * K + mg * 64) * 4));
+    } else if constexpr (GD == 2) {
       if (wave == kWW - 1) {
         const int valid = t < ntiles ? min(32, npix - t * 32) : 0;
         dma<float>(rpc, smem_raw + L.raw_cls, lane < valid ? static_cast<unsigned>(lane * 4) : kOOB,
                    static_cast<unsigned>(t * 32 * 4));
       }
     }
+  };
+  constexpr int kPieces = GD == 2 ? 13 : 12;
+  auto stage_dma = [&](int t) __attribute__((always_inline)) {
+    const Stage st = stage_of(t);
+#pragma unroll
+    for (int m = 0; m < kPieces; ++m) stage_piece(t, st, m);
   };
   // Raw tile -> split images. Lane (n = j, hh = h) of wave w: x channels chan_of(w, hh, 0..7) of
   // pixel n (chunk 2w + hh of the x image row n), the chunk's ||x||^2 piece in the family's fixed
@@ -328,9 +359,16 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
     gp[jb][0] = gp[jb][1] = gw[jb] = zero16();
     gsum[jb] = 0.f;
   }
-  bf16x8 ones;
+  // sum_p g_s per pixel: a 16x16x32 product of a selector A against the g_x product's B fragments
+  // (lane l: pixel l & 31, prototypes 16 s + 8 (l >> 5) + e), read as 16x16x32 operands (column
+  // l & 15, k = 8 (l >> 4) + e): A row 0 is one on k-groups 0 and 2 (pixels 0..15), row 1 on
+  // groups 1 and 3 (pixels 16..31), i.e. lanes 0, 32 and 17, 49
+  bf16x8 onesel;
+  {
+    const bf16 v = static_cast<bf16>(lane == 0 || lane == 32 || lane == 17 || lane == 49 ? 1.f : 0.f);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = static_cast<bf16>(1.f);
+    for (int e = 0; e < 8; ++e) onesel[e] = v;
+  }
 
   // ---- one tile. One wave per SIMD: nothing else fills the matrix pipe, so the instruction
   // stream itself puts VALU work between the MFMAs. Per block jb the work is a run of steps
@@ -341,16 +379,18 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
   //          operands are read one step ahead;
   //   B(jb): block jb's g_P / g_W products.
   // Then the last block's g_x products and the partial into the wave's LDS region.
-  auto compute_tile = [&]() __attribute__((always_inline)) {
-    // the A operand of the ||x||^2 + ||p||^2 k-step: row n = j holds (x2_hi, x2_lo, 1, 1) in
-    // k = 0..3 (half 0); its B operand per block (1, 1, p2_hi, p2_lo): the MFMA adds x2 + p2 to
-    // every element, so the S accumulator starts from zero (no per-element initialisation)
+  auto compute_tile = [&](int tn) __attribute__((always_inline)) {
+    // the A operand of the ||x||^2 + ||p||^2 k-step: row n = j holds (x2_hi, x2_mid, x2_lo, 1, 1,
+    // 1) in k = 0..5 (half 0); its B operand per block (1, 1, 1, p2_hi, p2_mid, p2_lo): three bf16
+    // terms hold each f32 exactly, so the MFMA adds the f32 x2 + p2 to every element and the S
+    // accumulator starts from zero (no per-element initialisation)
     u32x4 ax2;
     {
       const unsigned a = S0 + L.x2u + 4 * j;
       const float x2 = (lds_ld(a) + lds_ld(a + 128)) + (lds_ld(a + 256) + lds_ld(a + 384));
       const float x2h = static_cast<float>(static_cast<bf16>(x2));
-      ax2 = u32x4{h == 0 ? pack_bf16(x2h, x2 - x2h) : 0u, one2, 0u, 0u};
+      const float x2m = static_cast<float>(static_cast<bf16>(x2 - x2h));
+      ax2 = h == 0 ? u32x4{pack_bf16(x2h, x2m), pack_bf16((x2 - x2h) - x2m, 1.f), one2, 0u} : u32x4{0u, 0u, 0u, 0u};
     }
     const bf16x8 ax2f = __builtin_bit_cast(bf16x8, ax2);
 
@@ -403,7 +443,7 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
     };
     auto front_mfma = [&](int jb, int k, Front& fr, const FrontOps& o) __attribute__((always_inline)) {
       if (k == 0) {
-        const bf16x8 bp2 = __builtin_bit_cast(bf16x8, u32x4{one2, h == 0 ? p2pk[jb] : 0u, 0u, 0u});
+        const bf16x8 bp2 = __builtin_bit_cast(bf16x8, u32x4{one2, p2pk[jb][0], p2pk[jb][1], 0u});
         fr.acc = mfma_bf16(ax2f, bp2, zero16());
       }
       if (k < 4) {
@@ -455,23 +495,20 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
     };
     // g_P^T += X^T g_s, g_W += g_logits^T act (the accumulators are the B operands); X^T and
     // g_logits^T by transposed reads, k = n in the accumulator's row order; step s = 0, 1
-    struct GpwOps {
-      bf16x8 xt[2][kWT], glt[kWT];
+    // piece pc of k-step s: pc = 0, 1 g_P^T channel tile pc, pc = 2 g_W
+    struct WOps {
+      bf16x8 a[kWT];
     };
-    auto gpw_load = [&](int s, GpwOps& o) __attribute__((always_inline)) {
+    auto w_load = [&](int s, int pc, WOps& o) __attribute__((always_inline)) {
 #pragma unroll
-      for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-        for (int t = 0; t < kWT; ++t)
-          o.xt[ct][t] = lds_tr(a_xt[0][ct] + s * 2048 + t * 4096, a_xt[1][ct] + s * 2048 + t * 4096);
-#pragma unroll
-      for (int t = 0; t < kWT; ++t) o.glt[t] = lds_tr(a_glt[0] + s * 1024 + t * 2048, a_glt[1] + s * 1024 + t * 2048);
+      for (int t = 0; t < kWT; ++t)
+        o.a[t] = pc < 2 ? lds_tr(a_xt[0][pc] + s * 2048 + t * 4096, a_xt[1][pc] + s * 2048 + t * 4096)
+                        : lds_tr(a_glt[0] + s * 1024 + t * 2048, a_glt[1] + s * 1024 + t * 2048);
     };
-    auto gpw_mfma = [&](int jb, int s, const GpwOps& o, const bf16x8 (&gsf)[2][kWT], const bf16x8 (&actf)[2][kWT])
+    auto w_mfma = [&](int jb, int s, int pc, const WOps& o, const bf16x8 (&gsf)[2][kWT], const bf16x8 (&actf)[2][kWT])
         __attribute__((always_inline)) {
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct) gp[jb][ct] = mma_split<kWT>(o.xt[ct], gsf[s], gp[jb][ct]);
-      gw[jb] = mma_split<kWT>(o.glt, actf[s], gw[jb]);
+      if (pc < 2) gp[jb][pc] = mma_split<kWT>(o.a, gsf[s], gp[jb][pc]);
+      else gw[jb] = mma_split<kWT>(o.a, actf[s], gw[jb]);
     };
     // g_x^T [c][n] += (-2P)^T [c][p] g_s^T [p][n] over block jb's 32 prototypes (natural k
     // order: k = 8h + e is prototype 16s + 8h + e), sum_p g_s against ones; step (s, half):
@@ -493,89 +530,88 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
         o.pa[t] = lds_tr(a_pa[0][half] + op, a_pa[1][half] + op);
       }
     };
-    auto gx_mfma = [&](int half, const GxOps& o, const bf16x8 (&bt)[kWT], f32x16 (&gx)[2], f32x16& sg)
+    auto gx_mfma = [&](int half, const GxOps& o, const bf16x8 (&bt)[kWT], f32x16 (&gx)[2], f32x4& sg)
         __attribute__((always_inline)) {
       gx[half] = mma_split<kWT>(o.pa, bt, gx[half]);
       if (half == 1) {
-        sg = mfma_bf16(ones, bt[1], sg);
-        sg = mfma_bf16(ones, bt[0], sg);
+        sg = __builtin_amdgcn_mfma_f32_16x16x32_bf16(onesel, bt[1], sg, 0, 0, 0);
+        sg = __builtin_amdgcn_mfma_f32_16x16x32_bf16(onesel, bt[0], sg, 0, 0, 0);
       }
     };
 
     Front fr[2];
     bf16x8 gsf[2][kWT], actf[2][kWT];
     f32x16 gx[2] = {zero16(), zero16()};
-    f32x16 sg = zero16();
-    // block 0's front, not overlapped (the tile's first products)
+    f32x4 sg = {0.f, 0.f, 0.f, 0.f};
+    bf16x8 bt[kWT];
+    // fill: block 0's front, the next tile's staging pieces beside it (their issue cost hides
+    // behind the MFMAs; the raw region is free: this tile is converted)
     front_gd(0, fr[0]);
     {
-      FrontOps o[2];
-      front_load(0, 0, o[0]);
+      const Stage st = stage_of(tn);
 #pragma unroll
       for (int k = 0; k < 6; ++k) {
-        if (k + 1 < 6) front_load(0, k + 1, o[(k + 1) & 1]);
-        front_mfma(0, k, fr[0], o[k & 1]);
+        FrontOps o;
+        front_load(0, k, o);
+        stage_piece(tn, st, 2 * k);
+        stage_piece(tn, st, 2 * k + 1);
+        if (k == 5 && kPieces > 12) stage_piece(tn, st, 12);
+        front_mfma(0, k, fr[0], o);
+        WSCHED_FENCE();
       }
     }
-    WSCHED_FENCE();
+    WSTAMP(1);
+    // period jb, six steps; step k: the LDS operands of the step, block jb's epilogue step k, then
+    // the products: block jb+1's front k-step k, block jb-1's g_x half step k (k < 4), and the
+    // g_P / g_W pieces: block jb-1's k-step 1 (k < 3: its split fragments live until epilogue
+    // step 5 rewrites them) and block jb's k-step 0 (k >= 3: written by epilogue step 2)
 #pragma unroll
     for (int jb = 0; jb < NB; ++jb) {
       const bool nxt = jb + 1 < NB, prv = jb >= 1;
       Front& cur = fr[jb & 1];
       Front& fn = fr[(jb + 1) & 1];
       if (nxt) front_gd(jb + 1, fn);
-      // region A(jb): 6 steps. MFMA work: block jb+1's front steps 0..5; block jb-1's g_x in
-      // four half steps (s, half) = steps 0..3
-      FrontOps o[2];
-      GxOps xo[2];
-      bf16x8 bt[kWT];
-      if (nxt) front_load(jb + 1, 0, o[0]);
-      if (prv) gx_load(jb - 1, 0, 0, xo[0]);
-      WSCHED_FENCE();
 #pragma unroll
       for (int k = 0; k < 6; ++k) {
-        if (nxt) {
-          if (k + 1 < 6) front_load(jb + 1, k + 1, o[(k + 1) & 1]);
-          front_mfma(jb + 1, k, fn, o[k & 1]);
-        }
+        FrontOps o;
+        GxOps xo;
+        WOps wo;
+        if (nxt) front_load(jb + 1, k, o);
+        if (prv && k < 4) gx_load(jb - 1, k >> 1, k & 1, xo);
+        if (prv && k < 3) w_load(1, k, wo);
+        if (k >= 3) w_load(0, k - 3, wo);
+        epi_step(jb, k, cur, gsf, actf);
+        if (nxt) front_mfma(jb + 1, k, fn, o);
         if (prv && k < 4) {
-          if (k + 1 < 4) gx_load(jb - 1, (k + 1) >> 1, (k + 1) & 1, xo[(k + 1) & 1]);
           if ((k & 1) == 0) {
 #pragma unroll
-            for (int t = 0; t < kWT; ++t) bt[t] = xo[k & 1].bt[t];
+            for (int t = 0; t < kWT; ++t) bt[t] = xo.bt[t];
           }
-          gx_mfma(k & 1, xo[k & 1], bt, gx, sg);
+          gx_mfma(k & 1, xo, bt, gx, sg);
         }
-        epi_step(jb, k, cur, gsf, actf);
+        if (prv && k < 3) w_mfma(jb - 1, 1, k, wo, gsf, actf);
+        if (k >= 3) w_mfma(jb, 0, k - 3, wo, gsf, actf);
         WSCHED_FENCE();
       }
-      // region B(jb): g_P / g_W
-      {
-        GpwOps go[2];
-        gpw_load(0, go[0]);
-        gpw_load(1, go[1]);
-        gpw_mfma(jb, 0, go[0], gsf, actf);
-        WSCHED_FENCE();
-        gpw_mfma(jb, 1, go[1], gsf, actf);
-        WSCHED_FENCE();
-      }
+      WSTAMP(2 + jb);
     }
-    // the last block's g_x products
-    {
-      GxOps xo[2];
-      bf16x8 bt[kWT];
-      gx_load(NB - 1, 0, 0, xo[0]);
+    // drain: the last block's g_x products and its g_P / g_W k-step 1
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (k + 1 < 4) gx_load(NB - 1, (k + 1) >> 1, (k + 1) & 1, xo[(k + 1) & 1]);
-        if ((k & 1) == 0) {
+    for (int k = 0; k < 4; ++k) {
+      GxOps xo;
+      WOps wo;
+      gx_load(NB - 1, k >> 1, k & 1, xo);
+      if (k < 3) w_load(1, k, wo);
+      if ((k & 1) == 0) {
 #pragma unroll
-          for (int t = 0; t < kWT; ++t) bt[t] = xo[k & 1].bt[t];
-        }
-        gx_mfma(k & 1, xo[k & 1], bt, gx, sg);
+        for (int t = 0; t < kWT; ++t) bt[t] = xo.bt[t];
       }
+      gx_mfma(k & 1, xo, bt, gx, sg);
+      if (k < 3) w_mfma(NB - 1, 1, k, wo, gsf, actf);
+      WSCHED_FENCE();
     }
     WSCHED_FENCE();
+    WSTAMP(8);
     // the partial (rows: physical channel columns 32 ct + acc_row, cols: pixel j) and sum_p g_s
     // into this wave's region (the g_s image's bytes; the wave's own LDS operations run in order)
     asm volatile("" ::: "memory");
@@ -584,7 +620,11 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
     for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
       for (int r = 0; r < 16; ++r) lds_st(a_part + (32 * ct + row_of(r)) * 128, gx[ct][r]);
-    if (h == 0) lds_st(TWw + 64 * 128 + 4 * j, sg[0]);
+    if (lane < 16) {  // sum_p g_s of pixels j and j + 16 (rows 0, 1 of the 16x16 product)
+      lds_st(TWw + 64 * 128 + 4 * j, sg[0]);
+      lds_st(TWw + 64 * 128 + 4 * (j + 16), sg[1]);
+    }
+    WSTAMP(9);
   };
 
   // ---- g_x epilogue of a tile: wave w adds the four partials of its rows (physical columns
@@ -633,23 +673,40 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
   __syncthreads();
   if (iters > 0) convert(tile_of(0));
   lds_barrier();
+  WSTAMP(14);
   // (no branches in the loop body: past the last tile, the staging loads land zeros)
   for (int i = 0; i < iters; ++i) {
     const int t = tile_of(i);
-    stage_dma(tile_of(i + 1));  // the raw region is free: tile i is converted
-    compute_tile();
+    WSTAMP(0);
+#ifndef WAVE_ABL_NOCOMPUTE  // (WAVE_ABL_*: timing ablations of development builds; wrong results)
+    compute_tile(tile_of(i + 1));  // (+ the staging DMA of tile i + 1)
+#else
+    stage_dma(tile_of(i + 1));
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile i + 1 has landed
     lds_barrier();  // every partial of tile i and every raw piece of tile i + 1 written; images read
+    WSTAMP(10);
+#ifndef WAVE_ABL_NOREDCONV
     reduce_store(t);
+    WSTAMP(11);
     convert(tile_of(i + 1));
+    WSTAMP(12);
+#else
+    (void)t;
+#endif
     lds_barrier();  // images(i+1) written; every partial read
+    WSTAMP(13);
   }
 
   // ---- slab: this workgroup's g_P (x -2: the x image holds +x), g_W, sum_n g_s; the reduce
-  // kernel's layout [Ps * 64 | 32 * Ps | Ps], Ps = Pi ---------------------------------------------
+  // kernel's layout with g_P transposed [64 * Ps | 32 * Ps | Ps], Ps = Pi (every store: 32
+  // consecutive prototypes per half-wave) ---------------------------------------------------------
   const int Ps = Pi;
   const int E = Ps * kC + 32 * Ps + Ps;
   float* my_slab = slab + static_cast<size_t>(blockIdx.x) * E;
+#ifdef WAVE_ABL_NOSLAB
+  if (npix != -7) return;
+#endif
 #pragma unroll
   for (int jb = 0; jb < NB; ++jb) {
     if (32 * (NB * wave + jb) >= Ps) continue;  // blocks past the last prototype
@@ -658,13 +715,22 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
     for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        my_slab[static_cast<size_t>(p) * kC + chan_col(32 * ct + acc_row(r, h))] = -2.f * gp[jb][ct][r];
+        my_slab[static_cast<size_t>(chan_col(32 * ct + acc_row(r, h))) * Ps + p] = -2.f * gp[jb][ct][r];
 #pragma unroll
     for (int r = 0; r < 16; ++r) my_slab[static_cast<size_t>(Ps) * kC + acc_row(r, h) * Ps + p] = gw[jb][r];
     float s = gsum[jb];
     s += __shfl_xor(s, 32);
     if (h == 0) my_slab[static_cast<size_t>(Ps) * kC + 32 * Ps + p] = s;
   }
+#ifdef WAVE_STAMP
+  WSTAMP(15);
+  if (lane < 16) {
+    unsigned long long v = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v = lane == k ? st_acc[k] : v;
+    g_wave_stamp[(blockIdx.x * kWW + wave) * 16 + lane] = v;
+  }
+#endif
 }
 
 template <typename TX, int ACT, int GD, bool XSIG, int NB>
@@ -747,3 +813,9 @@ int launch_bwd_wave_bf16(const Geometry& g, bool x_bf16, const void* x, const vo
 }
 
 }  // namespace protoseg
+
+#ifdef WAVE_STAMP
+extern "C" int protoseg_dev_wave_stamps(unsigned long long* host, int n) {
+  return static_cast<int>(hipMemcpyFromSymbol(host, HIP_SYMBOL(protoseg::g_wave_stamp), sizeof(unsigned long long) * n));
+}
+#endif

@@ -84,7 +84,7 @@ int launch_bwd_onepass_bf16(const Geometry& g, bool x_bf16, const void* x, const
 // Wave-owned backward (l2_bwd_wave.hip): bf16x3, P <= 384 per launch, 4 waves (one per SIMD)
 // each owning a quarter of the prototypes for every product; reads the standard bf16 operand
 // image block (launch_prep_bf16, bf16_image_bytes(P)); g_x (+= when accumulate) and a g_P / g_W
-// slab per workgroup in the reduce kernel's layout (launch_bwd_reduce_bf16_chunks).
+// slab per workgroup in the reduce kernel's layout with g_P transposed (gp_t = 1).
 int bf16_wave_nb(int P);
 bool bf16_bwd_wave_fits(const Geometry& g, int terms);
 int bf16_bwd_wave_grid(const Geometry& g);
@@ -96,10 +96,10 @@ int launch_bwd_wave_bf16(const Geometry& g, bool x_bf16, const void* x, const vo
 int launch_bwd_reduce_bf16(const Geometry& g, const float* ws, int slabs, const float* protos, int act_kind,
                            float* g_protos, float* g_w, hipStream_t stream);
 // nchunk chunks of `per` prototypes (g.P in all, g_w columns at stride g.ldw); chunk c's slabs
-// at ws + c * chunk_elems.
+// at ws + c * chunk_elems. gp_t: the slabs hold g_P transposed ([c][Pp], the wave kernel's).
 int launch_bwd_reduce_bf16_chunks(const Geometry& g, int per, int nchunk, const float* ws, int slabs,
                                   size_t chunk_elems, const float* protos, int act_kind, float* g_protos, float* g_w,
-                                  hipStream_t stream);
+                                  hipStream_t stream, int gp_t = 0);
 int launch_bwd_pw_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const float* protos, const void* img,
                        float eps, int act_kind, const float* g_logits, const float* g_dist, float* g_protos,
                        float* g_w, float* ws, hipStream_t stream);

@@ -630,7 +630,9 @@ BwdKernel bwd_kernel(int P) {
   if (e && !strcmp(e, "wave")) return BwdKernel::kWave;
   if (e && !strcmp(e, "onepass")) return BwdKernel::kOnepass;
   if (e && !strcmp(e, "fused")) return BwdKernel::kFused;
-  return P > 192 ? BwdKernel::kOnepass : BwdKernel::kFused;
+  // P > 192: the wave-owned kernel (one pass over X for up to 384 prototypes per chunk, the
+  // forward's operand images); the fused kernel below (its 192-prototype LDS images)
+  return P > 192 ? BwdKernel::kWave : BwdKernel::kFused;
 }
 bool use_onepass(int P) { return bwd_kernel(P) == BwdKernel::kOnepass; }
 
@@ -996,7 +998,7 @@ int l2_bwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const fl
           return st;
       }
       return launch_bwd_reduce_bf16_chunks(geo, per, nchunk, ws, grid, chunk_elems, protos, act_kind, g_protos,
-                                           g_logits ? g_w : nullptr, s);
+                                           g_logits ? g_w : nullptr, s, 1);
     }
   }
   // Training backward at bf16x3: ONE pass over X for up to 384 prototypes (19 prototypes/class;

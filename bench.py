@@ -209,7 +209,7 @@ class LayerStep:
 
     @property
     def fused(self):
-        """bf16x3 at C = 64: the training backward is one kernel (l2_bwd_onepass.hip for P > 192,
+        """bf16x3 at C = 64: the training backward is one kernel (l2_bwd_wave.hip for P > 192,
         up to 384 prototypes per launch; l2_bwd_fused.hip at P <= 192); other precisions run
         the two-kernel backward."""
         return self.prec == _lib.PRECISIONS["bf16x3"] and self.C == 64

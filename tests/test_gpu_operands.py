@@ -1,6 +1,7 @@
 """One operand prep per training step (protoseg_l2_fwd_ex / protoseg_l2_bwd_ex / _kld_ex): the
-forward's prep launch also writes the training backward's operand images (the one-pass block for
-P in (192, 384], the fused kernel's images for P <= 192) into a caller buffer, and the backward
+forward's prep launch also writes the training backward's operand images (the standard image
+block the wave-owned and fused kernels read; the one-pass block under PROTOSEG_BWD=onepass) into a
+caller buffer, and the backward
 reads them instead of preparing its own. Same prep arithmetic, so every output is bit-identical
 to the plain calls; the autograd path (prototype_layer) passes the buffer through ctx."""
 import pytest
@@ -26,11 +27,11 @@ def _inputs(device, B, h, w, P, K, seed):
 
 
 @pytest.mark.parametrize("P,K,bwd,kind", [
-    (361, 19, None, "onepass"),      # the metric's 19 prototypes/class
-    (190, 19, None, "fused"),        # 10 prototypes/class
+    (361, 19, None, "fused"),        # the metric's 19 prototypes/class: the wave-owned backward
+    (190, 19, None, "fused"),        # 10 prototypes/class                 reads the standard block
     (96, 32, None, "fused"),
     (190, 19, "onepass", "onepass"),  # PROTOSEG_BWD override: the one-pass block at Pp 256
-    (361, 19, "wave", "fused"),      # the wave-owned backward reads the standard image block
+    (361, 19, "onepass", "onepass"),
     (190, 19, "wave", "fused"),
     (570, 19, None, "none"),         # two prototype chunks: no operands, plain calls
 ])

@@ -157,6 +157,25 @@ def main():
     for k, evs in times.items():
         ms = sorted(a.elapsed_time(b) for a, b in evs)
         print(f"{k:14s} median {ms[len(ms) // 2] * 1e3:8.1f} us  min {ms[0] * 1e3:8.1f} us")
+    # diagnostic builds (WAVE_STAMP): the last launch's per-phase s_memtime cycles, mean over waves
+    for k, lib in libs.items():
+        fn = getattr(lib, "protoseg_dev_wave_stamps", None)
+        if fn is None:
+            continue
+        buf = (ctypes.c_ulonglong * (1024 * 16))()
+        fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]
+        call(lib, k)
+        torch.cuda.synchronize()
+        assert fn(ctypes.addressof(buf), 1024 * 16) == 0
+        rows = [list(buf[i * 16:(i + 1) * 16]) for i in range(1024)]
+        rows = [r for r in rows if r[15] != 0]
+        names = ["dma", "front0", "A0", "A1", "A2", "B0", "B1", "B2", "gxlast", "part", "wait+bar", "reduce",
+                 "convert", "bar2", "prologue", "slab"]
+        tot = sum(sum(r) for r in rows) / len(rows)
+        print(f"{k}: stamps over {len(rows)} waves, total {tot:.0f} cyc/wave")
+        for i, n in enumerate(names):
+            v = sum(r[i] for r in rows) / len(rows)
+            print(f"   {n:9s} {v:9.0f} cyc  {100 * v / tot:5.1f}%")
 
 
 if __name__ == "__main__":
