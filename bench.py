@@ -936,7 +936,12 @@ def time_train_step(args, device, rank, world, accumulations=1, warm_accumulatio
             "ms_per_micro_step": round(elapsed / micro * 1e3, 2),
             "ms_per_optimizer_step": round(elapsed / accumulations * 1e3, 2),
             "micro_steps_timed": micro, "grad_exchange_mb": round(grad_mb, 1),
-            "buckets": len(step.buckets.buckets), "backbone_dtype": "f32"}
+            "buckets": len(step.buckets.buckets), "backbone_dtype": "f32",
+            "dominated_by": "the DeepLabV2-ResNet101 backbone (PyTorch-ROCm / MIOpen convolutions, outside this "
+                            "framework's scope), not the prototype layer: at 513x513 MIOpen picks GemmFwdRest / "
+                            "GemmBwdRest / GemmWrwUniversal solvers that ask for more workspace than it grants and "
+                            "fall back, so this line measures the backbone; the layer's own cost is the headline "
+                            "metric and the kld_step line"}
 
 
 def main():
