@@ -949,15 +949,17 @@ __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __
   if (g_protos) g_protos += static_cast<size_t>(p0) * kC;
   if (g_w) g_w += p0;
   P = P - p0 < per ? P - p0 : per;
+  // slab layout: [R][64] g_P | [KR][R] g_W | [R] sum_n g_s with R = Pp rows and KR = 32 class
+  // rows; gp_t (the wave kernel's): exact rows R = P, KR = K, and g_P transposed ([64][R])
   const int Pp = (P + 31) & ~31;
-  const int E = Pp * kC + 32 * Pp + Pp;
+  const int R = gp_t ? P : Pp, KR = gp_t ? K : 32;
+  const int E = R * kC + KR * R + R;
   const int e = blockIdx.x * 64 + (threadIdx.x & 63);
   const int grp = threadIdx.x >> 6;
-  const bool active = e < Pp * kC + 32 * Pp;
-  const bool is_gp = e < Pp * kC;
-  // gp_t: the slab's g_P block is [c][Pp] (element c * Pp + p), else [Pp][c]
-  const int p_of_e = is_gp ? (gp_t ? e % Pp : e / kC) : 0;
-  const int gs_e = Pp * kC + 32 * Pp + p_of_e;
+  const bool active = e < R * kC + KR * R;
+  const bool is_gp = e < R * kC;
+  const int p_of_e = is_gp ? (gp_t ? e % R : e / kC) : 0;
+  const int gs_e = R * kC + KR * R + p_of_e;
   float s = 0.f, gs = 0.f;
   if (active) {
     // this group's slabs grp, grp + 4, ... added in order, kReduceBatch loads in flight per step;
@@ -987,14 +989,14 @@ __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __
   const int l = threadIdx.x;
   const float tot = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
   if (is_gp) {
-    const int c = gp_t ? e / Pp : e - p_of_e * kC;
+    const int c = gp_t ? e / R : e - p_of_e * kC;
     if (p_of_e < P && g_protos) {
       const float gst = ((gpart[0][l] + gpart[1][l]) + gpart[2][l]) + gpart[3][l];
       g_protos[static_cast<size_t>(p_of_e) * kC + c] = tot + gst * (2.f * protos[static_cast<size_t>(p_of_e) * kC + c]);
     }
   } else {
-    const int e2 = e - Pp * kC;
-    const int k = e2 / Pp, pp = e2 - k * Pp;
+    const int e2 = e - R * kC;
+    const int k = e2 / R, pp = e2 - k * R;
     if (g_w && k < K && pp < P) g_w[static_cast<size_t>(k) * ldw + pp] = tot * w_unit;  // act = act_unit * act_base
   }
 }
@@ -1195,7 +1197,7 @@ int launch_bwd_reduce_bf16_chunks(const Geometry& g, int per, int nchunk, const 
                                   size_t chunk_elems, const float* protos, int act_kind, float* g_protos, float* g_w,
                                   hipStream_t stream, int gp_t) {
   const int Pp = static_cast<int>(ceil_div(per, 32) * 32);
-  const int elems = Pp * kC + 32 * Pp;
+  const int elems = gp_t ? per * (kC + g.K) : Pp * kC + 32 * Pp;
   hipLaunchKernelGGL(l2_bwd_reduce_bf16_kernel, dim3(static_cast<unsigned>(ceil_div(elems, 64)), nchunk), dim3(256),
                      0, stream, ws, slabs, g.P, per, g.K, g.ldw, protos, act_unit(act_kind), g_protos, g_w,
                      chunk_elems, gp_t);

@@ -702,29 +702,31 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
     WSTAMP(13);
   }
 
-  // ---- slab: this workgroup's g_P (x -2: the x image holds +x), g_W, sum_n g_s; the reduce
-  // kernel's layout with g_P transposed [64 * Ps | 32 * Ps | Ps], Ps = Pi (every store: 32
-  // consecutive prototypes per half-wave) ---------------------------------------------------------
-  const int Ps = Pi;
-  const int E = Ps * kC + 32 * Ps + Ps;
+  // ---- slab: this workgroup's g_P (x -2: the x image holds +x), g_W, sum_n g_s in the reduce
+  // kernel's exact layout (gp_t): [64][P] g_P^T | [K][P] g_W | [P] (every store: 32 consecutive
+  // prototypes per half-wave; rows past P and classes past K are not written)
+  const int E = P * kC + K * P + P;
   float* my_slab = slab + static_cast<size_t>(blockIdx.x) * E;
 #ifdef WAVE_ABL_NOSLAB
   if (npix != -7) return;
 #endif
 #pragma unroll
   for (int jb = 0; jb < NB; ++jb) {
-    if (32 * (NB * wave + jb) >= Ps) continue;  // blocks past the last prototype
+    if (32 * (NB * wave + jb) >= P) continue;  // blocks past the last prototype
     const int p = 32 * (NB * wave + jb) + j;
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        my_slab[static_cast<size_t>(chan_col(32 * ct + acc_row(r, h))) * Ps + p] = -2.f * gp[jb][ct][r];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) my_slab[static_cast<size_t>(Ps) * kC + acc_row(r, h) * Ps + p] = gw[jb][r];
     float s = gsum[jb];
     s += __shfl_xor(s, 32);
-    if (h == 0) my_slab[static_cast<size_t>(Ps) * kC + 32 * Ps + p] = s;
+    if (p < P) {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          my_slab[static_cast<size_t>(chan_col(32 * ct + acc_row(r, h))) * P + p] = -2.f * gp[jb][ct][r];
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (acc_row(r, h) < K) my_slab[static_cast<size_t>(P) * kC + acc_row(r, h) * P + p] = gw[jb][r];
+      if (h == 0) my_slab[static_cast<size_t>(P) * kC + K * P + p] = s;
+    }
   }
 #ifdef WAVE_STAMP
   WSTAMP(15);
@@ -772,8 +774,8 @@ int bf16_bwd_wave_grid(const Geometry& g) {
 }
 
 size_t bf16_bwd_wave_slab_elems(const Geometry& g) {
-  const size_t Ps = static_cast<size_t>(ceil_div(g.P, 32) * 32);
-  return static_cast<size_t>(bf16_bwd_wave_grid(g)) * (Ps * kC + 32 * Ps + Ps);
+  const size_t P = static_cast<size_t>(g.P);
+  return static_cast<size_t>(bf16_bwd_wave_grid(g)) * (P * kC + static_cast<size_t>(g.K) * P + P);
 }
 
 int launch_bwd_wave_bf16(const Geometry& g, bool x_bf16, const void* x, const void* img, float eps, int act_kind,
