@@ -55,6 +55,10 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
+// g_x partial rows: pixel n, 64 physical columns + sum_p g_s at column 64, padded to 68 floats
+// (16-B row accesses of 16 consecutive pixels land on distinct banks).
+constexpr int kPartRow = 68 * 4;
+
 // LDS regions (bytes).
 struct WaveLds {
   int pimg, xa, ga, raw, raw_gl, raw_cls, x2u, ro, cl, tw, tw_bytes, total;
@@ -72,9 +76,9 @@ __host__ __device__ constexpr WaveLds wave_lds(int NB) {
   o.ro = o.x2u + 4 * 32 * 4;           // [32] u32: g_dist byte offset per pixel (GD)
   o.cl = o.ro + 32 * 4;                // [32] int: the pixel's KLD class (GD = 2)
   // per wave: its g_s image for two blocks [T][2][32 p][32 n] bf16 (64-B rows, 8-B slots
-  // swizzled), then, in the same bytes, its g_x partial [64 physical columns][32 n] f32 + sum_p g_s
+  // swizzled), then, in the same bytes, its g_x partial [32 n][64 physical columns | sum_p g_s]
   o.tw = o.cl + 32 * 4;
-  o.tw_bytes = 64 * 32 * 4 + 32 * 4;  // >= kWT * 2 * 32 * 64 = 8192
+  o.tw_bytes = 32 * kPartRow;         // >= kWT * 2 * 32 * 64 = 8192
   o.total = o.tw + kWW * o.tw_bytes;
   return o;
 }
@@ -616,17 +620,20 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
     }
     WSCHED_FENCE();
     WSTAMP(8);
-    // the partial (rows: physical channel columns 32 ct + acc_row, cols: pixel j) and sum_p g_s
-    // into this wave's region (the g_s image's bytes; the wave's own LDS operations run in order)
+    // the partial (row: pixel j, columns: physical channel columns 32 ct + acc_row, 4 consecutive
+    // per 16-B store) and sum_p g_s (column 64) into this wave's region (the g_s image's bytes;
+    // the wave's own LDS operations run in order)
     asm volatile("" ::: "memory");
-    const unsigned a_part = TWw + (4 * h) * 128 + 4 * j;
+    const unsigned a_part = TWw + j * kPartRow + 16 * h;
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) lds_st(a_part + (32 * ct + row_of(r)) * 128, gx[ct][r]);
+      for (int g4 = 0; g4 < 4; ++g4)
+        *reinterpret_cast<__attribute__((address_space(3))) f32x4*>(static_cast<uintptr_t>(a_part + (32 * ct + 8 * g4) * 4)) =
+            f32x4{gx[ct][4 * g4], gx[ct][4 * g4 + 1], gx[ct][4 * g4 + 2], gx[ct][4 * g4 + 3]};
     if (lane < 16) {  // sum_p g_s of pixels j and j + 16 (rows 0, 1 of the 16x16 product)
-      lds_st(TWw + 64 * 128 + 4 * j, sg[0]);
-      lds_st(TWw + 64 * 128 + 4 * (j + 16), sg[1]);
+      lds_st(TWw + j * kPartRow + 64 * 4, sg[0]);
+      lds_st(TWw + (j + 16) * kPartRow + 64 * 4, sg[1]);
     }
     WSTAMP(9);
   };
@@ -642,21 +649,27 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
            static_cast<unsigned>(chan_of(wave, h, 0) * HW) * sz;
   };
   auto reduce_store = [&](int t) __attribute__((always_inline)) {
-    const unsigned pb = S0 + L.tw + 4 * j;
+    const unsigned pb = S0 + L.tw + j * kPartRow;
     constexpr int ps = L.tw_bytes;  // bytes between the waves' regions
-    const float sgt = ((lds_ld(pb + 64 * 128) + lds_ld(pb + ps + 64 * 128)) + lds_ld(pb + 2 * ps + 64 * 128)) +
-                      lds_ld(pb + 3 * ps + 64 * 128);
+    const float sgt = ((lds_ld(pb + 256) + lds_ld(pb + ps + 256)) + lds_ld(pb + 2 * ps + 256)) + lds_ld(pb + 3 * ps + 256);
     const unsigned vo = pix_off(t);
-    float old[8];
+    float old[8] = {};
+    if (accumulate) {  // (wave-uniform: a single-chunk call issues no loads and waits on none)
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
-      old[e] = BufIO<TX>::load(rgx, accumulate ? vo : kOOB, static_cast<unsigned>(chan_of(0, 0, e)) * chs);
+      for (int e = 0; e < 8; ++e) old[e] = BufIO<TX>::load(rgx, vo, static_cast<unsigned>(chan_of(0, 0, e)) * chs);
+    }
     const u32x4 xh = __builtin_bit_cast(u32x4, lds_frag(a_xrow)), xl = __builtin_bit_cast(u32x4, lds_frag(a_xrow + 32 * 128));
-    const unsigned pr = pb + (16 * wave + 8 * h) * 128;
+    // the 8 physical columns 16 w + 8 h .. + 7 of each wave's partial: two 16-B reads each
+    const unsigned pr = pb + (16 * wave + 8 * h) * 4;
+    typedef __attribute__((address_space(3))) f32x4 lds_f32x4;
+    f32x4 pq[kWW][2];
+#pragma unroll
+    for (int q = 0; q < kWW; ++q)
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) pq[q][hf] = *reinterpret_cast<const lds_f32x4*>(static_cast<uintptr_t>(pr + q * ps + 16 * hf));
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float tot = ((lds_ld(pr + e * 128) + lds_ld(pr + ps + e * 128)) + lds_ld(pr + 2 * ps + e * 128)) +
-                        lds_ld(pr + 3 * ps + e * 128);
+      const float tot = ((pq[0][e >> 2][e & 3] + pq[1][e >> 2][e & 3]) + pq[2][e >> 2][e & 3]) + pq[3][e >> 2][e & 3];
       const unsigned sh = (e & 1) ? 0u : 16u;
       const float xv = __uint_as_float((xh[e >> 1] << sh) & 0xFFFF0000u) + __uint_as_float((xl[e >> 1] << sh) & 0xFFFF0000u);
       float v;
