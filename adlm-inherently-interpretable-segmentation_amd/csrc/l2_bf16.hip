@@ -394,14 +394,24 @@ __global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
       for (int r = 0; r < 16; ++r) {
         const float d = relu_f(acc[r]);  // F.relu (model.py:219)
         const unsigned row_ok = (kFull || row_of(r) < prem) ? 0u : kOOB;
+#ifndef FWD_ABL_NODIST  // (FWD_ABL_*: timing ablations of development builds; wrong results)
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(d), rd, dbase | row_ok,
                                               static_cast<unsigned>((pt * 32 + row_of(r)) * HW * 4), FWD_DIST_CPOL);
+#endif
+#ifndef FWD_ABL_NOACT
         const float a = act_base<ACT>(d, eps);  // act_unit lives in the W image
+#else
+        const float a = d;
+#endif
         if constexpr (ACTS)
           BufIO<float>::store(ra, a * act_unit(ACT), abase | row_ok, static_cast<unsigned>((pt * 32 + row_of(r)) * 4));
         acc[r] = a;
       }
+#ifdef FWD_ABL_NOLOGITS
+      if constexpr (false) {
+#else
       if constexpr (LOGITS) {
+#endif
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           bf16x8 ab[T];

@@ -31,6 +31,9 @@
 #include "l2_launch.h"
 #include "protoseg_host.h"
 
+// (defined below, after the kernel families' launch helpers)
+bool use_wide(int C, int K, int P);
+
 namespace protoseg {
 
 namespace {
@@ -470,8 +473,10 @@ int validate(const void* x, int x_dtype, int B, int C, int H, int W, const float
   if (!x || !protos) return fail(PROTOSEG_ERR_INVALID, "x and protos must be non-null");
   if (B <= 0 || H <= 0 || W <= 0 || P <= 0 || K < 0)
     return fail(PROTOSEG_ERR_INVALID, "bad shape B=%d H=%d W=%d P=%d K=%d", B, H, W, P, K);
-  if (x_dtype != PROTOSEG_F32 && x_dtype != PROTOSEG_BF16)
-    return fail(PROTOSEG_ERR_UNSUPPORTED, "x_dtype %d (f32 or bf16 only)", x_dtype);
+  if (x_dtype != PROTOSEG_F32 && x_dtype != PROTOSEG_BF16 && x_dtype != PROTOSEG_F16)
+    return fail(PROTOSEG_ERR_UNSUPPORTED, "x_dtype %d (f32, bf16 or f16 only)", x_dtype);
+  if (x_dtype == PROTOSEG_F16 && C > 0 && P > 0 && K >= 0 && !use_wide(C, K, P))
+    return fail(PROTOSEG_ERR_UNSUPPORTED, "x_dtype f16: the wide family only (protoseg_l2_x_dtype_supported)");
   if (act_kind != PROTOSEG_ACT_LOG && act_kind != PROTOSEG_ACT_LINEAR)
     return fail(PROTOSEG_ERR_UNSUPPORTED, "act_kind %d", act_kind);
   if (precision < PROTOSEG_PREC_BF16X3 || precision > PROTOSEG_PREC_F32)
@@ -725,6 +730,12 @@ extern "C" size_t protoseg_l2_train_operands_bytes(int C, int P, int K, int prec
   return train_operands_bytes(C, P, K, train_operands_kind(C, P, K, precision));
 }
 
+extern "C" int protoseg_l2_x_dtype_supported(int C, int P, int K, int x_dtype) {
+  if (!protoseg_l2_supported(C, P, K)) return 0;
+  if (x_dtype == PROTOSEG_F32 || x_dtype == PROTOSEG_BF16) return 1;
+  return x_dtype == PROTOSEG_F16 && use_wide(C, K, P) ? 1 : 0;
+}
+
 extern "C" int protoseg_l2_supported(int C, int P, int K) {
   if (C <= 0 || P <= 0 || K < 0) return 0;
   if (!use_wide(C, K, P)) return 1;  // beyond one launch's LDS: prototype chunks
@@ -790,7 +801,7 @@ int l2_fwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const fl
     if (!wide_family_fits(geo)) return fail(PROTOSEG_ERR_UNSUPPORTED, "B*H*W*max(P, C) >= 2^31 elements");
     void* scratch = nullptr;
     if (int st = stream_block(wide_fwd_scratch_bytes(geo, !dist_out && logits_out), s, 2, &scratch)) return st;
-    return launch_fwd_wide(geo, x_dtype == PROTOSEG_BF16, x, protos, w_last, eps, act_kind, dist_out, act_out,
+    return launch_fwd_wide(geo, x_dtype, x, protos, w_last, eps, act_kind, dist_out, act_out,
                            logits_out, scratch, s);
   }
   const int terms = terms_of(precision);
@@ -967,7 +978,7 @@ int l2_bwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const fl
     if (xsig) return fail(PROTOSEG_ERR_UNSUPPORTED, "PROTOSEG_X_SIGMOID: C = 64, K <= 32 only");
     if (cgd.val) return fail(PROTOSEG_ERR_UNSUPPORTED, "compact KLD gradient on the wide family (K > 32 or P > 4096)");
     if (!wide_family_fits(geo)) return fail(PROTOSEG_ERR_UNSUPPORTED, "B*H*W*max(P, C) >= 2^31 elements");
-    return launch_bwd_wide(geo, xb, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_x, g_protos,
+    return launch_bwd_wide(geo, x_dtype, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_x, g_protos,
                            g_logits ? g_w : nullptr, workspace, s);
   }
   // Training backward at bf16x3, wave-owned prototypes (l2_bwd_wave.hip): up to 384 prototypes

@@ -437,13 +437,22 @@ size_t wide_fwd_scratch_bytes(const Geometry& g, bool need_dist) {
 
 size_t wide_bwd_workspace_bytes(const Geometry& g) { return wide_bwd_layout(g).total * sizeof(float); }
 
-int launch_fwd_wide(const Geometry& g, bool x_bf16, const void* x, const float* protos, const float* w_last, float eps,
+namespace {
+// D = distances of x in its stored dtype (F32 | BF16 | F16)
+int distances_of(const Geometry& g, int x_dtype, const void* x, const float* protos, float eps, int act_kind, float* D,
+                 float* act, hipStream_t s) {
+  if (x_dtype == PROTOSEG_BF16) return wide_distances(g, static_cast<const uint16_t*>(x), protos, eps, act_kind, D, act, s);
+  if (x_dtype == PROTOSEG_F16) return wide_distances(g, static_cast<const _Float16*>(x), protos, eps, act_kind, D, act, s);
+  return wide_distances(g, static_cast<const float*>(x), protos, eps, act_kind, D, act, s);
+}
+}  // namespace
+
+int launch_fwd_wide(const Geometry& g, int x_dtype, const void* x, const float* protos, const float* w_last, float eps,
                     int act_kind, float* dist, float* act, float* logits, void* scratch, hipStream_t s) {
   float* sc = static_cast<float*>(scratch);
   float* D = dist ? dist : sc;  // the logits read the distances back
   float* part = sc + (dist ? 0 : ((static_cast<size_t>(g.npix) * g.P + 63) & ~static_cast<size_t>(63)));
-  int st = x_bf16 ? wide_distances(g, static_cast<const uint16_t*>(x), protos, eps, act_kind, D, act, s)
-                  : wide_distances(g, static_cast<const float*>(x), protos, eps, act_kind, D, act, s);
+  int st = distances_of(g, x_dtype, x, protos, eps, act_kind, D, act, s);
   if (st || !logits) return st;
   // logits[b][n][k] = sum_p act(D[b][p][n]) W[k][p]; split over p into slabs [b][S][HW][K] when
   // the images' tiles are too few for the CUs
@@ -464,7 +473,7 @@ int launch_fwd_wide(const Geometry& g, bool x_bf16, const void* x, const float* 
   return check_launch("wide_finish_kernel");
 }
 
-int launch_bwd_wide(const Geometry& g, bool x_bf16, const void* x, const float* protos, const float* w_last, float eps,
+int launch_bwd_wide(const Geometry& g, int x_dtype, const void* x, const float* protos, const float* w_last, float eps,
                     int act_kind, const float* g_logits, const float* g_dist, void* g_x, float* g_protos, float* g_w,
                     void* workspace, hipStream_t s) {
   const WideBwdLayout l = wide_bwd_layout(g);
@@ -473,8 +482,7 @@ int launch_bwd_wide(const Geometry& g, bool x_bf16, const void* x, const float* 
   float* part = ws + l.part;
   const int B = g.npix / g.HW;
   const long long img = static_cast<long long>(g.P) * g.HW;
-  int st = x_bf16 ? wide_distances(g, static_cast<const uint16_t*>(x), protos, eps, act_kind, D, nullptr, s)
-                  : wide_distances(g, static_cast<const float*>(x), protos, eps, act_kind, D, nullptr, s);
+  int st = distances_of(g, x_dtype, x, protos, eps, act_kind, D, nullptr, s);
   if (st) return st;
   {  // G_s[b][p][n] = (sum_k W[k][p] GL[b][n][k]) act'(D) + g_dist, relu mask (K = 0: g_dist alone)
     WideArgs a{};
@@ -492,7 +500,9 @@ int launch_bwd_wide(const Geometry& g, bool x_bf16, const void* x, const float* 
     a.M = g.C, a.N = g.HW, a.Kd = g.P, a.nb = B;
     a.out = g_x, a.om = g.HW, a.on = 1, a.ob = static_cast<long long>(g.C) * g.HW;
     a.xo = x;
-    st = x_bf16 ? gemm<kEpiGx, float, float, -1, -1, uint16_t>(a, B, s) : gemm<kEpiGx, float, float, -1, -1, float>(a, B, s);
+    st = x_dtype == PROTOSEG_BF16  ? gemm<kEpiGx, float, float, -1, -1, uint16_t>(a, B, s)
+         : x_dtype == PROTOSEG_F16 ? gemm<kEpiGx, float, float, -1, -1, _Float16>(a, B, s)
+                                   : gemm<kEpiGx, float, float, -1, -1, float>(a, B, s);
     if (st) return st;
   }
   if (g_protos) {  // g_P[p][c] = -2 sum_{b,n} G_s[b][p][n] x[b][c][n] + 2 p rs[p]
@@ -504,8 +514,9 @@ int launch_bwd_wide(const Geometry& g, bool x_bf16, const void* x, const float* 
     a.B = op(x, g.HW, 1, static_cast<long long>(g.C) * g.HW);         // (c, n) of X[b][c][n]
     a.M = g.P, a.N = g.C, a.Kd = g.HW, a.nb = B, a.bk = 1, a.ksplit = S;
     a.out = part, a.om = g.C, a.on = 1, a.ob = static_cast<long long>(g.P) * g.C;
-    st = x_bf16 ? gemm<kEpiStore, float, uint16_t, -1, -1, float>(a, S, s)
-                : gemm<kEpiStore, float, float, -1, -1, float>(a, S, s);
+    st = x_dtype == PROTOSEG_BF16  ? gemm<kEpiStore, float, uint16_t, -1, -1, float>(a, S, s)
+         : x_dtype == PROTOSEG_F16 ? gemm<kEpiStore, float, _Float16, -1, -1, float>(a, S, s)
+                                   : gemm<kEpiStore, float, float, -1, -1, float>(a, S, s);
     if (st) return st;
     const long long e = static_cast<long long>(g.P) * g.C;
     hipLaunchKernelGGL(wide_finish_kernel, dim3(static_cast<unsigned>(ceil_div(e, 256))), dim3(256), 0, s, part, S, 1,

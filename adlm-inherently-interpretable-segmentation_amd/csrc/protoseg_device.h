@@ -41,6 +41,10 @@ template <> struct XIO<float> {
   static __device__ __forceinline__ float load(const float* p, size_t i) { return p[i]; }
   static __device__ __forceinline__ void store(float* p, size_t i, float v) { p[i] = v; }
 };
+template <> struct XIO<_Float16> {  // IEEE half (PROTOSEG_F16): exact widening, round-to-nearest-even narrowing
+  static __device__ __forceinline__ float load(const _Float16* p, size_t i) { return static_cast<float>(p[i]); }
+  static __device__ __forceinline__ void store(_Float16* p, size_t i, float v) { p[i] = static_cast<_Float16>(v); }
+};
 template <> struct XIO<uint16_t> {
   static __device__ __forceinline__ float load(const uint16_t* p, size_t i) {
     return __uint_as_float(static_cast<uint32_t>(p[i]) << 16);

@@ -23,7 +23,7 @@ LIB_PATH = pathlib.Path(os.environ.get("PROTOSEG_HIP_LIB", CSRC_DIR / "libprotos
 # status codes (enum protoseg_status)
 OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_HIP = 0, 1, 2, 3
 # enum protoseg_dtype
-F32, BF16, I64, I32, U8 = 0, 1, 2, 3, 4
+F32, BF16, I64, I32, U8, F16 = 0, 1, 2, 3, 4, 5
 # enum protoseg_act
 ACT_LOG, ACT_LINEAR, ACT_IDENTITY = 0, 1, 2
 X_SIGMOID = 0x100  # OR-ed into the layer's act_kind: sigmoid of the pre-activation on load
@@ -42,6 +42,7 @@ SIGNATURES = {
     "protoseg_timing_events_n": (_i, [ctypes.c_char_p, _vp, _vp, _i]),
     "protoseg_timing_launches": (_i, []),
     "protoseg_l2_supported": (_i, [_i, _i, _i]),
+    "protoseg_l2_x_dtype_supported": (_i, [_i, _i, _i, _i]),
     "protoseg_adam_step": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _f, _f, _f, _vp]),
     "protoseg_l2_max_protos": (_i, [_i, _i]),
     "protoseg_l2_x_sigmoid_supported": (_i, [_i, _i, _i, _i, _i, _i, _i]),

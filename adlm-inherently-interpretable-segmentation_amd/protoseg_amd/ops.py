@@ -38,11 +38,20 @@ def _x_dtype(x: Tensor) -> int:
         return _lib.F32
     if x.dtype == torch.bfloat16:
         return _lib.BF16
-    raise _lib.ProtosegError(f"feature map dtype {x.dtype} unsupported (float32 or bfloat16)")
+    if x.dtype == torch.float16:
+        return _lib.F16
+    raise _lib.ProtosegError(f"feature map dtype {x.dtype} unsupported (float32, bfloat16 or float16)")
 
 
 def supported(C: int, P: int, K: int) -> bool:
     return bool(_lib.load().protoseg_l2_supported(C, P, K))
+
+
+def x_dtype_supported(C: int, P: int, K: int, dtype: torch.dtype) -> bool:
+    """Whether the kernels read feature maps of `dtype` natively for (C, P, K)
+    (protoseg_l2_x_dtype_supported: fp16 in the wide family); else the layer widens to f32."""
+    code = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16, torch.float16: _lib.F16}.get(dtype)
+    return code is not None and bool(_lib.load().protoseg_l2_x_dtype_supported(C, P, K, code))
 
 
 def x_sigmoid_supported(x: Tensor, P: int, K: int, precision: Optional[str] = None) -> bool:
@@ -333,7 +342,8 @@ def prototype_layer(x: Tensor, prototype_vectors: Tensor, last_layer_weight: Ten
                     x_sigmoid: bool = False) -> Tuple[Tensor, Tensor, Tensor]:
     """Distances, logits and activations of the PPNet prototype layer.
 
-    x: [B, C, H, W] add-on-layer output (float32, bfloat16, or float16 widened to f32); prototype_vectors: [P, C, kh, kw]
+    x: [B, C, H, W] add-on-layer output (float32, bfloat16 or float16: read natively where
+    x_dtype_supported, else widened to f32); prototype_vectors: [P, C, kh, kw]
     or [P, C]; last_layer_weight: [K, P]. Returns (distances [B,P,H',W'], logits [B,H',W',K],
     activations [B*H'*W', P]) with unrequested outputs empty; H' = H - kh + 1, W' = W - kw + 1
     (k x k prototypes run on the unfolded map, C k k deep).
@@ -365,9 +375,11 @@ def prototype_layer(x: Tensor, prototype_vectors: Tensor, last_layer_weight: Ten
         x = torch.nn.functional.unfold(x, (kh, kw)).reshape(B, C * kh * kw, H - kh + 1, W - kw + 1)
     if protos.shape[1] != x.shape[1]:
         raise _lib.ProtosegError(f"prototype depth {protos.shape[1]} != feature channels {x.shape[1]}")
-    if x.dtype == torch.float16:
-        # fp16 feature maps (BASELINE config 5, DenseNet-161 fp16): widened exactly to f32 at the
-        # boundary; the layer computes as for f32 input and autograd narrows g_x back to fp16.
+    if x.dtype == torch.float16 and (x_sigmoid or not x_dtype_supported(x.shape[1], protos.shape[0],
+                                                                         last_layer_weight.shape[0], torch.float16)):
+        # fp16 feature maps (BASELINE config 5, DenseNet-161 fp16) outside the wide family: widened
+        # exactly to f32 at the boundary; autograd narrows g_x back to fp16. The wide family reads
+        # fp16 in its GEMM stages (no widening pass) and writes g_x as fp16.
         x = x.float()
     act_kind = ACT_KINDS[activation]
     if x_sigmoid:

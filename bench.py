@@ -84,7 +84,7 @@ class LayerStep:
         lib = _lib.load()
         self.ws_bytes = lib.protoseg_l2_bwd_workspace_size(B, C, h, w, P, K)
         self.ws = torch.empty(self.ws_bytes, device=device, dtype=torch.uint8)
-        self.xdt = _lib.F32 if x_dtype == torch.float32 else _lib.BF16
+        self.xdt = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16, torch.float16: _lib.F16}[x_dtype]
         self.device = device
         self.prec = _lib.PRECISIONS[precision]
         # The trained parameters (sharing storage with the kernels' buffers; the backward writes
@@ -864,9 +864,10 @@ def time_wide(device, B, C, h, w, P, K, x_dtype, steps=10, warmup=3, label=""):
     return out
 
 
-def time_small_batches(args, device, batches=(2, 4), protos=(361, 190)):
+def time_small_batches(args, device, batches=(2, 4), protos=(361, 190), kld=True):
     """The layer step at the reference's per-GPU micro-batches (gin joint_batch_size = 2;
-    configs[2]: 32 images over 8 GPUs = 4 per GPU), where launch and tail costs dominate."""
+    configs[2]: 32 images over 8 GPUs = 4 per GPU), where launch and tail costs dominate; each
+    with the KLD step (module.py:167-208 runs on every micro-step of configs[2]) beside it."""
     x_dtype = torch.float32 if args.x_dtype == "f32" else torch.bfloat16
     out = {}
     for P in protos:
@@ -874,8 +875,15 @@ def time_small_batches(args, device, batches=(2, 4), protos=(361, 190)):
             s = LayerStep(B, args.channels, args.fmap, args.fmap, P, args.classes, x_dtype, device, SEED,
                           args.precision)
             e, k, a = time_layer(s, args.steps, args.warmup, 1, args.launch == "graph")
-            out[f"B{B}_P{P}"] = {"img_per_s": round(B * args.steps / e, 1), "ms_per_step": round(e / args.steps * 1e3, 4),
-                                 "kernels_ms": {a[n]: round(v * 1e3, 4) for n, v in k.items()}}
+            line = {"img_per_s": round(B * args.steps / e, 1), "ms_per_step": round(e / args.steps * 1e3, 4),
+                    "kernels_ms": {a[n]: round(v * 1e3, 4) for n, v in k.items()}}
+            if kld and not args.no_kld:
+                # the KLD step at the drop-in's own micro-batch (cityscapes_kld_imnet.gin:23 / configs[2])
+                s.setup_kld(SEED)
+                kl = time_kld_step(s, max(5, args.steps // 2), 3)
+                line["kld_step"] = {key: kl[key] for key in ("ms_per_step", "kld_forward_ms", "kld_backward_ms")}
+                line["kld_step"]["ratio_to_plain_step"] = round(kl["ms_per_step"] / line["ms_per_step"], 3)
+            out[f"B{B}_P{P}"] = line
             del s
     return out
 
@@ -1055,10 +1063,10 @@ def main():
     if not args.no_wide and world == 1:
         # configs[4]: DenseNet-161 add-on depth (BASELINE names a 1024-channel map), 30 prototypes
         # per class x 19 classes, 513x513 crops at output stride 32 -> 16x16 maps, fp16 feature maps
-        # (widened exactly to f32 at the boundary); the reference's construct_PPNet default
+        # (read as fp16 by the GEMM stages, g_x written as fp16); the reference's construct_PPNet default
         # (prototype_shape (2000, 512, 1, 1), 200 classes, 224x224 -> 7x7 maps; model.py:394)
-        wide = {"configs4_densenet_c1024_p570": time_wide(device, args.batch, 1024, 16, 16, 570, 19, torch.float32,
-                                                          label="configs[4] DenseNet depth"),
+        wide = {"configs4_densenet_c1024_p570": time_wide(device, args.batch, 1024, 16, 16, 570, 19, torch.float16,
+                                                          label="configs[4] DenseNet depth, fp16 feature maps"),
                 "reference_default_c512_p2000_k200": time_wide(device, args.batch, 512, 7, 7, 2000, 200,
                                                                torch.float32, label="construct_PPNet default")}
     train = None

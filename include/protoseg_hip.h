@@ -42,7 +42,9 @@ enum protoseg_dtype {
   PROTOSEG_BF16 = 1,  /* bfloat16 bits in uint16_t                  */
   PROTOSEG_I64 = 2,   /* int64 labels (reference convert_targets)   */
   PROTOSEG_I32 = 3,
-  PROTOSEG_U8 = 4
+  PROTOSEG_U8 = 4,
+  PROTOSEG_F16 = 5    /* IEEE half in uint16_t: feature maps of the wide family (fp16 add-on
+                         output, BASELINE configs[4]); protoseg_l2_x_dtype_supported says where */
 };
 
 /* model.py:231-237 distance_2_similarity: 'log' -> log((d+1)/(d+eps)); 'linear' -> -d.
@@ -91,7 +93,8 @@ int protoseg_timing_launches(void);
  * branch: permute -> activation -> last_layer -> reshape), i.e. 2 conv2d + 9 elementwise
  * passes + 1 Linear, by one fused kernel.
  *
- *   x       [B, C, H, W]  x_dtype (PROTOSEG_F32 | PROTOSEG_BF16), the add-on-layer output
+ *   x       [B, C, H, W]  x_dtype (PROTOSEG_F32 | PROTOSEG_BF16 | PROTOSEG_F16 where
+ *                         protoseg_l2_x_dtype_supported), the add-on-layer output
  *   protos  [P, C]        f32 (prototype_vectors, 1x1 kernels flattened)
  *   w_last  [K, P]        f32 (last_layer.weight, no bias); may be NULL iff logits_out is NULL
  *   dist_out   [B, P, H, W]   f32 or NULL   distances (model.py:219, NCHW)
@@ -196,6 +199,11 @@ int protoseg_l2_bwd_kld_ex(const void* x, int x_dtype, int B, int C, int H, int 
 
 /* 1 if (C, P, K) is inside the compiled kernel family, else 0. */
 int protoseg_l2_supported(int C, int P, int K);
+
+/* 1 if protoseg_l2_fwd / _bwd read x (and write g_x) in x_dtype natively for (C, P, K), else 0:
+ * F32 and BF16 everywhere protoseg_l2_supported; F16 in the wide family (no widening pass: the
+ * GEMM stages convert on load, g_x is stored as fp16). */
+int protoseg_l2_x_dtype_supported(int C, int P, int K, int x_dtype);
 
 /* Largest P one protoseg_l2_fwd / _bwd call serves at (C, precision): 4096 (prototype chunks
  * inside the call, both families); 0 when C is outside the family or precision is unknown.

@@ -162,8 +162,8 @@ def test_ppnet_default_shape_constructs(device):
 def test_densenet_config_depth_fp16(device):
     """BASELINE configs[4] (DenseNet-161, 30 prototypes/class, fp16): the depth is not stated
     (the add-on maps the 1024-channel features to prototype_shape[1]); at the full 1024 the layer
-    runs on the wide family, fp16 feature maps widened exactly at the boundary and g_x returned
-    in fp16."""
+    runs on the wide family, which reads the fp16 feature maps in its GEMM stages (no widening
+    pass) and writes g_x in fp16."""
     from protoseg_amd import ops
     B, C, h, w, P, K = 2, 1024, 8, 8, 570, 19
     x, protos, w_last, g_logits, _ = _inputs(B, C, h, w, P, K, seed=161)
@@ -182,3 +182,25 @@ def test_densenet_config_depth_fp16(device):
     _close(xd.grad.float(), r_gx, "g_x (fp16)", rel=2e-3)
     _close(pd.grad, r_gp, "g_protos")
     _close(wd.grad, r_gw, "g_w")
+
+
+def test_fp16_native_matches_widened(device):
+    """The wide family's native fp16 read (PROTOSEG_F16) gives the same bits as the f32 path on
+    the exactly widened map: distances, logits, g_protos, g_w, and g_x rounded to fp16 once."""
+    from protoseg_amd import ops
+    B, C, h, w, P, K = 2, 256, 6, 7, 95, 19
+    x, protos, w_last, g_logits, _ = _inputs(B, C, h, w, P, K, seed=5)
+    assert ops.x_dtype_supported(C, P, K, torch.float16)
+    assert not ops.x_dtype_supported(64, 190, 19, torch.float16)  # C = 64 family: widened
+    xh = x.half().to(device)
+    outs = []
+    for xin in (xh, xh.float()):
+        xd = xin.clone().requires_grad_(True)
+        pd = protos.to(device).requires_grad_(True)
+        wd = w_last.to(device).requires_grad_(True)
+        dist, logits, _ = ops.prototype_layer(xd, pd, wd)
+        logits.backward(g_logits.to(device))
+        outs.append((dist.detach(), logits.detach(), xd.grad.half(), pd.grad, wd.grad))
+    torch.cuda.synchronize()
+    for name, a, b in zip(("dist", "logits", "g_x", "g_protos", "g_w"), outs[0], outs[1]):
+        assert torch.equal(a, b), name
