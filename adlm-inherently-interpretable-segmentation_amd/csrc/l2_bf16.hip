@@ -946,13 +946,19 @@ __global__ __launch_bounds__(MAXT) void l2_bwd_pw_bf16_kernel(
 // Slab sum: 64 elements x 4 slab groups per workgroup, groups combined in fixed order; each
 // thread keeps 8 independent loads in flight.
 // blockIdx.y = prototype chunk: its slabs start at y * chunk_elems, its prototypes at y * per.
-__global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __restrict__ slab, int S, int P,
+#ifndef REDUCE_GROUPS
+#define REDUCE_GROUPS 4
+#endif
+// Slab groups per reduce workgroup: group g adds slabs g, g + kRG, ... (kReduceBatch loads in
+// flight per step), then the groups' partials are added in group order.
+constexpr int kRG = REDUCE_GROUPS;
+__global__ __launch_bounds__(64 * kRG) void l2_bwd_reduce_bf16_kernel(const float* __restrict__ slab, int S, int P,
                                                                   int per, int K, int ldw, const float* __restrict__ protos,
                                                                   float w_unit, float* __restrict__ g_protos,
                                                                   float* __restrict__ g_w, size_t chunk_elems,
                                                                   int gp_t) {
-  __shared__ float part[4][64];
-  __shared__ float gpart[4][64];
+  __shared__ float part[kRG][64];
+  __shared__ float gpart[kRG][64];
   const int p0 = static_cast<int>(blockIdx.y) * per;
   slab += blockIdx.y * chunk_elems;
   protos += static_cast<size_t>(p0) * kC;
@@ -975,17 +981,17 @@ __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __
     // this group's slabs grp, grp + 4, ... added in order, kReduceBatch loads in flight per step;
     // the last step's loads are predicated, not issued one round trip at a time
     constexpr int kReduceBatch = 16;
-    for (int si = grp; si < S; si += 4 * kReduceBatch) {
+    for (int si = grp; si < S; si += kRG * kReduceBatch) {
       float v[kReduceBatch], u[kReduceBatch];
 #pragma unroll
       for (int k = 0; k < kReduceBatch; ++k) {
-        const bool ok = si + 4 * k < S;
-        v[k] = ok ? slab[static_cast<size_t>(si + 4 * k) * E + e] : 0.f;
-        u[k] = ok && is_gp ? slab[static_cast<size_t>(si + 4 * k) * E + gs_e] : 0.f;
+        const bool ok = si + kRG * k < S;
+        v[k] = ok ? slab[static_cast<size_t>(si + kRG * k) * E + e] : 0.f;
+        u[k] = ok && is_gp ? slab[static_cast<size_t>(si + kRG * k) * E + gs_e] : 0.f;
       }
 #pragma unroll
       for (int k = 0; k < kReduceBatch; ++k) {
-        if (si + 4 * k < S) {
+        if (si + kRG * k < S) {
           s += v[k];
           gs += u[k];
         }
@@ -997,11 +1003,15 @@ __global__ __launch_bounds__(256) void l2_bwd_reduce_bf16_kernel(const float* __
   __syncthreads();
   if (grp != 0 || !active) return;
   const int l = threadIdx.x;
-  const float tot = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
+  float tot = part[0][l], gst = gpart[0][l];
+#pragma unroll
+  for (int g2 = 1; g2 < kRG; ++g2) {
+    tot += part[g2][l];
+    gst += gpart[g2][l];
+  }
   if (is_gp) {
     const int c = gp_t ? e / R : e - p_of_e * kC;
     if (p_of_e < P && g_protos) {
-      const float gst = ((gpart[0][l] + gpart[1][l]) + gpart[2][l]) + gpart[3][l];
       g_protos[static_cast<size_t>(p_of_e) * kC + c] = tot + gst * (2.f * protos[static_cast<size_t>(p_of_e) * kC + c]);
     }
   } else {
@@ -1208,7 +1218,7 @@ int launch_bwd_reduce_bf16_chunks(const Geometry& g, int per, int nchunk, const 
                                   hipStream_t stream, int gp_t) {
   const int Pp = static_cast<int>(ceil_div(per, 32) * 32);
   const int elems = gp_t ? per * (kC + g.K) : Pp * kC + 32 * Pp;
-  hipLaunchKernelGGL(l2_bwd_reduce_bf16_kernel, dim3(static_cast<unsigned>(ceil_div(elems, 64)), nchunk), dim3(256),
+  hipLaunchKernelGGL(l2_bwd_reduce_bf16_kernel, dim3(static_cast<unsigned>(ceil_div(elems, 64)), nchunk), dim3(64 * kRG),
                      0, stream, ws, slabs, g.P, per, g.K, g.ldw, protos, act_unit(act_kind), g_protos, g_w,
                      chunk_elems, gp_t);
   return check_launch("l2_bwd_reduce_bf16_kernel");

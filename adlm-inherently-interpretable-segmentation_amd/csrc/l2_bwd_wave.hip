@@ -406,11 +406,12 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
       f32x16 acc, gacc;
       float gdv[16];
     };
-    auto front_gd = [&](int jb, Front& fr) __attribute__((always_inline)) {
+    // g_dist values of block jb, accumulator rows 8 hf .. 8 hf + 7 (epilogue steps 3 hf, 3 hf + 1)
+    auto front_gd = [&](int jb, Front& fr, int hf) __attribute__((always_inline)) {
       const int p = 32 * (NB * wave + jb) + j;
       if constexpr (GD == 2) {
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
+        for (int g4 = 2 * hf; g4 < 2 * hf + 2; ++g4) {
           const u32x4 ro = __builtin_bit_cast(u32x4, lds_frag(S0 + L.ro + 16 * h + 32 * g4));
           const u32x4 cl = __builtin_bit_cast(u32x4, lds_frag(S0 + L.cl + 16 * h + 32 * g4));
           const unsigned rv[4] = {ro[0], ro[1], ro[2], ro[3]};
@@ -423,7 +424,7 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
         const unsigned pcol = static_cast<unsigned>(p * HW * 4);
         const bool pvalid = p < P;
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
+        for (int g4 = 2 * hf; g4 < 2 * hf + 2; ++g4) {
           const u32x4 ro = __builtin_bit_cast(u32x4, lds_frag(S0 + L.ro + 16 * h + 32 * g4));
           const unsigned rv[4] = {ro[0], ro[1], ro[2], ro[3]};
 #pragma unroll
@@ -553,8 +554,10 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
     f32x4 sg = {0.f, 0.f, 0.f, 0.f};
     bf16x8 bt[kWT];
     // fill: block 0's front, the next tile's staging pieces beside it (their issue cost hides
-    // behind the MFMAs; the raw region is free: this tile is converted)
-    front_gd(0, fr[0]);
+    // behind the MFMAs; the raw region is free: this tile is converted). The g_dist rows of a
+    // block load in two halves: rows 0..7 a period ahead, rows 8..15 (used from epilogue step 3)
+    // at the start of the block's own period, so at most 16 of them are live at a time.
+    front_gd(0, fr[0], 0);
     {
       const Stage st = stage_of(tn);
 #pragma unroll
@@ -578,7 +581,8 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
       const bool nxt = jb + 1 < NB, prv = jb >= 1;
       Front& cur = fr[jb & 1];
       Front& fn = fr[(jb + 1) & 1];
-      if (nxt) front_gd(jb + 1, fn);
+      front_gd(jb, cur, 1);
+      if (nxt) front_gd(jb + 1, fn, 0);
 #pragma unroll
       for (int k = 0; k < 6; ++k) {
         FrontOps o;

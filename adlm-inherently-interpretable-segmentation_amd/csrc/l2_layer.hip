@@ -802,7 +802,7 @@ int l2_fwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const fl
     void* scratch = nullptr;
     if (int st = stream_block(wide_fwd_scratch_bytes(geo, !dist_out && logits_out), s, 2, &scratch)) return st;
     return launch_fwd_wide(geo, x_dtype, x, protos, w_last, eps, act_kind, dist_out, act_out,
-                           logits_out, scratch, s);
+                           logits_out, scratch, s, terms_of(precision) == 2);
   }
   const int terms = terms_of(precision);
   if (terms && bf16_fwd_fits(geo, terms)) {
@@ -979,7 +979,7 @@ int l2_bwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const fl
     if (cgd.val) return fail(PROTOSEG_ERR_UNSUPPORTED, "compact KLD gradient on the wide family (K > 32 or P > 4096)");
     if (!wide_family_fits(geo)) return fail(PROTOSEG_ERR_UNSUPPORTED, "B*H*W*max(P, C) >= 2^31 elements");
     return launch_bwd_wide(geo, x_dtype, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_x, g_protos,
-                           g_logits ? g_w : nullptr, workspace, s);
+                           g_logits ? g_w : nullptr, workspace, s, terms == 2);
   }
   // Training backward at bf16x3, wave-owned prototypes (l2_bwd_wave.hip): up to 384 prototypes
   // per launch over the standard operand images, prototype chunks beyond (chunk c > 0 adds its

@@ -3,8 +3,11 @@
 // reference's own construct_PPNet default, prototype_shape = (2000, 512, 1, 1) with 200 classes
 // (model.py:394), and the DenseNet-161 add-on depths of BASELINE configs[4].
 //
-// Exact f32 products (v_mfma_f32_32x32x2_f32: a k-ordered fma chain per output element), composed
-// as strided GEMMs whose epilogues carry the layer's elementwise math, reference model.py:
+// Products in one of two modes, composed as strided GEMMs whose epilogues carry the layer's
+// elementwise math: exact f32 (v_mfma_f32_32x32x2_f32: a k-ordered fma chain per output element;
+// precision F32 / BF16X6, and push), or bf16x3 (precision BF16X3: each operand split into bf16
+// hi + lo terms as it is staged, 3 v_mfma_f32_32x32x16_bf16 per 16-k step, f32 accumulation: the
+// C = 64 family's arithmetic, 5.3x the f32 MFMA rate). Reference model.py:
 //   forward   D[b]      = relu(x2 + p2 - 2 P X[b])                   M = P,  N = HW, K = C  (203-221)
 //             logits[b] = act(D[b])^T W^T  (act applied on the load)  M = HW, N = K,  K = P  (231-237, 266-278)
 //   backward (autograd of the same; D recomputed from x, never stored by the forward)
@@ -15,6 +18,7 @@
 // The two contractions over pixels (g_P, g_W) are split over workgroups (partial slabs summed in
 // a fixed order: deterministic, no atomics). Every operand is addressed by (row, k, batch) strides,
 // so no tensor is transposed or copied; NCHW rows give coalesced loads and stores along pixels.
+#include "bf16_split.h"
 #include "protoseg_device.h"
 #include "protoseg_host.h"
 #include "l2_launch.h"
@@ -34,6 +38,11 @@ constexpr int kWKs = 32;       // contraction per LDS stage
 constexpr int kWThreads = 256;
 
 enum WideEpi { kEpiStore = 0, kEpiDist = 1, kEpiGs = 2, kEpiGx = 3 };
+
+// bf16x3 stages: per operand, hi and lo terms as [row][k] bf16 rows of kWKs k, padded to kBRow
+// elements (80-B rows: the 16-row groups of a ds_read_b128 fragment read land on distinct banks)
+constexpr int kBRow = kWKs + 8;
+constexpr int kBTile = kWT * kBRow;  // elements of one term of one 64-row operand stage
 
 // Element (r, k) of batch b at p[b * sb + r * sr + k * sk]; r is the output row (A) or column (B).
 // Every operand of the layer's GEMMs is a row- or column-major view of an NCHW / [P, C] / [K, P]
@@ -59,6 +68,7 @@ struct WideArgs {
   const float* D;    // kEpiGs: the distance at the output's address
   const float* gd;   // kEpiGs: dense g_dist at the output's address, or null
   const void* xo;    // kEpiGx: x at the output's address
+  int bf3;           // 1: bf16x3 products (precision BF16X3), 0: exact f32 MFMA
 };
 
 template <typename T>
@@ -139,12 +149,22 @@ struct Stager {
       ++bb;
     }
   }
-  __device__ __forceinline__ void store(float* S, const float (&v)[kE], unsigned okm, float eps) const {
+  // F32S: the f32 [k][row] stage (the f32 MFMAs' operand, and the epilogue sums' source);
+  // Bh (bf16x3): hi / lo terms into the [row][k] stage at Bh, Bh + kBTile.
+  template <bool F32S = true>
+  __device__ __forceinline__ void store(float* S, const float (&v)[kE], unsigned okm, float eps, bf16* Bh = nullptr) const {
     const int t = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < kE; ++i) {
       const float x = ((okm >> i) & 1u) ? on_load<ACT>(v[i], eps) : 0.f;
-      S[k_of_e(t, i) * kLd + row_of_e(t, i)] = x;
+      if constexpr (F32S) S[k_of_e(t, i) * kLd + row_of_e(t, i)] = x;
+      if (Bh) {
+        bf16 tm[2];
+        split_terms<2>(x, tm);
+        const int o = row_of_e(t, i) * kBRow + k_of_e(t, i);
+        Bh[o] = tm[0];
+        Bh[o + kBTile] = tm[1];
+      }
     }
   }
 };
@@ -167,14 +187,18 @@ __device__ __forceinline__ unsigned stage_base(const Operand& o, int b, int kb, 
 // p2[m] = sum_c P[m][c]^2 (A rows); kEpiGx: cs[n] = sum_p G_s[p][n] (B columns). Thread t sums one
 // column (row) over a fixed slice of the stage's k rows; the slices' partials are added in a fixed
 // order: deterministic, the same bits in every workgroup of a column, no separate norms pass.
-template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO, int MA, int MB, int TM>
+template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO, int MA, int MB, int TM, bool BF>
 __global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
   constexpr int kLdA = TM + 1, kLdB = kWT + 1;
   constexpr int kNC = TM == 128 ? 2 : 1;  // 32-column blocks per wave
   constexpr int kQA = kWThreads / TM;     // k slices of the A-row sums
-  __shared__ float As[2][kWKs * kLdA];
-  __shared__ float Bs[2][kWKs * kLdB];
   constexpr bool kSumB = EPI == kEpiDist || EPI == kEpiGx, kSumA = EPI == kEpiDist, kSq = EPI == kEpiDist;
+  static_assert(!BF || TM == 64, "bf16x3 stages: 64-row tiles");
+  // f32 stages: the f32 MFMAs' operands; in bf16x3 mode only where the epilogue sums read them
+  constexpr bool kFA = !BF || kSumA, kFB = !BF || kSumB;
+  __shared__ float As[2][kFA ? kWKs * kLdA : 1];
+  __shared__ float Bs[2][kFB ? kWKs * kLdB : 1];
+  __shared__ __attribute__((aligned(16))) bf16 Bh[BF ? 2 : 1][2][BF ? 2 * kBTile : 8];  // [buffer][A | B][hi | lo rows]
   __shared__ float redB[kSumB ? 4 : 1][64];
   __shared__ float redA[kSumA ? kQA : 1][kSumA ? TM : 1];
   float sum_b = 0.f, sum_a = 0.f;
@@ -202,8 +226,8 @@ __global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
   if (nst > 0) {
     sa.load(stage_base<MA>(a.A, bsel, kbeg, a.bk), kend - kbeg, a.bk, va, oka);
     sb.load(stage_base<MB>(a.B, bsel, kbeg, a.bk), kend - kbeg, a.bk, vb, okb);
-    sa.store(As[0], va, oka, a.eps);
-    sb.store(Bs[0], vb, okb, a.eps);
+    sa.template store<kFA>(As[0], va, oka, a.eps, BF ? Bh[0][0] : nullptr);
+    sb.template store<kFB>(Bs[0], vb, okb, a.eps, BF ? Bh[0][1] : nullptr);
     __syncthreads();
   }
   // (two stages of loads in flight measured 1-3 % slower at the 4-waves-per-SIMD register cap
@@ -220,11 +244,24 @@ __global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
     }
     const float* Ac = As[cur];
     const float* Bc = Bs[cur];
+    if constexpr (BF) {  // two 16-k steps: hi / lo fragments of row j, k 16 kk + 8 h .. + 7
+      const bf16* Ab = Bh[cur][0] + (wm * 32 + j) * kBRow + 8 * h;
+      const bf16* Bb = Bh[cur][1] + (wn0 * 32 + j) * kBRow + 8 * h;
 #pragma unroll
-    for (int kk = 0; kk < kWKs / 2; ++kk) {
-      const float av = Ac[(2 * kk + h) * kLdA + wm * 32 + j];
+      for (int kk = 0; kk < kWKs / 16; ++kk) {
+        const bf16x8 af[2] = {*reinterpret_cast<const bf16x8*>(Ab + 16 * kk),
+                              *reinterpret_cast<const bf16x8*>(Ab + 16 * kk + kBTile)};
+        const bf16x8 bfr[2] = {*reinterpret_cast<const bf16x8*>(Bb + 16 * kk),
+                               *reinterpret_cast<const bf16x8*>(Bb + 16 * kk + kBTile)};
+        acc[0] = mma_split<2>(af, bfr, acc[0]);
+      }
+    } else {
 #pragma unroll
-      for (int c = 0; c < kNC; ++c) acc[c] = mfma32(av, Bc[(2 * kk + h) * kLdB + (wn0 + c) * 32 + j], acc[c]);
+      for (int kk = 0; kk < kWKs / 2; ++kk) {
+        const float av = Ac[(2 * kk + h) * kLdA + wm * 32 + j];
+#pragma unroll
+        for (int c = 0; c < kNC; ++c) acc[c] = mfma32(av, Bc[(2 * kk + h) * kLdB + (wn0 + c) * 32 + j], acc[c]);
+      }
     }
     if constexpr (kSumB) {
       const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
@@ -243,8 +280,8 @@ __global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
       }
     }
     if (more) {
-      sa.store(As[cur ^ 1], va, oka, a.eps);
-      sb.store(Bs[cur ^ 1], vb, okb, a.eps);
+      sa.template store<kFA>(As[cur ^ 1], va, oka, a.eps, BF ? Bh[cur ^ 1][0] : nullptr);
+      sb.template store<kFB>(Bs[cur ^ 1], vb, okb, a.eps, BF ? Bh[cur ^ 1][1] : nullptr);
     }
     __syncthreads();
   }
@@ -339,29 +376,30 @@ int stager_mode(const Operand& o, const WideArgs& a) {
 #ifndef WIDE_TM128
 #define WIDE_TM128 0  // 128-row tiles for M >= 256 (measured slower: DESIGN 5.4)
 #endif
-template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO, int TM>
+template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO, int TM, bool BF>
 int gemm_tm(const WideArgs& a, int grid_z, int ma, int mb, hipStream_t s) {
   const dim3 grid(static_cast<unsigned>(ceil_div(a.N, kWT)), static_cast<unsigned>(ceil_div(a.M, TM)),
                   static_cast<unsigned>(grid_z));
   if (ma == 0 && mb == 0)
-    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 0, 0, TM>), grid, dim3(kWThreads), 0, s, a);
+    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 0, 0, TM, BF>), grid, dim3(kWThreads), 0, s, a);
   else if (ma == 0)
-    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 0, 1, TM>), grid, dim3(kWThreads), 0, s, a);
+    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 0, 1, TM, BF>), grid, dim3(kWThreads), 0, s, a);
   else if (mb == 0)
-    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 1, 0, TM>), grid, dim3(kWThreads), 0, s, a);
+    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 1, 0, TM, BF>), grid, dim3(kWThreads), 0, s, a);
   else
-    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 1, 1, TM>), grid, dim3(kWThreads), 0, s, a);
+    hipLaunchKernelGGL((wide_gemm_kernel<EPI, TA, TB, AACT, BACT, TO, 1, 1, TM, BF>), grid, dim3(kWThreads), 0, s, a);
   return check_launch("wide_gemm_kernel");
 }
 
-// grid_z: batches x splits (or the bk splits); a.ksplit 0 means 1.
+// grid_z: batches x splits (or the bk splits); a.ksplit 0 means 1. a.bf3: bf16x3 products.
 template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO>
 int gemm(WideArgs a, int grid_z, hipStream_t s) {
   if (a.ksplit < 1) a.ksplit = 1;
   const int ma = stager_mode(a.A, a), mb = stager_mode(a.B, a);
   if (ma < 0 || mb < 0) return fail(PROTOSEG_ERR_UNSUPPORTED, "wide GEMM operand with no unit stride");
-  if (WIDE_TM128 && a.M >= 256) return gemm_tm<EPI, TA, TB, AACT, BACT, TO, 128>(a, grid_z, ma, mb, s);
-  return gemm_tm<EPI, TA, TB, AACT, BACT, TO, 64>(a, grid_z, ma, mb, s);
+  if (a.bf3) return gemm_tm<EPI, TA, TB, AACT, BACT, TO, 64, true>(a, grid_z, ma, mb, s);
+  if (WIDE_TM128 && a.M >= 256) return gemm_tm<EPI, TA, TB, AACT, BACT, TO, 128, false>(a, grid_z, ma, mb, s);
+  return gemm_tm<EPI, TA, TB, AACT, BACT, TO, 64, false>(a, grid_z, ma, mb, s);
 }
 
 // Workgroups along a contraction of `total` for `groups` output tiles (x batches): about 1024
@@ -406,7 +444,7 @@ Operand op(const void* p, long long sr, long long sk, long long sb) {
 // D[b][p][n] into `dist` (ld P per image), optional act[g][p].
 template <typename TX>
 int wide_distances(const Geometry& g, const TX* x, const float* protos, float eps, int act_kind, float* dist,
-                   float* act, hipStream_t s) {
+                   float* act, hipStream_t s, int bf3 = 0) {
   const int B = g.npix / g.HW;
   WideArgs a{};
   a.A = op(protos, g.C, 1, 0);                                   // P[p][c]
@@ -415,6 +453,7 @@ int wide_distances(const Geometry& g, const TX* x, const float* protos, float ep
   a.out = dist, a.om = g.HW, a.on = 1, a.ob = static_cast<long long>(g.P) * g.HW;
   a.eps = eps, a.act_kind = act_kind;
   a.act = act, a.am = 1, a.an = g.P, a.ab = static_cast<long long>(g.HW) * g.P;  // act[(b HW + n) P + p]
+  a.bf3 = bf3;
   return gemm<kEpiDist, float, TX, -1, -1, float>(a, B, s);
 }
 
@@ -440,19 +479,21 @@ size_t wide_bwd_workspace_bytes(const Geometry& g) { return wide_bwd_layout(g).t
 namespace {
 // D = distances of x in its stored dtype (F32 | BF16 | F16)
 int distances_of(const Geometry& g, int x_dtype, const void* x, const float* protos, float eps, int act_kind, float* D,
-                 float* act, hipStream_t s) {
-  if (x_dtype == PROTOSEG_BF16) return wide_distances(g, static_cast<const uint16_t*>(x), protos, eps, act_kind, D, act, s);
-  if (x_dtype == PROTOSEG_F16) return wide_distances(g, static_cast<const _Float16*>(x), protos, eps, act_kind, D, act, s);
-  return wide_distances(g, static_cast<const float*>(x), protos, eps, act_kind, D, act, s);
+                 float* act, hipStream_t s, int bf3) {
+  if (x_dtype == PROTOSEG_BF16)
+    return wide_distances(g, static_cast<const uint16_t*>(x), protos, eps, act_kind, D, act, s, bf3);
+  if (x_dtype == PROTOSEG_F16)
+    return wide_distances(g, static_cast<const _Float16*>(x), protos, eps, act_kind, D, act, s, bf3);
+  return wide_distances(g, static_cast<const float*>(x), protos, eps, act_kind, D, act, s, bf3);
 }
 }  // namespace
 
 int launch_fwd_wide(const Geometry& g, int x_dtype, const void* x, const float* protos, const float* w_last, float eps,
-                    int act_kind, float* dist, float* act, float* logits, void* scratch, hipStream_t s) {
+                    int act_kind, float* dist, float* act, float* logits, void* scratch, hipStream_t s, int bf3) {
   float* sc = static_cast<float*>(scratch);
   float* D = dist ? dist : sc;  // the logits read the distances back
   float* part = sc + (dist ? 0 : ((static_cast<size_t>(g.npix) * g.P + 63) & ~static_cast<size_t>(63)));
-  int st = distances_of(g, x_dtype, x, protos, eps, act_kind, D, act, s);
+  int st = distances_of(g, x_dtype, x, protos, eps, act_kind, D, act, s, bf3);
   if (st || !logits) return st;
   // logits[b][n][k] = sum_p act(D[b][p][n]) W[k][p]; split over p into slabs [b][S][HW][K] when
   // the images' tiles are too few for the CUs
@@ -462,7 +503,7 @@ int launch_fwd_wide(const Geometry& g, int x_dtype, const void* x, const float* 
   a.B = op(w_last, g.ldw, 1, 0);                              // (k, p) of W[k][p]
   a.M = g.HW, a.N = g.K, a.Kd = g.P, a.nb = B, a.ksplit = S;
   a.out = S > 1 ? static_cast<void*>(part) : logits, a.om = g.K, a.on = 1, a.ob = static_cast<long long>(g.HW) * g.K;
-  a.eps = eps;
+  a.eps = eps, a.bf3 = bf3;
   st = act_kind == PROTOSEG_ACT_LOG ? gemm<kEpiStore, float, float, 0, -1, float>(a, B * S, s)
                                     : gemm<kEpiStore, float, float, 1, -1, float>(a, B * S, s);
   if (st || S == 1) return st;
@@ -475,14 +516,14 @@ int launch_fwd_wide(const Geometry& g, int x_dtype, const void* x, const float* 
 
 int launch_bwd_wide(const Geometry& g, int x_dtype, const void* x, const float* protos, const float* w_last, float eps,
                     int act_kind, const float* g_logits, const float* g_dist, void* g_x, float* g_protos, float* g_w,
-                    void* workspace, hipStream_t s) {
+                    void* workspace, hipStream_t s, int bf3) {
   const WideBwdLayout l = wide_bwd_layout(g);
   float* ws = static_cast<float*>(workspace);
   float *D = ws + l.D, *G = ws + l.G, *rs = ws + l.rs;
   float* part = ws + l.part;
   const int B = g.npix / g.HW;
   const long long img = static_cast<long long>(g.P) * g.HW;
-  int st = distances_of(g, x_dtype, x, protos, eps, act_kind, D, nullptr, s);
+  int st = distances_of(g, x_dtype, x, protos, eps, act_kind, D, nullptr, s, bf3);
   if (st) return st;
   {  // G_s[b][p][n] = (sum_k W[k][p] GL[b][n][k]) act'(D) + g_dist, relu mask (K = 0: g_dist alone)
     WideArgs a{};
@@ -490,7 +531,7 @@ int launch_bwd_wide(const Geometry& g, int x_dtype, const void* x, const float* 
     a.B = op(g_logits, g.K, 1, static_cast<long long>(g.HW) * g.K);  // (n, k) of GL[b][n][k]
     a.M = g.P, a.N = g.HW, a.Kd = g_logits ? g.K : 0, a.nb = B;
     a.out = G, a.om = g.HW, a.on = 1, a.ob = img;
-    a.eps = eps, a.act_kind = act_kind, a.D = D, a.gd = g_dist;
+    a.eps = eps, a.act_kind = act_kind, a.D = D, a.gd = g_dist, a.bf3 = bf3;
     if ((st = gemm<kEpiGs, float, float, -1, -1, float>(a, B, s))) return st;
   }
   if (g_x) {  // g_x[b][c][n] = -2 sum_p P[p][c] G_s[b][p][n] + 2 x cs[b][n]
@@ -499,7 +540,7 @@ int launch_bwd_wide(const Geometry& g, int x_dtype, const void* x, const float* 
     a.B = op(G, 1, g.HW, img);            // (n, p) of G_s[b][p][n]
     a.M = g.C, a.N = g.HW, a.Kd = g.P, a.nb = B;
     a.out = g_x, a.om = g.HW, a.on = 1, a.ob = static_cast<long long>(g.C) * g.HW;
-    a.xo = x;
+    a.xo = x, a.bf3 = bf3;
     st = x_dtype == PROTOSEG_BF16  ? gemm<kEpiGx, float, float, -1, -1, uint16_t>(a, B, s)
          : x_dtype == PROTOSEG_F16 ? gemm<kEpiGx, float, float, -1, -1, _Float16>(a, B, s)
                                    : gemm<kEpiGx, float, float, -1, -1, float>(a, B, s);
@@ -514,6 +555,7 @@ int launch_bwd_wide(const Geometry& g, int x_dtype, const void* x, const float* 
     a.B = op(x, g.HW, 1, static_cast<long long>(g.C) * g.HW);         // (c, n) of X[b][c][n]
     a.M = g.P, a.N = g.C, a.Kd = g.HW, a.nb = B, a.bk = 1, a.ksplit = S;
     a.out = part, a.om = g.C, a.on = 1, a.ob = static_cast<long long>(g.P) * g.C;
+    a.bf3 = bf3;
     st = x_dtype == PROTOSEG_BF16  ? gemm<kEpiStore, float, uint16_t, -1, -1, float>(a, S, s)
          : x_dtype == PROTOSEG_F16 ? gemm<kEpiStore, float, _Float16, -1, -1, float>(a, S, s)
                                    : gemm<kEpiStore, float, float, -1, -1, float>(a, S, s);
@@ -530,7 +572,7 @@ int launch_bwd_wide(const Geometry& g, int x_dtype, const void* x, const float* 
     a.B = op(D, g.HW, 1, img);                                       // (p, n) of D[b][p][n], act on load
     a.M = g.K, a.N = g.P, a.Kd = g.HW, a.nb = B, a.bk = 1, a.ksplit = S;
     a.out = part, a.om = g.P, a.on = 1, a.ob = static_cast<long long>(g.K) * g.P;
-    a.eps = eps;
+    a.eps = eps, a.bf3 = bf3;
     st = act_kind == PROTOSEG_ACT_LOG ? gemm<kEpiStore, float, float, -1, 0, float>(a, S, s)
                                       : gemm<kEpiStore, float, float, -1, 1, float>(a, S, s);
     if (st) return st;

@@ -815,12 +815,13 @@ def cpu_smoke(args, rank, world):
         dist.destroy_process_group()
 
 
-def time_wide(device, B, C, h, w, P, K, x_dtype, steps=10, warmup=3, label=""):
+def time_wide(device, B, C, h, w, P, K, x_dtype, steps=10, warmup=3, label="", precision="bf16x3"):
     """The layer step on the wide family (l2_wide.hip: any C / K, exact f32 MFMA GEMMs with fused
     epilogues): BASELINE configs[4]'s DenseNet depth and the reference's own construct_PPNet default
     (model.py:394). Whole fwd / bwd calls are event-timed (each is a chain of GEMM launches); the
-    roofline is the call's algorithmic FLOPs against the f32 MFMA peak (f32 products)."""
-    step = LayerStep(B, C, h, w, P, K, x_dtype, device, SEED)
+    roofline is the call's algorithmic FLOPs against the product peak of the precision (bf16x3:
+    2.5 PF / 3 on v_mfma_f32_32x32x16_bf16; f32: v_mfma_f32_32x32x2_f32)."""
+    step = LayerStep(B, C, h, w, P, K, x_dtype, device, SEED, precision)
     stream = torch.cuda.Stream(device)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     t_f, t_b = [], []
@@ -853,13 +854,16 @@ def time_wide(device, B, C, h, w, P, K, x_dtype, steps=10, warmup=3, label=""):
     f_fwd = mm + last                # S, logits
     f_bwd = 3 * mm + 2 * last        # S recomputed, g_act, g_x, g_P, g_W
     tf, tb = float(np.median(t_f)), float(np.median(t_b))
-    out = {"workload": label + f" (B={B}, C={C}, {h}x{w} map, P={P}, K={K}, f32 products on v_mfma_f32_32x32x2_f32)",
+    prod = ("bf16x3 products on v_mfma_f32_32x32x16_bf16" if precision == "bf16x3"
+            else "f32 products on v_mfma_f32_32x32x2_f32")
+    peak = PRODUCT_PEAK_TFLOPS["bf16x3" if precision == "bf16x3" else "f32"]
+    out = {"workload": label + f" (B={B}, C={C}, {h}x{w} map, P={P}, K={K}, {prod})",
            "img_per_s": round(B * steps / elapsed, 1), "ms_per_step": round(elapsed / steps * 1e3, 4),
            "fwd_ms": round(tf * 1e3, 4), "bwd_ms": round(tb * 1e3, 4)}
     for name, f, t in (("fwd", f_fwd, tf), ("bwd", f_bwd, tb)):
         ach = f / t / 1e12
-        out[f"roofline_{name}"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_F32_MFMA_TFLOPS,
-                                   "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_MFMA_TFLOPS, 4)}
+        out[f"roofline_{name}"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1),
+                                   "unit": "TFLOP/s", "frac": round(ach / peak, 4)}
     del step
     return out
 

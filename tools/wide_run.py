@@ -12,10 +12,11 @@ import bench  # noqa: E402
 
 cfg = sys.argv[1]
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+prec = sys.argv[3] if len(sys.argv) > 3 else "bf16x3"
 dev = torch.device("cuda:0")
 if cfg in ("c4", "c4f32"):  # c4: fp16 feature maps as BASELINE states; c4f32: the same in f32
     dt = torch.float16 if cfg == "c4" else torch.float32
-    out = bench.time_wide(dev, 32, 1024, 16, 16, 570, 19, dt, steps=steps, label="configs4 " + str(dt))
+    out = bench.time_wide(dev, 32, 1024, 16, 16, 570, 19, dt, steps=steps, label="configs4 " + str(dt), precision=prec)
 else:
-    out = bench.time_wide(dev, 32, 512, 7, 7, 2000, 200, torch.float32, steps=steps, label="reference default")
+    out = bench.time_wide(dev, 32, 512, 7, 7, 2000, 200, torch.float32, steps=steps, label="reference default", precision=prec)
 print(json.dumps(out))
