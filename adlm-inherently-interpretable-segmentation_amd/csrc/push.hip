@@ -9,6 +9,7 @@
 //   push_top2_kernel    folds the pixel stripes' partial top-2
 //   push_merge_kernel   strict-'<' fold in image order + winner gather (push.py:265-281)
 //   push_top2_merge_kernel  the two above in one launch (protoseg_push_update, native path)
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -303,6 +304,220 @@ __global__ __launch_bounds__(kPushMaxTiles * kPushSplit * 64) void push_argmin_k
   }
 }
 
+// Wave-streamed push argmin (the default): every wave owns whole 32-pixel tiles of one image and
+// runs ALL of the launch chunk's prototype tiles on each, so the pixel loop has no workgroup
+// barrier. The tile's x comes straight from HBM into the registers the f32 MFMA reads as its A
+// operand (lane (j, h): x[ct * 32 + 16 h + r][pixel j], one tile prefetched ahead); the chunk's
+// prototype rows sit in LDS for the launch (one barrier after the prologue) and are read per
+// prototype tile as the B operand, two tiles' products interleaved on independent accumulators.
+// Same arithmetic as push_dist_kernel (channel order, fma chains, ||x||^2 per half then added),
+// so ties are the ties protoseg_push_distances shows. The workgroup's waves merge their top-2
+// keys in LDS at the end (order-free: min of keys), one partial per (workgroup, image).
+#ifndef PW_WAVES
+#define PW_WAVES 8
+#endif
+constexpr int kPwWaves = PW_WAVES;  // waves per workgroup (8: two per SIMD, the next tile's x prefetched; 12: three, no prefetch)
+constexpr bool kPwPrefetch = kPwWaves <= 8;
+constexpr int kPwMaxTiles = 8;  // prototype tiles per launch chunk (C = 32 / 64; C = 128 runs the block kernel)
+__host__ __device__ inline int pw_max_tiles(int) { return kPwMaxTiles; }
+// prototype rows in LDS at a pitch of C + 4 floats: the 16-lane groups of a ds_read_b128 of
+// 16 consecutive rows land on distinct banks (4 j mod 64)
+__host__ __device__ inline int pw_pitch(int C) { return C + 4; }
+__host__ __device__ inline size_t pw_lds_bytes(int C, int nptc) {
+  const size_t protos = static_cast<size_t>(nptc) * 32 * pw_pitch(C) * 4;
+  const size_t merge = static_cast<size_t>(kPwWaves) * nptc * 32 * 16;
+  return (protos > merge ? protos : merge) + static_cast<size_t>(kPwWaves) * 64 * 4;
+}
+
+template <int NC>
+__global__ __launch_bounds__(kPwWaves * 64) void push_argmin_wave_kernel(
+    const float* __restrict__ x, int HW, const float* __restrict__ protos, int P, int pt0, int nptc,
+    const int32_t* __restrict__ proto_class, const uint32_t* __restrict__ mask,
+    unsigned long long* __restrict__ part, int wgs) {
+  using namespace bf16l;
+  constexpr int C = NC * 32;
+  extern __shared__ __attribute__((aligned(16))) float pw_smem[];
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = wave_id();
+  const int wgi = blockIdx.x, img = blockIdx.y;
+  const int pbase = (pt0 + static_cast<int>(blockIdx.z) * nptc) * 32;  // chunk z of nptc tiles
+  constexpr int kPitch = C + 4;
+  float* PL = pw_smem;                                                   // [nptc * 32][kPitch] prototype rows
+  const size_t region = pw_lds_bytes(C, nptc) / 4 - kPwWaves * 64;
+  float* xw = pw_smem + region + wave * 64;  // this wave's rows: [32] ||x||^2, [32] class masks
+  const int nrow4 = nptc * 32 * C / 4;
+  for (int i = static_cast<int>(threadIdx.x); i < nrow4; i += kPwWaves * 64) {
+    const int row = i / (C / 4);
+    const float4 v = pbase + row < P ? reinterpret_cast<const float4*>(protos)[static_cast<size_t>(pbase) * (C / 4) + i]
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+    reinterpret_cast<float4*>(PL + row * kPitch)[i - row * (C / 4)] = v;
+  }
+  __syncthreads();
+  // per prototype tile of the chunk: this lane's ||p||^2 (fma chain over its half's channels in
+  // (ct, r) order, halves added), class bit, and the wave's OR of the tile's classes
+  float p2[kPwMaxTiles];
+  uint32_t clsbit[kPwMaxTiles], tcls[kPwMaxTiles];
+#pragma unroll
+  for (int pt = 0; pt < kPwMaxTiles; ++pt) {
+    p2[pt] = 0.f;
+    clsbit[pt] = tcls[pt] = 0u;
+    if (pt < nptc) {
+      const float* pr = PL + (pt * 32 + j) * kPitch + 16 * h;
+      float s = 0.f;
+#pragma unroll
+      for (int ct = 0; ct < NC; ++ct)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s = fmaf(pr[ct * 32 + r], pr[ct * 32 + r], s);
+      p2[pt] = s + __shfl_xor(s, 32);
+      const int p = pbase + pt * 32 + j;
+      const int cls = p < P ? proto_class[p] : -1;
+      clsbit[pt] = cls >= 0 && cls < 32 ? (1u << cls) : 0u;
+      tcls[pt] = __builtin_amdgcn_readfirstlane(wave_or(clsbit[pt]));  // uniform: scalar registers
+    }
+  }
+  const rsrc_t rx = make_rsrc(x + static_cast<size_t>(img) * C * HW, static_cast<unsigned>(C * HW * 4));
+  const rsrc_t rm = make_rsrc(mask + static_cast<size_t>(img) * HW, static_cast<unsigned>(HW * 4));
+  const int ntile = (HW + 31) / 32, nw = wgs * kPwWaves;
+  // tile t's A operand: xr[ct * 16 + r] = x[ct * 32 + 16 h + r][32 t + j] (0 past the map)
+  auto load_x = [&](int t, float (&xr)[NC * 16]) __attribute__((always_inline)) {
+    const int n = t * 32 + j;
+    const unsigned off = t < ntile && n < HW ? static_cast<unsigned>(((16 * h) * HW + n) * 4) : kOOB;
+#pragma unroll
+    for (int ct = 0; ct < NC; ++ct)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        xr[ct * 16 + r] = BufIO<float>::load(rx, off, static_cast<unsigned>((ct * 32 + r) * HW * 4));
+  };
+  float bd[kPwMaxTiles], sd[kPwMaxTiles];
+  uint32_t bi[kPwMaxTiles];
+#pragma unroll
+  for (int pt = 0; pt < kPwMaxTiles; ++pt) {
+    bd[pt] = sd[pt] = __builtin_inff();
+    bi[pt] = 0xffffffffu;
+  }
+  // one prototype tile's B operand (channels ct * 32 + 16 h + 4 q .. + 3: 16-B LDS reads)
+  auto load_pv = [&](int pt, float (&pv)[NC][16]) __attribute__((always_inline)) {
+    const float4* pr = reinterpret_cast<const float4*>(PL + (pt * 32 + j) * kPitch + 16 * h);
+#pragma unroll
+    for (int ct = 0; ct < NC; ++ct)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = pr[ct * 8 + q];
+        pv[ct][4 * q] = v.x;
+        pv[ct][4 * q + 1] = v.y;
+        pv[ct][4 * q + 2] = v.z;
+        pv[ct][4 * q + 3] = v.w;
+      }
+  };
+  // per lane (prototype j of tile pt): the tile's rows (pixels) in increasing order, strict '<'
+  auto epilogue = [&](int pt, const f32x16& acc, int nbase) __attribute__((always_inline)) {
+    float x2r[16], mkr[16];  // (re-read per prototype tile: not held across the MFMA chain)
+    load_rows16(xw + 4 * h, x2r);
+    load_rows16(xw + 32 + 4 * h, mkr);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float d = l2_distance(x2r[r], p2[pt], acc[r]);
+      const float dm = (__float_as_uint(mkr[r]) & clsbit[pt]) ? d : __builtin_inff();
+      const bool c = dm < bd[pt];
+      sd[pt] = c ? bd[pt] : fminf(sd[pt], dm);
+      bi[pt] = c ? static_cast<uint32_t>(nbase + acc_row(r, h)) : bi[pt];
+      bd[pt] = c ? dm : bd[pt];
+    }
+  };
+  // tile t's patch class mask of pixel j (0 past the map)
+  auto load_mk = [&](int t) __attribute__((always_inline)) -> uint32_t {
+    return __builtin_amdgcn_raw_buffer_load_b32(
+        rm, t < ntile && t * 32 + j < HW ? static_cast<unsigned>((t * 32 + j) * 4) : kOOB, 0, 0);
+  };
+  int t = wave * wgs + wgi;
+  float xr[NC * 16];
+  uint32_t mkn = 0u;
+  if constexpr (kPwPrefetch) {
+    load_x(t, xr);
+    mkn = load_mk(t);
+  }
+#pragma unroll 1
+  for (; t < ntile; t += nw) {
+    float cur[NC * 16];
+    uint32_t mk;
+    if constexpr (kPwPrefetch) {
+#pragma unroll
+      for (int i = 0; i < NC * 16; ++i) cur[i] = xr[i];
+      mk = mkn;
+      load_x(t + nw, xr);  // the next tile's loads, in flight under this tile's MFMAs
+      mkn = load_mk(t + nw);
+    } else {
+      load_x(t, cur);
+      mk = load_mk(t);
+    }
+    float x2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NC * 16; ++i) x2 = fmaf(cur[i], cur[i], x2);
+    x2 += __shfl_xor(x2, 32);
+    wave_lds_fence();  // the previous tile's row reads are done
+    if (h == 0) {
+      xw[j] = x2;
+      xw[32 + j] = __uint_as_float(mk);
+    }
+    wave_lds_fence();
+    const int nbase = t * 32;
+    // prototype tiles in pairs: two independent f32 chains interleaved (one chain per tile with
+    // the next tile's operand prefetched measured 3 % slower)
+#pragma unroll
+    for (int pa = 0; pa < kPwMaxTiles; pa += 2) {
+      if (pa >= nptc) break;
+      const int pb = pa + 1;
+      const bool has_b = pb < nptc;
+      // prototype tiles with no patch of their classes in this pixel tile are skipped
+      const bool run_a = __ballot((mk & tcls[pa]) != 0u) != 0ull;
+      const bool run_b = has_b && __ballot((mk & tcls[pb]) != 0u) != 0ull;
+      if (!run_a && !run_b) continue;
+      float pva[NC][16], pvb[NC][16];
+      load_pv(pa, pva);
+      load_pv(has_b ? pb : pa, pvb);
+      f32x16 acc_a = zero16(), acc_b = zero16();
+#pragma unroll
+      for (int ct = 0; ct < NC; ++ct)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          acc_a = mfma32(cur[ct * 16 + r], pva[ct][r], acc_a);
+          acc_b = mfma32(cur[ct * 16 + r], pvb[ct][r], acc_b);
+        }
+      if (run_a) epilogue(pa, acc_a, nbase);
+      if (run_b) epilogue(pb, acc_b, nbase);
+    }
+  }
+  // halves, then the workgroup's waves (LDS, after every wave is done with the prototype rows)
+  unsigned long long best[kPwMaxTiles], second[kPwMaxTiles];
+#pragma unroll
+  for (int pt = 0; pt < kPwMaxTiles; ++pt) {
+    best[pt] = bd[pt] == __builtin_inff() ? ~0ull : (static_cast<unsigned long long>(__float_as_uint(bd[pt])) << 32) | bi[pt];
+    second[pt] = sd[pt] == __builtin_inff() ? ~0ull
+                                            : (static_cast<unsigned long long>(__float_as_uint(sd[pt])) << 32) | 0xffffffffu;
+    top2_merge(best[pt], second[pt], shfl_xor_u64(best[pt], 32), shfl_xor_u64(second[pt], 32));
+  }
+  __syncthreads();
+  unsigned long long* MK = reinterpret_cast<unsigned long long*>(pw_smem);  // [waves][nptc * 32][2]
+  if (h == 0) {
+#pragma unroll
+    for (int pt = 0; pt < kPwMaxTiles; ++pt) {
+      if (pt < nptc) {
+        MK[(wave * nptc * 32 + pt * 32 + j) * 2] = best[pt];
+        MK[(wave * nptc * 32 + pt * 32 + j) * 2 + 1] = second[pt];
+      }
+    }
+  }
+  __syncthreads();
+  for (int q = static_cast<int>(threadIdx.x); q < nptc * 32; q += kPwWaves * 64) {
+    const int p = pbase + q;
+    if (p >= P) continue;
+    unsigned long long b = MK[q * 2], s = MK[q * 2 + 1];
+    for (int w = 1; w < kPwWaves; ++w) top2_merge(b, s, MK[(w * nptc * 32 + q) * 2], MK[(w * nptc * 32 + q) * 2 + 1]);
+    unsigned long long* o = part + ((static_cast<size_t>(img) * wgs + wgi) * P + p) * 2;
+    o[0] = b;
+    o[1] = s;
+  }
+}
+
 // Folds the stripes' partial top-2 of each (image, prototype): img_keys = the minimum key,
 // img_second (optional) = the runner-up key (another patch), UINT64_MAX when absent.
 __global__ __launch_bounds__(256) void push_top2_kernel(const unsigned long long* __restrict__ part, int n_img,
@@ -585,6 +800,49 @@ int push_argmin_impl(const float* x, int n_img, int C, int h, int w, const float
   const long long HW = static_cast<long long>(h) * w;
   if (HW >= (1LL << 31) / 2) return fail(PROTOSEG_ERR_UNSUPPORTED, "h*w=%lld", HW);
   const int npt = static_cast<int>(ceil_div(P, 32));
+  const char* pe = getenv("PROTOSEG_PUSH");  // "block": the block-staged kernel below (A/B)
+  if (nc <= 2 && !(pe && !strcmp(pe, "block"))) {
+    // wave-streamed kernel: prototype chunks of <= pw_max_tiles tiles, about one workgroup per
+    // CU over the images (every wave at least one pixel tile)
+    const int maxt = pw_max_tiles(nc);
+    const int per = static_cast<int>(ceil_div(npt, ceil_div(npt, maxt)));
+    const int full = npt / per, rem = npt - full * per;
+    const long long ntile = ceil_div(HW, 32);
+    long long wgs = ceil_div(256, static_cast<long long>(n_img));
+    if (wgs > ceil_div(ntile, kPwWaves)) wgs = ceil_div(ntile, kPwWaves);
+    if (wgs < 1) wgs = 1;
+    const size_t need = static_cast<size_t>(n_img) * wgs * P * 2 * sizeof(unsigned long long);
+    int st = PROTOSEG_OK;
+    auto* part = static_cast<unsigned long long*>(push_scratch(need, s, &st));
+    if (st) return st;
+    auto launch = [&](auto kern, int chunks, int pt0, int nptc) {
+      if (chunks <= 0) return;
+      KernelTimer timer("push_argmin_wave_kernel", s);
+      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(wgs), n_img, chunks), dim3(kPwWaves * 64),
+                         pw_lds_bytes(C, nptc), s, x, static_cast<int>(HW), protos, P, pt0, nptc, proto_class, mask,
+                         part, static_cast<int>(wgs));
+    };
+    if (nc == 1) {
+      if (int e = ensure_lds<push_argmin_wave_kernel<1>>()) return e;
+      launch(push_argmin_wave_kernel<1>, full, 0, per);
+      launch(push_argmin_wave_kernel<1>, rem ? 1 : 0, full * per, rem);
+    } else {
+      if (int e = ensure_lds<push_argmin_wave_kernel<2>>()) return e;
+      launch(push_argmin_wave_kernel<2>, full, 0, per);
+      launch(push_argmin_wave_kernel<2>, rem ? 1 : 0, full * per, rem);
+    }
+    if (int e = check_launch("push_argmin_wave_kernel")) return e;
+    if (parts_out) {
+      *part_out = part;
+      *parts_out = static_cast<int>(wgs);
+      return PROTOSEG_OK;
+    }
+    const long long n = static_cast<long long>(n_img) * P;
+    hipLaunchKernelGGL(push_top2_kernel, dim3(static_cast<unsigned>(ceil_div(n, 256))), dim3(256), 0, s, part, n_img,
+                       static_cast<int>(wgs), P, reinterpret_cast<unsigned long long*>(img_keys),
+                       reinterpret_cast<unsigned long long*>(img_second));
+    return check_launch("push_top2_kernel");
+  }
   // prototype chunks of equal width (P = 361: 6 + 6 tiles, not 8 + 4, so both launches keep 3
   // waves per SIMD): `per` tiles in `full` chunks, then the remainder chunk
   const int per = static_cast<int>(ceil_div(npt, ceil_div(npt, kPushMaxTiles)));

@@ -515,10 +515,10 @@ def make_push_inputs(n_img, C, H, W, h, w, P, K, device, seed):
     return x, protos, labels, pc
 
 
-def kernel_launch_times(name, fn, reps, npair=8):
-    """Per-launch device seconds of the kernel `name` over `reps` eager calls of fn(), from the
-    library's per-launch event hook (protoseg_timing_events_n). Returns (mean s per launch,
-    launches per call)."""
+def kernel_launch_times(name, fn, reps, npair=8, actual=None):
+    """Per-launch device seconds of the kernel `name` (a family prefix) over `reps` eager calls of
+    fn(), from the library's per-launch event hook (protoseg_timing_events_n). Returns (mean s per
+    launch, launches per call); `actual` (a list) receives the full name of the kernel bracketed."""
     lib = _lib.load()
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(npair)] for _ in range(2)]
     for row in ev:
@@ -539,6 +539,8 @@ def kernel_launch_times(name, fn, reps, npair=8):
                 raise RuntimeError(f"timing hook bracketed {k} launches of {name}")
             per_call = k
             times += [ev[0][i].elapsed_time(ev[1][i]) * 1e-3 for i in range(k)]
+        if actual is not None:
+            actual.append(lib.protoseg_timing_kernel().decode())
     finally:
         lib.protoseg_timing_events_n(None, None, None, 0)
     return float(np.mean(times)), per_call
@@ -565,7 +567,8 @@ def time_push(n_img, steps, warmup, device, C=64, H=1024, W=2048, h=129, w=257, 
         run()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    argmin_s, launches = kernel_launch_times("push_argmin_kernel", run, steps)
+    kname = []
+    argmin_s, launches = kernel_launch_times("push_argmin", run, steps, actual=kname)
     argmin_call = argmin_s * launches
     flops = 2.0 * n_img * h * w * P * C
     nbytes = n_img * (C * h * w * 4 + h * w * 4)  # x read once + the u32 patch mask
@@ -574,7 +577,7 @@ def time_push(n_img, steps, warmup, device, C=64, H=1024, W=2048, h=129, w=257, 
                         f"map {C}x{h}x{w} f32, P={P}, K={K}",
             "argmin_kernel_ms_per_img": round(argmin_call / n_img * 1e3, 4), "argmin_launches_per_call": launches,
             "roofline": roofline_entry(flops / launches, nbytes / launches, argmin_s, "f32") |
-            {"kernel": "push_argmin_kernel"}}
+            {"kernel": kname[0] if kname else "push_argmin"}}
 
 
 def cpu_push_baseline(budget_s, C=64, H=1024, W=2048, h=129, w=257, P=190, K=19):

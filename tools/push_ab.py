@@ -35,7 +35,7 @@ def main():
                   _lib.ptr(mask), _lib.ptr(keys), _lib.ptr(second), st)
     for _ in range(3):
         run()
-    t, n = bench.kernel_launch_times("push_argmin_kernel", run, a.reps)
+    t, n = bench.kernel_launch_times("push_argmin", run, a.reps)
     flops = 2.0 * a.images * h * w * a.protos * C
     print(f"{os.environ.get('PROTOSEG_HIP_LIB', 'main')[-60:]:60s} argmin {t * 1e6:8.1f} us/launch x{n} "
           f"{flops / (t * n) / 1e12:6.1f} TF/s ({flops / (t * n) / 1e12 / 157.3:.3f} of f32 MFMA)")
