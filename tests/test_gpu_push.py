@@ -223,6 +223,31 @@ def test_push_top2_keys_vs_brute_force(device, C, P, n_img, h, w):
                 assert float(d2[j]) >= float(d1[j])
 
 
+@pytest.mark.parametrize("C,P,n_img,h,w", [(64, 190, 8, 129, 257), (64, 361, 3, 65, 65), (32, 520, 2, 33, 47),
+                                           (64, 19, 1, 7, 9), (64, 190, 1, 129, 257)])
+def test_push_wave_kernel_equals_block_kernel(device, C, P, n_img, h, w, monkeypatch):
+    """The wave-streamed argmin (default for C = 32 / 64) and the block-staged one
+    (PROTOSEG_PUSH=block) give the same keys and runner-ups bit for bit: the same arithmetic
+    (push_dist_kernel's), ties to the lowest patch in both. Full Cityscapes-sized maps included."""
+    push = _push()
+    K = 19
+    gen = torch.Generator().manual_seed(C * 7 + P)
+    x = torch.sigmoid(2 * torch.randn(n_img, C, h, w, generator=gen)).to(device)
+    protos = torch.rand(P, C, generator=gen).to(device)
+    pc = torch.argmax(po.class_identity(P, K), dim=1).to(torch.int32)
+    pc[::5] = -1
+    rng = np.random.default_rng(P + h)
+    labels = rng.integers(0, K + 1, size=(n_img, 4 * h, 4 * w)).astype(np.int64)
+    mask = push.patch_class_mask(torch.from_numpy(labels).to(device), h, w)
+    out = {}
+    for mode in ("wave", "block"):
+        monkeypatch.setenv("PROTOSEG_PUSH", mode)
+        out[mode] = push.push_argmin(x, protos, pc.to(device), mask, with_second=True)
+    torch.cuda.synchronize()
+    assert torch.equal(out["wave"][0], out["block"][0])
+    assert torch.equal(out["wave"][1], out["block"][1])
+
+
 def test_near_tie_flag_fires_on_constructed_ties(device):
     """Exact ties built into the data: (a) a winning patch's feature vector copied to another
     patch of the same class in the same image, (b) a second image identical to the first
