@@ -84,8 +84,8 @@ __device__ __forceinline__ float on_load(float v, float eps) {
 }
 
 // One operand's share of a ROWS-row x 32-k stage (ROWS = 64 or 128): ROWS / 8 elements per thread.
-//   MODE 0 (rows fast): row t % ROWS, k = t / ROWS + (256 / ROWS) i — ROWS consecutive rows per
-//                       k, coalesced;
+//   MODE 0 (rows fast): row t % ROWS, k = (t / ROWS) ROWS / 8 + i — ROWS consecutive rows per k,
+//                       coalesced, and each thread's k consecutive (one 16-B bf16 row piece);
 //   MODE 1 (k fast):    k = t & 31, row (t >> 5) + 8i — 32 consecutive k per row, coalesced.
 // The element's row (and, MODE 0, k) offset is fixed for the whole contraction; the stage moves
 // a uniform base (non-bk) or, for a k-fast operand over the flattened (batch, pixel) contraction,
@@ -102,7 +102,7 @@ struct Stager {
   unsigned sb;
 
   __device__ __forceinline__ static int row_of_e(int t, int i) { return MODE == 0 ? (t % ROWS) : (t >> 5) + 8 * i; }
-  __device__ __forceinline__ static int k_of_e(int t, int i) { return MODE == 0 ? t / ROWS + (256 / ROWS) * i : (t & 31); }
+  __device__ __forceinline__ static int k_of_e(int t, int i) { return MODE == 0 ? (t / ROWS) * kE + i : (t & 31); }
 
   __device__ __forceinline__ void init(const Operand& o, int R, int r0, int kbeg, int Kd, int bk) {
     p = static_cast<const T*>(o.p);
@@ -150,20 +150,38 @@ struct Stager {
     }
   }
   // F32S: the f32 [k][row] stage (the f32 MFMAs' operand, and the epilogue sums' source);
-  // Bh (bf16x3): hi / lo terms into the [row][k] stage at Bh, Bh + kBTile.
+  // Bh (bf16x3): hi / lo terms into the [row][k] stage at Bh, Bh + bt (bt: elements per term).
   template <bool F32S = true>
-  __device__ __forceinline__ void store(float* S, const float (&v)[kE], unsigned okm, float eps, bf16* Bh = nullptr) const {
+  __device__ __forceinline__ void store(float* S, const float (&v)[kE], unsigned okm, float eps, bf16* Bh = nullptr,
+                                        int bt = kBTile) const {
     const int t = threadIdx.x;
+    float xs[kE];
 #pragma unroll
     for (int i = 0; i < kE; ++i) {
-      const float x = ((okm >> i) & 1u) ? on_load<ACT>(v[i], eps) : 0.f;
-      if constexpr (F32S) S[k_of_e(t, i) * kLd + row_of_e(t, i)] = x;
-      if (Bh) {
+      xs[i] = ((okm >> i) & 1u) ? on_load<ACT>(v[i], eps) : 0.f;
+      if constexpr (F32S) S[k_of_e(t, i) * kLd + row_of_e(t, i)] = xs[i];
+    }
+    if (!Bh) return;
+    if constexpr (MODE == 0) {  // the thread's kE consecutive k of one row: 16-B writes of 8
+#pragma unroll
+      for (int g = 0; g < kE / 8; ++g) {
+        float x8[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x8[i] = xs[8 * g + i];
+        bf16x8 f[2];
+        split8<2>(x8, f);
+        const int o = row_of_e(t, 0) * kBRow + k_of_e(t, 8 * g);
+        *reinterpret_cast<bf16x8*>(Bh + o) = f[0];
+        *reinterpret_cast<bf16x8*>(Bh + o + bt) = f[1];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < kE; ++i) {
         bf16 tm[2];
-        split_terms<2>(x, tm);
+        split_terms<2>(xs[i], tm);
         const int o = row_of_e(t, i) * kBRow + k_of_e(t, i);
         Bh[o] = tm[0];
-        Bh[o + kBTile] = tm[1];
+        Bh[o + bt] = tm[1];
       }
     }
   }
@@ -376,6 +394,157 @@ int stager_mode(const Operand& o, const WideArgs& a) {
 #ifndef WIDE_TM128
 #define WIDE_TM128 0  // 128-row tiles for M >= 256 (measured slower: DESIGN 5.4)
 #endif
+// bf16x3 GEMM on 128 x 128 output tiles (BF16X3 requests with M >= 128 and N >= 128): the
+// 64 x 64 tile above is bound by its stages (loads, LDS writes, a barrier per 32 k) once bf16x3
+// cuts the matrix-core cycles 5.3x, so here each of the 4 waves owns a 64 x 64 quarter (2 x 2
+// blocks of 32 x 32): per 32-k stage 24 v_mfma_f32_32x32x16_bf16 per wave against 16 fragment
+// reads, and every staged element feeds twice the products. Same stagers (128 rows: 16 elements
+// per thread), contraction split, epilogues and operations per output element as
+// wide_gemm_kernel; the epilogue sums come from f32 stages in two k slices (their own fixed order).
+constexpr int kW2 = 128;
+constexpr int kB2Tile = kW2 * kBRow;  // elements of one term of one 128-row operand stage
+template <int EPI>
+constexpr size_t bf3_lds_bytes() {
+  constexpr bool kSumB = EPI == kEpiDist || EPI == kEpiGx, kSumA = EPI == kEpiDist;
+  return static_cast<size_t>(2 * 2 * 2 * kB2Tile) * 2 + (kSumA ? 2 * kWKs * (kW2 + 1) * 4 : 0) +
+         (kSumB ? 2 * kWKs * (kW2 + 1) * 4 : 0) + 2 * 2 * kW2 * 4;
+}
+template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO, int MA, int MB>
+__global__ __launch_bounds__(kWThreads) void wide_bf3_kernel(WideArgs a) {
+  constexpr int kLd = kW2 + 1;
+  constexpr bool kSumB = EPI == kEpiDist || EPI == kEpiGx, kSumA = EPI == kEpiDist, kSq = EPI == kEpiDist;
+  constexpr int kQ = kWThreads / kW2;  // 2 k slices of 16 per stage for the row / column sums
+  extern __shared__ __attribute__((aligned(16))) unsigned char wsm[];
+  bf16* Bh = reinterpret_cast<bf16*>(wsm);  // [buffer][A | B][hi | lo][128][kBRow]
+  float* fb = reinterpret_cast<float*>(wsm + static_cast<size_t>(2 * 2 * 2 * kB2Tile) * 2);
+  float* As = fb;                                          // [buffer][32][129] (kSumA)
+  float* Bs = As + (kSumA ? 2 * kWKs * kLd : 0);           // [buffer][32][129] (kSumB)
+  float* redA = Bs + (kSumB ? 2 * kWKs * kLd : 0);         // [kQ][128]
+  float* redB = redA + kQ * kW2;                           // [kQ][128]
+  auto bh = [&](int buf, int op) __attribute__((always_inline)) { return Bh + (buf * 2 + op) * 2 * kB2Tile; };
+  float sum_b = 0.f, sum_a = 0.f;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = lane & 31, h = lane >> 5;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int m0 = blockIdx.y * kW2, n0 = blockIdx.x * kW2, z = blockIdx.z;
+  const int split = a.bk ? z : z % a.ksplit, bsel = a.bk ? 0 : z / a.ksplit;
+  const long long total = a.bk ? static_cast<long long>(a.nb) * a.Kd : a.Kd;
+  const long long chunks = (total + kWKs - 1) / kWKs;
+  const int kbeg = static_cast<int>((chunks * split / a.ksplit) * kWKs);
+  int kend = static_cast<int>((chunks * (split + 1) / a.ksplit) * kWKs);
+  if (kend > total) kend = static_cast<int>(total);
+  Stager<TA, AACT, MA, kW2> sa;
+  Stager<TB, BACT, MB, kW2> sb;
+  sa.init(a.A, a.M, m0, kbeg, a.Kd, a.bk);
+  sb.init(a.B, a.N, n0, kbeg, a.Kd, a.bk);
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+    for (int bn = 0; bn < 2; ++bn) acc[bm][bn] = zero16();
+  float va[kW2 / 8], vb[kW2 / 8];
+  unsigned oka = 0, okb = 0;
+  const int nst = kend > kbeg ? (kend - kbeg + kWKs - 1) / kWKs : 0;
+  if (nst > 0) {
+    sa.load(stage_base<MA>(a.A, bsel, kbeg, a.bk), kend - kbeg, a.bk, va, oka);
+    sb.load(stage_base<MB>(a.B, bsel, kbeg, a.bk), kend - kbeg, a.bk, vb, okb);
+    sa.template store<kSumA>(As, va, oka, a.eps, bh(0, 0), kB2Tile);
+    sb.template store<kSumB>(Bs, vb, okb, a.eps, bh(0, 1), kB2Tile);
+    __syncthreads();
+  }
+  for (int st = 0; st < nst; ++st) {
+    const int cur = st & 1;
+    const bool more = st + 1 < nst;
+    if (more) {  // the next stage's loads, in flight under this stage's MFMAs
+      const int kb = kbeg + (st + 1) * kWKs;
+      if (MA == 1 && a.bk) sa.advance(a.Kd);
+      if (MB == 1 && a.bk) sb.advance(a.Kd);
+      sa.load(stage_base<MA>(a.A, bsel, kb, a.bk), kend - kb, a.bk, va, oka);
+      sb.load(stage_base<MB>(a.B, bsel, kb, a.bk), kend - kb, a.bk, vb, okb);
+    }
+    const bf16* A0 = bh(cur, 0) + (wm * 64 + j) * kBRow + 8 * h;
+    const bf16* B0 = bh(cur, 1) + (wn * 64 + j) * kBRow + 8 * h;
+#pragma unroll
+    for (int kk = 0; kk < kWKs / 16; ++kk) {
+      bf16x8 af[2][2], bfr[2][2];  // [block][term]
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm) {
+          af[q][tm] = *reinterpret_cast<const bf16x8*>(A0 + q * 32 * kBRow + 16 * kk + tm * kB2Tile);
+          bfr[q][tm] = *reinterpret_cast<const bf16x8*>(B0 + q * 32 * kBRow + 16 * kk + tm * kB2Tile);
+        }
+#pragma unroll
+      for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+        for (int bn = 0; bn < 2; ++bn) acc[bm][bn] = mma_split<2>(af[bm], bfr[bn], acc[bm][bn]);
+    }
+    if constexpr (kSumB) {
+      const float* Bc = Bs + cur * kWKs * kLd;
+      const int c = threadIdx.x % kW2, q = threadIdx.x / kW2;
+#pragma unroll
+      for (int i = 0; i < kWKs / kQ; ++i) {
+        const float vbv = Bc[((kWKs / kQ) * q + i) * kLd + c];
+        sum_b = kSq ? fmaf(vbv, vbv, sum_b) : sum_b + vbv;
+      }
+    }
+    if constexpr (kSumA) {
+      const float* Ac = As + cur * kWKs * kLd;
+      const int r = threadIdx.x % kW2, q = threadIdx.x / kW2;
+#pragma unroll
+      for (int i = 0; i < kWKs / kQ; ++i) {
+        const float vav = Ac[((kWKs / kQ) * q + i) * kLd + r];
+        sum_a = fmaf(vav, vav, sum_a);
+      }
+    }
+    if (more) {
+      sa.template store<kSumA>(As + (cur ^ 1) * kWKs * kLd, va, oka, a.eps, bh(cur ^ 1, 0), kB2Tile);
+      sb.template store<kSumB>(Bs + (cur ^ 1) * kWKs * kLd, vb, okb, a.eps, bh(cur ^ 1, 1), kB2Tile);
+    }
+    __syncthreads();
+  }
+  if constexpr (kSumB) redB[(threadIdx.x / kW2) * kW2 + threadIdx.x % kW2] = sum_b;
+  if constexpr (kSumA) redA[(threadIdx.x / kW2) * kW2 + threadIdx.x % kW2] = sum_a;
+  if constexpr (kSumA || kSumB) __syncthreads();
+
+  const int bo = a.bk ? z : (a.ksplit > 1 ? z : bsel);  // output batch (or split slab) index
+#pragma unroll
+  for (int bn = 0; bn < 2; ++bn) {
+    const int cn = wn * 64 + bn * 32 + j;
+    const int n = n0 + cn;
+    if (n >= a.N) continue;
+    float colsum = 0.f;
+    if constexpr (kSumB) colsum = redB[cn] + redB[kW2 + cn];
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rm = wm * 64 + bm * 32 + acc_row(r, h);
+        const int m = m0 + rm;
+        if (m >= a.M) continue;
+        const long long o = bo * a.ob + m * a.om + static_cast<long long>(n) * a.on;
+        float v = acc[bm][bn][r];
+        if constexpr (EPI == kEpiDist) {
+          const float p2 = redA[rm] + redA[kW2 + rm];
+          const float d = l2_distance(colsum, p2, v);
+          v = d;
+          if (a.act) a.act[bo * a.ab + m * a.am + static_cast<long long>(n) * a.an] = activation(d, a.eps, a.act_kind);
+        } else if constexpr (EPI == kEpiGs) {
+          const float d = a.D[o];
+          float g = v * activation_grad(d, a.eps, a.act_kind);
+          if (a.gd) g += a.gd[o];
+          v = d > 0.f ? g : 0.f;  // relu backward
+        } else if constexpr (EPI == kEpiGx) {
+          v = -2.f * v + 2.f * load_elem<TO>(a.xo, o) * colsum;
+        }
+        TO* out = static_cast<TO*>(a.out);
+        if (a.accumulate) v += XIO<TO>::load(out, static_cast<size_t>(o));
+        XIO<TO>::store(out, static_cast<size_t>(o), v);
+      }
+    }
+  }
+}
+
 template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO, int TM, bool BF>
 int gemm_tm(const WideArgs& a, int grid_z, int ma, int mb, hipStream_t s) {
   const dim3 grid(static_cast<unsigned>(ceil_div(a.N, kWT)), static_cast<unsigned>(ceil_div(a.M, TM)),
@@ -391,12 +560,33 @@ int gemm_tm(const WideArgs& a, int grid_z, int ma, int mb, hipStream_t s) {
   return check_launch("wide_gemm_kernel");
 }
 
+#ifndef WIDE_BF3_128
+#define WIDE_BF3_128 0  // 128 x 128 bf16x3 tiles where M, N >= 128 (measured slower at configs[4]: DESIGN 5.5)
+#endif
+template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO>
+int gemm_bf3(const WideArgs& a, int grid_z, int ma, int mb, hipStream_t s) {
+  const dim3 grid(static_cast<unsigned>(ceil_div(a.N, kW2)), static_cast<unsigned>(ceil_div(a.M, kW2)),
+                  static_cast<unsigned>(grid_z));
+  constexpr size_t lds = bf3_lds_bytes<EPI>();
+  static_assert(lds <= kMaxLds, "bf16x3 128-tile LDS");
+  auto go = [&](auto kern) {
+    if (int e = ensure_lds<decltype(kern)::value, lds>()) return e;
+    hipLaunchKernelGGL(decltype(kern)::value, grid, dim3(kWThreads), lds, s, a);
+    return check_launch("wide_bf3_kernel");
+  };
+  if (ma == 0 && mb == 0) return go(std::integral_constant<decltype(&wide_bf3_kernel<EPI, TA, TB, AACT, BACT, TO, 0, 0>), &wide_bf3_kernel<EPI, TA, TB, AACT, BACT, TO, 0, 0>>());
+  if (ma == 0) return go(std::integral_constant<decltype(&wide_bf3_kernel<EPI, TA, TB, AACT, BACT, TO, 0, 1>), &wide_bf3_kernel<EPI, TA, TB, AACT, BACT, TO, 0, 1>>());
+  if (mb == 0) return go(std::integral_constant<decltype(&wide_bf3_kernel<EPI, TA, TB, AACT, BACT, TO, 1, 0>), &wide_bf3_kernel<EPI, TA, TB, AACT, BACT, TO, 1, 0>>());
+  return go(std::integral_constant<decltype(&wide_bf3_kernel<EPI, TA, TB, AACT, BACT, TO, 1, 1>), &wide_bf3_kernel<EPI, TA, TB, AACT, BACT, TO, 1, 1>>());
+}
+
 // grid_z: batches x splits (or the bk splits); a.ksplit 0 means 1. a.bf3: bf16x3 products.
 template <int EPI, typename TA, typename TB, int AACT, int BACT, typename TO>
 int gemm(WideArgs a, int grid_z, hipStream_t s) {
   if (a.ksplit < 1) a.ksplit = 1;
   const int ma = stager_mode(a.A, a), mb = stager_mode(a.B, a);
   if (ma < 0 || mb < 0) return fail(PROTOSEG_ERR_UNSUPPORTED, "wide GEMM operand with no unit stride");
+  if (a.bf3 && WIDE_BF3_128 && a.M >= kW2 && a.N >= kW2) return gemm_bf3<EPI, TA, TB, AACT, BACT, TO>(a, grid_z, ma, mb, s);
   if (a.bf3) return gemm_tm<EPI, TA, TB, AACT, BACT, TO, 64, true>(a, grid_z, ma, mb, s);
   if (WIDE_TM128 && a.M >= 256) return gemm_tm<EPI, TA, TB, AACT, BACT, TO, 128, false>(a, grid_z, ma, mb, s);
   return gemm_tm<EPI, TA, TB, AACT, BACT, TO, 64, false>(a, grid_z, ma, mb, s);

@@ -57,6 +57,14 @@ def test_version_and_supported_shapes():
     assert lib.protoseg_l2_x_sigmoid_supported(32, 64, 65, 65, 190, 19, _lib.PREC_F32) == 0
     assert lib.protoseg_l2_x_sigmoid_supported(2, 128, 9, 9, 38, 19, _lib.PREC_BF16X3) == 0
     assert lib.protoseg_l2_x_sigmoid_supported(4096, 64, 256, 256, 190, 19, _lib.PREC_BF16X3) == 0  # > 2^31 B
+    # native feature-map dtypes: f32 / bf16 everywhere, fp16 in the wide family only
+    for dt in (_lib.F32, _lib.BF16):
+        assert lib.protoseg_l2_x_dtype_supported(64, 361, 19, dt) == 1
+    assert lib.protoseg_l2_x_dtype_supported(1024, 570, 19, _lib.F16) == 1   # configs[4] depth
+    assert lib.protoseg_l2_x_dtype_supported(512, 2000, 200, _lib.F16) == 1  # construct_PPNet default
+    assert lib.protoseg_l2_x_dtype_supported(64, 190, 19, _lib.F16) == 0     # bf16 family: widened
+    assert lib.protoseg_l2_x_dtype_supported(64, 190, 19, _lib.I64) == 0
+    assert lib.protoseg_l2_x_dtype_supported(0, 190, 19, _lib.F32) == 0
 
 
 def test_workspace_size_is_host_only_and_aligned():
@@ -77,6 +85,8 @@ def test_argument_validation_returns_status_without_gpu():
     assert st == _lib.ERR_UNSUPPORTED
     st = lib.protoseg_l2_fwd(dummy, 0, 1, 8192, 2, 2, dummy, 19, dummy, 19, 1e-4, 0, 0, null, null, null, null)
     assert st == _lib.ERR_UNSUPPORTED
+    st = lib.protoseg_l2_fwd(dummy, _lib.F16, 1, 64, 2, 2, dummy, 19, dummy, 19, 1e-4, 0, 0, null, null, null, null)
+    assert st == _lib.ERR_UNSUPPORTED and b"f16" in lib.protoseg_last_error()  # fp16 x: wide family only
     st = lib.protoseg_l2_fwd(dummy, 0, 1, 64, 2, 2, dummy, 19, dummy, 19, 1e-4, 0, 9, null, null, null, null)
     assert st == _lib.ERR_UNSUPPORTED and b"precision" in lib.protoseg_last_error()
     st = lib.protoseg_l2_fwd(dummy, 0, 1, 64, 2, 2, dummy, 19, dummy, 19, 1e-4, _lib.X_SIGMOID, _lib.PREC_F32,
