@@ -966,7 +966,8 @@ __global__ __launch_bounds__(64 * kRG) void l2_bwd_reduce_bf16_kernel(const floa
   if (g_w) g_w += p0;
   P = P - p0 < per ? P - p0 : per;
   // slab layout: [R][64] g_P | [KR][R] g_W | [R] sum_n g_s with R = Pp rows and KR = 32 class
-  // rows; gp_t (the wave kernel's): exact rows R = P, KR = K, and g_P transposed ([64][R])
+  // rows; gp_t (the wave kernel's): exact rows R = P, KR = K, and g_P transposed ([64][R]);
+  // gp_t 2: the g_P slabs already hold 2 p sum_n g_s (no sum_n g_s loads, no 2 p term here)
   const int Pp = (P + 31) & ~31;
   const int R = gp_t ? P : Pp, KR = gp_t ? K : 32;
   const int E = R * kC + KR * R + R;
@@ -987,7 +988,7 @@ __global__ __launch_bounds__(64 * kRG) void l2_bwd_reduce_bf16_kernel(const floa
       for (int k = 0; k < kReduceBatch; ++k) {
         const bool ok = si + kRG * k < S;
         v[k] = ok ? slab[static_cast<size_t>(si + kRG * k) * E + e] : 0.f;
-        u[k] = ok && is_gp ? slab[static_cast<size_t>(si + kRG * k) * E + gs_e] : 0.f;
+        u[k] = ok && is_gp && gp_t != 2 ? slab[static_cast<size_t>(si + kRG * k) * E + gs_e] : 0.f;
       }
 #pragma unroll
       for (int k = 0; k < kReduceBatch; ++k) {
@@ -1012,7 +1013,8 @@ __global__ __launch_bounds__(64 * kRG) void l2_bwd_reduce_bf16_kernel(const floa
   if (is_gp) {
     const int c = gp_t ? e / R : e - p_of_e * kC;
     if (p_of_e < P && g_protos) {
-      g_protos[static_cast<size_t>(p_of_e) * kC + c] = tot + gst * (2.f * protos[static_cast<size_t>(p_of_e) * kC + c]);
+      g_protos[static_cast<size_t>(p_of_e) * kC + c] =
+          gp_t == 2 ? tot : tot + gst * (2.f * protos[static_cast<size_t>(p_of_e) * kC + c]);
     }
   } else {
     const int e2 = e - R * kC;

@@ -149,7 +149,7 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
     const TX* __restrict__ x, unsigned x_bytes, int HW, int npix, const unsigned char* __restrict__ img, int P,
     int K, float eps, const float* __restrict__ g_logits, unsigned gl_bytes, const float* __restrict__ g_dist,
     unsigned gd_bytes, int gd_ld, int gd_p0, CompactGd cg, TX* __restrict__ g_x, int accumulate,
-    float* __restrict__ slab) {
+    float* __restrict__ slab, const float* __restrict__ protos) {
   constexpr int Pp = 128 * NB;  // prototype rows of the LDS image
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   constexpr WaveLds L = wave_lds(NB);
@@ -719,9 +719,11 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
     WSTAMP(13);
   }
 
-  // ---- slab: this workgroup's g_P (x -2: the x image holds +x), g_W, sum_n g_s in the reduce
-  // kernel's exact layout (gp_t): [64][P] g_P^T | [K][P] g_W | [P] (every store: 32 consecutive
-  // prototypes per half-wave; rows past P and classes past K are not written)
+  // ---- slab: this workgroup's g_P^T = -2 X^T g_s + 2 p sum_n g_s (x -2: the x image holds +x;
+  // the conv(x^2, ones) term's 2 p sum g_s is added per workgroup, so the reduce sums g_P slabs
+  // alone) and g_W in the reduce kernel's layout (gp_t 2): [64][P] g_P^T | [K][P] g_W | [P]
+  // unused (every store: 32 consecutive prototypes per half-wave; rows past P and classes past K
+  // are not written)
   const int E = P * kC + K * P + P;
   float* my_slab = slab + static_cast<size_t>(blockIdx.x) * E;
 #ifdef WAVE_ABL_NOSLAB
@@ -734,15 +736,17 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
     float s = gsum[jb];
     s += __shfl_xor(s, 32);
     if (p < P) {
+      const float s2 = 2.f * s;
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          my_slab[static_cast<size_t>(chan_col(32 * ct + acc_row(r, h))) * P + p] = -2.f * gp[jb][ct][r];
+        for (int r = 0; r < 16; ++r) {
+          const int c = chan_col(32 * ct + acc_row(r, h));
+          my_slab[static_cast<size_t>(c) * P + p] = fmaf(s2, protos[static_cast<size_t>(p) * kC + c], -2.f * gp[jb][ct][r]);
+        }
 #pragma unroll
       for (int r = 0; r < 16; ++r)
         if (acc_row(r, h) < K) my_slab[static_cast<size_t>(P) * kC + acc_row(r, h) * P + p] = gw[jb][r];
-      if (h == 0) my_slab[static_cast<size_t>(P) * kC + K * P + p] = s;
     }
   }
 #ifdef WAVE_STAMP
@@ -770,7 +774,7 @@ int wave_t(const Geometry& g, const void* x, const unsigned char* img, float eps
   KernelTimer timer("l2_bwd_wave_bf16_kernel", stream);
   hipLaunchKernelGGL((l2_bwd_wave_bf16_kernel<TX, ACT, GD, XSIG, NB>), dim3(grid), dim3(kWThreads), lds, stream,
                      static_cast<const TX*>(x), xb, g.HW, g.npix, img, g.P, g.K, eps, g_logits, glb, g_dist, gdb,
-                     g.ldd, g.p0, g.cgd, static_cast<TX*>(g_x), accumulate, ws);
+                     g.ldd, g.p0, g.cgd, static_cast<TX*>(g_x), accumulate, ws, g.protos + static_cast<size_t>(g.p0) * kC);
   return check_launch("l2_bwd_wave_bf16_kernel");
 }
 
@@ -801,6 +805,7 @@ int launch_bwd_wave_bf16(const Geometry& g, bool x_bf16, const void* x, const vo
   const unsigned char* blk = static_cast<const unsigned char*>(img);
   const int grid = bf16_bwd_wave_grid(g);
   const int nb = bf16_wave_nb(g.P);
+  if (!g.protos) return fail(PROTOSEG_ERR_INVALID, "wave backward: Geometry::protos (the slab's 2 p sum g_s) is null");
   auto go = [&](auto tx, auto aa, auto gd) __attribute__((always_inline)) {
     using TX = std::remove_pointer_t<decltype(tx)>;
     constexpr int kA = decltype(aa)::value;

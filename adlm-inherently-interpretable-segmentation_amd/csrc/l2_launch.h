@@ -24,6 +24,7 @@ struct Geometry {
   int ldd = 0, p0 = 0;  // g_dist: prototypes per image (= P, or the full P) and the chunk's first
   int xsig = 0;         // x is the add-on's pre-activation: sigmoid on load (bf16 fwd + fused bwd)
   CompactGd cgd;        // cgd.val != nullptr: the compact KLD gradient instead of a dense g_dist
+  const float* protos = nullptr;  // wave backward: the chunk's prototype rows (2 p sum_n g_s in its slab)
 };
 
 // bf16 split family (C = 64). `terms` = 2 (3 products) or 3 (6 products).

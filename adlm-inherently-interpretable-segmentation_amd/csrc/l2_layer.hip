@@ -1004,12 +1004,13 @@ int l2_bwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const fl
         gq.p0 = p0;
         gq.xsig = xsig;
         gq.cgd = cgd;
+        gq.protos = protos;
         if (int st = launch_bwd_wave_bf16(gq, xb, x, static_cast<unsigned char*>(img.ptr) + c * cb, eps, act_kind,
                                           g_logits, g_dist, g_x, ws + c * chunk_elems, s, c > 0))
           return st;
       }
       return launch_bwd_reduce_bf16_chunks(geo, per, nchunk, ws, grid, chunk_elems, protos, act_kind, g_protos,
-                                           g_logits ? g_w : nullptr, s, 1);
+                                           g_logits ? g_w : nullptr, s, 2);
     }
   }
   // Training backward at bf16x3: ONE pass over X for up to 384 prototypes (19 prototypes/class;
