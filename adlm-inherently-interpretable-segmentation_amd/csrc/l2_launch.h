@@ -116,7 +116,8 @@ int launch_fwd_wide(const Geometry& g, int x_dtype, const void* x, const float* 
                     int bf3);  // bf3: bf16x3 products (precision BF16X3), else exact f32
 int launch_bwd_wide(const Geometry& g, int x_dtype, const void* x, const float* protos, const float* w_last, float eps,
                     int act_kind, const float* g_logits, const float* g_dist, void* g_x, float* g_protos, float* g_w,
-                    void* workspace, hipStream_t s, int bf3);
+                    void* workspace, hipStream_t s, int bf3,
+                    const float* dist_saved = nullptr);  // the forward's distances: read, not recomputed
 // The push's path for prototype depths push.hip does not hold (C outside {32, 64, 128}): the
 // image's distances by the wide GEMM, then a masked argmin per (image, prototype) with
 // protoseg_push_argmin's key contract; wide_push_distances_scratch = protoseg_push_distances.

@@ -938,7 +938,8 @@ bool kld_compact_path(const Geometry& geo, int x_dtype, int precision, int mpc) 
 int l2_bwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P, const float* w_last,
                 int K, float eps, int act_kind, int precision, const float* g_logits, const float* g_dist,
                 const CompactGd& cgd, void* g_x, float* g_protos, float* g_w, void* workspace, size_t workspace_bytes,
-                const void* operands, size_t operands_bytes, protoseg_stream_t stream) {
+                const void* operands, size_t operands_bytes, protoseg_stream_t stream,
+                const float* dist_saved = nullptr) {
   const int xsig = split_x_sigmoid(act_kind, B, C, H, W, P, K, precision);
   if (xsig < 0) return -xsig;
   Geometry geo;
@@ -979,7 +980,7 @@ int l2_bwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const fl
     if (cgd.val) return fail(PROTOSEG_ERR_UNSUPPORTED, "compact KLD gradient on the wide family (K > 32 or P > 4096)");
     if (!wide_family_fits(geo)) return fail(PROTOSEG_ERR_UNSUPPORTED, "B*H*W*max(P, C) >= 2^31 elements");
     return launch_bwd_wide(geo, x_dtype, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_x, g_protos,
-                           g_logits ? g_w : nullptr, workspace, s, terms == 2);
+                           g_logits ? g_w : nullptr, workspace, s, terms == 2, dist_saved);
   }
   // Training backward at bf16x3, wave-owned prototypes (l2_bwd_wave.hip): up to 384 prototypes
   // per launch over the standard operand images, prototype chunks beyond (chunk c > 0 adds its
@@ -1167,6 +1168,22 @@ extern "C" int protoseg_l2_bwd(const void* x, int x_dtype, int B, int C, int H, 
                                void* workspace, size_t workspace_bytes, protoseg_stream_t stream) {
   return l2_bwd_impl(x, x_dtype, B, C, H, W, protos, P, w_last, K, eps, act_kind, precision, g_logits, g_dist,
                      CompactGd{}, g_x, g_protos, g_w, workspace, workspace_bytes, nullptr, 0, stream);
+}
+
+extern "C" int protoseg_l2_bwd_reads_dist(int C, int P, int K, int precision) {
+  if (precision < PROTOSEG_PREC_BF16X3 || precision > PROTOSEG_PREC_F32) return 0;
+  return protoseg_l2_supported(C, P, K) && use_wide(C, K, P) ? 1 : 0;
+}
+
+extern "C" int protoseg_l2_bwd_saved(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos,
+                                     int P, const float* w_last, int K, float eps, int act_kind, int precision,
+                                     const float* dist, const float* g_logits, const float* g_dist, void* g_x,
+                                     float* g_protos, float* g_w, void* workspace, size_t workspace_bytes,
+                                     protoseg_stream_t stream) {
+  if (!dist) return fail(PROTOSEG_ERR_INVALID, "protoseg_l2_bwd_saved: dist is null");
+  return l2_bwd_impl(x, x_dtype, B, C, H, W, protos, P, w_last, K, eps, act_kind, precision, g_logits, g_dist,
+                     CompactGd{}, g_x, g_protos, g_w, workspace, workspace_bytes, nullptr, 0, stream,
+                     protoseg_l2_bwd_reads_dist(C, P, K, precision) ? dist : nullptr);
 }
 
 extern "C" int protoseg_l2_bwd_ex(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P,

@@ -706,15 +706,16 @@ int launch_fwd_wide(const Geometry& g, int x_dtype, const void* x, const float* 
 
 int launch_bwd_wide(const Geometry& g, int x_dtype, const void* x, const float* protos, const float* w_last, float eps,
                     int act_kind, const float* g_logits, const float* g_dist, void* g_x, float* g_protos, float* g_w,
-                    void* workspace, hipStream_t s, int bf3) {
+                    void* workspace, hipStream_t s, int bf3, const float* dist_saved) {
   const WideBwdLayout l = wide_bwd_layout(g);
   float* ws = static_cast<float*>(workspace);
   float *D = ws + l.D, *G = ws + l.G, *rs = ws + l.rs;
   float* part = ws + l.part;
   const int B = g.npix / g.HW;
   const long long img = static_cast<long long>(g.P) * g.HW;
-  int st = distances_of(g, x_dtype, x, protos, eps, act_kind, D, nullptr, s, bf3);
-  if (st) return st;
+  int st = PROTOSEG_OK;
+  if (dist_saved) D = const_cast<float*>(dist_saved);  // read-only below (G_s epilogue, g_W operand)
+  else if ((st = distances_of(g, x_dtype, x, protos, eps, act_kind, D, nullptr, s, bf3))) return st;
   {  // G_s[b][p][n] = (sum_k W[k][p] GL[b][n][k]) act'(D) + g_dist, relu mask (K = 0: g_dist alone)
     WideArgs a{};
     a.A = op(w_last, 1, g.ldw, 0);                               // (p, k) of W[k][p]

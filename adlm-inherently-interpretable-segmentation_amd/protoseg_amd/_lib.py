@@ -43,6 +43,9 @@ SIGNATURES = {
     "protoseg_timing_launches": (_i, []),
     "protoseg_l2_supported": (_i, [_i, _i, _i]),
     "protoseg_l2_x_dtype_supported": (_i, [_i, _i, _i, _i]),
+    "protoseg_l2_bwd_reads_dist": (_i, [_i, _i, _i, _i]),
+    "protoseg_l2_bwd_saved": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp,
+                                   _vp, _sz, _vp]),
     "protoseg_adam_step": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _f, _f, _f, _vp]),
     "protoseg_l2_max_protos": (_i, [_i, _i]),
     "protoseg_l2_x_sigmoid_supported": (_i, [_i, _i, _i, _i, _i, _i, _i]),

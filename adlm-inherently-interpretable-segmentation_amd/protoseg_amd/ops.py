@@ -54,6 +54,12 @@ def x_dtype_supported(C: int, P: int, K: int, dtype: torch.dtype) -> bool:
     return code is not None and bool(_lib.load().protoseg_l2_x_dtype_supported(C, P, K, code))
 
 
+def bwd_reads_dist(C: int, P: int, K: int, precision: int) -> bool:
+    """Whether the backward at this shape reads the forward's distances instead of recomputing
+    them (protoseg_l2_bwd_reads_dist: the wide family)."""
+    return bool(_lib.load().protoseg_l2_bwd_reads_dist(C, P, K, int(precision)))
+
+
 def x_sigmoid_supported(x: Tensor, P: int, K: int, precision: Optional[str] = None) -> bool:
     """Whether the kernels can apply the add-on's sigmoid on load for this call."""
     B, C, H, W = x.shape
@@ -118,10 +124,13 @@ def _operands_args(operands: Optional[Tensor]):
 @torch.library.custom_op("protoseg::l2_backward", mutates_args=(), device_types="cuda")
 def l2_backward(x: Tensor, protos: Tensor, w_last: Tensor, g_logits: Optional[Tensor], g_dist: Optional[Tensor],
                 eps: float, act_kind: int, precision: int, need_x: bool, need_protos: bool,
-                need_w: bool, operands: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor]:
+                need_w: bool, operands: Optional[Tensor] = None,
+                dist: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor]:
     """Backward of l2_forward with respect to (x, protos, w_last); unrequested grads are empty.
     With X_SIGMOID in act_kind, g_x is the gradient w.r.t. the pre-activation. operands: the
-    forward's with_operands output (same protos / w_last values), read instead of a prep launch."""
+    forward's with_operands output (same protos / w_last values), read instead of a prep launch.
+    dist: the forward's distances, read instead of recomputed where bwd_reads_dist (the wide
+    family: protoseg_l2_bwd_saved); same gradients bit for bit."""
     dev = _lib.require_device(x, protos, w_last, g_logits, g_dist)
     x = x.contiguous()
     protos = protos.contiguous()
@@ -143,15 +152,22 @@ def l2_backward(x: Tensor, protos: Tensor, w_last: Tensor, g_logits: Optional[Te
     ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8) if ws_bytes else None
     ops_ptr, ops_bytes = _operands_args(operands)
     with torch.cuda.device(dev):
-        _lib.call("protoseg_l2_bwd_ex", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P, _lib.ptr(w_last),
-                  K, float(eps), int(act_kind), int(precision), _lib.ptr(g_logits), _lib.ptr(g_dist),
-                  _lib.ptr(g_x), _lib.ptr(g_p), _lib.ptr(g_w), _lib.ptr(ws), ws_bytes, ops_ptr, ops_bytes,
-                  _lib.stream_of(dev))
+        if dist is not None and dist.numel():
+            _lib.call("protoseg_l2_bwd_saved", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P,
+                      _lib.ptr(w_last), K, float(eps), int(act_kind), int(precision), _lib.ptr(dist.contiguous()),
+                      _lib.ptr(g_logits), _lib.ptr(g_dist), _lib.ptr(g_x), _lib.ptr(g_p), _lib.ptr(g_w),
+                      _lib.ptr(ws), ws_bytes, _lib.stream_of(dev))
+        else:
+            _lib.call("protoseg_l2_bwd_ex", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P,
+                      _lib.ptr(w_last), K, float(eps), int(act_kind), int(precision), _lib.ptr(g_logits),
+                      _lib.ptr(g_dist), _lib.ptr(g_x), _lib.ptr(g_p), _lib.ptr(g_w), _lib.ptr(ws), ws_bytes, ops_ptr,
+                      ops_bytes, _lib.stream_of(dev))
     return g_x, g_p, g_w
 
 
 @l2_backward.register_fake
-def _(x, protos, w_last, g_logits, g_dist, eps, act_kind, precision, need_x, need_protos, need_w, operands=None):
+def _(x, protos, w_last, g_logits, g_dist, eps, act_kind, precision, need_x, need_protos, need_w, operands=None,
+      dist=None):
     B, C, H, W = x.shape
     P, K = protos.shape[0], w_last.shape[0]
     need_w = need_w and g_logits is not None
@@ -271,8 +287,11 @@ def _(x, protos, w_last, g_logits, g_cls, pix_cls, proto_slot, max_per_class, ep
 def _setup_context(ctx, inputs, output):
     x, protos, w_last, eps, act_kind, precision, with_dist, with_logits, with_act = inputs[:9]
     # the forward-built operand images are saved like the inputs, so saved-tensor hooks see them
-    # and the version check guards them (an empty tensor when the forward built none)
-    ctx.save_for_backward(x, protos, w_last, output[3])
+    # and the version check guards them (an empty tensor when the forward built none); so are the
+    # distances where the backward reads them instead of recomputing (the wide family)
+    dist_saved = output[0] if (with_dist and output[0].numel() and x.is_cuda and
+                               bwd_reads_dist(x.shape[1], protos.shape[0], w_last.shape[0], precision)) else None
+    ctx.save_for_backward(x, protos, w_last, output[3], dist_saved)
     ctx.eps = eps
     ctx.act_kind = act_kind
     ctx.precision = precision
@@ -302,7 +321,7 @@ def _act_grad_as_dist_grad(x, protos, w_last, g_act, eps, act_kind, precision):
 
 
 def _backward(ctx, g_dist, g_logits, g_act, g_operands=None):
-    x, protos, w_last, operands = ctx.saved_tensors
+    x, protos, w_last, operands, dist_saved = ctx.saved_tensors
     need_x, need_p, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
     sink = ctx.sink
     compact = sink.take() if sink is not None else []
@@ -328,7 +347,7 @@ def _backward(ctx, g_dist, g_logits, g_act, g_operands=None):
                                         ops_buf)
     else:
         g_x, g_p, g_w = l2_backward(x, protos, w_last, g_logits, g_dist, ctx.eps, ctx.act_kind, ctx.precision, need_x,
-                                    need_p, need_w and g_logits is not None, ops_buf)
+                                    need_p, need_w and g_logits is not None, ops_buf, dist_saved)
     return (g_x if need_x else None, g_p if need_p else None, g_w if (need_w and g_w.numel()) else None,
             None, None, None, None, None, None, None)
 

@@ -102,6 +102,9 @@ class LayerStep:
         # one operand prep per step: the forward's prep launch also writes the backward's
         # operand images (protoseg_l2_fwd_ex), as the autograd op does in training
         # (PROTOSEG_FWD_OPERANDS=0: the backward prepares its own, for A/B)
+        # the wide family's backward reads the forward's distances (protoseg_l2_bwd_saved), as the
+        # autograd op does in training
+        self.reads_dist = bool(lib.protoseg_l2_bwd_reads_dist(C, P, K, self.prec))
         nops = lib.protoseg_l2_train_operands_bytes(C, P, K, self.prec)
         if os.environ.get("PROTOSEG_FWD_OPERANDS", "1") == "0":
             nops = 0
@@ -133,7 +136,14 @@ class LayerStep:
 
     def bwd(self):
         """One backward call for g_x, g_prototypes and g_last_layer, as the autograd op makes it
-        (ops.l2_backward), reading the operand images the forward's prep wrote."""
+        (ops.l2_backward), reading the operand images the forward's prep wrote (the wide family:
+        the forward's distances)."""
+        if self.reads_dist:
+            _lib.call("protoseg_l2_bwd_saved", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w,
+                      _lib.ptr(self.protos), self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec,
+                      _lib.ptr(self.dist), _lib.ptr(self.g_logits), ctypes.c_void_p(None), _lib.ptr(self.g_x),
+                      _lib.ptr(self.g_p), _lib.ptr(self.g_w), _lib.ptr(self.ws), self.ws_bytes, self._stream())
+            return
         _lib.call("protoseg_l2_bwd_ex", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w,
                   _lib.ptr(self.protos), self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec,
                   _lib.ptr(self.g_logits), ctypes.c_void_p(None), _lib.ptr(self.g_x), _lib.ptr(self.g_p),
@@ -855,7 +865,8 @@ def time_wide(device, B, C, h, w, P, K, x_dtype, steps=10, warmup=3, label="", p
     n = B * h * w
     mm, last = 2.0 * n * P * C, 2.0 * n * P * K
     f_fwd = mm + last                # S, logits
-    f_bwd = 3 * mm + 2 * last        # S recomputed, g_act, g_x, g_P, g_W
+    # g_act, g_x, g_P, g_W (+ S recomputed unless the backward reads the forward's distances)
+    f_bwd = (2 if step.reads_dist else 3) * mm + 2 * last
     tf, tb = float(np.median(t_f)), float(np.median(t_b))
     prod = ("bf16x3 products on v_mfma_f32_32x32x16_bf16" if precision == "bf16x3"
             else "f32 products on v_mfma_f32_32x32x2_f32")

@@ -187,6 +187,23 @@ int protoseg_l2_bwd_ex(const void* x, int x_dtype, int B, int C, int H, int W,
                        void* g_x, float* g_protos, float* g_w,
                        void* workspace, size_t workspace_bytes,
                        const void* operands, size_t operands_bytes, protoseg_stream_t stream);
+/*
+ * Backward reading the forward's distances instead of recomputing them, where that is cheaper:
+ * the wide family (C outside {32, 64, 128}, K > 32 or P > 4096; e.g. BASELINE configs[4]'s
+ * C = 1024), whose distance GEMM costs as much as the g_x one while the distances are a small
+ * tensor. protoseg_l2_bwd_reads_dist says whether a shape reads `dist`; elsewhere the call is
+ * protoseg_l2_bwd_ex (the C = 32 / 64 / 128 families recompute: at C = 64 reading the
+ * [B, P, H, W] tensor costs more HBM time than the products). `dist` [B, P, H, W] f32 is the
+ * dist_out of protoseg_l2_fwd on the same x, protos, eps, act_kind and precision (the backward's
+ * own recompute gives the same bits, so the gradients are identical either way).
+ */
+int protoseg_l2_bwd_reads_dist(int C, int P, int K, int precision);
+int protoseg_l2_bwd_saved(const void* x, int x_dtype, int B, int C, int H, int W,
+                          const float* protos, int P, const float* w_last, int K,
+                          float eps, int act_kind, int precision, const float* dist,
+                          const float* g_logits, const float* g_dist,
+                          void* g_x, float* g_protos, float* g_w,
+                          void* workspace, size_t workspace_bytes, protoseg_stream_t stream);
 int protoseg_l2_bwd_kld_ex(const void* x, int x_dtype, int B, int C, int H, int W,
                            const float* protos, int P, const float* w_last, int K,
                            float eps, int act_kind, int precision,

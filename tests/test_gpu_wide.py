@@ -204,3 +204,29 @@ def test_fp16_native_matches_widened(device):
     torch.cuda.synchronize()
     for name, a, b in zip(("dist", "logits", "g_x", "g_protos", "g_w"), outs[0], outs[1]):
         assert torch.equal(a, b), name
+
+
+def test_wide_backward_from_saved_distances(device):
+    """protoseg_l2_bwd_saved (the wide family reads the forward's distances instead of
+    recomputing them) gives the recomputing backward's gradients bit for bit, and the autograd
+    op saves the distances for it."""
+    from protoseg_amd import ops
+    B, C, h, w, P, K = 2, 256, 6, 7, 95, 19
+    x, protos, w_last, g_logits, _ = _inputs(B, C, h, w, P, K, seed=21)
+    prec = ops.precision_code(None)
+    assert ops.bwd_reads_dist(C, P, K, prec) and not ops.bwd_reads_dist(64, 361, 19, prec)
+    xd, pd, wd, gl = x.to(device), protos.to(device), w_last.to(device), g_logits.to(device)
+    dist = ops.l2_forward(xd, pd, wd, 1e-4, 0, prec, True, True, False)[0]
+    a = ops.l2_backward(xd, pd, wd, gl, None, 1e-4, 0, prec, True, True, True)
+    b = ops.l2_backward(xd, pd, wd, gl, None, 1e-4, 0, prec, True, True, True, None, dist)
+    torch.cuda.synchronize()
+    for name, u, v in zip(("g_x", "g_p", "g_w"), a, b):
+        assert torch.equal(u, v), name
+    xr = xd.clone().requires_grad_(True)
+    pr = pd.clone().requires_grad_(True)
+    wr = wd.clone().requires_grad_(True)
+    dist2, logits, _ = ops.prototype_layer(xr, pr, wr)
+    logits.backward(gl)
+    torch.cuda.synchronize()
+    assert torch.equal(dist2, dist)
+    assert torch.equal(xr.grad, a[0]) and torch.equal(pr.grad, a[1]) and torch.equal(wr.grad, a[2])
