@@ -12,6 +12,7 @@
 // t = state[k][0] + 1 at its start; the last of tensor k's workgroups to finish (ticket in
 // state[k][1], a vector atomic) stores t and resets the ticket, after all of them have read it.
 // A tensor with no elements gets one workgroup, which only advances its count.
+#include "adam_update.h"
 #include "protoseg_host.h"
 
 namespace protoseg {
@@ -58,30 +59,23 @@ __global__ __launch_bounds__(kAdamBlock) void adam_kernel(AdamTensors ts, float 
     mi[r] = ok ? m[i] : 0.f;
     vi[r] = ok ? v[i] : 0.f;
   }
-  if (threadIdx.x == 0) {  // bias corrections once per workgroup: b^t by squaring in f64
-    const int t = __atomic_load_n(state, __ATOMIC_RELAXED) + 1;
-    double p1 = 1.0, p2 = 1.0, s1 = beta1, s2 = beta2;
-    for (int e = t; e > 0; e >>= 1, s1 *= s1, s2 *= s2)
-      if (e & 1) p1 *= s1, p2 *= s2;
-    t_sh = t;
-    corr[0] = static_cast<float>(1.0 - p1);
-    corr[1] = static_cast<float>(sqrt(1.0 - p2));
+  if (threadIdx.x == 0) {  // bias corrections once per workgroup (adam_update.h)
+    const AdamCorr ac = adam_corr(state, lr, beta1, beta2);
+    t_sh = ac.t;
+    corr[0] = ac.step_size;
+    corr[1] = ac.bc2_sqrt;
   }
   __syncthreads();
   const int t = t_sh;
-  const float bc1 = corr[0], bc2_sqrt = corr[1];
-  const float step_size = lr / bc1;
+  const float step_size = corr[0], bc2_sqrt = corr[1];
 #pragma unroll
   for (int r = 0; r < kAdamPerThread; ++r) {
     const long long i = base + r * kAdamBlock + threadIdx.x;
     if (i < ts.n[k]) {
-      float gr = gi[r];
-      if (wd != 0.f) gr = fmaf(wd, pi[r], gr);
-      const float mr = beta1 * mi[r] + (1.f - beta1) * gr;
-      const float vr = beta2 * vi[r] + (1.f - beta2) * gr * gr;
-      m[i] = mr;
-      v[i] = vr;
-      p[i] = pi[r] - step_size * mr / (sqrtf(vr) / bc2_sqrt + eps);
+      adam_update(pi[r], mi[r], vi[r], gi[r], step_size, bc2_sqrt, beta1, beta2, eps, wd);
+      m[i] = mi[r];
+      v[i] = vi[r];
+      p[i] = pi[r];
     }
   }
   // Step count: the last workgroup to arrive publishes t (all reads of state[0] are done by then:

@@ -21,6 +21,7 @@
 // the distance GEMM, so all three compute bit-identical distances for the same inputs.
 #include <type_traits>
 
+#include "adam_update.h"
 #include "bf16_split.h"
 #include "l2_bf16_common.h"
 #include "l2_launch.h"
@@ -210,6 +211,150 @@ __global__ __launch_bounds__(256) void l2_prep_bf16_kernel(const float* __restri
   }
 }
 
+
+// Adam step of (prototypes, last layer) fused with the operand prep of the updated values: the
+// image block l2_prep_bf16_kernel<2> builds (fwd_only 0, one chunk), so the next forward skips
+// its prep launch (PROTOSEG_OPERANDS_READY). One workgroup per 32-prototype tile: it updates rows
+// 32 pt .. of the prototypes and the same columns of the last layer (adam_update.h: adam_kernel's
+// arithmetic), keeps the new values in LDS, and writes the tile's part of every image region from
+// them with the stage_* functions' element order, scaling and zeroing (the same bits). The step
+// counts advance once per launch (the last workgroup's ticket, as adam_kernel).
+constexpr int kApPitch = kC + 1;  // LDS rows of the tile's prototypes (conflict-free column reads)
+__global__ __launch_bounds__(256) void l2_adam_prep_kernel(AdamPrepArgs a) {
+  __shared__ float sp[32 * kApPitch];
+  __shared__ float sw[32 * 33];
+  __shared__ float corr[4];
+  __shared__ int tk[2], last[2];
+  const int pt = blockIdx.x, tid = threadIdx.x, P = a.P, K = a.K;
+  const int Pp = (P + 31) & ~31, p0 = pt * 32;
+  // this tile's elements: prototypes (row r, channel c) = e, w (class k, column j) = e
+  float gi[8], pi[8], mi[8], vi[8], gwi[4], wi[4], mwi[4], vwi[4];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = tid + 256 * u, r = e >> 6;
+    const bool ok = p0 + r < P;
+    const size_t i = static_cast<size_t>(p0) * kC + e;
+    gi[u] = ok ? a.gp[i] : 0.f;
+    pi[u] = ok ? a.p[i] : 0.f;
+    mi[u] = ok ? a.mp[i] : 0.f;
+    vi[u] = ok ? a.vp[i] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = tid + 256 * u, k = e >> 5, j = e & 31;
+    const bool ok = k < K && p0 + j < P;
+    const size_t i = static_cast<size_t>(k) * P + p0 + j;
+    gwi[u] = ok ? a.gw[i] : 0.f;
+    wi[u] = ok ? a.w[i] : 0.f;
+    mwi[u] = ok ? a.mw[i] : 0.f;
+    vwi[u] = ok ? a.vw[i] : 0.f;
+  }
+  if (tid < 2 && (tid == 0 || K > 0)) {
+    const AdamCorr ac = tid == 0 ? adam_corr(a.stp, a.lr_p, a.beta1, a.beta2) : adam_corr(a.stw, a.lr_w, a.beta1, a.beta2);
+    tk[tid] = ac.t;
+    corr[2 * tid] = ac.step_size;
+    corr[2 * tid + 1] = ac.bc2_sqrt;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = tid + 256 * u, r = e >> 6, c = e & 63;
+    if (p0 + r < P) {
+      adam_update(pi[u], mi[u], vi[u], gi[u], corr[0], corr[1], a.beta1, a.beta2, a.eps, a.wd_p);
+      const size_t i = static_cast<size_t>(p0) * kC + e;
+      a.mp[i] = mi[u];
+      a.vp[i] = vi[u];
+      a.p[i] = pi[u];
+    }
+    sp[r * kApPitch + c] = pi[u];
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = tid + 256 * u, k = e >> 5, j = e & 31;
+    if (k < K && p0 + j < P) {
+      adam_update(wi[u], mwi[u], vwi[u], gwi[u], corr[2], corr[3], a.beta1, a.beta2, a.eps, a.wd_w);
+      const size_t i = static_cast<size_t>(k) * P + p0 + j;
+      a.mw[i] = mwi[u];
+      a.vw[i] = vwi[u];
+      a.w[i] = wi[u];
+    }
+    sw[k * 33 + j] = wi[u];
+  }
+  __syncthreads();
+  // the step counts: the last workgroup publishes t (every read of state[0] returned before the
+  // tickets, see adam_kernel)
+  if (tid < 2 && (tid == 0 || K > 0)) {
+    int* st = tid == 0 ? a.stp : a.stw;
+    last[tid] = atomicAdd(st + 1, 1) == static_cast<int>(gridDim.x) - 1;
+    if (last[tid]) {
+      atomicExch(st, tk[tid]);
+      atomicExch(st + 1, 0);
+    }
+  }
+  const ImgOffsets o = img_offsets(Pp, 2);
+  bf16* img_p = reinterpret_cast<bf16*>(a.block + o.p);
+  bf16* img_pt = reinterpret_cast<bf16*>(a.block + o.pt);
+  bf16* img_w = reinterpret_cast<bf16*>(a.block + o.w);
+  bf16* img_wt = reinterpret_cast<bf16*>(a.block + o.wt);
+  {  // (-2 P) rows (stage_p_rows): row p0 + (tid >> 3), chunk tid & 7
+    const int r = tid >> 3, e8 = tid & 7, q = e8 >> 1, h = e8 & 1, p = p0 + r;
+    float v[8];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) v[jj] = p < P ? -2.f * sp[r * kApPitch + chan_of(q, h, jj)] : 0.f;
+    bf16x8 f[2];
+    split8<2>(v, f);
+    store_frag<2>(img_p, Pp * kC, img_off<8>(p, e8), f);
+  }
+  {  // (-2 P)^T permuted (stage_pt_perm): channel (tid >> 2), chunk tid & 3
+    const int c = tid >> 2, e8 = tid & 3;
+    float v[8];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int r = perm_of(e8 * 8 + jj);
+      v[jj] = p0 + r < P ? -2.f * sp[r * kApPitch + c] : 0.f;
+    }
+    bf16x8 f[2];
+    split8<2>(v, f);
+    store_frag<2>(img_pt, Pp * kC, img_off<4>(pt * kC + c, e8), f);
+  }
+  if (tid < 128) {  // (act_unit W) permuted (stage_w_perm): class tid >> 2, chunk tid & 3
+    const int k = tid >> 2, e8 = tid & 3;
+    float v[8];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int j = perm_of(e8 * 8 + jj);
+      v[jj] = (k < K && p0 + j < P) ? a.w_scale * sw[k * 33 + j] : 0.f;
+    }
+    bf16x8 f[2];
+    split8<2>(v, f);
+    store_frag<2>(img_w, Pp * 32, img_off<4>(pt * 32 + k, e8), f);
+  } else {  // (grad_unit W)^T rows (stage_wt_rows): row p0 + ((tid - 128) >> 2), chunk tid & 3
+    const int j = (tid - 128) >> 2, e8 = tid & 3, p = p0 + j;
+    float v[8];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int k = e8 * 8 + jj;
+      v[jj] = (k < K && p < P) ? a.wt_scale * sw[k * 33 + j] : 0.f;
+    }
+    bf16x8 f[2];
+    split8<2>(v, f);
+    store_frag<2>(img_wt, Pp * 32, img_off<4>(p, e8), f);
+  }
+  float* p2 = reinterpret_cast<float*>(a.block + o.p2);
+  if (tid < 32) {  // ||p||^2 as proto_norm2_64: sequential, no contraction
+#pragma clang fp contract(off)
+    const int p = p0 + tid;
+    float s = 0.f;
+    for (int c = 0; c < kC; ++c) {
+      const float x = sp[tid * kApPitch + c];
+      s += x * x;
+    }
+    p2[p] = p < P ? s : 0.f;
+  } else if (pt == static_cast<int>(gridDim.x) - 1) {  // the region's padding past Pp
+    const int n1 = (o.pt - o.p2) / 4;
+    for (int p = Pp + tid - 32; p < n1; p += 224) p2[p] = 0.f;
+  }
+}
 
 // Byte offset of this lane's pixel at channel 4h of image b (layout A lane = pixel j), or kOOB.
 template <typename TX>
@@ -1213,6 +1358,14 @@ int launch_prep_bf16(const Geometry& g, int terms, const float* protos, const fl
                      void* img, hipStream_t stream, int fwd_only, void* onepass_block, int onepass_Pp) {
   return launch_prep_bf16_chunks(g, g.P, 1, terms, protos, w_last, act_kind, eps, img, stream, fwd_only, onepass_block,
                                  onepass_Pp);
+}
+
+int launch_adam_prep_bf16(const AdamPrepArgs& a, hipStream_t stream) {
+  if (a.P <= 0 || a.K < 0 || a.K > 32 || !a.p || !a.gp || !a.mp || !a.vp || !a.stp || !a.block ||
+      (a.K > 0 && (!a.w || !a.gw || !a.mw || !a.vw || !a.stw)))
+    return fail(PROTOSEG_ERR_INVALID, "adam_prep: null tensor or K outside 0..32");
+  hipLaunchKernelGGL(l2_adam_prep_kernel, dim3(static_cast<unsigned>(ceil_div(a.P, 32))), dim3(256), 0, stream, a);
+  return check_launch("l2_adam_prep_kernel");
 }
 
 int launch_bwd_reduce_bf16_chunks(const Geometry& g, int per, int nchunk, const float* ws, int slabs,

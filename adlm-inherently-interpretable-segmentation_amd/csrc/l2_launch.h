@@ -50,6 +50,27 @@ int launch_prep_bf16_chunks(const Geometry& g, int per, int nchunk, int terms, c
                             const float* w_last, int act_kind, float eps, void* img, hipStream_t stream,
                             int fwd_only = 0, void* onepass_block = nullptr, int onepass_Pp = 0);
 
+// Adam step of the prototypes [P][64] and the last layer [K][P] (adam_update.h) fused with the
+// operand prep of the updated values into `block` (launch_prep_bf16's bf16x3 block, fwd_only 0,
+// one chunk); w and its state null iff K = 0. w_scale / wt_scale: act_unit / act_grad_unit.
+struct AdamPrepArgs {
+  float* p;
+  const float* gp;
+  float* mp;
+  float* vp;
+  int* stp;
+  float* w;
+  const float* gw;
+  float* mw;
+  float* vw;
+  int* stw;
+  int P, K;
+  float lr_p, wd_p, lr_w, wd_w, beta1, beta2, eps;
+  float w_scale, wt_scale;
+  unsigned char* block;
+};
+int launch_adam_prep_bf16(const AdamPrepArgs& a, hipStream_t stream);
+
 // accumulate != 0: logits += this call's (prototype chunks of one forward).
 int launch_fwd_bf16(const Geometry& g, bool x_bf16, int terms, const void* x, const void* img, float eps, int act_kind,
                     float* dist, float* act, float* logits, hipStream_t stream,

@@ -28,6 +28,7 @@
 #include <utility>
 #include <vector>
 
+#include "bf16_split.h"
 #include "l2_launch.h"
 #include "protoseg_host.h"
 
@@ -730,6 +731,38 @@ extern "C" size_t protoseg_l2_train_operands_bytes(int C, int P, int K, int prec
   return train_operands_bytes(C, P, K, train_operands_kind(C, P, K, precision));
 }
 
+extern "C" int protoseg_l2_adam_prep_supported(int C, int P, int K, int precision) {
+  return K >= 0 && K <= 32 && train_operands_kind(C, P, K, precision) == TrainOperands::kFused ? 1 : 0;
+}
+
+extern "C" int protoseg_l2_adam_prep(int C, int P, int K, float eps, int act_kind, int precision, float* protos,
+                                     const float* g_protos, float* exp_avg_p, float* exp_avg_sq_p, int32_t* state_p,
+                                     float lr_p, float weight_decay_p, float* w_last, const float* g_w,
+                                     float* exp_avg_w, float* exp_avg_sq_w, int32_t* state_w, float lr_w,
+                                     float weight_decay_w, float beta1, float beta2, float adam_eps, void* operands,
+                                     size_t operands_bytes, protoseg_stream_t stream) {
+  if (!protoseg_l2_adam_prep_supported(C, P, K, precision))
+    return fail(PROTOSEG_ERR_UNSUPPORTED, "adam_prep: C = 64, K <= 32, BF16X3 one-chunk shapes only "
+                                          "(protoseg_l2_adam_prep_supported)");
+  if (act_kind != PROTOSEG_ACT_LOG && act_kind != PROTOSEG_ACT_LINEAR)
+    return fail(PROTOSEG_ERR_INVALID, "adam_prep: act_kind LOG or LINEAR");
+  if (!(beta1 >= 0.f && beta1 < 1.f && beta2 >= 0.f && beta2 < 1.f && adam_eps >= 0.f))
+    return fail(PROTOSEG_ERR_INVALID, "betas in [0, 1), eps >= 0");
+  if (!operands || operands_bytes < train_operands_bytes(C, P, K, TrainOperands::kFused))
+    return fail(PROTOSEG_ERR_INVALID, "operands %zu B < %zu B (protoseg_l2_train_operands_bytes)", operands_bytes,
+                train_operands_bytes(C, P, K, TrainOperands::kFused));
+  AdamPrepArgs a{};
+  a.p = protos, a.gp = g_protos, a.mp = exp_avg_p, a.vp = exp_avg_sq_p, a.stp = state_p;
+  a.w = K > 0 ? w_last : nullptr, a.gw = K > 0 ? g_w : nullptr, a.mw = K > 0 ? exp_avg_w : nullptr;
+  a.vw = K > 0 ? exp_avg_sq_w : nullptr, a.stw = K > 0 ? state_w : nullptr;
+  a.P = P, a.K = K;
+  a.lr_p = lr_p, a.wd_p = weight_decay_p, a.lr_w = lr_w, a.wd_w = weight_decay_w;
+  a.beta1 = beta1, a.beta2 = beta2, a.eps = adam_eps;
+  a.w_scale = act_unit(act_kind), a.wt_scale = act_grad_unit(act_kind, eps);
+  a.block = static_cast<unsigned char*>(operands);
+  return launch_adam_prep_bf16(a, reinterpret_cast<hipStream_t>(stream));
+}
+
 extern "C" int protoseg_l2_x_dtype_supported(int C, int P, int K, int x_dtype) {
   if (!protoseg_l2_supported(C, P, K)) return 0;
   if (x_dtype == PROTOSEG_F32 || x_dtype == PROTOSEG_BF16) return 1;
@@ -773,6 +806,8 @@ namespace {
 int l2_fwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const float* protos, int P, const float* w_last,
                 int K, float eps, int act_kind, int precision, float* dist_out, float* act_out, float* logits_out,
                 void* operands, size_t operands_bytes, protoseg_stream_t stream) {
+  const bool ready = (act_kind & PROTOSEG_OPERANDS_READY) != 0;
+  act_kind &= ~PROTOSEG_OPERANDS_READY;
   const int xsig = split_x_sigmoid(act_kind, B, C, H, W, P, K, precision);
   if (xsig < 0) return -xsig;
   Geometry geo;
@@ -780,6 +815,8 @@ int l2_fwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const fl
   geo.xsig = xsig;
   if (logits_out && (!w_last || K <= 0)) return fail(PROTOSEG_ERR_INVALID, "logits_out needs w_last and K > 0");
   const TrainOperands tk = operands ? train_operands_kind(C, P, K, precision) : TrainOperands::kNone;
+  if (ready && (tk != TrainOperands::kFused || !protoseg_l2_adam_prep_supported(C, P, K, precision)))
+    return fail(PROTOSEG_ERR_INVALID, "PROTOSEG_OPERANDS_READY needs operands of a shape protoseg_l2_adam_prep serves");
   if (tk != TrainOperands::kNone) {
     if (operands_bytes < train_operands_bytes(C, P, K, tk))
       return fail(PROTOSEG_ERR_INVALID, "operands %zu B < %zu B (protoseg_l2_train_operands_bytes)", operands_bytes,
@@ -790,7 +827,8 @@ int l2_fwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const fl
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const float* w_ops = K > 0 ? w_last : nullptr;  // the backward's W images (g_logits) from the real weights
   if (tk == TrainOperands::kFused) {  // the forward runs on the backward's full image block
-    if (int st = launch_prep_bf16(geo, 2, protos, w_ops, act_kind, eps, operands, s)) return st;
+    if (!ready)
+      if (int st = launch_prep_bf16(geo, 2, protos, w_ops, act_kind, eps, operands, s)) return st;
     if (!dist_out && !act_out && !logits_out) return PROTOSEG_OK;
     if (bf16_fwd_fits(geo, 2))
       return launch_fwd_bf16(geo, x_dtype == PROTOSEG_BF16, 2, x, operands, eps, act_kind, dist_out, act_out,

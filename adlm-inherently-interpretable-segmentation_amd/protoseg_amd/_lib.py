@@ -27,6 +27,7 @@ F32, BF16, I64, I32, U8, F16 = 0, 1, 2, 3, 4, 5
 # enum protoseg_act
 ACT_LOG, ACT_LINEAR, ACT_IDENTITY = 0, 1, 2
 X_SIGMOID = 0x100  # OR-ed into the layer's act_kind: sigmoid of the pre-activation on load
+OPERANDS_READY = 0x200  # OR-ed into protoseg_l2_fwd_ex's act_kind: operands hold these parameters' images
 # enum protoseg_precision
 PREC_BF16X3, PREC_BF16X6, PREC_F32 = 0, 1, 2
 PRECISIONS = {"bf16x3": PREC_BF16X3, "bf16x6": PREC_BF16X6, "f32": PREC_F32}
@@ -47,6 +48,9 @@ SIGNATURES = {
     "protoseg_l2_bwd_saved": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _vp, _sz, _vp]),
     "protoseg_adam_step": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _f, _f, _f, _vp]),
+    "protoseg_l2_adam_prep_supported": (_i, [_i, _i, _i, _i]),
+    "protoseg_l2_adam_prep": (_i, [_i, _i, _i, _f, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _f,
+                                   _f, _f, _f, _f, _vp, _sz, _vp]),
     "protoseg_l2_max_protos": (_i, [_i, _i]),
     "protoseg_l2_x_sigmoid_supported": (_i, [_i, _i, _i, _i, _i, _i, _i]),
     "protoseg_l2_fwd": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _i, _vp, _vp, _vp, _vp]),

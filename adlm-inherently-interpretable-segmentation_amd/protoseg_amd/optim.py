@@ -77,6 +77,56 @@ class Adam(torch.optim.Optimizer):
                               _lib.stream_of(chunk[0].device))
         return loss
 
+    def _group_of(self, p: torch.Tensor):
+        for group in self.param_groups:
+            if any(q is p for q in group["params"]):
+                return group
+        raise _lib.ProtosegError("protoseg Adam: tensor is not one of this optimizer's parameters")
+
+    def _ensure_state(self, p: torch.Tensor):
+        st = self.state[p]
+        if "exp_avg" not in st:
+            st["exp_avg"] = torch.zeros_like(p)
+            st["exp_avg_sq"] = torch.zeros_like(p)
+            st.setdefault("step", torch.tensor(0.0))
+        return st
+
+    @torch.no_grad()
+    def layer_step_with_operands(self, protos: torch.Tensor, w_last: torch.Tensor, operands: torch.Tensor,
+                                 eps: float, act_kind: int, precision: int) -> bool:
+        """step() for the prototype layer's two parameters fused with the next forward's operand
+        prep (protoseg_l2_adam_prep): the same updates, plus the images of the updated values in
+        ``operands``, so that forward passes ``_lib.OPERANDS_READY`` and launches no prep. Each
+        tensor uses its own group's lr / weight_decay (betas and eps must agree). Returns False,
+        having run nothing, where the fused entry does not serve the shape or the groups differ in
+        betas / eps; the caller then runs step() and a plain forward."""
+        if protos.grad is None or w_last.grad is None:
+            return False
+        P, C = protos.shape[0], protos[0].numel()
+        K = w_last.shape[0]
+        gp, gw = self._group_of(protos), self._group_of(w_last)
+        if gp["betas"] != gw["betas"] or gp["eps"] != gw["eps"]:
+            return False
+        lib = _lib.load()
+        if not lib.protoseg_l2_adam_prep_supported(C, P, K, precision):
+            return False
+        for p in (protos, w_last):
+            _lib.require_device(p, p.grad)
+            if p.dtype != torch.float32 or p.grad.dtype != torch.float32 or not p.is_contiguous() \
+                    or not p.grad.is_contiguous():
+                raise _lib.ProtosegError("protoseg Adam: contiguous float32 parameters and gradients only")
+        sp, sw = self._ensure_state(protos), self._ensure_state(w_last)
+        b1, b2 = gp["betas"]
+        with torch.cuda.device(protos.device):
+            _lib.call("protoseg_l2_adam_prep", C, P, K, float(eps), int(act_kind), int(precision),
+                      _lib.ptr(protos), _lib.ptr(protos.grad), _lib.ptr(sp["exp_avg"]), _lib.ptr(sp["exp_avg_sq"]),
+                      _lib.ptr(self._counter(protos)), float(gp["lr"]), float(gp["weight_decay"]),
+                      _lib.ptr(w_last), _lib.ptr(w_last.grad), _lib.ptr(sw["exp_avg"]), _lib.ptr(sw["exp_avg_sq"]),
+                      _lib.ptr(self._counter(w_last)), float(gw["lr"]), float(gw["weight_decay"]),
+                      float(b1), float(b2), float(gp["eps"]), _lib.ptr(operands), operands.numel(),
+                      _lib.stream_of(protos.device))
+        return True
+
     def state_dict(self):
         """torch's layout: state[p] = {'step': float scalar, 'exp_avg', 'exp_avg_sq'} (the step
         copied from the device counter; this synchronises with it)."""

@@ -110,6 +110,12 @@ class LayerStep:
             nops = 0
         self.ops_bytes = nops
         self.ops = torch.empty(max(nops, 1), device=device, dtype=torch.uint8)
+        # the optimizer step writes the next forward's operand images (protoseg_l2_adam_prep), so
+        # the step is forward, backward (+ slab reduce) and update, with no prep launch
+        # (PROTOSEG_FOLD_PREP=0: Adam and the forward's prep launch separately, for A/B)
+        self.fold = (nops > 0 and os.environ.get("PROTOSEG_FOLD_PREP", "1") != "0"
+                     and bool(lib.protoseg_l2_adam_prep_supported(C, P, K, self.prec)))
+        self.ops_ready = False  # the operand block holds the current parameters' images
 
     def _stream(self):
         return _lib.stream_of(self.device)
@@ -118,8 +124,9 @@ class LayerStep:
         return (_lib.ptr(self.ops) if self.ops_bytes else ctypes.c_void_p(None)), self.ops_bytes
 
     def fwd(self):
+        act = _lib.ACT_LOG | (_lib.OPERANDS_READY if self.ops_ready else 0)
         _lib.call("protoseg_l2_fwd_ex", _lib.ptr(self.x), self.xdt, self.B, self.C, self.h, self.w,
-                  _lib.ptr(self.protos), self.P, _lib.ptr(self.w_last), self.K, 1e-4, _lib.ACT_LOG, self.prec,
+                  _lib.ptr(self.protos), self.P, _lib.ptr(self.w_last), self.K, 1e-4, act, self.prec,
                   _lib.ptr(self.dist), ctypes.c_void_p(None), _lib.ptr(self.logits), *self._ops(), self._stream())
 
     def bwd_x(self):
@@ -202,7 +209,12 @@ class LayerStep:
                   _lib.ptr(self.g_w), _lib.ptr(self.ws), self.ws_bytes, *self._ops(), self._stream())
 
     def opt_step(self):
+        if self.fold and self.opt.layer_step_with_operands(self.params[0], self.params[1], self.ops, 1e-4,
+                                                           _lib.ACT_LOG, self.prec):
+            self.ops_ready = True
+            return
         self.opt.step()
+        self.ops_ready = False
 
     def exchange(self, world):
         """Data-parallel gradient exchange: the training step's GradientBuckets (bucketed RCCL

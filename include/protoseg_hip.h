@@ -57,6 +57,12 @@ enum protoseg_act { PROTOSEG_ACT_LOG = 0, PROTOSEG_ACT_LINEAR = 1, PROTOSEG_ACT_
  * (g_x * s (1 - s)). Served where protoseg_l2_x_sigmoid_supported() says so (BF16X3, C = 64),
  * PROTOSEG_ERR_UNSUPPORTED elsewhere. A backward with this flag always needs the workspace. */
 enum { PROTOSEG_X_SIGMOID = 0x100 };
+/* Flag OR-ed into protoseg_l2_fwd_ex's act_kind: `operands` already holds the images of these
+ * protos / w_last (protoseg_l2_adam_prep wrote them with the step that produced the values, or an
+ * earlier _ex forward on unchanged values), so the forward launches no prep. Needs a non-NULL
+ * `operands` that protoseg_l2_train_operands_bytes sizes for the shape and protoseg_l2_adam_prep_supported;
+ * PROTOSEG_ERR_INVALID otherwise. */
+enum { PROTOSEG_OPERANDS_READY = 0x200 };
 
 /* Arithmetic of the x.p / W.act / gradient products (always f32 accumulation):
  *  BF16X3  operands split in 2 bf16 terms, 3 bf16 MFMAs per product (|rel err| ~ 1e-5 on d)
@@ -527,6 +533,27 @@ int protoseg_adam_step(int n_tensors, float* const* params, const float* const* 
                        float* const* exp_avg, float* const* exp_avg_sq, const int64_t* numel,
                        int32_t* const* state, float lr, float beta1, float beta2, float eps, float weight_decay,
                        protoseg_stream_t stream);
+
+/*
+ * The layer's optimizer step fused with the next forward's operand prep: protoseg_adam_step of
+ * the prototype vectors [P, C] and the last layer [K, P] (each with its group's lr and
+ * weight_decay, shared betas / eps; the same arithmetic, the same bits), then the operand images
+ * protoseg_l2_fwd_ex would build from the updated values, written into `operands` (the same
+ * bits), in ONE launch. The step's next protoseg_l2_fwd_ex then passes PROTOSEG_OPERANDS_READY
+ * and launches no prep: the training step runs forward, backward (+ its slab reduce) and this
+ * call. eps / act_kind / precision are the forward's. Served where
+ * protoseg_l2_adam_prep_supported (BF16X3, C = 64, K <= 32, the shapes whose backward reads the
+ * one-chunk image block); PROTOSEG_ERR_UNSUPPORTED elsewhere (nothing launched: run
+ * protoseg_adam_step and a plain _ex forward). w_last and its state NULL iff K = 0.
+ */
+int protoseg_l2_adam_prep_supported(int C, int P, int K, int precision);
+int protoseg_l2_adam_prep(int C, int P, int K, float eps, int act_kind, int precision,
+                          float* protos, const float* g_protos, float* exp_avg_p, float* exp_avg_sq_p,
+                          int32_t* state_p, float lr_p, float weight_decay_p,
+                          float* w_last, const float* g_w, float* exp_avg_w, float* exp_avg_sq_w,
+                          int32_t* state_w, float lr_w, float weight_decay_w,
+                          float beta1, float beta2, float adam_eps,
+                          void* operands, size_t operands_bytes, protoseg_stream_t stream);
 
 #ifdef __cplusplus
 }

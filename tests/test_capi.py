@@ -94,6 +94,22 @@ def test_argument_validation_returns_status_without_gpu():
     assert st == _lib.ERR_UNSUPPORTED and b"X_SIGMOID" in lib.protoseg_last_error()
     st = lib.protoseg_adam_step(0, null, null, null, null, null, null, 1e-3, 0.9, 0.999, 1e-8, 0.0, null)
     assert st == _lib.ERR_INVALID
+    # the fused update + prep: the bf16x3 one-chunk shapes only, refused before any launch
+    bf3 = _lib.PRECISIONS["bf16x3"]
+    assert lib.protoseg_l2_adam_prep_supported(64, 361, 19, bf3) == 1
+    assert lib.protoseg_l2_adam_prep_supported(64, 190, 19, bf3) == 1
+    assert lib.protoseg_l2_adam_prep_supported(64, 570, 19, bf3) == 0  # prototype chunks
+    assert lib.protoseg_l2_adam_prep_supported(128, 361, 19, bf3) == 0
+    assert lib.protoseg_l2_adam_prep_supported(64, 361, 19, _lib.PREC_F32) == 0
+    assert lib.protoseg_l2_adam_prep_supported(64, 361, 200, bf3) == 0
+    args = [dummy] * 5 + [1e-3, 0.0] + [dummy] * 5 + [1e-3, 0.0, 0.9, 0.999, 1e-8, dummy, 1 << 20, null]
+    st = lib.protoseg_l2_adam_prep(64, 570, 19, 1e-4, 0, bf3, *args)
+    assert st == _lib.ERR_UNSUPPORTED and b"adam_prep" in lib.protoseg_last_error()
+    st = lib.protoseg_l2_adam_prep(64, 361, 19, 1e-4, 0, bf3, *args[:-3], null, 0, null)
+    assert st == _lib.ERR_INVALID and b"operands" in lib.protoseg_last_error()
+    st = lib.protoseg_l2_fwd_ex(dummy, 0, 1, 64, 2, 2, dummy, 570, dummy, 19, 1e-4, _lib.OPERANDS_READY, bf3,
+                                dummy, null, null, null, 0, null)
+    assert st == _lib.ERR_INVALID and b"OPERANDS_READY" in lib.protoseg_last_error()
     st = lib.protoseg_patch_class_mask(null, 2, 1, 4, 4, 2, 2, null, 0, null, null)
     assert st == _lib.ERR_INVALID
     st = lib.protoseg_push_argmin(dummy, 1, 8192, 2, 2, dummy, 3, dummy, dummy, dummy, null, null)

@@ -126,3 +126,74 @@ def test_autograd_layer_uses_forward_operands(device, P):
     torch.cuda.synchronize()
     assert torch.equal(xr.grad, ref2[0]) and torch.equal(pr.grad.reshape(P, 64), ref2[1])
     assert torch.equal(wr.grad, ref2[2])
+
+
+def _fwd_operands(_lib, x, protos, w_last, act, prec, buf, ready=False):
+    B, C, H, W = x.shape
+    P, K = protos.shape[0], w_last.shape[0]
+    d = torch.empty(B, P, H, W, device=x.device)
+    lg = torch.empty(B, H, W, K, device=x.device)
+    _lib.call("protoseg_l2_fwd_ex", _lib.ptr(x), _lib.F32, B, C, H, W, _lib.ptr(protos), P, _lib.ptr(w_last), K,
+              1e-4, act | (_lib.OPERANDS_READY if ready else 0), prec, _lib.ptr(d), None, _lib.ptr(lg),
+              _lib.ptr(buf), buf.numel(), _lib.stream_of(x.device))
+    return d, lg
+
+
+@pytest.mark.parametrize("P,K", [(361, 19), (190, 19), (100, 7), (96, 32)])
+@pytest.mark.parametrize("activation", ["log", "linear"])
+def test_adam_prep_equals_adam_then_prep(device, P, K, activation):
+    """protoseg_l2_adam_prep (Adam.layer_step_with_operands) = protoseg_adam_step of both tensors
+    (per-group lr / weight decay) followed by the forward's prep of the updated values, bit for
+    bit: parameters, moments, step counts and every byte of the operand block; a forward with
+    PROTOSEG_OPERANDS_READY on that block equals the forward that builds its own."""
+    _lib, ops = _ops()
+    from protoseg_amd.optim import Adam
+    prec, act = ops.PRECISIONS["bf16x3"], ops.ACT_KINDS[activation]
+    assert _lib.load().protoseg_l2_adam_prep_supported(64, P, K, prec)
+    x, protos, w_last, _, _ = _inputs(device, 2, 13, 11, P, K, seed=3 * P + K)
+    gen = torch.Generator().manual_seed(P + 17 * K)
+    rnd = lambda *s: torch.randn(*s, generator=gen).to(device)  # noqa: E731
+    g_p, g_w = 1e-2 * rnd(P, 64), 1e-2 * rnd(K, P)
+    m0 = (1e-3 * rnd(P, 64), 1e-3 * rnd(K, P))
+    v0 = (1e-5 * rnd(P, 64).abs(), 1e-5 * rnd(K, P).abs())
+    nbytes = ops.train_operands_bytes(64, P, K, prec)
+    runs = []
+    for fused in (False, True):
+        p = torch.nn.Parameter(protos.contiguous().clone())
+        w = torch.nn.Parameter(w_last.contiguous().clone())  # (the identity init is a transpose)
+        p.grad, w.grad = g_p.clone(), g_w.clone()
+        opt = Adam([{"params": [p], "lr": 2.5e-3, "weight_decay": 0.0},
+                    {"params": [w], "lr": 1e-3, "weight_decay": 5e-4}])
+        for t, m, v in ((p, m0[0], v0[0]), (w, m0[1], v0[1])):
+            opt.state[t] = {"exp_avg": m.clone(), "exp_avg_sq": v.clone(), "step": torch.tensor(4.0)}
+        buf = torch.full((nbytes,), 0xAB, device=device, dtype=torch.uint8)
+        for _ in range(2):  # two steps: the device step counts advance once per call
+            if fused:
+                assert opt.layer_step_with_operands(p, w, buf, 1e-4, act, prec)
+            else:
+                opt.step()
+                _fwd_operands(_lib, x, p.detach(), w.detach(), act, prec, buf)
+        torch.cuda.synchronize()
+        runs.append((p.detach(), w.detach(), opt.state[p]["exp_avg"], opt.state[p]["exp_avg_sq"],
+                     opt.state[w]["exp_avg"], opt.state[w]["exp_avg_sq"], opt._counter(p), opt._counter(w), buf))
+    names = ("protos", "w_last", "m_p", "v_p", "m_w", "v_w", "step_p", "step_w", "operands")
+    for name, a, b in zip(names, *runs):
+        assert torch.equal(a, b), name
+    assert int(runs[1][6][0]) == 6 and int(runs[1][7][0]) == 6
+    p, w, buf = runs[1][0], runs[1][1], runs[1][8]
+    ref = _fwd_operands(_lib, x, p, w, act, prec, torch.empty(nbytes, device=device, dtype=torch.uint8))
+    got = _fwd_operands(_lib, x, p, w, act, prec, buf, ready=True)
+    torch.cuda.synchronize()
+    assert torch.equal(ref[0], got[0]) and torch.equal(ref[1], got[1])
+
+
+def test_operands_ready_refused_without_a_served_block(device):
+    _lib, ops = _ops()
+    prec = ops.PRECISIONS["bf16x3"]
+    x, protos, w_last, _, _ = _inputs(device, 1, 9, 9, 570, 19, seed=2)  # two chunks: no block
+    assert not _lib.load().protoseg_l2_adam_prep_supported(64, 570, 19, prec)
+    d = torch.empty(1, 570, 9, 9, device=device)
+    with pytest.raises(_lib.ProtosegError, match="OPERANDS_READY"):
+        _lib.call("protoseg_l2_fwd_ex", _lib.ptr(x), _lib.F32, 1, 64, 9, 9, _lib.ptr(protos), 570, _lib.ptr(w_last),
+                  19, 1e-4, _lib.ACT_LOG | _lib.OPERANDS_READY, prec, _lib.ptr(d), None, None, None, 0,
+                  _lib.stream_of(device))
