@@ -464,7 +464,8 @@ __global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
   // The first tile's x loads are issued before the operand-image DMA, so the barrier's wait
   // covers both round trips at once instead of one after the other.
   constexpr bool kPrefetch = kWavesF <= 8;
-  int t = blockIdx.x * kWavesF + wave;
+  const int vb = xcd_block();
+  int t = vb * kWavesF + wave;
   float raw[kNQ * 8];
   if constexpr (kPrefetch)
     load_x_raw<TX>(rx, x_lane_off<TX>(t < sched.full_end ? t : ntiles, ntiles, npix, HW), cs, raw);
@@ -608,15 +609,15 @@ __global__ __launch_bounds__(kWavesF * 64) void l2_fwd_bf16_kernel(
     } else {
       load_x_raw<TX>(rx, x_lane_off<TX>(t, ntiles, npix, HW), cs, cur);
     }
-    if (t == static_cast<int>(blockIdx.x) * kWavesF + wave) STAMP(2);
+    if (t == vb * kWavesF + wave) STAMP(2);
     const f32x16 lacc = run_tile(t, cur, 0, 1);
     if constexpr (LOGITS) store_logits(t, lacc);
-    if (t == static_cast<int>(blockIdx.x) * kWavesF + wave) STAMP(3);
+    if (t == vb * kWavesF + wave) STAMP(3);
   }
   STAMP(4);
 
   // ---- remainder: one tile per workgroup, prototype tiles split over the waves
-  for (int tt = sched.full_end + static_cast<int>(blockIdx.x); tt < ntiles; tt += gridDim.x) {
+  for (int tt = sched.full_end + vb; tt < ntiles; tt += gridDim.x) {
     float rt[kNQ * 8];
     load_x_raw<TX>(rx, x_lane_off<TX>(tt, ntiles, npix, HW), cs, rt);
     const f32x16 lacc = run_tile(tt, rt, wave, kWavesF);

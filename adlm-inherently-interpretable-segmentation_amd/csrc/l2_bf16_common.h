@@ -42,6 +42,22 @@ __device__ __forceinline__ void load_rows16(const float* rows, float (&v)[16]) {
   }
 }
 
+// XCD-aware workgroup index. The dispatcher deals workgroups round-robin over the 8 XCDs
+// (workgroup i on XCD i % 8), each with its own L2. Workgroup i runs as virtual workgroup
+// (i % 8) * (G / 8) + i / 8, so the workgroups of one XCD take neighbouring pixel tiles. A 32-pixel
+// tile's NCHW rows start at any 4-B offset (65 x 65 maps), so the line two neighbouring tiles
+// share is then written (and read) through one L2 instead of two (store probe: 48.2 -> 42.9 us
+// for the forward's distance pattern, tools/probe/store_bw.hip). A grid that is not a multiple
+// of 8 keeps the plain order (a bijection either way: only the placement changes).
+#ifndef XCD_MAP
+#define XCD_MAP 1
+#endif
+__device__ __forceinline__ int xcd_block() {
+  const int G = static_cast<int>(gridDim.x), b = static_cast<int>(blockIdx.x);
+  if (!XCD_MAP || (G & 7)) return b;
+  return (b & 7) * (G >> 3) + (b >> 3);
+}
+
 // Wave index as a provably wave-uniform value (SGPR): threadIdx.x / 64 is uniform but the
 // compiler cannot prove it, and a "divergent" LDS-DMA base or buffer soffset derived from it
 // makes hipcc wrap every such memory op in a waterfall loop (cdna_hip_programming.md T20).

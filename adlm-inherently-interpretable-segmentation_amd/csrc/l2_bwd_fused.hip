@@ -147,7 +147,8 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = wave_id();
   const int ntiles = (npix + 31) / 32;
   const int npt = NPT ? NPT : Pp / 32;
-  const int iters = (ntiles - static_cast<int>(blockIdx.x) + static_cast<int>(gridDim.x) - 1) / static_cast<int>(gridDim.x);
+  const int vb = xcd_block();  // neighbouring tiles on one XCD (l2_bf16_common.h); slab vb as well
+  const int iters = (ntiles - vb + static_cast<int>(gridDim.x) - 1) / static_cast<int>(gridDim.x);
   const bool owner = wave < kOwners;
   const int xw = wave - kOwners;  // x wave index (channel tile), valid when !owner
   const unsigned sz = sizeof(TX);
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
   // GD = 2: g_dist points at the compact values (gd_bytes = npix * mpc * 4)
   const rsrc_t rgd = make_rsrc(GD == 2 ? cg.val : g_dist, gd_bytes), rgx = make_rsrc(g_x, g_x ? x_bytes : 0u);
   const rsrc_t rpc = make_rsrc(cg.pix, GD == 2 ? static_cast<unsigned>(npix) * 4u : 0u);
-  auto tile_of = [&](int i) __attribute__((always_inline)) { return static_cast<int>(blockIdx.x) + i * static_cast<int>(gridDim.x); };
+  auto tile_of = [&](int i) __attribute__((always_inline)) { return vb + i * static_cast<int>(gridDim.x); };
   auto xa_slot = [&](int sb) __attribute__((always_inline)) { return reinterpret_cast<bf16*>(smem_raw + L.xa) + sb * kT * 32 * kC; };
   auto ga_slot = [&](int sb) __attribute__((always_inline)) { return reinterpret_cast<bf16*>(smem_raw + L.ga) + sb * kT * 32 * 32; };
   auto x2_slot = [&](int sb) __attribute__((always_inline)) { return reinterpret_cast<float*>(smem_raw + L.x2s) + sb * 32; };
@@ -594,7 +595,7 @@ __global__ __launch_bounds__(kThreads) void l2_bwd_fused_bf16_kernel(
   // ---- slab: this workgroup's g_P (x -2: XA holds +x), g_W, sum_n g_s -------------------------
   if (owner && wave < npt) {
     const int E = Pp * kC + 32 * Pp + Pp;
-    float* my_slab = slab + static_cast<size_t>(blockIdx.x) * E;
+    float* my_slab = slab + static_cast<size_t>(vb) * E;
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct)
 #pragma unroll

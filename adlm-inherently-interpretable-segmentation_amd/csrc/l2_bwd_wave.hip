@@ -163,7 +163,9 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
   unsigned long long st_acc[16] = {}, st_last = __builtin_amdgcn_s_memtime();
 #endif
   const int G = static_cast<int>(gridDim.x);
-  const int iters = (ntiles - static_cast<int>(blockIdx.x) + G - 1) / G;
+  const int vb = xcd_block();  // neighbouring tiles on one XCD (l2_bf16_common.h); slab vb as well,
+                               // so the reduce's fixed slab order sums the same tiles as before
+  const int iters = (ntiles - vb + G - 1) / G;
   const unsigned sz = sizeof(TX);
   const unsigned chs = static_cast<unsigned>(HW) * sz;  // one channel plane
   const rsrc_t rx = make_rsrc(x, x_bytes), rg = make_rsrc(g_logits, gl_bytes);
@@ -171,7 +173,7 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
   const rsrc_t rgd = make_rsrc(GD == 2 ? cg.val : g_dist, gd_bytes), rgx = make_rsrc(g_x, g_x ? x_bytes : 0u);
   const rsrc_t rimg = make_rsrc(img, static_cast<unsigned>(io.total));
   const rsrc_t rpc = make_rsrc(cg.pix, GD == 2 ? static_cast<unsigned>(npix) * 4u : 0u);
-  auto tile_of = [&](int i) __attribute__((always_inline)) { return static_cast<int>(blockIdx.x) + i * G; };
+  auto tile_of = [&](int i) __attribute__((always_inline)) { return vb + i * G; };
   const unsigned TWw = S0 + L.tw + wave * L.tw_bytes;  // this wave's g_s image / g_x partial
 
   // ---- prologue: the (-2P) image -> LDS (for the launch; term t of the block's Pi rows at term t
@@ -725,7 +727,7 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
   // unused (every store: 32 consecutive prototypes per half-wave; rows past P and classes past K
   // are not written)
   const int E = P * kC + K * P + P;
-  float* my_slab = slab + static_cast<size_t>(blockIdx.x) * E;
+  float* my_slab = slab + static_cast<size_t>(vb) * E;
 #ifdef WAVE_ABL_NOSLAB
   if (npix != -7) return;
 #endif

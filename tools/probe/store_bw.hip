@@ -15,14 +15,18 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 constexpr unsigned kOOB = 0x80000000u;
 __device__ __forceinline__ int row_of(int r) { return (r & 3) + 8 * (r >> 2); }
 
-template <int POL>
+// XCD: workgroup i runs as virtual workgroup (i % 8) * (G / 8) + i / 8, so the workgroups one XCD
+// holds (dispatch is round-robin over the 8 XCDs) take one contiguous range of tiles per round
+template <int POL, int XCD = 0>
 __global__ __launch_bounds__(512) void dstore(const float* x, unsigned xb, float* d, unsigned db, int HW, int npix, int P,
                                               int npt, float v0) {
   const rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), (short)0, (int)xb, 0x00020000);
   const rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(d, (short)0, (int)db, 0x00020000);
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
   const int ntiles = (npix + 31) / 32;
-  for (int t = blockIdx.x * 8 + wave; t < ntiles; t += gridDim.x * 8) {
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int vb = XCD ? (bid & 7) * (G >> 3) + (bid >> 3) : bid;
+  for (int t = vb * 8 + wave; t < ntiles; t += gridDim.x * 8) {
     const int g = t * 32 + j;
     const bool valid = g < npix;
     const int b = valid ? g / HW : 0, n = valid ? g - b * HW : 0;
@@ -98,7 +102,7 @@ int main(int argc, char** argv) {
   hipEventCreate(&b);
   const int grids[] = {256, 512, 1024};
   for (int gi = 0; gi < 3; ++gi) {
-    for (int v = 0; v < 4; ++v) {
+    for (int v = 0; v < 5; ++v) {
       float best = 1e9f;
       for (int rep = 0; rep < 20; ++rep) {
         hipEventRecord(a);
@@ -108,6 +112,9 @@ int main(int argc, char** argv) {
         else if (v == 1)
           hipLaunchKernelGGL(dstore<2>, dim3(grids[gi]), dim3(512), 0, 0, x, (unsigned)(xn * 4), d, (unsigned)(dn * 4), HW,
                              npix, P, npt, 1.f);
+        else if (v == 4)
+          hipLaunchKernelGGL((dstore<0, 1>), dim3(grids[gi]), dim3(512), 0, 0, x, (unsigned)(xn * 4), d, (unsigned)(dn * 4),
+                             HW, npix, P, npt, 1.f);
         else if (v == 3)
           hipLaunchKernelGGL(dstore4, dim3(grids[gi]), dim3(512), 0, 0, x, (unsigned)(xn * 4), d, (unsigned)(dn * 4), HW,
                              npix, P, npt, 1.f);
