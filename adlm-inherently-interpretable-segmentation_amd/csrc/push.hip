@@ -329,6 +329,53 @@ __host__ __device__ inline size_t pw_lds_bytes(int C, int nptc) {
   return (protos > merge ? protos : merge) + static_cast<size_t>(kPwWaves) * 64 * 4;
 }
 
+// Launch plan of the wave-streamed kernel: the prototype tiles go in chunks of `per` (one
+// launch's blockIdx.z; a remainder chunk is a second launch), each (image, chunk) over `wgs`
+// workgroups of kPwWaves waves, one workgroup per CU resident (176 / 208 VGPRs: 2 waves per
+// SIMD). A wave's work is ceil(ntile / (wgs waves)) pixel tiles x per prototype tiles, plus about
+// one tile-pass of prologue (its rows into LDS, ||p||^2, the final merge), times the generations
+// the launch needs. The plan minimises that over the launches with at most kPwMaxChunks chunks
+// (each chunk reads x again); ties go to wider chunks. One Cityscapes image (1036 tiles, P = 190)
+// thus runs 3 chunks of 2 tiles on 255 workgroups instead of 1 chunk of 6 on 130, which left
+// half the CUs idle.
+#ifndef PUSH_CHUNK_PLAN
+#define PUSH_CHUNK_PLAN 1
+#endif
+constexpr int kPwMaxChunks = 3;
+struct PushPlan {
+  int per;
+  long long wgs;
+};
+inline PushPlan push_wave_plan(int npt, int maxt, int n_img, long long ntile, int cus) {
+  const long long wmax = (ntile + kPwWaves - 1) / kPwWaves;
+  auto fit_w = [&](int chunks) {  // workgroups per (image, chunk) for one generation
+    long long w = cus / (static_cast<long long>(n_img) * chunks);
+    return w < 1 ? 1 : w > wmax ? wmax : w;
+  };
+  auto cost = [&](int chunks, int per, long long w) {
+    const long long rounds = (ntile + w * kPwWaves - 1) / (w * kPwWaves);
+    const long long gens = (static_cast<long long>(n_img) * chunks * w + cus - 1) / cus;
+    return gens * (rounds * per + 1);
+  };
+  PushPlan best{npt < maxt ? npt : maxt, 1};
+  long long best_cost = -1;
+  for (int per = maxt < npt ? maxt : npt; per >= 1; --per) {
+    const int full = npt / per, rem = npt - full * per;
+    if (per < npt && full + (rem ? 1 : 0) > kPwMaxChunks) continue;
+    long long w = fit_w(full);
+    if (rem) {
+      const long long wr = fit_w(1);
+      w = wr < w ? wr : w;  // one wgs for both launches (the partials' layout)
+    }
+    const long long c = cost(full, per, w) + (rem ? cost(1, rem, w) : 0);
+    if (best_cost < 0 || c < best_cost) {
+      best_cost = c;
+      best = {per, w};
+    }
+  }
+  return best;
+}
+
 template <int NC>
 __global__ __launch_bounds__(kPwWaves * 64) void push_argmin_wave_kernel(
     const float* __restrict__ x, int HW, const float* __restrict__ protos, int P, int pt0, int nptc,
@@ -805,12 +852,21 @@ int push_argmin_impl(const float* x, int n_img, int C, int h, int w, const float
     // wave-streamed kernel: prototype chunks of <= pw_max_tiles tiles, about one workgroup per
     // CU over the images (every wave at least one pixel tile)
     const int maxt = pw_max_tiles(nc);
-    const int per = static_cast<int>(ceil_div(npt, ceil_div(npt, maxt)));
-    const int full = npt / per, rem = npt - full * per;
     const long long ntile = ceil_div(HW, 32);
+    int per = static_cast<int>(ceil_div(npt, ceil_div(npt, maxt)));
     long long wgs = ceil_div(256, static_cast<long long>(n_img));
     if (wgs > ceil_div(ntile, kPwWaves)) wgs = ceil_div(ntile, kPwWaves);
     if (wgs < 1) wgs = 1;
+#if PUSH_CHUNK_PLAN
+    {  // the chunk width and workgroups per (image, chunk) that minimise the busiest wave's work
+      int cus = 256, dev = 0;
+      if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      const PushPlan pl = push_wave_plan(npt, maxt, n_img, ntile, cus);
+      per = pl.per;
+      wgs = pl.wgs;
+    }
+#endif
+    const int full = npt / per, rem = npt - full * per;
     const size_t need = static_cast<size_t>(n_img) * wgs * P * 2 * sizeof(unsigned long long);
     int st = PROTOSEG_OK;
     auto* part = static_cast<unsigned long long*>(push_scratch(need, s, &st));
