@@ -29,8 +29,11 @@ __device__ inline AdamCorr adam_corr(const int* state, float lr, float beta1, fl
 
 //   g = grad + wd p;  m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g g
 //   p -= step_size m / (sqrt(v) / sqrt(1 - b2^t) + eps)
+// No contraction: the compiler's choice of fused multiply-adds would otherwise depend on the
+// calling kernel, and the two kernels must give the same bits (the weight-decay fma is explicit).
 __device__ __forceinline__ void adam_update(float& p, float& m, float& v, float grad, float step_size, float bc2_sqrt,
                                             float beta1, float beta2, float eps, float wd) {
+#pragma clang fp contract(off)
   float gr = grad;
   if (wd != 0.f) gr = fmaf(wd, p, gr);
   m = beta1 * m + (1.f - beta1) * gr;

@@ -220,7 +220,11 @@ __global__ __launch_bounds__(256) void l2_prep_bf16_kernel(const float* __restri
 // them with the stage_* functions' element order, scaling and zeroing (the same bits). The step
 // counts advance once per launch (the last workgroup's ticket, as adam_kernel).
 constexpr int kApPitch = kC + 1;  // LDS rows of the tile's prototypes (conflict-free column reads)
-__global__ __launch_bounds__(256) void l2_adam_prep_kernel(AdamPrepArgs a) {
+// 1024 threads: 2 prototype elements and 1 last-layer element per thread, then one image item
+// each (the tile's 768 of them) — 12 workgroups at P = 361 carry the whole step, so the work per
+// wave is kept short
+constexpr int kApThreads = 1024;
+__global__ __launch_bounds__(kApThreads) void l2_adam_prep_kernel(AdamPrepArgs a) {
   __shared__ float sp[32 * kApPitch];
   __shared__ float sw[32 * 33];
   __shared__ float corr[4];
@@ -228,10 +232,11 @@ __global__ __launch_bounds__(256) void l2_adam_prep_kernel(AdamPrepArgs a) {
   const int pt = blockIdx.x, tid = threadIdx.x, P = a.P, K = a.K;
   const int Pp = (P + 31) & ~31, p0 = pt * 32;
   // this tile's elements: prototypes (row r, channel c) = e, w (class k, column j) = e
-  float gi[8], pi[8], mi[8], vi[8], gwi[4], wi[4], mwi[4], vwi[4];
+  constexpr int kPE = 32 * kC / kApThreads, kWE = 32 * 32 / kApThreads;
+  float gi[kPE], pi[kPE], mi[kPE], vi[kPE], gwi[kWE], wi[kWE], mwi[kWE], vwi[kWE];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int e = tid + 256 * u, r = e >> 6;
+  for (int u = 0; u < kPE; ++u) {
+    const int e = tid + kApThreads * u, r = e >> 6;
     const bool ok = p0 + r < P;
     const size_t i = static_cast<size_t>(p0) * kC + e;
     gi[u] = ok ? a.gp[i] : 0.f;
@@ -240,8 +245,8 @@ __global__ __launch_bounds__(256) void l2_adam_prep_kernel(AdamPrepArgs a) {
     vi[u] = ok ? a.vp[i] : 0.f;
   }
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int e = tid + 256 * u, k = e >> 5, j = e & 31;
+  for (int u = 0; u < kWE; ++u) {
+    const int e = tid + kApThreads * u, k = e >> 5, j = e & 31;
     const bool ok = k < K && p0 + j < P;
     const size_t i = static_cast<size_t>(k) * P + p0 + j;
     gwi[u] = ok ? a.gw[i] : 0.f;
@@ -257,8 +262,8 @@ __global__ __launch_bounds__(256) void l2_adam_prep_kernel(AdamPrepArgs a) {
   }
   __syncthreads();
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int e = tid + 256 * u, r = e >> 6, c = e & 63;
+  for (int u = 0; u < kPE; ++u) {
+    const int e = tid + kApThreads * u, r = e >> 6, c = e & 63;
     if (p0 + r < P) {
       adam_update(pi[u], mi[u], vi[u], gi[u], corr[0], corr[1], a.beta1, a.beta2, a.eps, a.wd_p);
       const size_t i = static_cast<size_t>(p0) * kC + e;
@@ -269,8 +274,8 @@ __global__ __launch_bounds__(256) void l2_adam_prep_kernel(AdamPrepArgs a) {
     sp[r * kApPitch + c] = pi[u];
   }
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int e = tid + 256 * u, k = e >> 5, j = e & 31;
+  for (int u = 0; u < kWE; ++u) {
+    const int e = tid + kApThreads * u, k = e >> 5, j = e & 31;
     if (k < K && p0 + j < P) {
       adam_update(wi[u], mwi[u], vwi[u], gwi[u], corr[2], corr[3], a.beta1, a.beta2, a.eps, a.wd_w);
       const size_t i = static_cast<size_t>(k) * P + p0 + j;
@@ -296,7 +301,7 @@ __global__ __launch_bounds__(256) void l2_adam_prep_kernel(AdamPrepArgs a) {
   bf16* img_pt = reinterpret_cast<bf16*>(a.block + o.pt);
   bf16* img_w = reinterpret_cast<bf16*>(a.block + o.w);
   bf16* img_wt = reinterpret_cast<bf16*>(a.block + o.wt);
-  {  // (-2 P) rows (stage_p_rows): row p0 + (tid >> 3), chunk tid & 7
+  if (tid < 256) {  // (-2 P) rows (stage_p_rows): row p0 + (tid >> 3), chunk tid & 7
     const int r = tid >> 3, e8 = tid & 7, q = e8 >> 1, h = e8 & 1, p = p0 + r;
     float v[8];
 #pragma unroll
@@ -304,9 +309,8 @@ __global__ __launch_bounds__(256) void l2_adam_prep_kernel(AdamPrepArgs a) {
     bf16x8 f[2];
     split8<2>(v, f);
     store_frag<2>(img_p, Pp * kC, img_off<8>(p, e8), f);
-  }
-  {  // (-2 P)^T permuted (stage_pt_perm): channel (tid >> 2), chunk tid & 3
-    const int c = tid >> 2, e8 = tid & 3;
+  } else if (tid < 512) {  // (-2 P)^T permuted (stage_pt_perm): channel (tid - 256) >> 2, chunk tid & 3
+    const int c = (tid - 256) >> 2, e8 = tid & 3;
     float v[8];
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
@@ -316,9 +320,8 @@ __global__ __launch_bounds__(256) void l2_adam_prep_kernel(AdamPrepArgs a) {
     bf16x8 f[2];
     split8<2>(v, f);
     store_frag<2>(img_pt, Pp * kC, img_off<4>(pt * kC + c, e8), f);
-  }
-  if (tid < 128) {  // (act_unit W) permuted (stage_w_perm): class tid >> 2, chunk tid & 3
-    const int k = tid >> 2, e8 = tid & 3;
+  } else if (tid < 640) {  // (act_unit W) permuted (stage_w_perm): class (tid - 512) >> 2, chunk tid & 3
+    const int k = (tid - 512) >> 2, e8 = tid & 3;
     float v[8];
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
@@ -328,8 +331,8 @@ __global__ __launch_bounds__(256) void l2_adam_prep_kernel(AdamPrepArgs a) {
     bf16x8 f[2];
     split8<2>(v, f);
     store_frag<2>(img_w, Pp * 32, img_off<4>(pt * 32 + k, e8), f);
-  } else {  // (grad_unit W)^T rows (stage_wt_rows): row p0 + ((tid - 128) >> 2), chunk tid & 3
-    const int j = (tid - 128) >> 2, e8 = tid & 3, p = p0 + j;
+  } else if (tid < 768) {  // (grad_unit W)^T rows (stage_wt_rows): row p0 + ((tid - 640) >> 2), chunk tid & 3
+    const int j = (tid - 640) >> 2, e8 = tid & 3, p = p0 + j;
     float v[8];
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
@@ -339,20 +342,18 @@ __global__ __launch_bounds__(256) void l2_adam_prep_kernel(AdamPrepArgs a) {
     bf16x8 f[2];
     split8<2>(v, f);
     store_frag<2>(img_wt, Pp * 32, img_off<4>(p, e8), f);
-  }
-  float* p2 = reinterpret_cast<float*>(a.block + o.p2);
-  if (tid < 32) {  // ||p||^2 as proto_norm2_64: sequential, no contraction
+  } else if (tid < 800) {  // ||p||^2 as proto_norm2_64: sequential, no contraction
 #pragma clang fp contract(off)
-    const int p = p0 + tid;
+    const int r = tid - 768, p = p0 + r;
     float s = 0.f;
     for (int c = 0; c < kC; ++c) {
-      const float x = sp[tid * kApPitch + c];
+      const float x = sp[r * kApPitch + c];
       s += x * x;
     }
-    p2[p] = p < P ? s : 0.f;
-  } else if (pt == static_cast<int>(gridDim.x) - 1) {  // the region's padding past Pp
+    reinterpret_cast<float*>(a.block + o.p2)[p] = p < P ? s : 0.f;
+  } else if (pt == static_cast<int>(gridDim.x) - 1) {  // the p2 region's padding past Pp
     const int n1 = (o.pt - o.p2) / 4;
-    for (int p = Pp + tid - 32; p < n1; p += 224) p2[p] = 0.f;
+    for (int p = Pp + tid - 800; p < n1; p += kApThreads - 800) reinterpret_cast<float*>(a.block + o.p2)[p] = 0.f;
   }
 }
 
@@ -1365,7 +1366,7 @@ int launch_adam_prep_bf16(const AdamPrepArgs& a, hipStream_t stream) {
   if (a.P <= 0 || a.K < 0 || a.K > 32 || !a.p || !a.gp || !a.mp || !a.vp || !a.stp || !a.block ||
       (a.K > 0 && (!a.w || !a.gw || !a.mw || !a.vw || !a.stw)))
     return fail(PROTOSEG_ERR_INVALID, "adam_prep: null tensor or K outside 0..32");
-  hipLaunchKernelGGL(l2_adam_prep_kernel, dim3(static_cast<unsigned>(ceil_div(a.P, 32))), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(l2_adam_prep_kernel, dim3(static_cast<unsigned>(ceil_div(a.P, 32))), dim3(kApThreads), 0, stream, a);
   return check_launch("l2_adam_prep_kernel");
 }
 

@@ -348,13 +348,14 @@ struct PushPlan {
 };
 inline PushPlan push_wave_plan(int npt, int maxt, int n_img, long long ntile, int cus) {
   const long long wmax = (ntile + kPwWaves - 1) / kPwWaves;
+  const long long slots = static_cast<long long>(cus) * (kPwWaves < 8 ? 8 / kPwWaves : 1);  // 8 waves per CU
   auto fit_w = [&](int chunks) {  // workgroups per (image, chunk) for one generation
-    long long w = cus / (static_cast<long long>(n_img) * chunks);
+    long long w = slots / (static_cast<long long>(n_img) * chunks);
     return w < 1 ? 1 : w > wmax ? wmax : w;
   };
   auto cost = [&](int chunks, int per, long long w) {
     const long long rounds = (ntile + w * kPwWaves - 1) / (w * kPwWaves);
-    const long long gens = (static_cast<long long>(n_img) * chunks * w + cus - 1) / cus;
+    const long long gens = (static_cast<long long>(n_img) * chunks * w + slots - 1) / slots;
     return gens * (rounds * per + 1);
   };
   PushPlan best{npt < maxt ? npt : maxt, 1};
