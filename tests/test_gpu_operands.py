@@ -197,3 +197,36 @@ def test_operands_ready_refused_without_a_served_block(device):
         _lib.call("protoseg_l2_fwd_ex", _lib.ptr(x), _lib.F32, 1, 64, 9, 9, _lib.ptr(protos), 570, _lib.ptr(w_last),
                   19, 1e-4, _lib.ACT_LOG | _lib.OPERANDS_READY, prec, _lib.ptr(d), None, None, None, 0,
                   _lib.stream_of(device))
+
+
+@pytest.mark.parametrize("B,P", [(2, 361), (3, 190)])
+def test_folded_layer_step_graph_matches_separate_launches(device, monkeypatch, B, P):
+    """bench.py's layer step with the prep folded into the optimizer launch (forward with
+    PROTOSEG_OPERANDS_READY reading the images the previous step's protoseg_l2_adam_prep wrote),
+    eager and then replayed as one HIP graph, gives the parameters and moments of the same step
+    run with Adam and the forward's prep as separate launches, bit for bit, over 6 steps."""
+    import bench
+    steps = {}
+    for fold in ("1", "0"):
+        monkeypatch.setenv("PROTOSEG_FOLD_PREP", fold)
+        s = bench.LayerStep(B, 64, 17, 19, P, 19, torch.float32, device, bench.SEED)
+        assert s.fold == (fold == "1")
+        stream = torch.cuda.Stream(device)
+        with torch.cuda.stream(stream):
+            for _ in range(3):
+                s.fwd(), s.bwd(), s.opt_step()
+            torch.cuda.synchronize()
+            g = bench.capture(lambda s=s: [s.fwd(), s.bwd(), s.opt_step()], stream)
+            for _ in range(3):
+                g.replay()
+            torch.cuda.synchronize()
+        steps[fold] = (s, g)  # the graph points into the step's buffers: keep both alive
+    a, b = steps["1"][0], steps["0"][0]
+    assert a.ops_ready and not b.ops_ready
+    for name, x, y in (("protos", a.protos, b.protos), ("w_last", a.w_last, b.w_last),
+                       ("logits", a.logits, b.logits), ("g_p", a.g_p, b.g_p)):
+        assert torch.equal(x, y), name
+    for pa, pb in zip(a.params, b.params):
+        assert torch.equal(a.opt.state[pa]["exp_avg"], b.opt.state[pb]["exp_avg"])
+        assert torch.equal(a.opt.state[pa]["exp_avg_sq"], b.opt.state[pb]["exp_avg_sq"])
+        assert int(a.opt._counter(pa)[0]) == int(b.opt._counter(pb)[0]) == 6
