@@ -658,15 +658,32 @@ __global__ __launch_bounds__(256) void push_top2_merge_kernel(const unsigned lon
   uint32_t patch = 0;
   for (int i0 = 0; i0 < n_img; i0 += 8) {
     unsigned long long kb[8], ks[8];
+    {  // every image's first partial slot (pt = lane) in one batch: clamped, unconditional loads
+       // pinned before the guards select (a guarded load waits on its own: 8 round trips)
+      const int pt = lane < parts ? lane : 0;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      kb[u] = ks[u] = ~0ull;
+      for (int u = 0; u < 8; ++u) {
+        const int iu = i0 + u < n_img ? i0 + u : n_img - 1;
+        const unsigned long long* o = part + ((static_cast<size_t>(iu) * parts + pt) * P + p) * 2;
+        kb[u] = o[0];
+        ks[u] = o[1];
+      }
+      pin_batch(kb);
+      pin_batch(ks);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const bool ok = i0 + u < n_img && lane < parts;
+        kb[u] = ok ? kb[u] : ~0ull;
+        ks[u] = ok ? ks[u] : ~0ull;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)  // more than 64 partials per image: the rest (top-2 of a set: order-free)
       if (i0 + u < n_img)
-        for (int pt = lane; pt < parts; pt += 64) {
+        for (int pt = lane + 64; pt < parts; pt += 64) {
           const unsigned long long* o = part + ((static_cast<size_t>(i0 + u) * parts + pt) * P + p) * 2;
           top2_merge(kb[u], ks[u], o[0], o[1]);
         }
-    }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
 #pragma unroll
