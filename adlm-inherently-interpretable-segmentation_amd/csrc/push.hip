@@ -24,8 +24,12 @@ namespace protoseg {
 
 namespace {
 
+// Up to 512 threads x 4 columns: for a call of few images a Cityscapes patch row (2048 columns)
+// in one pass, so the 129 workgroups of a 1-image call do not each walk the row twice (9.2 -> 7.3
+// us); at 4+ images 256 threads (more workgroups resident: 14.5 vs 16.0 us at 8 images)
+constexpr int kMaskThreads = 512;
 template <typename TL>
-__global__ __launch_bounds__(256) void patch_mask_kernel(const TL* __restrict__ label, int H, int W, int h, int w,
+__global__ __launch_bounds__(kMaskThreads) void patch_mask_kernel(const TL* __restrict__ label, int H, int W, int h, int w,
                                                          const int32_t* __restrict__ lut, int lut_size,
                                                          int base, uint32_t* __restrict__ mask) {
   // base: this mask word's first class (32 per word; classes base+1 .. base+32 -> bits 0 .. 31)
@@ -798,20 +802,21 @@ extern "C" int protoseg_patch_class_mask_words(const void* label, int label_dtyp
   if (static_cast<size_t>(w) * 4 > kMaxLds) return fail(PROTOSEG_ERR_UNSUPPORTED, "w=%d too wide", w);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const dim3 grid(h, n_img);
+  const int mt = n_img >= 4 ? 256 : kMaskThreads;
   const size_t lds = static_cast<size_t>(w) * sizeof(uint32_t);
   for (int wd = 0; wd < words; ++wd) {  // word wd: classes 32 wd + 1 .. 32 wd + 32, plane [n_img][h*w]
     uint32_t* mw = mask + static_cast<size_t>(wd) * n_img * h * w;
     switch (label_dtype) {
       case PROTOSEG_I64:
-        hipLaunchKernelGGL(patch_mask_kernel<int64_t>, grid, dim3(256), lds, s, static_cast<const int64_t*>(label),
+        hipLaunchKernelGGL(patch_mask_kernel<int64_t>, grid, dim3(mt), lds, s, static_cast<const int64_t*>(label),
                            H_img, W_img, h, w, lut, lut_size, 32 * wd, mw);
         break;
       case PROTOSEG_I32:
-        hipLaunchKernelGGL(patch_mask_kernel<int32_t>, grid, dim3(256), lds, s, static_cast<const int32_t*>(label),
+        hipLaunchKernelGGL(patch_mask_kernel<int32_t>, grid, dim3(mt), lds, s, static_cast<const int32_t*>(label),
                            H_img, W_img, h, w, lut, lut_size, 32 * wd, mw);
         break;
       case PROTOSEG_U8:
-        hipLaunchKernelGGL(patch_mask_kernel<uint8_t>, grid, dim3(256), lds, s, static_cast<const uint8_t*>(label),
+        hipLaunchKernelGGL(patch_mask_kernel<uint8_t>, grid, dim3(mt), lds, s, static_cast<const uint8_t*>(label),
                            H_img, W_img, h, w, lut, lut_size, 32 * wd, mw);
         break;
       default:
