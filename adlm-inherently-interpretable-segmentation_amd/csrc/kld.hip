@@ -1134,18 +1134,33 @@ extern "C" int protoseg_kld_forward(const float* dist, int B, int P, int HW, con
   return check_launch("kld_finalize_kernel");
 }
 
+extern "C" size_t protoseg_kld_coef_bytes(int B, int K) {
+  return B > 0 && K > 0 ? static_cast<size_t>(B) * K * kKldCoefFloats * sizeof(float) : 0;
+}
+
 extern "C" int protoseg_kld_backward(const float* dist, int B, int P, int HW, const void* label, int label_dtype,
                                      const int32_t* proto_class, int K, int max_per_class, const float* g_loss,
                                      void* workspace, size_t workspace_bytes, float* g_dist,
                                      protoseg_stream_t stream) {
+  // the range partials are dead after the forward: their space holds the backward coefficients
+  return protoseg_kld_backward_ex(dist, B, P, HW, label, label_dtype, proto_class, K, max_per_class, g_loss, workspace,
+                                  workspace_bytes, nullptr, 0, g_dist, stream);
+}
+
+extern "C" int protoseg_kld_backward_ex(const float* dist, int B, int P, int HW, const void* label, int label_dtype,
+                                        const int32_t* proto_class, int K, int max_per_class, const float* g_loss,
+                                        const void* workspace, size_t workspace_bytes, float* coef_buf,
+                                        size_t coef_bytes, float* g_dist, protoseg_stream_t stream) {
   if (int st = kld_check(dist, B, P, HW, label, label_dtype, proto_class, K, max_per_class, workspace, workspace_bytes))
     return st;
   if (!g_dist) return fail(PROTOSEG_ERR_INVALID, "g_dist must be non-null");
+  if (coef_buf && coef_bytes < protoseg_kld_coef_bytes(B, K))
+    return fail(PROTOSEG_ERR_INVALID, "coef_bytes %zu < protoseg_kld_coef_bytes %zu", coef_bytes,
+                protoseg_kld_coef_bytes(B, K));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const KldLayout l = kld_layout(B, P, HW, K);
-  const KldPtrs w = kld_ptrs(workspace, l);
-  // the range partials are dead after the forward: their space holds the backward coefficients
-  float* coef = w.part;
+  const KldPtrs w = kld_ptrs(const_cast<void*>(workspace), l);
+  float* coef = coef_buf ? coef_buf : w.part;
   hipLaunchKernelGGL(kld_coef_kernel, dim3(K, B), dim3(64), 0, s, K, max_per_class, w.off, w.cnt, w.kl, w.stat, g_loss,
                      coef);
   if (int st = check_launch("kld_coef_kernel")) return st;

@@ -25,7 +25,6 @@
 #include "bf16_split.h"
 #include "l2_bf16_common.h"
 #include "l2_launch.h"
-#include "l2_onepass_layout.h"
 #include "protoseg_host.h"
 
 namespace protoseg {
@@ -160,15 +159,12 @@ __device__ float proto_norm2_64(const float* __restrict__ protos, int p, bool va
 // blockIdx.z the prototype chunk (rows z*per .. of `P` in all; chunk z's images at z*chunk_bytes),
 // so a chunked call builds every chunk's images in one launch.
 // fwd_only: the forward's images only (P rows, W, p2: the backward families build their own).
-// ob != null (bf16x3, one chunk): also the one-pass backward's operand block (Pp = oPp,
-// l2_onepass_layout.h) for a backward on the same operands (PROTOSEG_OPERANDS_FROM_FWD):
-// blockIdx.y 5 = its (-2P) image, 6 = its W^T fragments, and case 4 writes its p2 too.
 template <int T>
 __global__ __launch_bounds__(256) void l2_prep_bf16_kernel(const float* __restrict__ protos, int P, int per,
                                                            const float* __restrict__ w_last, int K, int ldw,
                                                            float w_scale, float wt_scale,
                                                            unsigned char* __restrict__ block, unsigned chunk_bytes,
-                                                           int fwd_only, unsigned char* __restrict__ ob, int oPp) {
+                                                           int fwd_only) {
   const int p0 = static_cast<int>(blockIdx.z) * per;
   protos += static_cast<size_t>(p0) * kC;
   if (w_last) w_last += p0;
@@ -191,23 +187,11 @@ __global__ __launch_bounds__(256) void l2_prep_bf16_kernel(const float* __restri
     case 3:
       stage_w_perm<T>(reinterpret_cast<bf16*>(block + o.w), w_last, w_last ? K : 0, P, ldw, Pp, w_scale, tid, nth);
       break;
-    case 4: {
+    default: {
       float* p2 = reinterpret_cast<float*>(block + o.p2);
       const int n1 = (o.pt - o.p2) / 4;
-      const int n2 = ob ? (onepass::offsets(oPp).total - onepass::offsets(oPp).p2) / 4 : 0;
-      float* q2 = ob ? reinterpret_cast<float*>(ob + onepass::offsets(oPp).p2) : nullptr;
-      for (int p = tid; p < (n1 > n2 ? n1 : n2); p += nth) {
-        const float v = proto_norm2_64(protos, p, p < P);  // the one-pass block's p2 is the same value
-        if (p < n1) p2[p] = v;
-        if (p < n2) q2[p] = v;
-      }
-      break;
+      for (int p = tid; p < n1; p += nth) p2[p] = proto_norm2_64(protos, p, p < P);
     }
-    case 5:
-      onepass::fill_pi(protos, P, oPp, ob, tid);
-      break;
-    default:
-      onepass::fill_wt(w_last, K, ldw, P, oPp, wt_scale, ob, tid);
   }
 }
 
@@ -1337,29 +1321,25 @@ size_t bf16_image_bytes(const Geometry& g, int terms) {
 }
 
 int launch_prep_bf16_chunks(const Geometry& g, int per, int nchunk, int terms, const float* protos,
-                            const float* w_last, int act_kind, float eps, void* img, hipStream_t stream, int fwd_only,
-                            void* onepass_block, int onepass_Pp) {
+                            const float* w_last, int act_kind, float eps, void* img, hipStream_t stream, int fwd_only) {
   const int Pp = static_cast<int>(ceil_div(per, 32) * 32);
-  const bool ob = onepass_block != nullptr && terms == 2 && nchunk == 1;
-  const int items = (ob && onepass_Pp > Pp ? onepass_Pp : Pp) * 8;  // the largest image loop (rows x 8 chunks)
-  const dim3 grid(static_cast<unsigned>(ceil_div(items, 256)), ob ? 7 : 5, static_cast<unsigned>(nchunk));
+  const int items = Pp * 8;  // the largest image loop (rows x 8 chunks)
+  const dim3 grid(static_cast<unsigned>(ceil_div(items, 256)), 5, static_cast<unsigned>(nchunk));
   unsigned char* blk = static_cast<unsigned char*>(img);
-  unsigned char* obk = ob ? static_cast<unsigned char*>(onepass_block) : nullptr;
   const unsigned cb = static_cast<unsigned>(img_offsets(Pp, terms).total);
   const float ws = act_unit(act_kind), wts = act_grad_unit(act_kind, eps);
   if (terms == 2)
     hipLaunchKernelGGL(l2_prep_bf16_kernel<2>, grid, dim3(256), 0, stream, protos, g.P, per, w_last, g.K, g.ldw, ws,
-                       wts, blk, cb, fwd_only, obk, onepass_Pp);
+                       wts, blk, cb, fwd_only);
   else
     hipLaunchKernelGGL(l2_prep_bf16_kernel<3>, grid, dim3(256), 0, stream, protos, g.P, per, w_last, g.K, g.ldw, ws,
-                       wts, blk, cb, fwd_only, obk, onepass_Pp);
+                       wts, blk, cb, fwd_only);
   return check_launch("l2_prep_bf16_kernel");
 }
 
 int launch_prep_bf16(const Geometry& g, int terms, const float* protos, const float* w_last, int act_kind, float eps,
-                     void* img, hipStream_t stream, int fwd_only, void* onepass_block, int onepass_Pp) {
-  return launch_prep_bf16_chunks(g, g.P, 1, terms, protos, w_last, act_kind, eps, img, stream, fwd_only, onepass_block,
-                                 onepass_Pp);
+                     void* img, hipStream_t stream, int fwd_only) {
+  return launch_prep_bf16_chunks(g, g.P, 1, terms, protos, w_last, act_kind, eps, img, stream, fwd_only);
 }
 
 int launch_adam_prep_bf16(const AdamPrepArgs& a, hipStream_t stream) {

@@ -267,7 +267,6 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
   // order (chunk fma chain, the pair (q, 0) + (q, 1) here, the q pairs in compute_tile); lanes
   // h = 0 also g_logits classes 8w .. 8w + 7 of pixel n (chunk w of the g_logits image row n).
   const unsigned a_xrow = S0 + L.xa + j * 128 + (((2 * wave + h) ^ swz<8>(j)) << 4);  // XA chunk (2w + h), row j
-  using XS = std::conditional_t<sizeof(TX) == 4, float, uint32_t>;
   auto convert = [&](int t) __attribute__((always_inline)) {
     const int gp = t * 32 + j;
     const bool ok = gp < npix;
@@ -789,8 +788,7 @@ bool bf16_bwd_wave_fits(const Geometry& g, int terms) {
 }
 
 int bf16_bwd_wave_grid(const Geometry& g) {
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int cus = device_cus();
   // as many workgroups as the rounds need, no more (every slab the reduce reads did work)
   const int rounds = static_cast<int>(ceil_div(g.ntiles, cus));
   return static_cast<int>(ceil_div(g.ntiles, rounds > 0 ? rounds : 1));

@@ -39,16 +39,14 @@ size_t bf16_bwd_pw_workspace(const Geometry& g);
 // built once per call by launch_prep_bf16 and shared by the kernels of that call.
 size_t bf16_image_bytes(const Geometry& g, int terms);
 // act_kind / eps select the constant factors folded into the W and W^T images (bf16_split.h).
-// fwd_only: only the forward's images. onepass_block (bf16x3, one chunk): also build the one-pass
-// backward's operand block (Pp onepass_Pp) in the same launch.
+// fwd_only: only the forward's images.
 int launch_prep_bf16(const Geometry& g, int terms, const float* protos, const float* w_last, int act_kind, float eps,
-                     void* img, hipStream_t stream, int fwd_only = 0, void* onepass_block = nullptr,
-                     int onepass_Pp = 0);
+                     void* img, hipStream_t stream, int fwd_only = 0);
 // The images of nchunk prototype chunks of `per` rows (g.P rows in all, W columns at stride
 // g.ldw) in one launch; chunk c's images at c * bf16_image_bytes(Pp(per)).
 int launch_prep_bf16_chunks(const Geometry& g, int per, int nchunk, int terms, const float* protos,
                             const float* w_last, int act_kind, float eps, void* img, hipStream_t stream,
-                            int fwd_only = 0, void* onepass_block = nullptr, int onepass_Pp = 0);
+                            int fwd_only = 0);
 
 // Adam step of the prototypes [P][64] and the last layer [K][P] (adam_update.h) fused with the
 // operand prep of the updated values into `block` (launch_prep_bf16's bf16x3 block, fwd_only 0,
@@ -88,21 +86,6 @@ int launch_bwd_fused_bf16(const Geometry& g, bool x_bf16, const void* x, const f
                           float* g_protos, float* g_w, float* ws, hipStream_t stream, int accumulate = 0,
                           int reduce = 1);
 int bf16_bwd_fused_grid(const Geometry& g);
-// One-pass backward (l2_bwd_onepass.hip): bf16x3, P <= 384 in one launch (8 waves per
-// workgroup, all with the same roles); its own fragment-ordered operand block
-// (launch_prep_onepass); g_x (+= when accumulate) and a g_P / g_W slab per workgroup for
-// launch_bwd_reduce_bf16_chunks. bf16_onepass_npt: 16-prototype tiles per wave (Pp = 128 npt).
-int bf16_onepass_npt(int P);
-int bf16_onepass_pp(int P);  // the block's padded prototype count (128 npt)
-bool bf16_bwd_onepass_fits(const Geometry& g, int terms);
-int bf16_bwd_onepass_grid(const Geometry& g);
-size_t bf16_onepass_image_bytes(const Geometry& g);
-size_t bf16_bwd_onepass_slab_elems(const Geometry& g);
-int launch_prep_onepass(const Geometry& g, const float* protos, const float* w_last, int act_kind, float eps,
-                        void* img, hipStream_t stream);
-int launch_bwd_onepass_bf16(const Geometry& g, bool x_bf16, const void* x, const void* img, float eps, int act_kind,
-                            const float* g_logits, const float* g_dist, void* g_x, float* ws, hipStream_t stream,
-                            int accumulate = 0);
 // Wave-owned backward (l2_bwd_wave.hip): bf16x3, P <= 384 per launch, 4 waves (one per SIMD)
 // each owning a quarter of the prototypes for every product; reads the standard bf16 operand
 // image block (launch_prep_bf16, bf16_image_bytes(P)); g_x (+= when accumulate) and a g_P / g_W

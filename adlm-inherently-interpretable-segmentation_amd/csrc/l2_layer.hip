@@ -20,6 +20,7 @@
 //                      partial slabs, reduced by l2_bwd_reduce_kernel in a fixed order
 //                      (bitwise reproducible, no atomics).
 #include "protoseg_device.h"
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -626,21 +627,28 @@ constexpr size_t kImageBlockMin = 512 * 1024;
 // Backward kernel choice for the bf16x3 training backward (C = 64):
 //   wave    l2_bwd_wave.hip: 4 waves, one per SIMD, each owning a quarter of the prototypes for
 //           every product (P <= 384 per launch, prototype chunks beyond);
-//   onepass l2_bwd_onepass.hip: 8 waves, owner phase + g_x phase (P <= 384 per launch);
 //   fused   l2_bwd_fused.hip: 6 owner + 2 g_x waves (P <= 192 per launch).
-// PROTOSEG_BWD=wave / onepass / fused forces one (read per call: tests and measurement A/B
-// switch it in one process).
-enum class BwdKernel { kWave, kOnepass, kFused };
-BwdKernel bwd_kernel(int P) {
-  const char* e = getenv("PROTOSEG_BWD");
+// Automatic: wave for P > 192, fused below. protoseg_set_backward_kernel("wave" / "fused" / "")
+// overrides it (tests and A/B measurement); the initial override is PROTOSEG_BWD, read once.
+enum class BwdKernel { kAuto = 0, kWave, kFused };
+std::atomic<int> g_bwd_override{-1};  // -1: PROTOSEG_BWD not read yet
+BwdKernel bwd_kernel_of_name(const char* e) {
   if (e && !strcmp(e, "wave")) return BwdKernel::kWave;
-  if (e && !strcmp(e, "onepass")) return BwdKernel::kOnepass;
   if (e && !strcmp(e, "fused")) return BwdKernel::kFused;
+  return BwdKernel::kAuto;
+}
+BwdKernel bwd_kernel(int P) {
+  int o = g_bwd_override.load(std::memory_order_relaxed);
+  if (o < 0) {
+    int expected = -1;
+    o = static_cast<int>(bwd_kernel_of_name(getenv("PROTOSEG_BWD")));
+    if (!g_bwd_override.compare_exchange_strong(expected, o)) o = expected;
+  }
+  if (o != static_cast<int>(BwdKernel::kAuto)) return static_cast<BwdKernel>(o);
   // P > 192: the wave-owned kernel (one pass over X for up to 384 prototypes per chunk, the
   // forward's operand images); the fused kernel below (its 192-prototype LDS images)
   return P > 192 ? BwdKernel::kWave : BwdKernel::kFused;
 }
-bool use_onepass(int P) { return bwd_kernel(P) == BwdKernel::kOnepass; }
 
 int stream_block(size_t need, hipStream_t s, int kind, void** out) {
   return stream_scratch(static_cast<ScratchKind>(kind), need, kImageBlockMin, s, out);
@@ -649,39 +657,23 @@ int stream_block(size_t need, hipStream_t s, int kind, void** out) {
 struct ImageBlock {
   void* ptr = nullptr;
   // per > 0: the images of ceil(g.P / per) prototype chunks of `per` rows, one prep launch.
-  // fwd_only: the forward's images only; onepass_block: the one-pass backward's block too (same launch).
+  // fwd_only: the forward's images only.
   int build(const Geometry& g, int terms, const float* protos, const float* w_last, int act_kind, float eps,
-            hipStream_t s, int per = 0, int fwd_only = 0, void* onepass_block = nullptr, int onepass_Pp = 0) {
+            hipStream_t s, int per = 0, int fwd_only = 0) {
     const int nchunk = per > 0 ? static_cast<int>(ceil_div(g.P, per)) : 1;
     const size_t need = per > 0 ? nchunk * bf16_image_bytes(geometry_of(1, g.C, 1, 1, per, g.K), terms)
                                 : bf16_image_bytes(g, terms);
     if (int st = stream_block(need, s, 0, &ptr)) return st;
     if (per > 0)
       return launch_prep_bf16_chunks(g, per, nchunk, terms, protos, w_last, act_kind, eps, ptr, s, fwd_only);
-    return launch_prep_bf16(g, terms, protos, w_last, act_kind, eps, ptr, s, fwd_only, onepass_block, onepass_Pp);
-  }
-  // The fragment-ordered blocks of the one-pass backward (l2_bwd_onepass.hip): nchunk chunks of
-  // `per` prototypes (the last may be shorter), chunk c's block at c * chunk_bytes(per).
-  int build_onepass(const Geometry& g, int per, int nchunk, const float* protos, const float* w_last, int act_kind,
-                    float eps, hipStream_t s) {
-    const size_t cb = bf16_onepass_image_bytes(geometry_of(1, g.C, 1, 1, per, g.K));
-    if (int st = stream_block(cb * nchunk, s, 1, &ptr)) return st;
-    for (int c = 0; c < nchunk; ++c) {
-      const int p0 = c * per, pc = g.P - p0 < per ? g.P - p0 : per;
-      Geometry gc = geometry_of(1, g.C, 1, 1, pc, g.K);
-      gc.ldw = g.P;
-      if (int st = launch_prep_onepass(gc, protos + static_cast<size_t>(p0) * g.C, w_last ? w_last + p0 : nullptr,
-                                       act_kind, eps, static_cast<unsigned char*>(ptr) + c * cb, s))
-        return st;
-    }
-    return PROTOSEG_OK;
+    return launch_prep_bf16(g, terms, protos, w_last, act_kind, eps, ptr, s, fwd_only);
   }
 };
 
 // The training backward's operand images built by the forward into a caller buffer
-// (protoseg_l2_fwd_ex / protoseg_l2_bwd_ex): the one-pass block (P in (192, 384] by default) or
-// the fused kernel's images (P <= 192): the layouts the backward's own prep would write.
-enum class TrainOperands { kNone, kOnepass, kFused };
+// (protoseg_l2_fwd_ex / protoseg_l2_bwd_ex): the standard image block the wave (P <= 384) and
+// fused (P <= 192) kernels read, the layout the backward's own prep would write.
+enum class TrainOperands { kNone, kFused };
 }  // namespace
 
 // Largest P the bf16 family serves through prototype chunks (C = 64).
@@ -712,8 +704,6 @@ TrainOperands train_operands_kind(int C, int P, int K, int precision) {
   switch (bwd_kernel(P)) {
     case BwdKernel::kWave:  // the standard image block (launch_prep_bf16), one chunk
       return P <= 384 && bf16_bwd_wave_fits(g, 2) ? TrainOperands::kFused : TrainOperands::kNone;
-    case BwdKernel::kOnepass:
-      return P <= 384 && bf16_bwd_onepass_fits(g, 2) ? TrainOperands::kOnepass : TrainOperands::kNone;
     default:
       return P <= 192 && bf16_bwd_fused_fits(g, 2) ? TrainOperands::kFused : TrainOperands::kNone;
   }
@@ -721,11 +711,16 @@ TrainOperands train_operands_kind(int C, int P, int K, int precision) {
 
 size_t train_operands_bytes(int C, int P, int K, TrainOperands kind) {
   const Geometry g = geometry_of(1, C, 1, 1, P, K);
-  return kind == TrainOperands::kOnepass ? bf16_onepass_image_bytes(g)
-         : kind == TrainOperands::kFused ? bf16_image_bytes(g, 2)
-                                         : 0;
+  return kind == TrainOperands::kFused ? bf16_image_bytes(g, 2) : 0;
 }
 }  // namespace
+
+extern "C" int protoseg_set_backward_kernel(const char* name) {
+  if (name && *name && strcmp(name, "wave") && strcmp(name, "fused"))
+    return fail(PROTOSEG_ERR_INVALID, "backward kernel '%s': \"wave\", \"fused\" or \"\" (automatic)", name);
+  g_bwd_override.store(static_cast<int>(bwd_kernel_of_name(name)), std::memory_order_relaxed);
+  return PROTOSEG_OK;
+}
 
 extern "C" size_t protoseg_l2_train_operands_bytes(int C, int P, int K, int precision) {
   return train_operands_bytes(C, P, K, train_operands_kind(C, P, K, precision));
@@ -844,18 +839,13 @@ int l2_fwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const fl
   }
   const int terms = terms_of(precision);
   if (terms && bf16_fwd_fits(geo, terms)) {
-    // one prep launch: the forward's images (+ the one-pass backward's block when asked)
-    const bool ob = tk == TrainOperands::kOnepass;
+    // one prep launch: the forward's images
     ImageBlock img;
-    if (int st = img.build(geo, terms, protos, ob ? w_ops : logits_out ? w_last : nullptr, act_kind, eps, s, 0, 1,
-                           ob ? operands : nullptr, ob ? bf16_onepass_pp(P) : 0))
-      return st;
+    if (int st = img.build(geo, terms, protos, logits_out ? w_last : nullptr, act_kind, eps, s, 0, 1)) return st;
     if (!dist_out && !act_out && !logits_out) return PROTOSEG_OK;
     return launch_fwd_bf16(geo, x_dtype == PROTOSEG_BF16, terms, x, img.ptr, eps, act_kind, dist_out, act_out,
                            logits_out, s);
   }
-  if (tk == TrainOperands::kOnepass)  // (not reached at C = 64, P <= 384: the forward fits one launch)
-    if (int st = launch_prep_onepass(geo, protos, w_ops, act_kind, eps, operands, s)) return st;
   // P beyond the forward's LDS images (Pp > 384, e.g. 30 prototypes/class): prototype chunks of
   // <= 384. Distance / activation rows land at (b * P + p0 + p); the logits are a sum over
   // prototypes, so chunk c > 0 adds to them.
@@ -937,14 +927,6 @@ extern "C" size_t protoseg_l2_bwd_workspace_size(int B, int C, int H, int W, int
   size_t need = f32_pw_workspace(g);
   const size_t b16 = bf16_bwd_pw_workspace(g);
   if (C == 64 && b16 > need) need = b16;
-  if (C == 64) {  // one-pass backward: one slab per workgroup and prototype chunk of <= 384
-    const int nchunk = static_cast<int>(ceil_div(P, 384)), per = static_cast<int>(ceil_div(P, nchunk));
-    const Geometry gc = geometry_of(B, C, H, W, per, K);
-    if (bf16_bwd_onepass_fits(gc, 2)) {
-      const size_t q = static_cast<size_t>(nchunk) * bf16_bwd_onepass_slab_elems(gc) * sizeof(float);
-      if (q > need) need = q;
-    }
-  }
   if (C == 64) {  // wave backward: one slab per workgroup and prototype chunk of <= 384
     const int nchunk = static_cast<int>(ceil_div(P, 384)), per = static_cast<int>(ceil_div(P, nchunk));
     const Geometry gc = geometry_of(B, C, H, W, per, K);
@@ -1050,37 +1032,6 @@ int l2_bwd_impl(const void* x, int x_dtype, int B, int C, int H, int W, const fl
       }
       return launch_bwd_reduce_bf16_chunks(geo, per, nchunk, ws, grid, chunk_elems, protos, act_kind, g_protos,
                                            g_logits ? g_w : nullptr, s, 2);
-    }
-  }
-  // Training backward at bf16x3: ONE pass over X for up to 384 prototypes (19 prototypes/class;
-  // l2_bwd_onepass.hip), prototype chunks of <= 384 beyond (chunk c > 0 adds its g_x), one slab
-  // reduce. P <= 192 keeps the 192-prototype fused kernel unless PROTOSEG_BWD=onepass.
-  if (terms == 2 && (xsig || (g_x && (g_protos || g_w))) && use_onepass(P)) {
-    const int nchunk = static_cast<int>(ceil_div(P, 384)), per = static_cast<int>(ceil_div(P, nchunk));
-    Geometry gc = geometry_of(B, C, H, W, per, K);
-    if (bf16_bwd_onepass_fits(gc, terms)) {
-      KernelSpan span(nchunk > 1 ? "l2_bwd_onepass_bf16_kernel" : "", "", s);
-      ImageBlock img;
-      if (tk == TrainOperands::kOnepass && nchunk == 1)
-        img.ptr = const_cast<void*>(operands);
-      else if (int st = img.build_onepass(geo, per, nchunk, protos, g_logits ? w_last : nullptr, act_kind, eps, s))
-        return st;
-      const size_t cb = bf16_onepass_image_bytes(gc);
-      const size_t chunk_elems = bf16_bwd_onepass_slab_elems(gc);
-      const int grid = bf16_bwd_onepass_grid(gc);
-      for (int c = 0; c < nchunk; ++c) {
-        const int p0 = c * per, pc = P - p0 < per ? P - p0 : per;
-        Geometry gq = geometry_of(B, C, H, W, pc, K);
-        gq.ldw = gq.ldd = P;
-        gq.p0 = p0;
-        gq.xsig = xsig;
-        gq.cgd = cgd;
-        if (int st = launch_bwd_onepass_bf16(gq, xb, x, static_cast<unsigned char*>(img.ptr) + c * cb, eps, act_kind,
-                                             g_logits, g_dist, g_x, ws + c * chunk_elems, s, c > 0))
-          return st;
-      }
-      return launch_bwd_reduce_bf16_chunks(geo, per, nchunk, ws, grid, chunk_elems, protos, act_kind, g_protos,
-                                           g_logits ? g_w : nullptr, s);
     }
   }
   // Training backward (g_x and g_P / g_W) at bf16x3: one fused kernel per chunk of <= 192

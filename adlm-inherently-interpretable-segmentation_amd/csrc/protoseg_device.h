@@ -62,10 +62,12 @@ template <> struct XIO<uint16_t> {
 
 // model.py:217-219: relu(x2_patch_sum + (-2 * xp + p2)); -2*xp is exact, so the
 // expression below rounds exactly where the reference does.
-__device__ __forceinline__ float l2_distance(float x2, float p2, float xp) {
+__device__ __forceinline__ float l2_pre_relu(float x2, float p2, float xp) {
   const float inter = p2 - 2.f * xp;
-  const float s = x2 + inter;
-  return __builtin_fmaxf(s, 0.f);  // F.relu (v_max_f32; NaN inputs are out of scope)
+  return x2 + inter;
+}
+__device__ __forceinline__ float l2_distance(float x2, float p2, float xp) {
+  return __builtin_fmaxf(l2_pre_relu(x2, p2, xp), 0.f);  // F.relu (v_max_f32; NaN inputs are out of scope)
 }
 
 // model.py:231-237

@@ -1,6 +1,7 @@
 // protoseg_host.h — host-side helpers for the C ABI launchers (status, errors, LDS opt-in).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <mutex>
 #include <type_traits>
 
@@ -20,7 +21,7 @@ int check_launch(const char* what);
 // call's kernels still read. A call that needs more takes a new block (1.5x growth, at least
 // `min_bytes`) and retires the old one without freeing it: a graph that captured an earlier call
 // still points there, and a replay must not touch freed memory.
-enum class ScratchKind : int { kImages = 0, kOnepassImages = 1, kWideForward = 2, kWidePush = 3, kPush = 4, kPushUpdate = 5 };
+enum class ScratchKind : int { kImages = 0, kUnused1 = 1, kWideForward = 2, kWidePush = 3, kPush = 4, kPushUpdate = 5 };
 int stream_scratch(ScratchKind kind, size_t need, size_t min_bytes, hipStream_t s, void** out);
 
 // gfx950 has 160 KiB of LDS per CU; a kernel opts in once to dynamic LDS above 64 KiB.
@@ -74,6 +75,20 @@ class KernelSpan {
   hipEvent_t stop_ = nullptr;
   hipStream_t s_ = nullptr;
 };
+
+// Compute units of the current device, queried once per device (launch shapes read it per call).
+inline int device_cus() {
+  constexpr int kMaxDev = 64;
+  static std::atomic<int> cache[kMaxDev] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 256;
+  int c = cache[dev].load(std::memory_order_relaxed);
+  if (c > 0) return c;
+  c = 256;
+  if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c < 1) c = 256;
+  cache[dev].store(c, std::memory_order_relaxed);
+  return c;
+}
 
 // Workgroups of `kernel` resident on the whole device at (threads, lds): CUs x blocks per CU
 // from the occupancy calculator (VGPRs and LDS), at least the CU count. Cached per

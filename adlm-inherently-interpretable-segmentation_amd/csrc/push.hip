@@ -385,7 +385,7 @@ template <int NC>
 __global__ __launch_bounds__(kPwWaves * 64) void push_argmin_wave_kernel(
     const float* __restrict__ x, int HW, const float* __restrict__ protos, int P, int pt0, int nptc,
     const int32_t* __restrict__ proto_class, const uint32_t* __restrict__ mask,
-    unsigned long long* __restrict__ part, int wgs) {
+    unsigned long long* __restrict__ part, int wgs, const float* __restrict__ sd0) {
   using namespace bf16l;
   constexpr int C = NC * 32;
   extern __shared__ __attribute__((aligned(16))) float pw_smem[];
@@ -439,11 +439,19 @@ __global__ __launch_bounds__(kPwWaves * 64) void push_argmin_wave_kernel(
       for (int r = 0; r < 16; ++r)
         xr[ct * 16 + r] = BufIO<float>::load(rx, off, static_cast<unsigned>((ct * 32 + r) * HW * 4));
   };
-  float bd[kPwMaxTiles], sd[kPwMaxTiles];
+  // bnd: the caller's bound (protoseg_push_update: the running runner-up distance before this
+  // call, sd0[p]) or +inf. A candidate d >= min(sd, bnd) changes neither this lane's top-2 below
+  // bnd nor the merged state (it cannot become the running best, best <= runner-up <= bnd, nor
+  // lower the runner-up), so the epilogue skips a prototype tile whose candidates are all above
+  // that threshold in every lane: two VALU per candidate instead of the ~12 of the masked update.
+  // The per-image top-2 below bnd is then exact, above it partial (only the merge reads it).
+  float bd[kPwMaxTiles], sd[kPwMaxTiles], bnd[kPwMaxTiles];
   uint32_t bi[kPwMaxTiles];
 #pragma unroll
   for (int pt = 0; pt < kPwMaxTiles; ++pt) {
+    const int p = pbase + pt * 32 + j;
     bd[pt] = sd[pt] = __builtin_inff();
+    bnd[pt] = sd0 && pt < nptc && p < P ? sd0[p] : __builtin_inff();
     bi[pt] = 0xffffffffu;
   }
   // one prototype tile's B operand (channels ct * 32 + 16 h + 4 q .. + 3: 16-B LDS reads)
@@ -464,10 +472,19 @@ __global__ __launch_bounds__(kPwWaves * 64) void push_argmin_wave_kernel(
   auto epilogue = [&](int pt, const f32x16& acc, int nbase) __attribute__((always_inline)) {
     float x2r[16], mkr[16];  // (re-read per prototype tile: not held across the MFMA chain)
     load_rows16(xw + 4 * h, x2r);
+    float s[16];  // l2_distance before its relu: relu(s) < thr implies s < thr (thr >= 0)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = l2_pre_relu(x2r[r], p2[pt], acc[r]);
+    float m4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) m4[q] = fminf(fminf(s[4 * q], s[4 * q + 1]), fminf(s[4 * q + 2], s[4 * q + 3]));
+    const float thr = fminf(sd[pt], bnd[pt]);
+    if (!__builtin_amdgcn_ballot_w64(fminf(fminf(m4[0], m4[1]), fminf(m4[2], m4[3])) < thr))
+      return;  // no candidate below any lane's threshold: nothing changes (wave-uniform)
     load_rows16(xw + 32 + 4 * h, mkr);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float d = l2_distance(x2r[r], p2[pt], acc[r]);
+      const float d = __builtin_fmaxf(s[r], 0.f);  // = l2_distance(x2r[r], p2[pt], acc[r])
       const float dm = (__float_as_uint(mkr[r]) & clsbit[pt]) ? d : __builtin_inff();
       const bool c = dm < bd[pt];
       sd[pt] = c ? bd[pt] : fminf(sd[pt], dm);
@@ -850,7 +867,8 @@ extern "C" int protoseg_push_argmin(const float* x, int n_img, int C, int h, int
 // push_top2_merge_kernel); *parts_out = 0 when the wide path ran and wrote img_keys itself.
 int push_argmin_impl(const float* x, int n_img, int C, int h, int w, const float* protos, int P,
                      const int32_t* proto_class, const uint32_t* mask, int words, uint64_t* img_keys,
-                     uint64_t* img_second, hipStream_t s, const unsigned long long** part_out, int* parts_out) {
+                     uint64_t* img_second, hipStream_t s, const unsigned long long** part_out, int* parts_out,
+                     const float* sd0) {
   if (words < 1 || words > 64) return fail(PROTOSEG_ERR_INVALID, "words=%d outside [1, 64]", words);
   if (!x || !protos || !proto_class || !mask || !img_keys)
     return fail(PROTOSEG_ERR_INVALID, "null pointer argument");
@@ -882,9 +900,7 @@ int push_argmin_impl(const float* x, int n_img, int C, int h, int w, const float
     if (wgs < 1) wgs = 1;
 #if PUSH_CHUNK_PLAN
     {  // the chunk width and workgroups per (image, chunk) that minimise the busiest wave's work
-      int cus = 256, dev = 0;
-      if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      const PushPlan pl = push_wave_plan(npt, maxt, n_img, ntile, cus);
+      const PushPlan pl = push_wave_plan(npt, maxt, n_img, ntile, device_cus());
       per = pl.per;
       wgs = pl.wgs;
     }
@@ -899,7 +915,7 @@ int push_argmin_impl(const float* x, int n_img, int C, int h, int w, const float
       KernelTimer timer("push_argmin_wave_kernel", s);
       hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(wgs), n_img, chunks), dim3(kPwWaves * 64),
                          pw_lds_bytes(C, nptc), s, x, static_cast<int>(HW), protos, P, pt0, nptc, proto_class, mask,
-                         part, static_cast<int>(wgs));
+                         part, static_cast<int>(wgs), sd0);
     };
     if (nc == 1) {
       if (int e = ensure_lds<push_argmin_wave_kernel<1>>()) return e;
@@ -977,7 +993,7 @@ extern "C" int protoseg_push_argmin_words(const float* x, int n_img, int C, int 
                                           const int32_t* proto_class, const uint32_t* mask, int words,
                                           uint64_t* img_keys, uint64_t* img_second, protoseg_stream_t stream) {
   return push_argmin_impl(x, n_img, C, h, w, protos, P, proto_class, mask, words, img_keys, img_second,
-                          reinterpret_cast<hipStream_t>(stream), nullptr, nullptr);
+                          reinterpret_cast<hipStream_t>(stream), nullptr, nullptr, nullptr);
 }
 
 extern "C" int protoseg_push_distances(const float* x, int C, int h, int w, const float* protos, int m, float* dist,
@@ -1054,7 +1070,11 @@ extern "C" int protoseg_push_update(const void* label, int label_dtype, int n_im
     return st;
   const unsigned long long* part = nullptr;
   int parts = 0;
-  if (int st = push_argmin_impl(x, n_img, C, h, w, protos, P, proto_class, mask, words, keys, second, s, &part, &parts))
+  // the running runner-up (or, without one, the running best) bounds the candidates that can
+  // still change the state: the argmin's per-image top-2 drops the rest (push_argmin_wave_kernel)
+  const float* bound = global_second ? global_second : global_dist;
+  if (int st = push_argmin_impl(x, n_img, C, h, w, protos, P, proto_class, mask, words, keys, second, s, &part, &parts,
+                                bound))
     return st;
   if (parts == 0)  // the wide path wrote the per-image keys
     return protoseg_push_merge(keys, second, n_img, first_img, x, C, static_cast<int>(hw), P, global_dist,

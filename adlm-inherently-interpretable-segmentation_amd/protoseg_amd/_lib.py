@@ -60,6 +60,7 @@ SIGNATURES = {
     "protoseg_l2_bwd_kld": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _i, _vp, _vp, _vp, _vp, _i, _vp,
                                  _vp, _vp, _vp, _sz, _vp]),
     "protoseg_l2_bwd_kld_supported": (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _i]),
+    "protoseg_set_backward_kernel": (_i, [ctypes.c_char_p]),
     "protoseg_l2_train_operands_bytes": (_sz, [_i, _i, _i, _i]),
     "protoseg_l2_fwd_ex": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
     "protoseg_l2_bwd_ex": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _i, _f, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp,
@@ -78,6 +79,8 @@ SIGNATURES = {
     "protoseg_kld_workspace_size": (_sz, [_i, _i, _i, _i]),
     "protoseg_kld_forward": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _vp, _sz, _vp]),
     "protoseg_kld_backward": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _sz, _vp, _vp]),
+    "protoseg_kld_coef_bytes": (_sz, [_i, _i]),
+    "protoseg_kld_backward_ex": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _sz, _vp, _sz, _vp, _vp]),
     "protoseg_kld_backward_compact": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _sz, _vp, _vp, _vp,
                                            _vp]),
     "protoseg_kld_expand": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),

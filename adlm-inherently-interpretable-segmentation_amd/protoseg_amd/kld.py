@@ -13,6 +13,7 @@ class-0 prototypes and label value ``num_classes`` is skipped (module.py:170-178
 """
 from __future__ import annotations
 
+import warnings
 import weakref
 from typing import Optional, Tuple
 
@@ -63,10 +64,10 @@ def _(distances, target_img, proto_class, num_classes, max_per_class):
             distances.new_empty((n,), dtype=torch.uint8))
 
 
-# protoseg_kld_backward writes its per-pair coefficients into the workspace's range-partial
-# region (dead after the forward). The op runs it on a private copy of the workspace, so it really
-# mutates none of its inputs (mutates_args=() holds for torch.library.opcheck and
-# functionalization). This is the dense fallback path (hooks, explicit-input passes, the wide
+# protoseg_kld_backward_ex writes its per-pair coefficients into a buffer of its own
+# (protoseg_kld_coef_bytes) and only reads the workspace, so the op mutates none of its inputs
+# (mutates_args=() holds for torch.library.opcheck and functionalization) without copying the
+# workspace. This is the dense fallback path (hooks, explicit-input passes, the wide
 # family); the training path's compact backward computes its coefficients in LDS and writes nothing
 # into the workspace.
 @torch.library.custom_op("protoseg::kld_backward", mutates_args=(), device_types="cuda")
@@ -81,11 +82,11 @@ def kld_backward(distances: Tensor, target_img: Tensor, proto_class: Tensor, num
     pc = proto_class.to(torch.int32).contiguous()
     g = g_loss.to(torch.float32).contiguous()
     g_dist = torch.empty_like(d)
-    ws = workspace.clone()  # the coefficients go into the copy's range-partial region
+    coef = torch.empty(_lib.load().protoseg_kld_coef_bytes(B, int(num_classes)), dtype=torch.uint8, device=dev)
     with torch.cuda.device(dev):
-        _lib.call("protoseg_kld_backward", _lib.ptr(d), B, P, HW, _lib.ptr(t), ldt, _lib.ptr(pc), int(num_classes),
-                  int(max_per_class), _lib.ptr(g), _lib.ptr(ws), ws.numel(), _lib.ptr(g_dist),
-                  _lib.stream_of(dev))
+        _lib.call("protoseg_kld_backward_ex", _lib.ptr(d), B, P, HW, _lib.ptr(t), ldt, _lib.ptr(pc), int(num_classes),
+                  int(max_per_class), _lib.ptr(g), _lib.ptr(workspace), workspace.numel(), _lib.ptr(coef),
+                  coef.numel(), _lib.ptr(g_dist), _lib.stream_of(dev))
     return g_dist
 
 
@@ -157,6 +158,7 @@ def _pass_runs_every_node(probe_node) -> bool:
     try:
         return bool(torch._C._will_engine_execute_node(probe_node))
     except (AttributeError, RuntimeError):  # no engine introspection: treat as explicit inputs
+        _warn_no_introspection()
         return False
 
 
@@ -169,7 +171,21 @@ def _layer_backward_runs(layer_node) -> bool:
     try:
         return any(torch._C._will_engine_execute_node(n) for n, _ in layer_node.next_functions if n is not None)
     except (AttributeError, RuntimeError):  # no engine introspection: always the dense gradient
+        _warn_no_introspection()
         return False
+
+
+_warned_introspection = False
+
+
+def _warn_no_introspection():
+    """Once per process: this torch has no autograd-engine introspection, so every KLD backward
+    takes the dense [B, P, H, W] gradient instead of the compact hand-off (slower, same values)."""
+    global _warned_introspection
+    if not _warned_introspection:
+        _warned_introspection = True
+        warnings.warn("protoseg KLD: torch._C._will_engine_execute_node is unavailable; the KLD gradient takes "
+                      "the dense path", RuntimeWarning, stacklevel=3)
 
 
 class _KldToLayer(torch.autograd.Function):

@@ -235,7 +235,8 @@ class PPNet(nn.Module):
     def set_last_layer_incorrect_connection(self, incorrect_strength):
         """model.py:359-371: 1 for the prototype's own class, ``incorrect_strength`` elsewhere."""
         positive = torch.t(self.prototype_class_identity)
-        self.last_layer.weight.data.copy_(1 * positive + incorrect_strength * (1 - positive))
+        with torch.no_grad():
+            self.last_layer.weight.copy_(1 * positive + incorrect_strength * (1 - positive))
 
     def _initialize_weights(self):
         for m in self.add_on_layers.modules():

@@ -146,12 +146,14 @@ def l2_backward(x: Tensor, protos: Tensor, w_last: Tensor, g_logits: Optional[Te
     if need_w is False and g_logits is None and need_protos is False and need_x is False:
         return g_x, g_p, g_w
     lib = _lib.load()
-    # slabs of g_P / g_W, every X_SIGMOID backward, and the wide family's D / G_s buffers (any
-    # request, g_x alone included): the size query is host-only, torch's allocator caches the block
-    ws_bytes = lib.protoseg_l2_bwd_workspace_size(B, C, H, W, P, K)
-    ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8) if ws_bytes else None
     ops_ptr, ops_bytes = _operands_args(operands)
     with torch.cuda.device(dev):
+        # slabs of g_P / g_W, every X_SIGMOID backward, and the wide family's D / G_s buffers (any
+        # request, g_x alone included): the size query is host-only but depends on the device's
+        # CU count (one slab per workgroup), so it runs inside the device context; torch's
+        # allocator caches the block
+        ws_bytes = lib.protoseg_l2_bwd_workspace_size(B, C, H, W, P, K)
+        ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8) if ws_bytes else None
         if dist is not None and dist.numel():
             _lib.call("protoseg_l2_bwd_saved", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P,
                       _lib.ptr(w_last), K, float(eps), int(act_kind), int(precision), _lib.ptr(dist.contiguous()),
@@ -262,10 +264,10 @@ def l2_backward_kld(x: Tensor, protos: Tensor, w_last: Tensor, g_logits: Optiona
     g_p = torch.empty((P, C), device=dev, dtype=torch.float32) if need_protos else x.new_empty(0, dtype=torch.float32)
     g_w = torch.empty((K, P), device=dev, dtype=torch.float32) if need_w else x.new_empty(0, dtype=torch.float32)
     lib = _lib.load()
-    ws_bytes = lib.protoseg_l2_bwd_workspace_size(B, C, H, W, P, K)
-    ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
     ops_ptr, ops_bytes = _operands_args(operands)
     with torch.cuda.device(dev):
+        ws_bytes = lib.protoseg_l2_bwd_workspace_size(B, C, H, W, P, K)  # (per device: see l2_backward)
+        ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
         _lib.call("protoseg_l2_bwd_kld_ex", _lib.ptr(x), _x_dtype(x), B, C, H, W, _lib.ptr(protos), P,
                   _lib.ptr(w_last), K, float(eps), int(act_kind), int(precision), _lib.ptr(g_logits),
                   _lib.ptr(g_cls), _lib.ptr(pix_cls), _lib.ptr(proto_slot), int(max_per_class), _lib.ptr(g_x),

@@ -29,6 +29,12 @@ class Adam(torch.optim.Optimizer):
             raise ValueError("invalid Adam hyper-parameters")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self._steps: Dict[torch.Tensor, torch.Tensor] = {}
+        # parameters layer_step_with_operands already updated for the current iteration: the next
+        # step() skips them (and forgets the mark), so step() can follow the fused call for the
+        # optimizer's other groups without a second update of the two layer tensors
+        self._stepped: Dict[int, torch.Tensor] = {}
+        # what the last fused update wrote into which operand block (operands_ready)
+        self._operands = None
 
     def _counter(self, p: torch.Tensor) -> torch.Tensor:
         """Device {step count, ticket} of parameter p, seeded from state[p]['step'] (a loaded
@@ -47,8 +53,9 @@ class Adam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        stepped, self._stepped = self._stepped, {}
         for group in self.param_groups:
-            ps = [p for p in group["params"] if p.grad is not None]
+            ps = [p for p in group["params"] if p.grad is not None and stepped.get(id(p)) is not p]
             if not ps:
                 continue
             for p in ps:
@@ -99,7 +106,10 @@ class Adam(torch.optim.Optimizer):
         ``operands``, so that forward passes ``_lib.OPERANDS_READY`` and launches no prep. Each
         tensor uses its own group's lr / weight_decay (betas and eps must agree). Returns False,
         having run nothing, where the fused entry does not serve the shape or the groups differ in
-        betas / eps; the caller then runs step() and a plain forward."""
+        betas / eps; the caller then runs a plain forward. Either way the caller runs step() next
+        for the rest of the optimizer's parameters (the reference's single joint Adam,
+        module.py:391): after a fused update the two layer tensors are marked as stepped for this
+        iteration, and that step() skips them."""
         if protos.grad is None or w_last.grad is None:
             return False
         P, C = protos.shape[0], protos[0].numel()
@@ -125,7 +135,26 @@ class Adam(torch.optim.Optimizer):
                       _lib.ptr(self._counter(w_last)), float(gw["lr"]), float(gw["weight_decay"]),
                       float(b1), float(b2), float(gp["eps"]), _lib.ptr(operands), operands.numel(),
                       _lib.stream_of(protos.device))
+        self._stepped[id(protos)] = protos
+        self._stepped[id(w_last)] = w_last
+        self._operands = (operands.data_ptr(), operands.numel(), protos, protos._version, protos.data_ptr(), w_last,
+                          w_last._version, w_last.data_ptr(), float(eps), int(act_kind), int(precision))
         return True
+
+    def operands_ready(self, protos: torch.Tensor, w_last: torch.Tensor, operands: torch.Tensor, eps: float,
+                       act_kind: int, precision: int) -> bool:
+        """Whether ``operands`` holds the images of exactly these parameter values for this
+        (eps, activation, precision): the last layer_step_with_operands wrote them into this block
+        and nothing has changed either tensor since: a tracked in-place write bumps its version
+        counter (``push_prototypes``' copy, ``load_state_dict``, another torch optimizer), a new
+        ``.data`` tensor moves its address (``prune_prototypes``). Writes through ``.data.copy_``
+        are invisible to torch's counter: a caller that writes that way passes ``OPERANDS_READY``
+        on its own responsibility. Pass the flag only when this is True."""
+        o = self._operands
+        return (o is not None and o[0] == operands.data_ptr() and o[1] == operands.numel() and o[2] is protos
+                and o[3] == protos._version and o[4] == protos.data_ptr() and o[5] is w_last
+                and o[6] == w_last._version and o[7] == w_last.data_ptr()
+                and o[8:] == (float(eps), int(act_kind), int(precision)))
 
     def state_dict(self):
         """torch's layout: state[p] = {'step': float scalar, 'exp_avg', 'exp_avg_sq'} (the step

@@ -448,7 +448,8 @@ def dedup_and_prune(ppnet, fmap: np.ndarray, root_dir: Optional[str], log: Calla
     """push.py:143-155: write prototypes, np.unique(axis=0) dedup, prune, unique_prototypes.json."""
     shape = tuple(ppnet.prototype_shape)
     update = np.reshape(fmap.astype(np.float64), shape)
-    ppnet.prototype_vectors.data.copy_(torch.tensor(update, dtype=torch.float32).to(ppnet.prototype_vectors.device))
+    with torch.no_grad():  # (a tracked in-place write: Adam.operands_ready sees the version move)
+        ppnet.prototype_vectors.copy_(torch.tensor(update, dtype=torch.float32).to(ppnet.prototype_vectors.device))
     _, unique_index = np.unique(update, axis=0, return_index=True)
     unique_set = set(int(i) for i in unique_index)
     duplicate_idx = [i for i in range(ppnet.num_prototypes) if i not in unique_set]

@@ -209,12 +209,9 @@ class LayerStep:
                   _lib.ptr(self.g_w), _lib.ptr(self.ws), self.ws_bytes, *self._ops(), self._stream())
 
     def opt_step(self):
-        if self.fold and self.opt.layer_step_with_operands(self.params[0], self.params[1], self.ops, 1e-4,
-                                                           _lib.ACT_LOG, self.prec):
-            self.ops_ready = True
-            return
-        self.opt.step()
-        self.ops_ready = False
+        self.ops_ready = bool(self.fold and self.opt.layer_step_with_operands(self.params[0], self.params[1], self.ops,
+                                                                              1e-4, _lib.ACT_LOG, self.prec))
+        self.opt.step()  # the other parameters (none here: a no-op after the fused update)
 
     def exchange(self, world):
         """Data-parallel gradient exchange: the training step's GradientBuckets (bucketed RCCL
@@ -568,37 +565,47 @@ def kernel_launch_times(name, fn, reps, npair=8, actual=None):
     return float(np.mean(times)), per_call
 
 
-def time_push(n_img, steps, warmup, device, C=64, H=1024, W=2048, h=129, w=257, P=190, K=19):
+def time_push(n_img, steps, warmup, device, C=64, H=1024, W=2048, h=129, w=257, P=190, K=19, scan_images=64):
     """The shipped push driver's inner step (push.push_update, one call per batch of n_img
     equal-geometry images, as push_prototypes issues it with images_per_batch = n_img):
-    patch mask -> top-2 argmin -> strict-'<' merge. Wall time per image over `steps` calls;
-    the argmin kernel's per-launch device time from the library's event hook."""
+    patch mask -> top-2 argmin -> strict-'<' merge. One timed step is a SCAN of `scan_images`
+    DISTINCT images (scan_images / n_img batches, first_img advancing) from a fresh running state,
+    as push_prototypes walks dataset.img_ids (push.py:101): the argmin's skip of candidates above
+    the running runner-up sees what a real scan sees, never images it has already merged. Wall
+    time per image over `steps` scans; the argmin kernel's per-launch device time from the
+    library's event hook over one scan."""
     from protoseg_amd import push as dpush
-    x, protos, labels, pc = make_push_inputs(n_img, C, H, W, h, w, P, K, device, SEED)
-    state = dpush.PushState.create(P, C, device)
+    nb = max(1, scan_images // n_img)
+    batches = [make_push_inputs(n_img, C, H, W, h, w, P, K, device, SEED + 1000 * i) for i in range(nb)]
+    pc = batches[0][3]
+    protos = batches[0][1]  # one set of prototypes for the whole scan
     words = dpush.mask_words(K)  # push_prototypes computes it once per push (no per-call host sync)
+    states = [dpush.PushState.create(P, C, device) for _ in range(steps + warmup + 1)]
 
-    def run():
-        dpush.push_update(state, x, labels, protos, pc, 0, words=words)
+    def scan(state):
+        for i, (x, _, labels, _) in enumerate(batches):
+            dpush.push_update(state, x, labels, protos, pc, i * n_img, words=words)
 
-    for _ in range(warmup):
-        run()
+    for i in range(warmup):
+        scan(states[i])
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        run()
+    for i in range(steps):
+        scan(states[warmup + i])
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kname = []
-    argmin_s, launches = kernel_launch_times("push_argmin", run, steps, actual=kname)
-    argmin_call = argmin_s * launches
+    argmin_s, launches = kernel_launch_times("push_argmin", lambda: scan(states[-1]), 1, npair=2 * nb, actual=kname)
+    launches_per_call = launches // nb
+    argmin_call = argmin_s * launches_per_call
     flops = 2.0 * n_img * h * w * P * C
     nbytes = n_img * (C * h * w * 4 + h * w * 4)  # x read once + the u32 patch mask
-    return {"ms_per_img": round(elapsed / (steps * n_img) * 1e3, 4), "images_per_call": n_img,
-            "workload": f"push_prototypes inner step (push_update: mask+top-2 argmin+merge), labels {H}x{W} u8, "
-                        f"map {C}x{h}x{w} f32, P={P}, K={K}",
-            "argmin_kernel_ms_per_img": round(argmin_call / n_img * 1e3, 4), "argmin_launches_per_call": launches,
-            "roofline": roofline_entry(flops / launches, nbytes / launches, argmin_s, "f32") |
+    return {"ms_per_img": round(elapsed / (steps * nb * n_img) * 1e3, 4), "images_per_call": n_img,
+            "workload": f"push_prototypes inner step (push_update: mask+top-2 argmin+merge), a scan of {nb * n_img} "
+                        f"distinct images from a fresh state, labels {H}x{W} u8, map {C}x{h}x{w} f32, P={P}, K={K}",
+            "argmin_kernel_ms_per_img": round(argmin_call / n_img * 1e3, 4),
+            "argmin_launches_per_call": launches_per_call,
+            "roofline": roofline_entry(flops / launches_per_call, nbytes / launches_per_call, argmin_s, "f32") |
             {"kernel": kname[0] if kname else "push_argmin"}}
 
 
@@ -999,6 +1006,7 @@ def main():
     ap.add_argument("--push-images", type=int, default=8)
     ap.add_argument("--push-steps", type=int, default=5)
     ap.add_argument("--no-push", action="store_true")
+    ap.add_argument("--no-f32-line", action="store_true", help="skip the exact-f32 side line")
     ap.add_argument("--no-kld", action="store_true")
     ap.add_argument("--no-knn", action="store_true")
     ap.add_argument("--no-eval", action="store_true")
@@ -1066,6 +1074,20 @@ def main():
             line["plain_step_ms"] = round(e_plain / args.steps * 1e3, 4)
             line["ratio_to_plain_step"] = round(line["ms_per_step"] / line["plain_step_ms"], 3)
             kld[f"P{kstep.P}"] = line
+
+    # The same step with exact f32 products (v_mfma_f32_32x32x2_f32, the fma chain of the
+    # reference's fp32 conv): what the headline's bf16x3 products trade for their speed.
+    exact = None
+    if world == 1 and args.precision != "f32" and not args.no_f32_line:
+        fstep = LayerStep(args.batch, args.channels, args.fmap, args.fmap, args.protos, args.classes, x_dtype,
+                          device, SEED + rank, "f32")
+        e_f32, k_f32, a_f32 = time_layer(fstep, max(5, args.steps // 2), 3, 1, args.launch == "graph")
+        n_f = max(5, args.steps // 2)
+        exact = {"precision": "f32 (exact f32 products, v_mfma_f32_32x32x2_f32)", "prototypes": args.protos,
+                 "img_per_s": round(args.batch * n_f / e_f32, 1), "ms_per_step": round(e_f32 / n_f * 1e3, 4),
+                 "ratio_to_headline_step": round((e_f32 / n_f) / (elapsed / args.steps), 3),
+                 "kernels": {a_f32.get(k, k): {"ms": round(v * 1e3, 4)} for k, v in k_f32.items()}}
+        del fstep
 
     sigmoid = None
     if world == 1 and args.precision == "bf16x3" and args.channels == 64 and not args.no_sigmoid:
@@ -1137,6 +1159,8 @@ def main():
                 "roofline": roof_s, "kernels": kernels_s}
         if sigmoid is not None:
             out["add_on_sigmoid"] = sigmoid
+        if exact is not None:
+            out["exact_f32"] = exact
         if kld is not None:
             out["kld_step"] = kld
         if push is not None:

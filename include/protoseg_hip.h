@@ -166,6 +166,15 @@ int protoseg_l2_bwd_kld_supported(int B, int C, int H, int W, int P, int K, int 
                                   int max_per_class);
 
 /*
+ * Backward kernel override of the bf16x3 training backward at C = 64 (measurement and tests):
+ * "wave" (l2_bwd_wave.hip, 4 waves each owning a quarter of the prototypes), "fused"
+ * (l2_bwd_fused.hip, P <= 192 per launch), or "" / NULL for the automatic choice (wave above 192
+ * prototypes, fused below). The initial value is the PROTOSEG_BWD environment variable, read once.
+ * Replaces nothing in the reference (its backward is autograd); process-wide.
+ */
+int protoseg_set_backward_kernel(const char* name);
+
+/*
  * One operand prep per training step: the forward builds the backward's operand images (the
  * split P / W^T images and ||p||^2 in the backward kernel's layout) in the same prep launch as its
  * own, into a caller buffer the backward then reads instead of preparing them again.
@@ -177,7 +186,8 @@ int protoseg_l2_bwd_kld_supported(int B, int C, int H, int W, int P, int K, int 
  *   protoseg_l2_bwd_ex / protoseg_l2_bwd_kld_ex: protoseg_l2_bwd / _kld reading `operands`
  *     (NULL: prepared inside the call). The caller guarantees that protos, w_last, P, K, C, eps,
  *     act_kind (X_SIGMOID aside) and precision are those of the forward that filled it, that its
- *     values are unchanged since, and that PROTOSEG_BWD (the kernel override) did not change.
+ *     values are unchanged since, and that the backward kernel override (protoseg_set_backward_kernel)
+ *     did not change.
  * Results are bit-identical to the plain calls (the same prep arithmetic, tests/test_gpu_operands.py).
  */
 size_t protoseg_l2_train_operands_bytes(int C, int P, int K, int precision);
@@ -380,6 +390,16 @@ int protoseg_kld_backward(const float* dist, int B, int P, int HW, const void* l
                           const int32_t* proto_class, int K, int max_per_class, const float* g_loss,
                           void* workspace, size_t workspace_bytes, float* g_dist,
                           protoseg_stream_t stream);
+/*
+ * protoseg_kld_backward with the per-pair coefficients in a caller buffer of
+ * protoseg_kld_coef_bytes(B, K) bytes instead of the workspace's (dead) range-partial region, so
+ * the workspace is only read: a caller that must not mutate it (an autograd op) needs no copy.
+ */
+size_t protoseg_kld_coef_bytes(int B, int K);
+int protoseg_kld_backward_ex(const float* dist, int B, int P, int HW, const void* label, int label_dtype,
+                             const int32_t* proto_class, int K, int max_per_class, const float* g_loss,
+                             const void* workspace, size_t workspace_bytes, float* coef, size_t coef_bytes,
+                             float* g_dist, protoseg_stream_t stream);
 /*
  * The backward in the compact layout protoseg_l2_bwd_kld consumes (no [B, P, HW] tensor): the
  * gradient is non-zero only at the prototypes of each pixel's own class (module.py:173-178), so

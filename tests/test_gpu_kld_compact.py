@@ -63,14 +63,13 @@ def _layer_inputs(B, h, w, P, K, seed):
     return x, protos, w_last, g_logits
 
 
-@pytest.mark.parametrize("P,bwd", [(190, "fused"), (190, "onepass"), (361, "onepass"), (570, "onepass"),
-                                   (570, "fused"), (38, "fused"), (38, "wave"), (190, "wave"), (361, "wave"),
-                                   (570, "wave")])
-def test_l2_bwd_kld_equals_dense(device, monkeypatch, P, bwd):
+@pytest.mark.parametrize("P,bwd", [(190, "fused"), (570, "fused"), (38, "fused"), (38, "wave"), (190, "wave"),
+                                   (361, "wave"), (570, "wave")])
+def test_l2_bwd_kld_equals_dense(device, bwd_kernel, P, bwd):
     """protoseg_l2_bwd_kld == protoseg_l2_bwd on the expanded g_dist, bit for bit, for the fused
-    (P <= 192 per chunk) and one-pass (P <= 384 per chunk) kernels, chunked P included."""
+    (P <= 192 per chunk) and wave-owned (P <= 384 per chunk) kernels, chunked P included."""
     _lib, kld, ops = _mods()
-    monkeypatch.setenv("PROTOSEG_BWD", bwd)
+    bwd_kernel(bwd)
     B, h, w, K = 2, 33, 35, 19
     x, protos, w_last, g_logits = _layer_inputs(B, h, w, P, K, seed=P + 3)
     xd, pd, wd, gl = (t.to(device) for t in (x, protos, w_last, g_logits))

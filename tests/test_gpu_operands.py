@@ -1,6 +1,6 @@
 """One operand prep per training step (protoseg_l2_fwd_ex / protoseg_l2_bwd_ex / _kld_ex): the
 forward's prep launch also writes the training backward's operand images (the standard image
-block the wave-owned and fused kernels read; the one-pass block under PROTOSEG_BWD=onepass) into a
+block the wave-owned and fused kernels read) into a
 caller buffer, and the backward
 reads them instead of preparing its own. Same prep arithmetic, so every output is bit-identical
 to the plain calls; the autograd path (prototype_layer) passes the buffer through ctx."""
@@ -30,16 +30,14 @@ def _inputs(device, B, h, w, P, K, seed):
     (361, 19, None, "fused"),        # the metric's 19 prototypes/class: the wave-owned backward
     (190, 19, None, "fused"),        # 10 prototypes/class                 reads the standard block
     (96, 32, None, "fused"),
-    (190, 19, "onepass", "onepass"),  # PROTOSEG_BWD override: the one-pass block at Pp 256
-    (361, 19, "onepass", "onepass"),
     (190, 19, "wave", "fused"),
     (570, 19, None, "none"),         # two prototype chunks: no operands, plain calls
 ])
 @pytest.mark.parametrize("activation", ["log", "linear"])
-def test_fwd_bwd_with_operands_bit_identical(device, monkeypatch, P, K, bwd, kind, activation):
+def test_fwd_bwd_with_operands_bit_identical(device, bwd_kernel, P, K, bwd, kind, activation):
     _lib, ops = _ops()
     if bwd:
-        monkeypatch.setenv("PROTOSEG_BWD", bwd)
+        bwd_kernel(bwd)
     B, h, w = 2, 33, 31
     x, protos, w_last, g_logits, g_dist = _inputs(device, B, h, w, P, K, seed=P + K)
     act, prec = ops.ACT_KINDS[activation], ops.PRECISIONS["bf16x3"]
@@ -185,6 +183,73 @@ def test_adam_prep_equals_adam_then_prep(device, P, K, activation):
     got = _fwd_operands(_lib, x, p, w, act, prec, buf, ready=True)
     torch.cuda.synchronize()
     assert torch.equal(ref[0], got[0]) and torch.equal(ref[1], got[1])
+
+
+def test_adam_prep_with_other_groups_steps_each_tensor_once(device):
+    """An optimizer that also holds other groups (the reference's one joint Adam over backbone,
+    add-on, prototypes and last layer, module.py:391): layer_step_with_operands then step() updates
+    every tensor exactly once per iteration, the same bits and step counts as step() alone."""
+    _lib, ops = _ops()
+    from protoseg_amd.optim import Adam
+    prec, act = ops.PRECISIONS["bf16x3"], ops.ACT_KINDS["log"]
+    P, K = 190, 19
+    x, protos, w_last, _, _ = _inputs(device, 1, 9, 9, P, K, seed=11)
+    gen = torch.Generator().manual_seed(12)
+    rnd = lambda *s: torch.randn(*s, generator=gen).to(device)  # noqa: E731
+    grads = (1e-2 * rnd(P, 64), 1e-2 * rnd(K, P), 1e-2 * rnd(33, 7))
+    other = rnd(33, 7)
+    nbytes = ops.train_operands_bytes(64, P, K, prec)
+    runs = []
+    for fused in (False, True):
+        p = torch.nn.Parameter(protos.contiguous().clone())
+        w = torch.nn.Parameter(w_last.contiguous().clone())
+        o = torch.nn.Parameter(other.clone())
+        opt = Adam([{"params": [o], "lr": 1e-4, "weight_decay": 5e-4},
+                    {"params": [p], "lr": 2.5e-3, "weight_decay": 0.0},
+                    {"params": [w], "lr": 1e-3, "weight_decay": 5e-4}])
+        buf = torch.empty((nbytes,), device=device, dtype=torch.uint8)
+        for _ in range(3):
+            p.grad, w.grad, o.grad = (g.clone() for g in grads)
+            if fused:
+                assert opt.layer_step_with_operands(p, w, buf, 1e-4, act, prec)
+            opt.step()
+        torch.cuda.synchronize()
+        runs.append([t.detach().clone() for t in (p, w, o)] +
+                    [opt.state[t][k].clone() for t in (p, w, o) for k in ("exp_avg", "exp_avg_sq")] +
+                    [opt._counter(t).clone() for t in (p, w, o)])
+    for i, (a, b) in enumerate(zip(*runs)):
+        assert torch.equal(a, b), i
+    assert [int(c[0]) for c in runs[1][-3:]] == [3, 3, 3]
+
+
+def test_operands_ready_tracks_parameter_writes(device):
+    """Adam.operands_ready: True right after the fused update for the same block / eps / activation
+    / precision, False after any other write to either parameter (push's in-place copy) or for
+    another block or activation."""
+    _lib, ops = _ops()
+    from protoseg_amd.optim import Adam
+    prec, act = ops.PRECISIONS["bf16x3"], ops.ACT_KINDS["log"]
+    _, protos, w_last, _, _ = _inputs(device, 1, 9, 9, 190, 19, seed=13)
+    p = torch.nn.Parameter(protos.contiguous().clone())
+    w = torch.nn.Parameter(w_last.contiguous().clone())
+    opt = Adam([p, w], lr=1e-3)
+    buf = torch.empty((ops.train_operands_bytes(64, 190, 19, prec),), device=device, dtype=torch.uint8)
+    assert not opt.operands_ready(p, w, buf, 1e-4, act, prec)
+    p.grad, w.grad = torch.ones_like(p), torch.ones_like(w)
+    assert opt.layer_step_with_operands(p, w, buf, 1e-4, act, prec)
+    opt.step()
+    assert opt.operands_ready(p, w, buf, 1e-4, act, prec)
+    assert not opt.operands_ready(p, w, buf, 1e-4, ops.ACT_KINDS["linear"], prec)
+    assert not opt.operands_ready(p, w, buf.clone(), 1e-4, act, prec)
+    with torch.no_grad():
+        p.copy_(p.detach().clone())  # push_prototypes' write of the projected prototypes
+    assert not opt.operands_ready(p, w, buf, 1e-4, act, prec)
+    p.grad, w.grad = torch.ones_like(p), torch.ones_like(w)
+    assert opt.layer_step_with_operands(p, w, buf, 1e-4, act, prec)
+    opt.step()
+    assert opt.operands_ready(p, w, buf, 1e-4, act, prec)
+    w.data = w.data[:, :150].contiguous()  # prune_prototypes' column selection (a new address)
+    assert not opt.operands_ready(p, w, buf, 1e-4, act, prec)
 
 
 def test_operands_ready_refused_without_a_served_block(device):

@@ -447,6 +447,43 @@ def test_push_update_one_call_equals_three_calls(device):
         assert torch.equal(getattr(a, f), getattr(b, f)), f
 
 
+@pytest.mark.parametrize("P", [40, 190, 361])
+def test_push_update_scan_bound_keeps_state(device, P):
+    """A scan of many batches through protoseg_push_update, whose argmin skips candidates above
+    the running runner-up (push_argmin_wave_kernel's bound), leaves the same state bit for bit as
+    the unbounded mask -> argmin -> merge sequence: best distance, runner-up, image, patch and
+    winning feature vector. Later batches are pruned almost entirely (the bound is tight), and
+    one batch repeats an earlier image exactly, so exact cross-image ties meet the bound too."""
+    from protoseg_amd import _lib
+    push = _push()
+    C, h, w, K, n = 64, 33, 65, 19, 4
+    gen = torch.Generator().manual_seed(5)
+    pc = torch.argmax(po.class_identity(P, K), dim=1).to(torch.int32).to(device)
+    protos = torch.rand(P, C, generator=gen).to(device)
+    a, b = push.PushState.create(P, C, device), push.PushState.create(P, C, device)
+    xs = []
+    for bi in range(8):
+        x = torch.sigmoid(2 * torch.randn(n, C, h, w, generator=gen)).to(device)
+        if bi == 5:
+            x[1] = xs[0][2]  # an exact repeat of an earlier image: ties at the running best
+        xs.append(x)
+        lab = torch.from_numpy(np.random.default_rng(bi).integers(0, K + 1, size=(n, 4 * h, 4 * w))).to(device)
+        if bi == 5:
+            lab[1] = torch.from_numpy(np.random.default_rng(0).integers(0, K + 1, size=(n, 4 * h, 4 * w))[2]).to(device)
+        first = bi * n
+        push.push_update(a, x, lab, protos, pc, first)
+        mask = push.patch_class_mask(lab, h, w)
+        keys, second = push.push_argmin(x, protos, pc, mask, with_second=True)
+        with torch.cuda.device(device):
+            _lib.call("protoseg_push_merge", _lib.ptr(keys), _lib.ptr(second), n, first, _lib.ptr(x), C, h * w, P,
+                      _lib.ptr(b.dist), _lib.ptr(b.second), _lib.ptr(b.img), _lib.ptr(b.patch), _lib.ptr(b.fmap),
+                      _lib.stream_of(device))
+    torch.cuda.synchronize()
+    for f in ("dist", "second", "img", "patch", "fmap"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    assert (a.img >= 0).all()
+
+
 def test_push_prototypes_kxk_prototypes(device, tmp_path):
     """push_prototypes with 2 x 2 prototypes (push.py:276-280 keeps the k x k window
     protoL_input_[:, i:i+h, j:j+w]): the scan runs on the unfolded map; winners, patches and the

@@ -1,12 +1,11 @@
-"""The training backwards that serve up to 384 prototypes per launch, against the oracle's autograd
+"""The training backward that serves up to 384 prototypes per launch, against the oracle's autograd
 of model.py:203-283 and against the 192-prototype fused kernel:
-  onepass  l2_bwd_onepass.hip: 8 waves with equal roles, 16x16x32 bf16 MFMA;
   wave     l2_bwd_wave.hip: 4 waves, one per SIMD, each owning a quarter of the prototypes for
-           every product, 32x32x16 bf16 MFMA.
-Both bf16x3 products. PROTOSEG_BWD selects the kernel per call (wave / onepass / fused).
+           every product, 32x32x16 bf16 MFMA (bf16x3 products).
+protoseg_set_backward_kernel (the bwd_kernel fixture) selects the kernel per call (wave / fused).
 Tolerance: rtol 1e-4 of each gradient's own scale, as tests/test_gpu_l2.py."""
 
-KERNELS = ["onepass", "wave"]
+KERNELS = ["wave"]
 import pytest
 import torch
 
@@ -28,7 +27,7 @@ def assert_scaled_close(a, ref, rtol=1e-4, name=""):
 
 
 @pytest.mark.parametrize("B,h,w,P,K", [
-    (2, 17, 17, 38, 19),     # one 16-prototype tile per wave (Pp 128)
+    (2, 17, 17, 38, 19),     # one 32-prototype block (Pp 128)
     (1, 9, 11, 100, 5),      # ragged pixel tail, 5 classes
     (2, 65, 65, 190, 19),    # cityscapes_*_imnet.gin, 10 prototypes/class (Pp 256)
     (2, 41, 41, 210, 21),    # pascal: 21 classes
@@ -38,8 +37,8 @@ def assert_scaled_close(a, ref, rtol=1e-4, name=""):
 ])
 @pytest.mark.parametrize("activation", ["log", "linear"])
 @pytest.mark.parametrize("kernel", KERNELS)
-def test_onepass_backward_vs_oracle(device, monkeypatch, B, h, w, P, K, activation, kernel):
-    monkeypatch.setenv("PROTOSEG_BWD", kernel)
+def test_wave_backward_vs_oracle(device, bwd_kernel, B, h, w, P, K, activation, kernel):
+    bwd_kernel(kernel)
     ops = _ops()
     x, protos, w_last = po.synthetic_inputs(B, 64, h, w, P, K, seed=B * 100 + h + P)
     gen = torch.Generator().manual_seed(11)
@@ -56,8 +55,8 @@ def test_onepass_backward_vs_oracle(device, monkeypatch, B, h, w, P, K, activati
 
 @pytest.mark.parametrize("P", [190, 361])
 @pytest.mark.parametrize("kernel", KERNELS)
-def test_onepass_backward_with_g_dist(device, monkeypatch, P, kernel):
-    monkeypatch.setenv("PROTOSEG_BWD", kernel)
+def test_wave_backward_with_g_dist(device, bwd_kernel, P, kernel):
+    bwd_kernel(kernel)
     ops = _ops()
     B, h, w, K = 2, 33, 31, 19
     x, protos, w_last = po.synthetic_inputs(B, 64, h, w, P, K, seed=P)
@@ -75,7 +74,7 @@ def test_onepass_backward_with_g_dist(device, monkeypatch, P, kernel):
 
 @pytest.mark.parametrize("P", [190, 361])
 @pytest.mark.parametrize("kernel", KERNELS)
-def test_onepass_equals_fused_within_rounding(device, monkeypatch, P, kernel):
+def test_wave_equals_fused_within_rounding(device, bwd_kernel, P, kernel):
     """The same gradients from both kernels (different MFMA shapes and summation orders)."""
     ops = _ops()
     B, h, w, K = 4, 65, 65, 19
@@ -83,9 +82,9 @@ def test_onepass_equals_fused_within_rounding(device, monkeypatch, P, kernel):
     g_logits = torch.randn(B, h, w, K, generator=torch.Generator().manual_seed(2))
     args = (x.to(device), protos.to(device), w_last.to(device), g_logits.to(device), None, 1e-4, 0,
             ops.PRECISIONS["bf16x3"], True, True, True)
-    monkeypatch.setenv("PROTOSEG_BWD", "fused")
+    bwd_kernel("fused")
     a = ops.l2_backward(*args)
-    monkeypatch.setenv("PROTOSEG_BWD", kernel)
+    bwd_kernel(kernel)
     b = ops.l2_backward(*args)
     torch.cuda.synchronize()
     for u, v, name in zip(a, b, ("g_x", "g_protos", "g_w")):
@@ -93,8 +92,8 @@ def test_onepass_equals_fused_within_rounding(device, monkeypatch, P, kernel):
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
-def test_onepass_deterministic(device, monkeypatch, kernel):
-    monkeypatch.setenv("PROTOSEG_BWD", kernel)
+def test_wave_deterministic(device, bwd_kernel, kernel):
+    bwd_kernel(kernel)
     ops = _ops()
     B, h, w, P, K = 8, 65, 65, 361, 19
     x, protos, w_last = po.synthetic_inputs(B, 64, h, w, P, K, seed=1)
@@ -109,11 +108,11 @@ def test_onepass_deterministic(device, monkeypatch, kernel):
 
 @pytest.mark.parametrize("xdtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("kernel", KERNELS)
-def test_onepass_x_sigmoid_and_bf16_features(device, monkeypatch, xdtype, kernel):
+def test_wave_x_sigmoid_and_bf16_features(device, bwd_kernel, xdtype, kernel):
     from protoseg_amd import _lib
     """PROTOSEG_X_SIGMOID (the add-on nn.Sigmoid on the x load) and bf16 feature maps at P = 361:
     against the oracle on sigmoid(pre-activation), gradient taken w.r.t. the pre-activation."""
-    monkeypatch.setenv("PROTOSEG_BWD", "onepass")
+    bwd_kernel("wave")
     ops = _ops()
     B, h, w, P, K = 2, 21, 23, 361, 19
     gen = torch.Generator().manual_seed(9)

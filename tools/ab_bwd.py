@@ -1,8 +1,8 @@
-"""Interleaved A/B of the training-backward kernels selected by PROTOSEG_BWD (wave / onepass /
-fused) at one shape, in one process: per rep, each kernel's forward + backward call on its own
+"""Interleaved A/B of the training-backward kernels selected by protoseg_set_backward_kernel
+(wave / fused) at one shape, in one process: per rep, each kernel's forward + backward call on its own
 LayerStep (same seed, same inputs), the backward call timed with HIP events and the backward
 kernel alone with the library's per-launch event hook. Also checks that the gradients agree.
-usage: python tools/ab_bwd.py --protos 361 --batch 32 --kernels onepass,wave [--reps 30]"""
+usage: python tools/ab_bwd.py --protos 190 --batch 32 --kernels fused,wave [--reps 30]"""
 import argparse
 import ctypes
 import os
@@ -25,13 +25,13 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--fmap", type=int, default=65)
     ap.add_argument("--reps", type=int, default=30)
-    ap.add_argument("--kernels", default="onepass,wave")
+    ap.add_argument("--kernels", default="fused,wave")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     kernels = a.kernels.split(",")
     steps = {}
     for k in kernels:
-        os.environ["PROTOSEG_BWD"] = k
+        _lib.call("protoseg_set_backward_kernel", k.encode())
         steps[k] = LayerStep(a.batch, 64, a.fmap, a.fmap, a.protos, 19, torch.float32, dev, 20220227)
     lib = _lib.load()
     s = torch.cuda.Stream(dev)
@@ -46,7 +46,7 @@ def main():
         call, kern = {k: [] for k in kernels}, {k: [] for k in kernels}
         for rep in range(a.reps + 3):
             for k in kernels:
-                os.environ["PROTOSEG_BWD"] = k
+                _lib.call("protoseg_set_backward_kernel", k.encode())
                 st = steps[k]
                 st.fwd()
                 ev[0].record(s)

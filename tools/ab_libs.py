@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--fmap", type=int, default=65)
     ap.add_argument("--reps", type=int, default=40)
-    ap.add_argument("--main-bwd", default="", help="PROTOSEG_BWD values to run the main library with")
+    ap.add_argument("--main-bwd", default="", help="backward kernels (protoseg_set_backward_kernel) to run the main library with")
     ap.add_argument("--call", default="bwd_full", choices=["bwd_full", "bwd_full_xsig", "fwd", "fwd_xsig", "push", "mask", "kld", "kldb", "kldc",
                                                        "bwdk"])
     args = ap.parse_args()
@@ -48,7 +48,7 @@ def main():
     logits = torch.empty(B, h, w, K, device=dev)
     gx, gp, gw = torch.empty_like(x), torch.empty(P, C, device=dev), torch.empty(K, P, device=dev)
     libs = {"main": load(os.path.join(CSRC, "libprotoseg_hip.so"))}
-    # PROTOSEG_BWD per library: --main-bwd for main (several: main@k1, main@k2 entries), a BWD file
+    # backward kernel per library: --main-bwd for main (several: main@k1, main@k2 entries), a BWD file
     # in a variant's directory for that variant (else the process environment)
     bwd_of = {}
     if args.main_bwd:
@@ -106,7 +106,8 @@ def main():
 
     def call(lib, name=None):
         if name in bwd_of:
-            os.environ["PROTOSEG_BWD"] = bwd_of[name]
+            if hasattr(lib, "protoseg_set_backward_kernel"):
+                lib.protoseg_set_backward_kernel(bwd_of[name].encode())
         if args.call == "mask":
             st = lib.protoseg_patch_class_mask(P_(lab), _lib.U8, n_img, 1024, 2048, ph, pw, None, 0, P_(mask), s)
         elif args.call in ("kld", "kldb", "kldc"):

@@ -1,5 +1,5 @@
 """Runs the training backward (protoseg_l2_bwd: g_x, g_P, g_W) a few times at one shape, for
-rocprofv3 kernel traces / counter passes. PROTOSEG_BWD selects the kernel (fused / onepass)."""
+rocprofv3 kernel traces / counter passes. PROTOSEG_BWD (read once by the library) selects the kernel (fused / wave)."""
 import argparse
 import ctypes
 import os
