@@ -19,6 +19,7 @@
 // a fixed order: deterministic, no atomics). Every operand is addressed by (row, k, batch) strides,
 // so no tensor is transposed or copied; NCHW rows give coalesced loads and stores along pixels.
 #include "bf16_split.h"
+#include "l2_bf16_common.h"
 #include "protoseg_device.h"
 #include "protoseg_host.h"
 #include "l2_launch.h"
@@ -631,6 +632,299 @@ Operand op(const void* p, long long sr, long long sk, long long sb) {
   return Operand{p, static_cast<unsigned>(sr), static_cast<unsigned>(sk), static_cast<unsigned>(sb)};
 }
 
+#ifndef WIDE_F16_MFMA
+#define WIDE_F16_MFMA 1  // the fp16 distance GEMM below (0: the bf16x3 64 x 64 tile, for A/B)
+#endif
+// ---- fp16 feature maps (BASELINE configs[4]): the distance GEMM on v_mfma_f32_32x32x16_f16 ----
+// x is exact in fp16. Each prototype row p is scaled by a power of two s_p (its largest |value|
+// lands in [2^13, 2^14): no fp16 overflow, small values kept normal) and split into two fp16
+// terms, p s_p = hi + lo (22 significant bits, |err| <= 2^-22 |p| s_p: finer than bf16x3's
+// 3 x 2^-16). Then x.p = (x.hi + x.lo) / s_p: two f16 MFMAs per product instead of bf16x3's
+// three, and no operand conversion in the GEMM (the split rows are built once per call by
+// wide_f16_prep_kernel, x is read as stored). Epilogue as wide_gemm_kernel's kEpiDist: x2 from
+// the staged x (fixed order), p2 exact in f32 from the prep, relu(x2 + p2 - 2 x.p).
+// Workgroup: a 192-prototype x 128-pixel tile (4 waves, one per SIMD, each 3 x 2 blocks of
+// 32 x 32), K in 32-channel stages, three LDS stages in flight by 16-B LDS-DMA (lane-linear
+// pieces, swizzled through the source addresses), one barrier per stage.
+constexpr int kF16TM = 192, kF16TN = 128, kF16TK = 32, kF16NS = 3;
+constexpr int kF16ATerm = kF16TM * kF16TK * 2;             // one term's A stage [192 rows][64 B]
+constexpr int kF16BTile = kF16TK * kF16TN * 2;             // the x stage [32 channels][256 B]
+constexpr int kF16Stage = 2 * kF16ATerm + kF16BTile;       // 32 KiB
+constexpr int kF16Lds = kF16NS * kF16Stage + 4 * kF16TN * 4 + 2 * kF16TM * 4;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef short f16s4 __attribute__((ext_vector_type(4)));
+
+struct F16DistArgs {
+  const _Float16* x;      // [B][C][HW]
+  unsigned x_bytes;
+  const _Float16* ahi;    // [Mpad][Kpad]: scaled hi terms
+  const _Float16* alo;    //               scaled lo terms
+  unsigned a_bytes;       // bytes of one term
+  const float* p2;        // [Mpad]: ||p||^2 (exact f32)
+  const float* inv_s;     // [Mpad]: 1 / s_p (a power of two)
+  int P, C, Kpad, HW, ntot;
+  float* dist;            // [B][P][HW]
+  unsigned d_bytes;
+  float* act;             // optional [(b HW + n)][P]
+  int act_kind;
+  float eps;
+};
+
+// One wave per prototype row: s_p, the two fp16 terms of p s_p ([Mpad][Kpad], zero padding), ||p||^2.
+__global__ __launch_bounds__(256) void wide_f16_prep_kernel(const float* __restrict__ protos, int P, int C, int Mpad,
+                                                           int Kpad, _Float16* __restrict__ ahi,
+                                                           _Float16* __restrict__ alo, float* __restrict__ p2,
+                                                           float* __restrict__ inv_s) {
+  const int lane = threadIdx.x & 63, row = static_cast<int>(blockIdx.x) * 4 + static_cast<int>(threadIdx.x >> 6);
+  if (row >= Mpad) return;
+  const bool valid = row < P;
+  const float* pr = protos + static_cast<size_t>(valid ? row : 0) * C;
+  float mx = 0.f, sq = 0.f;
+  for (int c = lane; c < C; c += 64) {
+    const float v = valid ? pr[c] : 0.f;
+    mx = fmaxf(mx, fabsf(v));
+    sq = fmaf(v, v, sq);
+  }
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {  // butterfly: every lane ends with the same (fixed-order) sums
+    mx = fmaxf(mx, __shfl_xor(mx, m));
+    sq += __shfl_xor(sq, m);
+  }
+  int e = 0;
+  (void)frexpf(mx, &e);  // mx < 2^e
+  if (!(mx < 3.0e38f) || mx == 0.f) e = 14;  // zero / non-finite rows: s_p = 1
+  e = e < -100 ? -100 : e;
+  const float scale = ldexpf(1.f, 14 - e), inv = ldexpf(1.f, e - 14);
+  _Float16* hr = ahi + static_cast<size_t>(row) * Kpad;
+  _Float16* lr = alo + static_cast<size_t>(row) * Kpad;
+  for (int k = lane; k < Kpad; k += 64) {
+    const float v = (valid && k < C ? pr[k] : 0.f) * scale;  // exact (power of two)
+    const _Float16 hi = static_cast<_Float16>(v);
+    hr[k] = hi;
+    lr[k] = static_cast<_Float16>(v - static_cast<float>(hi));  // v - hi exact in f32
+  }
+  if (lane == 0) {
+    p2[row] = valid ? sq : 0.f;
+    inv_s[row] = inv;
+  }
+}
+
+// 16-B LDS-DMA of one wave-instruction (1 KiB, lane-linear at lds + 16 lane); out-of-range
+// lanes land as zeros. Inline asm so the compiler does not drain it before unrelated LDS reads
+// (the dma<> note in l2_bf16_common.h); the kernel waits for it itself.
+__device__ __forceinline__ void dma16(rsrc_t r, unsigned lds, unsigned voff, unsigned soff) {
+  unsigned so = __builtin_amdgcn_readfirstlane(soff);
+  asm volatile("" : "+s"(so));
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(__builtin_amdgcn_readfirstlane(lds)), "s"(r), "s"(so)
+               : "memory");
+}
+
+// x stage image: 256-B rows (one channel, 128 pixels), 16-B chunk ch of row r at
+// 256 r + 16 (ch ^ swz) (cdna_hip_programming.md T10 image (b): the transposed reads of the
+// 32x32x16 B operand are conflict-free)
+__device__ __forceinline__ constexpr int f16_bswz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+// A stage image: 64-B rows, 16-B chunk ch of row r at 64 r + 16 (ch ^ ((r >> 2) & 3)) (the
+// ds_read_b128 row reads of 16 rows per lane group land on distinct banks)
+__device__ __forceinline__ constexpr int f16_aswz(int r) { return (r >> 2) & 3; }
+
+__global__ __launch_bounds__(256, 1) void wide_dist_f16_kernel(F16DistArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
+  const unsigned S0 = static_cast<unsigned>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)fsm));
+  const int lane = threadIdx.x & 63, wave = bf16l::wave_id(), j = lane & 31, h = lane >> 5;
+  const int n0 = static_cast<int>(blockIdx.x) * kF16TN, m0 = static_cast<int>(blockIdx.y) * kF16TM;
+  const rsrc_t rx = make_rsrc(a.x, a.x_bytes), rah = make_rsrc(a.ahi, a.a_bytes), ral = make_rsrc(a.alo, a.a_bytes);
+  float* red = reinterpret_cast<float*>(fsm + kF16NS * kF16Stage);     // [4][128] x2 partials
+  float* rowv = red + 4 * kF16TN;                                     // [192] p2, [192] 1 / s_p
+  for (int i = static_cast<int>(threadIdx.x); i < kF16TM; i += 256) {
+    rowv[i] = a.p2[m0 + i];
+    rowv[kF16TM + i] = a.inv_s[m0 + i];
+  }
+
+  // DMA pieces of a stage: 24 of A (term q / 12, rows 16 (q % 12) ..) and 8 of x (channels
+  // 4 (q - 24) ..); wave w issues pieces 8 w .. 8 w + 7. Per-lane source offsets (k0 = 0):
+  unsigned voff[8];
+  int crow_of[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int q = 8 * wave + i;
+    crow_of[i] = -1;
+    if (q < 24) {
+      const int r = 16 * (q % 12) + (lane >> 2), pc = lane & 3, lc = pc ^ f16_aswz(r);
+      voff[i] = static_cast<unsigned>(((m0 + r) * a.Kpad + 8 * lc) * 2);
+    } else {
+      const int crow = 4 * (q - 24) + (lane >> 4), pc = lane & 15, lc = pc ^ f16_bswz(crow);
+      const int col = n0 + 8 * lc;
+      crow_of[i] = crow;
+      if (col < a.ntot) {
+        const int b = col / a.HW, n = col - b * a.HW;
+        voff[i] = static_cast<unsigned>(((b * a.C + crow) * a.HW + n) * 2);
+      } else {
+        voff[i] = kOOB;
+      }
+    }
+  }
+  auto issue = [&](int st) __attribute__((always_inline)) {
+    const int k0 = st * kF16TK;
+    const unsigned base = S0 + static_cast<unsigned>((st % kF16NS) * kF16Stage);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int q = 8 * wave + i;  // wave-uniform
+      if (q < 24) {
+        dma16(q < 12 ? rah : ral, base + static_cast<unsigned>((q / 12) * kF16ATerm + (q % 12) * 1024), voff[i],
+              static_cast<unsigned>(k0 * 2));
+      } else {
+        const bool ok = voff[i] != kOOB && k0 + crow_of[i] < a.C;
+        dma16(rx, base + static_cast<unsigned>(2 * kF16ATerm + (q - 24) * 1024), ok ? voff[i] : kOOB,
+              static_cast<unsigned>(k0 * a.HW * 2));
+      }
+    }
+  };
+
+  // wave w: prototype rows 96 (w & 1) + 32 i (i < 3), pixel columns 64 (w >> 1) + 32 jj (jj < 2)
+  const int rg = wave & 1, cp = wave >> 1;
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  f32x16 acc[3][2];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) acc[i][0] = acc[i][1] = zero16();
+  // x2: thread t sums columns 2 (t & 63), 2 (t & 63) + 1 over channel rows 8 (t >> 6) .. + 7 of each stage
+  float xs0 = 0.f, xs1 = 0.f;
+  const int xcp = threadIdx.x & 63, xsl = threadIdx.x >> 6;
+
+  const int nst = a.Kpad / kF16TK;
+  issue(0);
+  if (nst > 1) issue(1);
+  for (int st = 0; st < nst; ++st) {
+    if (st + 1 < nst) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    if (st + 2 < nst) issue(st + 2);
+    const unsigned sb = S0 + static_cast<unsigned>((st % kF16NS) * kF16Stage);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f16x8 af[3][2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int r = 96 * rg + 32 * i + j;
+        const unsigned ao = static_cast<unsigned>(r * 64 + 16 * ((2 * ks + h) ^ f16_aswz(r)));
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          af[i][t] = *reinterpret_cast<const __attribute__((address_space(3))) f16x8*>(
+              static_cast<uintptr_t>(sb + static_cast<unsigned>(t * kF16ATerm) + ao));
+      }
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        // block (channel rows 16 ks + 8 h (+4), pixel columns 64 cp + 32 jj + 16 (g & 1) ..):
+        // lane 4 q + p of the 16-lane group supplies row r0 + q, columns + 4 p .. + 3
+        const int ch = 8 * cp + 4 * jj + 2 * (g & 1) + (p4 >> 1);
+        f16s4 v[2];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          const int r = 16 * ks + 8 * h + 4 * hf + q4;
+          const unsigned bo = static_cast<unsigned>(2 * kF16ATerm + 256 * r + 16 * (ch ^ f16_bswz(r)) + 8 * (p4 & 1));
+          v[hf] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              reinterpret_cast<__attribute__((address_space(3))) f16s4*>(static_cast<uintptr_t>(sb + bo)));
+        }
+        bfr[jj] = __builtin_bit_cast(f16x8, __builtin_shufflevector(v[0], v[1], 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i][1], bfr[jj], acc[i][jj], 0, 0, 0);
+          acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i][0], bfr[jj], acc[i][jj], 0, 0, 0);
+        }
+    }
+    // this thread's x2 rows of the stage (zeros past C / past the pixels: the DMA filled them so)
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) {
+      const int r = 8 * xsl + rr, col = 2 * xcp;
+      const unsigned o = static_cast<unsigned>(2 * kF16ATerm + 256 * r + 16 * ((col >> 3) ^ f16_bswz(r)) + 2 * (col & 7));
+      const uint32_t w2 = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(static_cast<uintptr_t>(sb + o));
+      const float v0 = static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(w2 & 0xffffu)));
+      const float v1 = static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(w2 >> 16)));
+      xs0 = fmaf(v0, v0, xs0);
+      xs1 = fmaf(v1, v1, xs1);
+    }
+  }
+  red[xsl * kF16TN + 2 * xcp] = xs0;
+  red[xsl * kF16TN + 2 * xcp + 1] = xs1;
+  __syncthreads();
+
+  const rsrc_t rd = make_rsrc(a.dist, a.d_bytes);
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int cn = 64 * cp + 32 * jj + j, col = n0 + cn;
+    const float x2 = ((red[cn] + red[kF16TN + cn]) + red[2 * kF16TN + cn]) + red[3 * kF16TN + cn];
+    const int b = col < a.ntot ? col / a.HW : 0, n = col - b * a.HW;
+    // the lane's part of the address (pixel, row 4h) in the voffset, the register's row in the
+    // (uniform) soffset
+    const unsigned cbase = col < a.ntot ? static_cast<unsigned>((b * a.P * a.HW + n + 4 * h * a.HW) * 4) : kOOB;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int rl = 96 * rg + 32 * i;
+      float p2r[16], isr[16];
+      bf16l::load_rows16(rowv + rl + 4 * h, p2r);
+      bf16l::load_rows16(rowv + kF16TM + rl + 4 * h, isr);
+      float d[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mu = m0 + rl + row_of(r);  // wave-uniform; this lane's row is mu + 4h
+        d[r] = l2_distance(x2, p2r[r], acc[i][jj][r] * isr[r]);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(d[r]), rd, mu + 4 * h < a.P ? cbase : kOOB,
+                                              static_cast<unsigned>(mu * a.HW * 4), 0);
+      }
+      if (a.act && col < a.ntot) {  // (return_activations: [pixel][P], uncoalesced; not the training path)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + rl + row_of(r) + 4 * h;
+          if (m < a.P) a.act[static_cast<size_t>(col) * a.P + m] = activation(d[r], a.eps, a.act_kind);
+        }
+      }
+    }
+  }
+}
+
+int wide_distances_f16(const Geometry& g, const _Float16* x, const float* protos, float eps, int act_kind,
+                       float* dist, float* act, hipStream_t s) {
+  const int Mpad = static_cast<int>(ceil_div(g.P, kF16TM)) * kF16TM;
+  const int Kpad = static_cast<int>(ceil_div(g.C, kF16TK)) * kF16TK;
+  const size_t term = static_cast<size_t>(Mpad) * Kpad * 2;
+  void* sc = nullptr;
+  if (int st = stream_scratch(ScratchKind::kWideF16, 2 * term + static_cast<size_t>(Mpad) * 8, 1u << 20, s, &sc))
+    return st;
+  auto* ahi = static_cast<_Float16*>(sc);
+  auto* alo = reinterpret_cast<_Float16*>(static_cast<unsigned char*>(sc) + term);
+  auto* p2 = reinterpret_cast<float*>(static_cast<unsigned char*>(sc) + 2 * term);
+  float* inv_s = p2 + Mpad;
+  hipLaunchKernelGGL(wide_f16_prep_kernel, dim3(static_cast<unsigned>(Mpad / 4)), dim3(256), 0, s, protos, g.P, g.C,
+                     Mpad, Kpad, ahi, alo, p2, inv_s);
+  if (int st = check_launch("wide_f16_prep_kernel")) return st;
+  if (int e = ensure_lds<wide_dist_f16_kernel, kF16Lds>()) return e;
+  F16DistArgs a{};
+  a.x = x;
+  a.x_bytes = static_cast<unsigned>(static_cast<size_t>(g.npix) * g.C * 2);
+  a.ahi = ahi, a.alo = alo, a.a_bytes = static_cast<unsigned>(term);
+  a.p2 = p2, a.inv_s = inv_s;
+  a.P = g.P, a.C = g.C, a.Kpad = Kpad, a.HW = g.HW, a.ntot = g.npix;
+  a.dist = dist, a.d_bytes = static_cast<unsigned>(static_cast<size_t>(g.npix) * g.P * 4);
+  a.act = act, a.act_kind = act_kind, a.eps = eps;
+  KernelTimer timer("wide_dist_f16_kernel", s);
+  hipLaunchKernelGGL(wide_dist_f16_kernel, dim3(static_cast<unsigned>(ceil_div(g.npix, kF16TN)),
+                                                static_cast<unsigned>(Mpad / kF16TM)),
+                     dim3(256), kF16Lds, s, a);
+  return check_launch("wide_dist_f16_kernel");
+}
+
+// The fp16 path serves bf16x3 requests on fp16 maps whose 8-pixel runs stay inside one image
+// and whose tensors stay below 2^31 bytes (buffer offsets).
+bool wide_f16_fits(const Geometry& g, const void* x) {
+  return g.HW % 8 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0 &&
+         static_cast<long long>(g.npix) * g.C * 2 < (1LL << 31) && static_cast<long long>(g.npix) * g.P * 4 < (1LL << 31) &&
+         static_cast<long long>(ceil_div(g.P, kF16TM)) * kF16TM * ceil_div(g.C, kF16TK) * kF16TK * 2 < (1LL << 31);
+}
+
 // D[b][p][n] into `dist` (ld P per image), optional act[g][p].
 template <typename TX>
 int wide_distances(const Geometry& g, const TX* x, const float* protos, float eps, int act_kind, float* dist,
@@ -644,6 +938,9 @@ int wide_distances(const Geometry& g, const TX* x, const float* protos, float ep
   a.eps = eps, a.act_kind = act_kind;
   a.act = act, a.am = 1, a.an = g.P, a.ab = static_cast<long long>(g.HW) * g.P;  // act[(b HW + n) P + p]
   a.bf3 = bf3;
+  if constexpr (std::is_same_v<TX, _Float16>) {
+    if (bf3 && WIDE_F16_MFMA && wide_f16_fits(g, x)) return wide_distances_f16(g, x, protos, eps, act_kind, dist, act, s);
+  }
   return gemm<kEpiDist, float, TX, -1, -1, float>(a, B, s);
 }
 

@@ -21,7 +21,7 @@ int check_launch(const char* what);
 // call's kernels still read. A call that needs more takes a new block (1.5x growth, at least
 // `min_bytes`) and retires the old one without freeing it: a graph that captured an earlier call
 // still points there, and a replay must not touch freed memory.
-enum class ScratchKind : int { kImages = 0, kUnused1 = 1, kWideForward = 2, kWidePush = 3, kPush = 4, kPushUpdate = 5 };
+enum class ScratchKind : int { kImages = 0, kWideF16 = 1, kWideForward = 2, kWidePush = 3, kPush = 4, kPushUpdate = 5 };
 int stream_scratch(ScratchKind kind, size_t need, size_t min_bytes, hipStream_t s, void** out);
 
 // gfx950 has 160 KiB of LDS per CU; a kernel opts in once to dynamic LDS above 64 KiB.

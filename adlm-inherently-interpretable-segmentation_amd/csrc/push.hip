@@ -5,7 +5,8 @@
 // image to the host and runs (a) a 2M-iteration Python loop mapping pixels to patch sets,
 // (b) a per-prototype gather + np.argmin. Here both stay on the device:
 //   patch_mask_kernel   label map -> uint32 class bitmask per patch (push.py:184-186, 214-223)
-//   push_argmin_kernel  fused distance + masked per-prototype top-2 keys (push.py:249-263)
+//   push_argmin_wave_kernel  fused distance (bf16x6 products, C = 32 / 64) + masked per-prototype
+//                       top-2 keys (push.py:249-263); push_argmin_kernel the same for C = 128 (f32)
 //   push_top2_kernel    folds the pixel stripes' partial top-2
 //   push_merge_kernel   strict-'<' fold in image order + winner gather (push.py:265-281)
 //   push_top2_merge_kernel  the two above in one launch (protoseg_push_update, native path)
@@ -308,14 +309,55 @@ __global__ __launch_bounds__(kPushMaxTiles * kPushSplit * 64) void push_argmin_k
   }
 }
 
-// Wave-streamed push argmin (the default): every wave owns whole 32-pixel tiles of one image and
+// ---- push distances on bf16 MFMA with exact three-term splits (bf16x6), C = 32 / 64 ---------
+// Each f32 operand is split exactly into three bf16 terms (8 + 8 + 8 significant bits), and a
+// product x.p is the sum of the six largest cross products (the three dropped ones are below
+// 2^-24 relative): f32-class distances, as the f32 fma chain's, at 2.7x the v_mfma_f32_32x32x2_f32
+// rate (6 v_mfma_f32_32x32x16_bf16 of 32 cycles per 16 channels, against 8 of 64). Layout B of
+// the f32 kernel (rows = pixels, columns = prototypes); k-step s (16 channels) of lane half h
+// holds channels push_chan(s, h, 0..7) = 32 (s >> 1) + 16 h + 8 (s & 1) + e, which are the
+// channels a lane's x registers hold (xr[16 ct + r] = x[32 ct + 16 h + r]). push_dist_kernel forms
+// the same products in the same order, so a tie is exactly a tie the argmin saw.
+__device__ __forceinline__ constexpr int push_chan(int s, int h, int e) { return 32 * (s >> 1) + 16 * h + 8 * (s & 1) + e; }
+// the x registers of a pixel tile -> the A fragments of the 2 NC k-steps (3 terms each)
+template <int NC>
+__device__ __forceinline__ void push_split_x(const float (&xr)[NC * 16], bf16x8 (&af)[2 * NC][3]) {
+#pragma unroll
+  for (int s = 0; s < 2 * NC; ++s) {
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = xr[16 * (s >> 1) + 8 * (s & 1) + e];
+    split8<3>(v, af[s]);
+  }
+}
+// (x || p)^T products of one prototype tile, k-steps in order, terms smallest first (mma_split<3>)
+template <int NC>
+__device__ __forceinline__ f32x16 push_xp(const bf16x8 (&af)[2 * NC][3], const bf16x8 (&bf)[2 * NC][3]) {
+  f32x16 acc = zero16();
+#pragma unroll
+  for (int s = 0; s < 2 * NC; ++s) acc = mma_split<3>(af[s], bf[s], acc);
+  return acc;
+}
+// ||p||^2 of prototype row pr (f32, C = 32 NC) in the lane half's fixed order, halves added: the
+// value every push distance of the row uses
+template <int NC>
+__device__ __forceinline__ float push_p2(const float* __restrict__ pr, int h) {
+  float s = 0.f;
+#pragma unroll
+  for (int ct = 0; ct < NC; ++ct)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s = fmaf(pr[ct * 32 + 16 * h + r], pr[ct * 32 + 16 * h + r], s);
+  return s + __shfl_xor(s, 32);
+}
+
+// Wave-streamed push argmin (C = 32 / 64): every wave owns whole 32-pixel tiles of one image and
 // runs ALL of the launch chunk's prototype tiles on each, so the pixel loop has no workgroup
-// barrier. The tile's x comes straight from HBM into the registers the f32 MFMA reads as its A
-// operand (lane (j, h): x[ct * 32 + 16 h + r][pixel j], one tile prefetched ahead); the chunk's
-// prototype rows sit in LDS for the launch (one barrier after the prologue) and are read per
-// prototype tile as the B operand, two tiles' products interleaved on independent accumulators.
-// Same arithmetic as push_dist_kernel (channel order, fma chains, ||x||^2 per half then added),
-// so ties are the ties protoseg_push_distances shows. The workgroup's waves merge their top-2
+// barrier. The tile's x comes straight from HBM into registers (lane (j, h): x[ct * 32 + 16 h + r]
+// [pixel j], one tile prefetched ahead) and is split once per tile into the bf16x6 A fragments;
+// the chunk's prototype rows sit in LDS for the launch as three bf16 term images (one barrier
+// after the prologue) and are read per prototype tile as the B fragments, two tiles' products
+// interleaved on independent accumulators. Same arithmetic as push_dist_kernel (push_xp, the
+// fma chains of ||x||^2 and push_p2), so ties are the ties protoseg_push_distances shows. The workgroup's waves merge their top-2
 // keys in LDS at the end (order-free: min of keys), one partial per (workgroup, image).
 #ifndef PW_WAVES
 #define PW_WAVES 8
@@ -324,11 +366,13 @@ constexpr int kPwWaves = PW_WAVES;  // waves per workgroup (8: two per SIMD, the
 constexpr bool kPwPrefetch = kPwWaves <= 8;
 constexpr int kPwMaxTiles = 8;  // prototype tiles per launch chunk (C = 32 / 64; C = 128 runs the block kernel)
 __host__ __device__ inline int pw_max_tiles(int) { return kPwMaxTiles; }
-// prototype rows in LDS at a pitch of C + 4 floats: the 16-lane groups of a ds_read_b128 of
-// 16 consecutive rows land on distinct banks (4 j mod 64)
-__host__ __device__ inline int pw_pitch(int C) { return C + 4; }
+// prototype rows in LDS as three bf16 term images [3][nptc * 32 rows][C], 16-B chunk ch of row r
+// at chunk ch ^ swz<C / 8>(r) (the 16-lane groups of a ds_read_b128 of 16 rows land on distinct
+// banks, bf16_split.h)
+__host__ __device__ inline size_t pw_term_bytes(int C, int nptc) { return static_cast<size_t>(nptc) * 32 * C * 2; }
 __host__ __device__ inline size_t pw_lds_bytes(int C, int nptc) {
-  const size_t protos = static_cast<size_t>(nptc) * 32 * pw_pitch(C) * 4;
+  // term images + per prototype of the chunk: ||p||^2, the caller's bound, the class bit
+  const size_t protos = 3 * pw_term_bytes(C, nptc) + static_cast<size_t>(3) * nptc * 32 * 4;
   const size_t merge = static_cast<size_t>(kPwWaves) * nptc * 32 * 16;
   return (protos > merge ? protos : merge) + static_cast<size_t>(kPwWaves) * 64 * 4;
 }
@@ -392,40 +436,49 @@ __global__ __launch_bounds__(kPwWaves * 64) void push_argmin_wave_kernel(
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = wave_id();
   const int wgi = blockIdx.x, img = blockIdx.y;
   const int pbase = (pt0 + static_cast<int>(blockIdx.z) * nptc) * 32;  // chunk z of nptc tiles
-  constexpr int kPitch = C + 4;
-  float* PL = pw_smem;                                                   // [nptc * 32][kPitch] prototype rows
+  constexpr int kCpr = C / 8;  // 16-B chunks per bf16 row
+  bf16* PL = reinterpret_cast<bf16*>(pw_smem);               // [3][nptc * 32][C] bf16 terms
+  const int term_elems = nptc * 32 * C;
   const size_t region = pw_lds_bytes(C, nptc) / 4 - kPwWaves * 64;
   float* xw = pw_smem + region + wave * 64;  // this wave's rows: [32] ||x||^2, [32] class masks
-  const int nrow4 = nptc * 32 * C / 4;
-  for (int i = static_cast<int>(threadIdx.x); i < nrow4; i += kPwWaves * 64) {
-    const int row = i / (C / 4);
-    const float4 v = pbase + row < P ? reinterpret_cast<const float4*>(protos)[static_cast<size_t>(pbase) * (C / 4) + i]
-                                     : make_float4(0.f, 0.f, 0.f, 0.f);
-    reinterpret_cast<float4*>(PL + row * kPitch)[i - row * (C / 4)] = v;
+  for (int i = static_cast<int>(threadIdx.x); i < nptc * 32 * kCpr; i += kPwWaves * 64) {
+    const int row = i / kCpr, ch = i - row * kCpr;
+    const bool ok = pbase + row < P;
+    const float4* src = reinterpret_cast<const float4*>(protos + static_cast<size_t>(ok ? pbase + row : 0) * C + 8 * ch);
+    const float4 u = src[0], w = src[1];
+    float v[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = ok ? v[e] : 0.f;
+    bf16x8 f[3];
+    split8<3>(v, f);
+    const int o = row * C + 8 * (ch ^ swz<kCpr>(row));
+#pragma unroll
+    for (int t = 0; t < 3; ++t) *reinterpret_cast<bf16x8*>(PL + t * term_elems + o) = f[t];
   }
-  __syncthreads();
-  // per prototype tile of the chunk: this lane's ||p||^2 (fma chain over its half's channels in
-  // (ct, r) order, halves added), class bit, and the wave's OR of the tile's classes
-  float p2[kPwMaxTiles];
-  uint32_t clsbit[kPwMaxTiles], tcls[kPwMaxTiles];
+  // per prototype of the chunk, in LDS (read per prototype tile in the epilogue, not held in
+  // registers): ||p||^2 (push_p2: the fixed order of every push distance), the caller's bound
+  // (see bd / sd below) and the class bit; the wave's OR of each tile's classes in scalar registers
+  float* pv_p2 = reinterpret_cast<float*>(PL + 3 * term_elems);
+  float* pv_bnd = pv_p2 + nptc * 32;
+  uint32_t* pv_cls = reinterpret_cast<uint32_t*>(pv_bnd + nptc * 32);
+  uint32_t tcls[kPwMaxTiles];
 #pragma unroll
   for (int pt = 0; pt < kPwMaxTiles; ++pt) {
-    p2[pt] = 0.f;
-    clsbit[pt] = tcls[pt] = 0u;
+    tcls[pt] = 0u;
     if (pt < nptc) {
-      const float* pr = PL + (pt * 32 + j) * kPitch + 16 * h;
-      float s = 0.f;
-#pragma unroll
-      for (int ct = 0; ct < NC; ++ct)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s = fmaf(pr[ct * 32 + r], pr[ct * 32 + r], s);
-      p2[pt] = s + __shfl_xor(s, 32);
       const int p = pbase + pt * 32 + j;
+      const float p2v = p < P ? push_p2<NC>(protos + static_cast<size_t>(p) * C, h) : 0.f;
       const int cls = p < P ? proto_class[p] : -1;
-      clsbit[pt] = cls >= 0 && cls < 32 ? (1u << cls) : 0u;
-      tcls[pt] = __builtin_amdgcn_readfirstlane(wave_or(clsbit[pt]));  // uniform: scalar registers
+      const uint32_t cb = cls >= 0 && cls < 32 ? (1u << cls) : 0u;
+      tcls[pt] = __builtin_amdgcn_readfirstlane(wave_or(cb));  // uniform: scalar registers
+      if (wave == 0 && h == 0) {
+        pv_p2[pt * 32 + j] = p2v;
+        pv_bnd[pt * 32 + j] = sd0 && p < P ? sd0[p] : __builtin_inff();
+        pv_cls[pt * 32 + j] = cb;
+      }
     }
   }
+  __syncthreads();
   const rsrc_t rx = make_rsrc(x + static_cast<size_t>(img) * C * HW, static_cast<unsigned>(C * HW * 4));
   const rsrc_t rm = make_rsrc(mask + static_cast<size_t>(img) * HW, static_cast<unsigned>(HW * 4));
   const int ntile = (HW + 31) / 32, nw = wgs * kPwWaves;
@@ -445,28 +498,19 @@ __global__ __launch_bounds__(kPwWaves * 64) void push_argmin_wave_kernel(
   // lower the runner-up), so the epilogue skips a prototype tile whose candidates are all above
   // that threshold in every lane: two VALU per candidate instead of the ~12 of the masked update.
   // The per-image top-2 below bnd is then exact, above it partial (only the merge reads it).
-  float bd[kPwMaxTiles], sd[kPwMaxTiles], bnd[kPwMaxTiles];
+  float bd[kPwMaxTiles], sd[kPwMaxTiles];
   uint32_t bi[kPwMaxTiles];
 #pragma unroll
   for (int pt = 0; pt < kPwMaxTiles; ++pt) {
-    const int p = pbase + pt * 32 + j;
     bd[pt] = sd[pt] = __builtin_inff();
-    bnd[pt] = sd0 && pt < nptc && p < P ? sd0[p] : __builtin_inff();
     bi[pt] = 0xffffffffu;
   }
-  // one prototype tile's B operand (channels ct * 32 + 16 h + 4 q .. + 3: 16-B LDS reads)
-  auto load_pv = [&](int pt, float (&pv)[NC][16]) __attribute__((always_inline)) {
-    const float4* pr = reinterpret_cast<const float4*>(PL + (pt * 32 + j) * kPitch + 16 * h);
+  // one prototype tile's B fragments of k-step s (prototype j, channels push_chan(s, h, 0..7))
+  auto load_pf = [&](int pt, int s, bf16x8 (&bf)[3]) __attribute__((always_inline)) {
+    const int row = pt * 32 + j;
+    const int o = row * C + 8 * ((push_chan(s, h, 0) >> 3) ^ swz<kCpr>(row));
 #pragma unroll
-    for (int ct = 0; ct < NC; ++ct)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 v = pr[ct * 8 + q];
-        pv[ct][4 * q] = v.x;
-        pv[ct][4 * q + 1] = v.y;
-        pv[ct][4 * q + 2] = v.z;
-        pv[ct][4 * q + 3] = v.w;
-      }
+    for (int t = 0; t < 3; ++t) bf[t] = *reinterpret_cast<const bf16x8*>(PL + t * term_elems + o);
   };
   // per lane (prototype j of tile pt): the tile's rows (pixels) in increasing order, strict '<'
   auto epilogue = [&](int pt, const f32x16& acc, int nbase) __attribute__((always_inline)) {
@@ -474,18 +518,19 @@ __global__ __launch_bounds__(kPwWaves * 64) void push_argmin_wave_kernel(
     load_rows16(xw + 4 * h, x2r);
     float s[16];  // l2_distance before its relu: relu(s) < thr implies s < thr (thr >= 0)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) s[r] = l2_pre_relu(x2r[r], p2[pt], acc[r]);
+    for (int r = 0; r < 16; ++r) s[r] = l2_pre_relu(x2r[r], pv_p2[pt * 32 + j], acc[r]);
     float m4[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) m4[q] = fminf(fminf(s[4 * q], s[4 * q + 1]), fminf(s[4 * q + 2], s[4 * q + 3]));
-    const float thr = fminf(sd[pt], bnd[pt]);
+    const float thr = fminf(sd[pt], pv_bnd[pt * 32 + j]);
     if (!__builtin_amdgcn_ballot_w64(fminf(fminf(m4[0], m4[1]), fminf(m4[2], m4[3])) < thr))
       return;  // no candidate below any lane's threshold: nothing changes (wave-uniform)
     load_rows16(xw + 32 + 4 * h, mkr);
+    const uint32_t clsb = pv_cls[pt * 32 + j];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float d = __builtin_fmaxf(s[r], 0.f);  // = l2_distance(x2r[r], p2[pt], acc[r])
-      const float dm = (__float_as_uint(mkr[r]) & clsbit[pt]) ? d : __builtin_inff();
+      const float dm = (__float_as_uint(mkr[r]) & clsb) ? d : __builtin_inff();
       const bool c = dm < bd[pt];
       sd[pt] = c ? bd[pt] : fminf(sd[pt], dm);
       bi[pt] = c ? static_cast<uint32_t>(nbase + acc_row(r, h)) : bi[pt];
@@ -522,6 +567,8 @@ __global__ __launch_bounds__(kPwWaves * 64) void push_argmin_wave_kernel(
 #pragma unroll
     for (int i = 0; i < NC * 16; ++i) x2 = fmaf(cur[i], cur[i], x2);
     x2 += __shfl_xor(x2, 32);
+    bf16x8 af[2 * NC][3];
+    push_split_x<NC>(cur, af);
     wave_lds_fence();  // the previous tile's row reads are done
     if (h == 0) {
       xw[j] = x2;
@@ -529,8 +576,8 @@ __global__ __launch_bounds__(kPwWaves * 64) void push_argmin_wave_kernel(
     }
     wave_lds_fence();
     const int nbase = t * 32;
-    // prototype tiles in pairs: two independent f32 chains interleaved (one chain per tile with
-    // the next tile's operand prefetched measured 3 % slower)
+    // prototype tiles in pairs: two independent accumulator chains interleaved, each in
+    // push_xp's order (k-steps, terms smallest first)
 #pragma unroll
     for (int pa = 0; pa < kPwMaxTiles; pa += 2) {
       if (pa >= nptc) break;
@@ -540,17 +587,15 @@ __global__ __launch_bounds__(kPwWaves * 64) void push_argmin_wave_kernel(
       const bool run_a = __ballot((mk & tcls[pa]) != 0u) != 0ull;
       const bool run_b = has_b && __ballot((mk & tcls[pb]) != 0u) != 0ull;
       if (!run_a && !run_b) continue;
-      float pva[NC][16], pvb[NC][16];
-      load_pv(pa, pva);
-      load_pv(has_b ? pb : pa, pvb);
       f32x16 acc_a = zero16(), acc_b = zero16();
 #pragma unroll
-      for (int ct = 0; ct < NC; ++ct)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          acc_a = mfma32(cur[ct * 16 + r], pva[ct][r], acc_a);
-          acc_b = mfma32(cur[ct * 16 + r], pvb[ct][r], acc_b);
-        }
+      for (int s2 = 0; s2 < 2 * NC; ++s2) {
+        bf16x8 fa[3], fb[3];
+        load_pf(pa, s2, fa);
+        load_pf(has_b ? pb : pa, s2, fb);
+        acc_a = mma_split<3>(af[s2], fa, acc_a);
+        acc_b = mma_split<3>(af[s2], fb, acc_b);
+      }
       if (run_a) epilogue(pa, acc_a, nbase);
       if (run_b) epilogue(pb, acc_b, nbase);
     }
@@ -775,14 +820,35 @@ __global__ __launch_bounds__(64) void push_dist_kernel(const float* __restrict__
   const int n = n0 + j;
   f32x16 acc = zero16();
   float x2 = 0.f;
+  if constexpr (NC <= 2) {  // the wave-streamed argmin's arithmetic (bf16x6 products, push_xp)
+    float xr[NC * 16];
 #pragma unroll
-  for (int ct = 0; ct < NC; ++ct)
+    for (int ct = 0; ct < NC; ++ct)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float xa = n < HW ? x[static_cast<size_t>(ct * 32 + 16 * h + r) * HW + n] : 0.f;
-      x2 = fmaf(xa, xa, x2);
-      acc = mfma32(xa, pv[ct][r], acc);
+      for (int r = 0; r < 16; ++r) xr[ct * 16 + r] = n < HW ? x[static_cast<size_t>(ct * 32 + 16 * h + r) * HW + n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NC * 16; ++i) x2 = fmaf(xr[i], xr[i], x2);
+    bf16x8 af[2 * NC][3], bf[2 * NC][3];
+    push_split_x<NC>(xr, af);
+#pragma unroll
+    for (int s = 0; s < 2 * NC; ++s) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = pv[(s >> 1)][8 * (s & 1) + e];  // channel push_chan(s, h, e)
+      split8<3>(v, bf[s]);
     }
+    acc = push_xp<NC>(af, bf);
+    p2 = push_p2<NC>(protos + static_cast<size_t>(pvalid ? p : m - 1) * C, h);
+  } else {  // C = 128: the block kernel's exact f32 fma chain
+#pragma unroll
+    for (int ct = 0; ct < NC; ++ct)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float xa = n < HW ? x[static_cast<size_t>(ct * 32 + 16 * h + r) * HW + n] : 0.f;
+        x2 = fmaf(xa, xa, x2);
+        acc = mfma32(xa, pv[ct][r], acc);
+      }
+  }
   x2 += __shfl_xor(x2, 32);
   if (h == 0) xs[j] = x2;
   __syncthreads();
@@ -888,8 +954,7 @@ int push_argmin_impl(const float* x, int n_img, int C, int h, int w, const float
   const long long HW = static_cast<long long>(h) * w;
   if (HW >= (1LL << 31) / 2) return fail(PROTOSEG_ERR_UNSUPPORTED, "h*w=%lld", HW);
   const int npt = static_cast<int>(ceil_div(P, 32));
-  const char* pe = getenv("PROTOSEG_PUSH");  // "block": the block-staged kernel below (A/B)
-  if (nc <= 2 && !(pe && !strcmp(pe, "block"))) {
+  if (nc <= 2) {
     // wave-streamed kernel: prototype chunks of <= pw_max_tiles tiles, about one workgroup per
     // CU over the images (every wave at least one pixel tile)
     const int maxt = pw_max_tiles(nc);

@@ -225,10 +225,12 @@ def test_push_top2_keys_vs_brute_force(device, C, P, n_img, h, w):
 
 @pytest.mark.parametrize("C,P,n_img,h,w", [(64, 190, 8, 129, 257), (64, 361, 3, 65, 65), (32, 520, 2, 33, 47),
                                            (64, 19, 1, 7, 9), (64, 190, 1, 129, 257)])
-def test_push_wave_kernel_equals_block_kernel(device, C, P, n_img, h, w, monkeypatch):
-    """The wave-streamed argmin (default for C = 32 / 64) and the block-staged one
-    (PROTOSEG_PUSH=block) give the same keys and runner-ups bit for bit: the same arithmetic
-    (push_dist_kernel's), ties to the lowest patch in both. Full Cityscapes-sized maps included."""
+def test_push_argmin_exact_in_its_own_arithmetic(device, C, P, n_img, h, w):
+    """The argmin kernel and protoseg_push_distances (the distances the host re-resolves exact ties
+    with) use the same arithmetic bit for bit: each key's distance is push_distances' value at the
+    key's patch, no class patch has a smaller one, an equal one only at a higher patch index, and
+    the runner-up is the second smallest of push_distances over the class patches (another patch).
+    Full Cityscapes-sized maps included, one and eight images per call."""
     push = _push()
     K = 19
     gen = torch.Generator().manual_seed(C * 7 + P)
@@ -239,13 +241,33 @@ def test_push_wave_kernel_equals_block_kernel(device, C, P, n_img, h, w, monkeyp
     rng = np.random.default_rng(P + h)
     labels = rng.integers(0, K + 1, size=(n_img, 4 * h, 4 * w)).astype(np.int64)
     mask = push.patch_class_mask(torch.from_numpy(labels).to(device), h, w)
-    out = {}
-    for mode in ("wave", "block"):
-        monkeypatch.setenv("PROTOSEG_PUSH", mode)
-        out[mode] = push.push_argmin(x, protos, pc.to(device), mask, with_second=True)
+    keys, second = push.push_argmin(x, protos, pc.to(device), mask, with_second=True)
     torch.cuda.synchronize()
-    assert torch.equal(out["wave"][0], out["block"][0])
-    assert torch.equal(out["wave"][1], out["block"][1])
+    mm = mask.cpu().numpy().view(np.uint32)
+    pcn = pc.numpy()
+    checked = 0
+    for i in range(n_img):
+        d = push.push_distances(x[i], protos).cpu().numpy()  # [P, h*w] in the argmin's arithmetic
+        kd, kp, found = (t.numpy() for t in push.decode_keys(keys[i].cpu()))
+        sd, _, sfound = (t.numpy() for t in push.decode_keys(second[i].cpu()))
+        for j in range(P):
+            if pcn[j] < 0:
+                assert not bool(found[j])
+                continue
+            member = ((mm[i] >> int(pcn[j])) & 1).astype(bool)
+            if not member.any():
+                assert not bool(found[j])
+                continue
+            rows = np.nonzero(member)[0]
+            vals = d[j, rows]
+            q = int(kp[j])
+            assert member[q] and np.float32(kd[j]) == d[j, q], (i, j)
+            assert vals.min() == d[j, q] and q == int(rows[np.argmin(vals)]), (i, j)  # first index of the minimum
+            if len(rows) > 1:
+                srt = np.sort(vals)
+                assert bool(sfound[j]) and np.float32(sd[j]) == srt[1], (i, j)
+            checked += 1
+    assert checked > 0
 
 
 def test_near_tie_flag_fires_on_constructed_ties(device):

@@ -184,9 +184,12 @@ def test_densenet_config_depth_fp16(device):
     _close(wd.grad, r_gw, "g_w")
 
 
-def test_fp16_native_matches_widened(device):
-    """The wide family's native fp16 read (PROTOSEG_F16) gives the same bits as the f32 path on
-    the exactly widened map: distances, logits, g_protos, g_w, and g_x rounded to fp16 once."""
+@pytest.mark.parametrize("precision", ["f32", "bf16x6"])
+def test_fp16_native_matches_widened(device, precision):
+    """With exact-f32-class products (F32 / BF16X6 requests) the wide family's native fp16 read
+    (PROTOSEG_F16) gives the same bits as the f32 path on the exactly widened map: distances,
+    logits, g_protos, g_w, and g_x rounded to fp16 once. (BF16X3 requests on fp16 maps take the
+    fp16 MFMA distance GEMM: test_fp16_distance_gemm_*.)"""
     from protoseg_amd import ops
     B, C, h, w, P, K = 2, 256, 6, 7, 95, 19
     x, protos, w_last, g_logits, _ = _inputs(B, C, h, w, P, K, seed=5)
@@ -198,12 +201,68 @@ def test_fp16_native_matches_widened(device):
         xd = xin.clone().requires_grad_(True)
         pd = protos.to(device).requires_grad_(True)
         wd = w_last.to(device).requires_grad_(True)
-        dist, logits, _ = ops.prototype_layer(xd, pd, wd)
+        dist, logits, _ = ops.prototype_layer(xd, pd, wd, precision=precision)
         logits.backward(g_logits.to(device))
         outs.append((dist.detach(), logits.detach(), xd.grad.half(), pd.grad, wd.grad))
     torch.cuda.synchronize()
     for name, a, b in zip(("dist", "logits", "g_x", "g_protos", "g_w"), outs[0], outs[1]):
         assert torch.equal(a, b), name
+
+
+def _f32_bound(x, protos):
+    """f32 rounding bound of the expanded distance x2 + p2 - 2 x.p over C f32 sums:
+    2e-6 (||x||^2 + ||p||^2). bf16x3 products (3 x 2^-16 per product) exceed it about 8x at C = 1024."""
+    return 2e-6 * ((x.double() ** 2).sum(1)[:, None] + (protos.double() ** 2).sum(1)[None, :, None, None])
+
+
+@pytest.mark.parametrize("B,C,h,w,P,K", [
+    (2, 1024, 16, 16, 570, 19),  # BASELINE configs[4]: DenseNet depth, 30 prototypes/class
+    (1, 200, 9, 8, 77, 7),       # ragged: C % 32, P % 192, pixels % 128 all non-zero
+    (3, 96, 4, 6, 400, 40),      # pixel tiles straddling images (HW = 24)
+])
+def test_fp16_distance_gemm_vs_float64(device, B, C, h, w, P, K):
+    """The fp16 distance GEMM (wide_dist_f16_kernel: x exact in fp16, prototypes scaled by a power
+    of two and split into two fp16 terms, v_mfma_f32_32x32x16_f16) against float64 distances: within
+    the f32 rounding bound of the expanded form, i.e. as accurate as exact f32 products (bf16x3
+    products would not meet this bound at C = 1024). Prototypes with large and tiny entries exercise
+    the per-row scale. Logits against the oracle on the fp16 map."""
+    from protoseg_amd import ops
+    x, protos, w_last, g_logits, _ = _inputs(B, C, h, w, P, K, seed=C + P)
+    protos[::5] *= 3000.0      # rows far above fp16's comfortable range before scaling
+    protos[1::5] *= 1e-3       # and far below it
+    xh = x.half()
+    dist, logits, _ = ops.prototype_layer(xh.to(device), protos.to(device), w_last.to(device))
+    torch.cuda.synchronize()
+    xd = xh.double()
+    ref = ((xd[:, None] - protos.double()[None, :, :, None, None]) ** 2).sum(2)
+    err = (dist.double().cpu() - ref).abs()
+    assert bool((err <= _f32_bound(xh.float(), protos)).all()), f"max err {err.max().item():.3e}"
+    r_logits = po.forward_from_conv_features(xh.float(), protos[:, :, None, None], w_last)[0]
+    _close(logits, r_logits, "logits", rel=1e-4)
+
+
+def test_fp16_distance_gemm_near_zero(device):
+    """configs[4] depth with every prototype copied from a feature-map patch (d ~ 0, the state right
+    after push): the fp16 GEMM's distances stay within the f32 rounding bound of float64, as the
+    exact-f32 path's do, and its log activations are log((d+1)/(d+1e-4)) of those distances."""
+    from protoseg_amd import ops
+    B, C, h, w, P, K = 2, 1024, 16, 16, 570, 19
+    x, _, w_last, _, _ = _inputs(B, C, h, w, P, K, seed=7)
+    xh = x.half()
+    flat = xh.float().permute(0, 2, 3, 1).reshape(-1, C)
+    protos = flat[torch.randperm(flat.shape[0], generator=torch.Generator().manual_seed(1))[:P]].clone()
+    xd, pd, wd = xh.to(device), protos.to(device), w_last.to(device)
+    ref = ((xh.double()[:, None] - protos.double()[None, :, :, None, None]) ** 2).sum(2)
+    bound = _f32_bound(xh.float(), protos)
+    assert int((ref == 0).sum()) >= P  # every prototype has an exact match
+    for prec in ("bf16x3", "f32"):  # bf16x3 requests take the fp16 GEMM; f32 the exact f32 path
+        dist, _, act = ops.prototype_layer(xd, pd, wd, with_act=True, precision=prec)
+        torch.cuda.synchronize()
+        err = (dist.double().cpu() - ref).abs()
+        assert bool((err <= bound).all()), f"{prec}: max err {err.max().item():.3e}"
+        d = dist.double().cpu().permute(0, 2, 3, 1).reshape(-1, P)
+        r_act = torch.log((d + 1) / (d + 1e-4))
+        _close(act.double().cpu().reshape(-1, P), r_act, f"{prec} act", rel=1e-5)
 
 
 def test_wide_backward_from_saved_distances(device):
