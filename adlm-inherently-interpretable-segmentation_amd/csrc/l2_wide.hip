@@ -38,7 +38,14 @@ constexpr int kWT = 64;        // workgroup output tile (rows and columns)
 constexpr int kWKs = 32;       // contraction per LDS stage
 constexpr int kWThreads = 256;
 
-enum WideEpi { kEpiStore = 0, kEpiDist = 1, kEpiGs = 2, kEpiGx = 3 };
+// the pre-split backward GEMMs' tile (wide_pre_gemm_kernel, below)
+constexpr int kPreTM = 192, kPreTN = 128, kPreTK = 32, kPreNS = 3;
+constexpr int kPreAPlane = kPreTM * kPreTK * 2;      // 12 KiB
+constexpr int kPreBPlane = kPreTN * kPreTK * 2;      // 8 KiB
+constexpr int kPreStage = 2 * kPreAPlane + 2 * kPreBPlane;  // 40 KiB
+constexpr int kPreLds = kPreNS * kPreStage + 4 * kPreTN * 4;
+
+enum WideEpi { kEpiStore = 0, kEpiDist = 1, kEpiGs = 2, kEpiGx = 3, kEpiGsSplit = 4 };
 
 // bf16x3 stages: per operand, hi and lo terms as [row][k] bf16 rows of kWKs k, padded to kBRow
 // elements (80-B rows: the 16-row groups of a ds_read_b128 fragment read land on distinct banks)
@@ -70,6 +77,7 @@ struct WideArgs {
   const float* gd;   // kEpiGs: dense g_dist at the output's address, or null
   const void* xo;    // kEpiGx: x at the output's address
   int bf3;           // 1: bf16x3 products (precision BF16X3), 0: exact f32 MFMA
+  void* out2;        // kEpiGsSplit: G_s as two bf16 planes, hi at out, lo at out2 (same offsets)
 };
 
 template <typename T>
@@ -331,11 +339,17 @@ __global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
         const float d = l2_distance(colsum, p2, v);
         v = d;
         if (a.act) a.act[bo * a.ab + m * a.am + static_cast<long long>(n) * a.an] = activation(d, a.eps, a.act_kind);
-      } else if constexpr (EPI == kEpiGs) {
+      } else if constexpr (EPI == kEpiGs || EPI == kEpiGsSplit) {
         const float d = a.D[o];
         float g = v * activation_grad(d, a.eps, a.act_kind);
         if (a.gd) g += a.gd[o];
         v = d > 0.f ? g : 0.f;  // relu backward
+        if constexpr (EPI == kEpiGsSplit) {  // the pre-split GEMMs' operand: hi, lo planes
+          const bf16 vh = static_cast<bf16>(v);
+          static_cast<uint16_t*>(a.out)[o] = __builtin_bit_cast(uint16_t, vh);
+          static_cast<uint16_t*>(a.out2)[o] = __builtin_bit_cast(uint16_t, static_cast<bf16>(v - static_cast<float>(vh)));
+          continue;
+        }
       } else if constexpr (EPI == kEpiGx) {
         // conv(x^2, ones) backward: 2x sum_p g_s; conv(x, P) backward: -2 P^T g_s
         v = -2.f * v + 2.f * load_elem<TO>(a.xo, o) * colsum;
@@ -611,20 +625,41 @@ int logits_split(const Geometry& g) {
   return groups >= 512 ? 1 : split_of(groups, g.P);
 }
 
+// Pre-split backward (wide_pre_gemm_kernel): served for bf16x3 requests whose per-image pixel
+// count keeps every 32-pixel k stage inside one image, and whose planes stay below 2^31 bytes.
+bool wide_pre_fits(const Geometry& g) {
+  const long long big = 1LL << 31;
+  return g.HW % 32 == 0 && static_cast<long long>(g.npix) * g.C * 2 < big &&
+         static_cast<long long>(g.npix) * g.P * 2 < big && static_cast<long long>(g.C) * (g.P + 32) * 2 < big;
+}
+int pre_split(const Geometry& g) {  // workgroups along the g_P contraction: about 256 in all, >= 4 stages each
+  const long long tiles = ceil_div(g.P, kPreTM) * ceil_div(g.C, kPreTN);
+  long long s2 = ceil_div(256, tiles);
+  const long long cap = ceil_div(static_cast<long long>(g.npix), 4 * kPreTK);
+  if (s2 > cap) s2 = cap;
+  return static_cast<int>(s2 < 1 ? 1 : s2 > 64 ? 64 : s2);
+}
 struct WideBwdLayout {
-  size_t D, G, rs, part, total;  // float offsets
+  size_t D, G, rs, part, xs, pt, total;  // float offsets (G holds f32 G_s, or its two bf16 planes)
 };
 WideBwdLayout wide_bwd_layout(const Geometry& g) {
   WideBwdLayout l{};
   const size_t dp = static_cast<size_t>(g.npix) * g.P;
-  const size_t sp = static_cast<size_t>(split_of(g.P, g.C, g.npix)) * g.P * g.C;
+  size_t sp = static_cast<size_t>(split_of(g.P, g.C, g.npix)) * g.P * g.C;
   const size_t sw = static_cast<size_t>(split_of(g.K, g.P, g.npix)) * g.K * g.P;
+  const bool pre = wide_pre_fits(g);
+  if (pre) {
+    const size_t sq = static_cast<size_t>(pre_split(g)) * g.P * g.C;
+    sp = sp > sq ? sp : sq;
+  }
   auto al = [](size_t v) { return (v + 63) & ~static_cast<size_t>(63); };
   l.D = 0;
   l.G = al(dp);
   l.rs = l.G + al(dp);
   l.part = l.rs + al(g.P);
-  l.total = l.part + al(sp > sw ? sp : sw);
+  l.xs = l.part + al(sp > sw ? sp : sw);                                  // x as two bf16 planes
+  l.pt = l.xs + (pre ? al(static_cast<size_t>(g.npix) * g.C) : 0);       // P^T as two bf16 planes
+  l.total = l.pt + (pre ? al(static_cast<size_t>(g.C) * (ceil_div(g.P, kPreTK) * kPreTK)) : 0);
   return l;
 }
 
@@ -925,6 +960,267 @@ bool wide_f16_fits(const Geometry& g, const void* x) {
          static_cast<long long>(ceil_div(g.P, kF16TM)) * kF16TM * ceil_div(g.C, kF16TK) * kF16TK * 2 < (1LL << 31);
 }
 
+// ---- the wide backward's two large GEMMs on pre-split bf16 operands --------------------------
+// g_x = -2 P^T G_s + 2 x sum_p G_s (M = C, N = pixels, K = P) and g_P = -2 G_s X^T + 2 p sum G_s
+// (M = P, N = C, K = pixels, split over workgroups) with every operand stored as two bf16 planes
+// (hi, lo) by its producer: the G_s GEMM's epilogue (kEpiGsSplit), wide_pt_split_kernel (P^T) and
+// wide_x_split_kernel (x). The GEMM stages are then byte copies (16-B LDS-DMA, three stages in
+// flight) and each 16-k step is 3 v_mfma_f32_32x32x16_bf16 (hi.lo + lo.hi + hi.hi): bf16x3
+// products, the same split as the 64 x 64 tile's, without its per-stage conversion (which bound
+// that kernel). Tile 192 x 128 x 32, 4 waves x (3 x 2) blocks, as wide_dist_f16_kernel.
+
+struct PreArgs {
+  const uint16_t *ahi, *alo;  // A planes: element (row, kg) at (kg / akb) sab + row lda + kg % akb
+  unsigned a_bytes;
+  long long sab;
+  int lda, akb, arows;        // rows >= arows read 0
+  const uint16_t *bhi, *blo;  // B planes. BT = 0: (col, kg) as A (ldb, bkb, sbb, bcols);
+  unsigned b_bytes;           // BT = 1: (kg, col): col -> (cb, n) = (col / bnb, col % bnb),
+  long long sbb;              //         cb sbb + kg ldb + n; kg >= bk read 0
+  int ldb, bkb, bcols, bnb, bk;
+  int M, N, K;                // K: the flattened contraction (a multiple of 32)
+  int ksplit;
+  float* slab;                // EPI 0: slab z: [M][N] f32 at z M N
+  void* gx;                   // EPI 1: g_x (TO) at (b, c, n): (b C + c) HW + n, col = b HW + n
+  const void* x;              //        x at the same offset
+  unsigned o_bytes;
+  int C, HW;
+};
+
+// Buffer-resource element IO of g_x / x in the feature map's dtype (out-of-range: load 0, store dropped).
+template <typename T> struct BufIO2 : BufIO<T> {};
+template <> struct BufIO2<_Float16> {
+  static __device__ __forceinline__ float load(rsrc_t r, unsigned voff, unsigned soff) {
+    return static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(__builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0))));
+  }
+  static __device__ __forceinline__ void store(rsrc_t r, float v, unsigned voff, unsigned soff) {
+    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, static_cast<_Float16>(v)), r, voff, soff, 0);
+  }
+};
+
+template <int EPI, bool BT, typename TO>
+__global__ __launch_bounds__(256, 1) void wide_pre_gemm_kernel(PreArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
+  const unsigned S0 = static_cast<unsigned>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)psm));
+  const int lane = threadIdx.x & 63, wave = bf16l::wave_id(), j = lane & 31, h = lane >> 5;
+  const int n0 = static_cast<int>(blockIdx.x) * kPreTN, m0 = static_cast<int>(blockIdx.y) * kPreTM;
+  const int z = static_cast<int>(blockIdx.z);
+  const rsrc_t rah = make_rsrc(a.ahi, a.a_bytes), ral = make_rsrc(a.alo, a.a_bytes);
+  const rsrc_t rbh = make_rsrc(a.bhi, a.b_bytes), rbl = make_rsrc(a.blo, a.b_bytes);
+  const int nst_all = a.K / kPreTK;
+  const int st0 = static_cast<int>((static_cast<long long>(nst_all) * z) / a.ksplit);
+  const int st1 = static_cast<int>((static_cast<long long>(nst_all) * (z + 1)) / a.ksplit);
+  const int nst = st1 - st0;
+
+  // 40 DMA pieces per stage, 10 per wave: 0..23 A (plane q / 12, rows 16 (q % 12) ..), 24..39 B
+  // (plane (q - 24) / 8; BT = 0: rows = columns 16 ((q - 24) % 8) ..; BT = 1: k rows 4 ((q - 24) % 8) ..)
+  unsigned voff[10];
+  int krow[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const int q = 10 * wave + i;
+    krow[i] = -1;
+    if (q < 24) {
+      const int r = 16 * (q % 12) + (lane >> 2), lc = (lane & 3) ^ f16_aswz(r);
+      voff[i] = m0 + r < a.arows ? static_cast<unsigned>((static_cast<long long>(m0 + r) * a.lda + 8 * lc) * 2) : kOOB;
+    } else if (!BT) {
+      const int r = 16 * ((q - 24) % 8) + (lane >> 2), lc = (lane & 3) ^ f16_aswz(r);
+      voff[i] = n0 + r < a.bcols ? static_cast<unsigned>((static_cast<long long>(n0 + r) * a.ldb + 8 * lc) * 2) : kOOB;
+    } else {
+      const int kr = 4 * ((q - 24) % 8) + (lane >> 4), lc = (lane & 15) ^ f16_bswz(kr);
+      const int col = n0 + 8 * lc;
+      krow[i] = kr;
+      if (col < a.bcols) {
+        const int cb = col / a.bnb, n = col - cb * a.bnb;
+        voff[i] = static_cast<unsigned>((cb * a.sbb + static_cast<long long>(kr) * a.ldb + n) * 2);
+      } else {
+        voff[i] = kOOB;
+      }
+    }
+  }
+  auto issue = [&](int st) __attribute__((always_inline)) {  // global stage st0 + st into buffer st % 3
+    const int kg = (st0 + st) * kPreTK;
+    const unsigned base = S0 + static_cast<unsigned>((st % kPreNS) * kPreStage);
+    const unsigned sa = static_cast<unsigned>(((kg / a.akb) * a.sab + kg % a.akb) * 2);
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      const int q = 10 * wave + i;  // wave-uniform
+      if (q < 24) {
+        dma16(q < 12 ? rah : ral, base + static_cast<unsigned>((q / 12) * kPreAPlane + (q % 12) * 1024), voff[i], sa);
+      } else {
+        const int qb = q - 24;
+        const unsigned dst = base + static_cast<unsigned>(2 * kPreAPlane + (qb / 8) * kPreBPlane + (qb % 8) * 1024);
+        if constexpr (!BT) {
+          const unsigned sb = static_cast<unsigned>(((kg / a.bkb) * a.sbb + kg % a.bkb) * 2);
+          dma16(qb < 8 ? rbh : rbl, dst, voff[i], sb);
+        } else {
+          const bool ok = voff[i] != kOOB && kg + krow[i] < a.bk;
+          dma16(qb < 8 ? rbh : rbl, dst, ok ? voff[i] : kOOB, static_cast<unsigned>(static_cast<long long>(kg) * a.ldb * 2));
+        }
+      }
+    }
+  };
+
+  const int rg = wave & 1, cp = wave >> 1;
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  f32x16 acc[3][2];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) acc[i][0] = acc[i][1] = zero16();
+  float cs0 = 0.f, cs1 = 0.f;  // EPI 1: column sums of B (sum_p G_s) over this thread's slice
+  const int xcp = threadIdx.x & 63, xsl = threadIdx.x >> 6;
+
+  if (nst > 0) issue(0);
+  if (nst > 1) issue(1);
+  for (int st = 0; st < nst; ++st) {
+    if (st + 1 < nst) asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    if (st + 2 < nst) issue(st + 2);
+    const unsigned sb = S0 + static_cast<unsigned>((st % kPreNS) * kPreStage);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[3][2], bfr[2][2];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int r = 96 * rg + 32 * i + j;
+        const unsigned ao = static_cast<unsigned>(r * 64 + 16 * ((2 * ks + h) ^ f16_aswz(r)));
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          af[i][t] = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(
+              static_cast<uintptr_t>(sb + static_cast<unsigned>(t * kPreAPlane) + ao));
+      }
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const unsigned pb = sb + static_cast<unsigned>(2 * kPreAPlane + t * kPreBPlane);
+          if constexpr (!BT) {
+            const int c = 64 * cp + 32 * jj + j;
+            bfr[jj][t] = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(
+                static_cast<uintptr_t>(pb + static_cast<unsigned>(c * 64 + 16 * ((2 * ks + h) ^ f16_aswz(c)))));
+          } else {
+            const int ch = 8 * cp + 4 * jj + 2 * (g & 1) + (p4 >> 1);
+            f16s4 v[2];
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+              const int r = 16 * ks + 8 * h + 4 * hf + q4;
+              v[hf] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(reinterpret_cast<__attribute__((address_space(3))) f16s4*>(
+                  static_cast<uintptr_t>(pb + static_cast<unsigned>(256 * r + 16 * (ch ^ f16_bswz(r)) + 8 * (p4 & 1)))));
+            }
+            bfr[jj][t] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v[0], v[1], 0, 1, 2, 3, 4, 5, 6, 7));
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mma_split<2>(af[i], bfr[jj], acc[i][jj]);
+    }
+    if constexpr (EPI == 1) {  // sum_p G_s: this thread's 8 k rows of the stage, columns 2 xcp, 2 xcp + 1
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr) {
+        const int r = 8 * xsl + rr, col = 2 * xcp;
+        const unsigned o = static_cast<unsigned>(2 * kPreAPlane + 256 * r + 16 * ((col >> 3) ^ f16_bswz(r)) + 2 * (col & 7));
+        const uint32_t wh = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(static_cast<uintptr_t>(sb + o));
+        const uint32_t wl = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
+            static_cast<uintptr_t>(sb + o + kPreBPlane));
+        cs0 += __uint_as_float(wh << 16) + __uint_as_float(wl << 16);
+        cs1 += __uint_as_float(wh & 0xffff0000u) + __uint_as_float(wl & 0xffff0000u);
+      }
+    }
+  }
+  float* red = reinterpret_cast<float*>(psm + kPreNS * kPreStage);
+  if constexpr (EPI == 1) {
+    red[xsl * kPreTN + 2 * xcp] = cs0;
+    red[xsl * kPreTN + 2 * xcp + 1] = cs1;
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int cn = 64 * cp + 32 * jj + j, col = n0 + cn;
+    if constexpr (EPI == 0) {  // slab z: [M][N] f32, lane = column
+      const rsrc_t rs = make_rsrc(a.slab + static_cast<size_t>(z) * a.M * a.N, static_cast<unsigned>(static_cast<size_t>(a.M) * a.N * 4));
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int mu = m0 + 96 * rg + 32 * i + row_of(r);  // wave-uniform; the lane's row is mu + 4h
+          const bool ok = mu + 4 * h < a.M && col < a.N;
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][jj][r]), rs,
+                                                ok ? static_cast<unsigned>(((4 * h) * a.N + col) * 4) : kOOB,
+                                                static_cast<unsigned>(mu * a.N * 4), 0);
+        }
+    } else {  // g_x (TO) at (b C + c) HW + n: -2 acc + 2 x sum_p G_s
+      const float csum = ((red[cn] + red[kPreTN + cn]) + red[2 * kPreTN + cn]) + red[3 * kPreTN + cn];
+      const int b = col < a.N ? col / a.HW : 0, n = col - b * a.HW;
+      const unsigned cbase = col < a.N ? static_cast<unsigned>((b * a.C * a.HW + n + 4 * h * a.HW) * sizeof(TO)) : kOOB;
+      const rsrc_t ro = make_rsrc(a.gx, a.o_bytes), rxo = make_rsrc(a.x, a.o_bytes);
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int mu = m0 + 96 * rg + 32 * i + row_of(r);
+          const unsigned vo = mu + 4 * h < a.M ? cbase : kOOB, so = static_cast<unsigned>(mu * a.HW * sizeof(TO));
+          const float xv = BufIO2<TO>::load(rxo, vo, so);
+          BufIO2<TO>::store(ro, -2.f * acc[i][jj][r] + 2.f * xv * csum, vo, so);
+        }
+    }
+  }
+}
+
+// P^T as bf16 planes [C][kp] (k = p; zero past P): 64 x 64 tiles through LDS (coalesced both ways).
+__global__ __launch_bounds__(256) void wide_pt_split_kernel(const float* __restrict__ protos, int P, int C, int kp,
+                                                            uint16_t* __restrict__ hi, uint16_t* __restrict__ lo) {
+  __shared__ float t[64][65];
+  const int p0 = static_cast<int>(blockIdx.x) * 64, c0 = static_cast<int>(blockIdx.y) * 64;
+  for (int i = static_cast<int>(threadIdx.x); i < 64 * 64; i += 256) {
+    const int pr = i >> 6, cc = i & 63;
+    t[pr][cc] = p0 + pr < P && c0 + cc < C ? protos[static_cast<size_t>(p0 + pr) * C + c0 + cc] : 0.f;
+  }
+  __syncthreads();
+  for (int i = static_cast<int>(threadIdx.x); i < 64 * 64; i += 256) {
+    const int cc = i >> 6, pr = i & 63;
+    if (c0 + cc >= C || p0 + pr >= kp) continue;
+    const float v = t[pr][cc];
+    const bf16 vh = static_cast<bf16>(v);
+    const size_t o = static_cast<size_t>(c0 + cc) * kp + p0 + pr;
+    hi[o] = __builtin_bit_cast(uint16_t, vh);
+    lo[o] = __builtin_bit_cast(uint16_t, static_cast<bf16>(v - static_cast<float>(vh)));
+  }
+}
+
+// x (TX) -> bf16 planes of the same shape (hi = bf16(x), lo = bf16(x - hi); exact for fp16 / bf16 x).
+template <typename TX>
+__global__ __launch_bounds__(256) void wide_x_split_kernel(const TX* __restrict__ x, long long n, uint16_t* __restrict__ hi,
+                                                           uint16_t* __restrict__ lo) {
+  for (long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x; i < n; i += static_cast<long long>(gridDim.x) * 256) {
+    const float v = XIO<TX>::load(x, static_cast<size_t>(i));
+    const bf16 vh = static_cast<bf16>(v);
+    hi[i] = __builtin_bit_cast(uint16_t, vh);
+    lo[i] = __builtin_bit_cast(uint16_t, static_cast<bf16>(v - static_cast<float>(vh)));
+  }
+}
+
+// rs[p] = sum_{b, n} G_s[b][p][n] from the split planes (hi + lo per element), fixed-order tree.
+__global__ __launch_bounds__(256) void wide_rowsum_split_kernel(const uint16_t* __restrict__ gh, const uint16_t* __restrict__ gl,
+                                                                int P, int HW, int B, float* __restrict__ rs) {
+  __shared__ float red[256];
+  const int p = blockIdx.x;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const size_t o = (static_cast<size_t>(b) * P + p) * HW;
+    for (int n = threadIdx.x; n < HW; n += 256)
+      s += __uint_as_float(static_cast<uint32_t>(gh[o + n]) << 16) + __uint_as_float(static_cast<uint32_t>(gl[o + n]) << 16);
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (static_cast<int>(threadIdx.x) < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) rs[p] = red[0];
+}
+
 // D[b][p][n] into `dist` (ld P per image), optional act[g][p].
 template <typename TX>
 int wide_distances(const Geometry& g, const TX* x, const float* protos, float eps, int act_kind, float* dist,
@@ -1001,6 +1297,118 @@ int launch_fwd_wide(const Geometry& g, int x_dtype, const void* x, const float* 
   return check_launch("wide_finish_kernel");
 }
 
+namespace {
+#ifndef WIDE_PRE
+#define WIDE_PRE 1  // the pre-split backward GEMMs (0: the 64 x 64 bf16x3 tile, for A/B)
+#endif
+template <int EPI, bool BT, typename TO>
+int pre_gemm(const PreArgs& a, int grid_x, int grid_y, int grid_z, hipStream_t s) {
+  if (int e = ensure_lds<wide_pre_gemm_kernel<EPI, BT, TO>, kPreLds>()) return e;
+  KernelTimer timer(EPI == 0 ? "wide_pre_gp_kernel" : "wide_pre_gx_kernel", s);
+  hipLaunchKernelGGL((wide_pre_gemm_kernel<EPI, BT, TO>), dim3(grid_x, grid_y, grid_z), dim3(256), kPreLds, s, a);
+  return check_launch("wide_pre_gemm_kernel");
+}
+
+// The wide backward on pre-split operands: G_s as bf16 planes (kEpiGsSplit), then g_x and g_P on
+// wide_pre_gemm_kernel, g_W on the 64 x 64 tile (M = K classes is small).
+int launch_bwd_wide_pre(const Geometry& g, int x_dtype, const void* x, const float* protos, const float* w_last,
+                        float eps, int act_kind, const float* g_logits, const float* g_dist, void* g_x, float* g_protos,
+                        float* g_w, float* ws, const WideBwdLayout& l, const float* D, hipStream_t s) {
+  const int B = g.npix / g.HW;
+  const long long img = static_cast<long long>(g.P) * g.HW;
+  const size_t dp = static_cast<size_t>(g.npix) * g.P;
+  uint16_t* gh = reinterpret_cast<uint16_t*>(ws + l.G);
+  uint16_t* gl = gh + dp;
+  int st = PROTOSEG_OK;
+  {  // G_s as two bf16 planes [B][P][HW]
+    WideArgs a{};
+    a.A = op(w_last, 1, g.ldw, 0);
+    a.B = op(g_logits, g.K, 1, static_cast<long long>(g.HW) * g.K);
+    a.M = g.P, a.N = g.HW, a.Kd = g_logits ? g.K : 0, a.nb = B;
+    a.out = gh, a.out2 = gl, a.om = g.HW, a.on = 1, a.ob = img;
+    a.eps = eps, a.act_kind = act_kind, a.D = D, a.gd = g_dist, a.bf3 = 1;
+    if ((st = gemm<kEpiGsSplit, float, float, -1, -1, float>(a, B, s))) return st;
+  }
+  if (g_x) {  // g_x[b][c][n] = -2 sum_p P[p][c] G_s[b][p][n] + 2 x sum_p G_s
+    const int kp = static_cast<int>(ceil_div(g.P, kPreTK)) * kPreTK;
+    uint16_t* ph = reinterpret_cast<uint16_t*>(ws + l.pt);
+    uint16_t* pl = ph + static_cast<size_t>(g.C) * kp;
+    hipLaunchKernelGGL(wide_pt_split_kernel, dim3(static_cast<unsigned>(ceil_div(kp, 64)), static_cast<unsigned>(ceil_div(g.C, 64))),
+                       dim3(256), 0, s, protos, g.P, g.C, kp, ph, pl);
+    if ((st = check_launch("wide_pt_split_kernel"))) return st;
+    PreArgs a{};
+    a.ahi = ph, a.alo = pl, a.a_bytes = static_cast<unsigned>(static_cast<size_t>(g.C) * kp * 2);
+    a.sab = 0, a.lda = kp, a.akb = kp, a.arows = g.C;
+    a.bhi = gh, a.blo = gl, a.b_bytes = static_cast<unsigned>(dp * 2);
+    a.sbb = img, a.ldb = g.HW, a.bcols = g.npix, a.bnb = g.HW, a.bk = g.P;
+    a.M = g.C, a.N = g.npix, a.K = kp, a.ksplit = 1;
+    a.gx = g_x, a.x = x, a.C = g.C, a.HW = g.HW;
+    const int gx_ = static_cast<int>(ceil_div(g.npix, kPreTN)), gy = static_cast<int>(ceil_div(g.C, kPreTM));
+    if (x_dtype == PROTOSEG_BF16) {
+      a.o_bytes = static_cast<unsigned>(static_cast<size_t>(g.npix) * g.C * 2);
+      st = pre_gemm<1, true, uint16_t>(a, gx_, gy, 1, s);
+    } else if (x_dtype == PROTOSEG_F16) {
+      a.o_bytes = static_cast<unsigned>(static_cast<size_t>(g.npix) * g.C * 2);
+      st = pre_gemm<1, true, _Float16>(a, gx_, gy, 1, s);
+    } else {
+      a.o_bytes = static_cast<unsigned>(static_cast<size_t>(g.npix) * g.C * 4);
+      st = pre_gemm<1, true, float>(a, gx_, gy, 1, s);
+    }
+    if (st) return st;
+  }
+  if (g_protos) {  // g_P[p][c] = -2 sum_{b,n} G_s[b][p][n] x[b][c][n] + 2 p rs[p]
+    float* rs = ws + l.rs;
+    hipLaunchKernelGGL(wide_rowsum_split_kernel, dim3(static_cast<unsigned>(g.P)), dim3(256), 0, s, gh, gl, g.P, g.HW, B, rs);
+    if ((st = check_launch("wide_rowsum_split_kernel"))) return st;
+    uint16_t* xh = reinterpret_cast<uint16_t*>(ws + l.xs);
+    uint16_t* xl = xh + static_cast<size_t>(g.npix) * g.C;
+    const long long nx = static_cast<long long>(g.npix) * g.C;
+    const unsigned xg = static_cast<unsigned>(ceil_div(nx, 256) < 4096 ? ceil_div(nx, 256) : 4096);
+    if (x_dtype == PROTOSEG_BF16)
+      hipLaunchKernelGGL(wide_x_split_kernel<uint16_t>, dim3(xg), dim3(256), 0, s, static_cast<const uint16_t*>(x), nx, xh, xl);
+    else if (x_dtype == PROTOSEG_F16)
+      hipLaunchKernelGGL(wide_x_split_kernel<_Float16>, dim3(xg), dim3(256), 0, s, static_cast<const _Float16*>(x), nx, xh, xl);
+    else
+      hipLaunchKernelGGL(wide_x_split_kernel<float>, dim3(xg), dim3(256), 0, s, static_cast<const float*>(x), nx, xh, xl);
+    if ((st = check_launch("wide_x_split_kernel"))) return st;
+    const int S = pre_split(g);
+    float* part = ws + l.part;
+    PreArgs a{};
+    a.ahi = gh, a.alo = gl, a.a_bytes = static_cast<unsigned>(dp * 2);
+    a.sab = img, a.lda = g.HW, a.akb = g.HW, a.arows = g.P;
+    a.bhi = xh, a.blo = xl, a.b_bytes = static_cast<unsigned>(nx * 2);
+    a.sbb = static_cast<long long>(g.C) * g.HW, a.ldb = g.HW, a.bkb = g.HW, a.bcols = g.C;
+    a.M = g.P, a.N = g.C, a.K = g.npix, a.ksplit = S;
+    a.slab = part;
+    if ((st = pre_gemm<0, false, float>(a, static_cast<int>(ceil_div(g.C, kPreTN)), static_cast<int>(ceil_div(g.P, kPreTM)),
+                                        S, s)))
+      return st;
+    const long long e = static_cast<long long>(g.P) * g.C;
+    hipLaunchKernelGGL(wide_finish_kernel, dim3(static_cast<unsigned>(ceil_div(e, 256))), dim3(256), 0, s, part, S, 1,
+                       g.P, g.C, 1, protos, rs, g_protos, static_cast<long long>(g.C), 0LL);
+    if ((st = check_launch("wide_finish_kernel"))) return st;
+  }
+  if (g_w && g_logits) {  // g_W[k][p] = sum_{b,n} GL[b][n][k] act(D[b][p][n]) (64 x 64 tile)
+    const int S = split_of(g.K, g.P, g.npix);
+    float* part = ws + l.part;
+    WideArgs a{};
+    a.A = op(g_logits, 1, g.K, static_cast<long long>(g.HW) * g.K);
+    a.B = op(D, g.HW, 1, img);
+    a.M = g.K, a.N = g.P, a.Kd = g.HW, a.nb = B, a.bk = 1, a.ksplit = S;
+    a.out = part, a.om = g.P, a.on = 1, a.ob = static_cast<long long>(g.K) * g.P;
+    a.eps = eps, a.bf3 = 1;
+    st = act_kind == PROTOSEG_ACT_LOG ? gemm<kEpiStore, float, float, -1, 0, float>(a, S, s)
+                                      : gemm<kEpiStore, float, float, -1, 1, float>(a, S, s);
+    if (st) return st;
+    const long long e = static_cast<long long>(g.K) * g.P;
+    hipLaunchKernelGGL(wide_finish_kernel, dim3(static_cast<unsigned>(ceil_div(e, 256))), dim3(256), 0, s, part, S, 1,
+                       g.K, g.P, 0, nullptr, nullptr, g_w, static_cast<long long>(g.ldw), 0LL);
+    if ((st = check_launch("wide_finish_kernel"))) return st;
+  }
+  return PROTOSEG_OK;
+}
+}  // namespace
+
 int launch_bwd_wide(const Geometry& g, int x_dtype, const void* x, const float* protos, const float* w_last, float eps,
                     int act_kind, const float* g_logits, const float* g_dist, void* g_x, float* g_protos, float* g_w,
                     void* workspace, hipStream_t s, int bf3, const float* dist_saved) {
@@ -1013,6 +1421,9 @@ int launch_bwd_wide(const Geometry& g, int x_dtype, const void* x, const float* 
   int st = PROTOSEG_OK;
   if (dist_saved) D = const_cast<float*>(dist_saved);  // read-only below (G_s epilogue, g_W operand)
   else if ((st = distances_of(g, x_dtype, x, protos, eps, act_kind, D, nullptr, s, bf3))) return st;
+  if (bf3 && WIDE_PRE && wide_pre_fits(g))
+    return launch_bwd_wide_pre(g, x_dtype, x, protos, w_last, eps, act_kind, g_logits, g_dist, g_x, g_protos, g_w,
+                               ws, l, D, s);
   {  // G_s[b][p][n] = (sum_k W[k][p] GL[b][n][k]) act'(D) + g_dist, relu mask (K = 0: g_dist alone)
     WideArgs a{};
     a.A = op(w_last, 1, g.ldw, 0);                               // (p, k) of W[k][p]

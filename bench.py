@@ -605,8 +605,14 @@ def time_push(n_img, steps, warmup, device, C=64, H=1024, W=2048, h=129, w=257, 
                         f"distinct images from a fresh state, labels {H}x{W} u8, map {C}x{h}x{w} f32, P={P}, K={K}",
             "argmin_kernel_ms_per_img": round(argmin_call / n_img * 1e3, 4),
             "argmin_launches_per_call": launches_per_call,
-            "roofline": roofline_entry(flops / launches_per_call, nbytes / launches_per_call, argmin_s, "f32") |
-            {"kernel": kname[0] if kname else "push_argmin"}}
+            # the argmin computes on bf16 MFMA with exact three-term splits (bf16x6: six products per
+            # f32 multiply-add), so its peak is the bf16 dense peak / 6; the flops are the algorithmic
+            # 2*P*C per pixel, including the candidates the runner-up bound lets it skip (an
+            # effective rate); f32_mfma_frac prices the same rate against the f32 MFMA peak
+            "roofline": (lambda r: r | {"kernel": kname[0] if kname else "push_argmin", "arith": "bf16x6",
+                                        "f32_mfma_frac": round(r["achieved"] / PEAK_F32_MFMA_TFLOPS, 4)
+                                        if r["unit"] == "TFLOP/s" else None})(
+                roofline_entry(flops / launches_per_call, nbytes / launches_per_call, argmin_s, "bf16x6"))}
 
 
 def cpu_push_baseline(budget_s, C=64, H=1024, W=2048, h=129, w=257, P=190, K=19):

@@ -250,7 +250,7 @@ def test_fp16_distance_gemm_near_zero(device):
     x, _, w_last, _, _ = _inputs(B, C, h, w, P, K, seed=7)
     xh = x.half()
     flat = xh.float().permute(0, 2, 3, 1).reshape(-1, C)
-    protos = flat[torch.randperm(flat.shape[0], generator=torch.Generator().manual_seed(1))[:P]].clone()
+    protos = flat[torch.randint(0, flat.shape[0], (P,), generator=torch.Generator().manual_seed(1))].clone()
     xd, pd, wd = xh.to(device), protos.to(device), w_last.to(device)
     ref = ((xh.double()[:, None] - protos.double()[None, :, :, None, None]) ** 2).sum(2)
     bound = _f32_bound(xh.float(), protos)
