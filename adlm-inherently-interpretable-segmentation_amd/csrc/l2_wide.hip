@@ -43,7 +43,7 @@ constexpr int kPreTM = 192, kPreTN = 128, kPreTK = 32, kPreNS = 3;
 constexpr int kPreAPlane = kPreTM * kPreTK * 2;      // 12 KiB
 constexpr int kPreBPlane = kPreTN * kPreTK * 2;      // 8 KiB
 constexpr int kPreStage = 2 * kPreAPlane + 2 * kPreBPlane;  // 40 KiB
-constexpr int kPreLds = kPreNS * kPreStage + 4 * kPreTN * 4;
+constexpr int kPreLds = kPreNS * kPreStage + 16 * kPreTN * 4;
 
 enum WideEpi { kEpiStore = 0, kEpiDist = 1, kEpiGs = 2, kEpiGx = 3, kEpiGsSplit = 4 };
 
@@ -392,8 +392,17 @@ __global__ __launch_bounds__(256) void wide_finish_kernel(const float* __restric
   const long long b = e / mn, r = e - b * mn;
   const int m = static_cast<int>(r / N), n = static_cast<int>(r - static_cast<long long>(m) * N);
   const float* pp = part + static_cast<size_t>(b) * S * mn + r;
+  // slab order kept (the same sum bit for bit), 8 loads in flight (one at a time, a 64-slab
+  // finish was a chain of L2 round trips)
   float s = 0.f;
-  for (int i = 0; i < S; ++i) s += pp[static_cast<size_t>(i) * mn];
+  for (int i0 = 0; i0 < S; i0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = i0 + u < S ? pp[static_cast<size_t>(i0 + u) * mn] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (i0 + u < S) s += v[u];
+  }
   if (kind == 1) s = -2.f * s + 2.f * protos[r] * rs[m];
   out[b * obatch + m * ldo + n] = s;
 }
@@ -685,7 +694,7 @@ constexpr int kF16TM = 192, kF16TN = 128, kF16TK = 32, kF16NS = 3;
 constexpr int kF16ATerm = kF16TM * kF16TK * 2;             // one term's A stage [192 rows][64 B]
 constexpr int kF16BTile = kF16TK * kF16TN * 2;             // the x stage [32 channels][256 B]
 constexpr int kF16Stage = 2 * kF16ATerm + kF16BTile;       // 32 KiB
-constexpr int kF16Lds = kF16NS * kF16Stage + 4 * kF16TN * 4 + 2 * kF16TM * 4;
+constexpr int kF16Lds = kF16NS * kF16Stage + 16 * kF16TN * 4 + 2 * kF16TM * 4;
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef short f16s4 __attribute__((ext_vector_type(4)));
 
@@ -715,10 +724,20 @@ __global__ __launch_bounds__(256) void wide_f16_prep_kernel(const float* __restr
   const bool valid = row < P;
   const float* pr = protos + static_cast<size_t>(valid ? row : 0) * C;
   float mx = 0.f, sq = 0.f;
-  for (int c = lane; c < C; c += 64) {
-    const float v = valid ? pr[c] : 0.f;
-    mx = fmaxf(mx, fabsf(v));
-    sq = fmaf(v, v, sq);
+  // 8 loads in flight per lane (a plain strided loop waits on each one); the same per-lane
+  // summation order as one element at a time
+  for (int c0 = 0; c0 < C; c0 += 8 * 64) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int c = c0 + 64 * u + lane;
+      v[u] = valid && c < C ? pr[c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      mx = fmaxf(mx, fabsf(v[u]));
+      sq = fmaf(v[u], v[u], sq);
+    }
   }
 #pragma unroll
   for (int m = 1; m < 64; m <<= 1) {  // butterfly: every lane ends with the same (fixed-order) sums
@@ -732,11 +751,22 @@ __global__ __launch_bounds__(256) void wide_f16_prep_kernel(const float* __restr
   const float scale = ldexpf(1.f, 14 - e), inv = ldexpf(1.f, e - 14);
   _Float16* hr = ahi + static_cast<size_t>(row) * Kpad;
   _Float16* lr = alo + static_cast<size_t>(row) * Kpad;
-  for (int k = lane; k < Kpad; k += 64) {
-    const float v = (valid && k < C ? pr[k] : 0.f) * scale;  // exact (power of two)
-    const _Float16 hi = static_cast<_Float16>(v);
-    hr[k] = hi;
-    lr[k] = static_cast<_Float16>(v - static_cast<float>(hi));  // v - hi exact in f32
+  for (int k0 = 0; k0 < Kpad; k0 += 8 * 64) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + 64 * u + lane;
+      v[u] = (valid && k < C ? pr[k] : 0.f) * scale;  // exact (power of two)
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + 64 * u + lane;
+      if (k < Kpad) {
+        const _Float16 hi = static_cast<_Float16>(v[u]);
+        hr[k] = hi;
+        lr[k] = static_cast<_Float16>(v[u] - static_cast<float>(hi));  // v - hi exact in f32
+      }
+    }
   }
   if (lane == 0) {
     p2[row] = valid ? sq : 0.f;
@@ -765,57 +795,55 @@ __device__ __forceinline__ constexpr int f16_bswz(int r) { return ((r & 3) << 2)
 // ds_read_b128 row reads of 16 rows per lane group land on distinct banks)
 __device__ __forceinline__ constexpr int f16_aswz(int r) { return (r >> 2) & 3; }
 
-__global__ __launch_bounds__(256, 1) void wide_dist_f16_kernel(F16DistArgs a) {
+__global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void wide_dist_f16_kernel(F16DistArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
   const unsigned S0 = static_cast<unsigned>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)fsm));
   const int lane = threadIdx.x & 63, wave = bf16l::wave_id(), j = lane & 31, h = lane >> 5;
   const int n0 = static_cast<int>(blockIdx.x) * kF16TN, m0 = static_cast<int>(blockIdx.y) * kF16TM;
   const rsrc_t rx = make_rsrc(a.x, a.x_bytes), rah = make_rsrc(a.ahi, a.a_bytes), ral = make_rsrc(a.alo, a.a_bytes);
-  float* red = reinterpret_cast<float*>(fsm + kF16NS * kF16Stage);     // [4][128] x2 partials
-  float* rowv = red + 4 * kF16TN;                                     // [192] p2, [192] 1 / s_p
+  float* red = reinterpret_cast<float*>(fsm + kF16NS * kF16Stage);     // [16][128] x2 partials
+  float* rowv = red + 16 * kF16TN;                                     // [192] p2, [192] 1 / s_p
   for (int i = static_cast<int>(threadIdx.x); i < kF16TM; i += 256) {
     rowv[i] = a.p2[m0 + i];
     rowv[kF16TM + i] = a.inv_s[m0 + i];
   }
 
-  // DMA pieces of a stage: 24 of A (term q / 12, rows 16 (q % 12) ..) and 8 of x (channels
-  // 4 (q - 24) ..); wave w issues pieces 8 w .. 8 w + 7. Per-lane source offsets (k0 = 0):
-  unsigned voff[8];
-  int crow_of[8];
+  // DMA pieces of a stage (1 KiB each): 12 per A term (16 rows each) and 8 of x (4 channel rows
+  // each). Wave w issues A pieces 6 (w & 1) .. + 5 of term w >> 1 and x pieces 2 w, 2 w + 1: one
+  // buffer resource per operand, no wave-dependent branches in the stage loop.
+  const int pl = wave >> 1, half = wave & 1;
+  const rsrc_t ra = pl ? ral : rah;
+  unsigned voa[6], vox[2];
+  int crow_of[2];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int q = 8 * wave + i;
-    crow_of[i] = -1;
-    if (q < 24) {
-      const int r = 16 * (q % 12) + (lane >> 2), pc = lane & 3, lc = pc ^ f16_aswz(r);
-      voff[i] = static_cast<unsigned>(((m0 + r) * a.Kpad + 8 * lc) * 2);
+  for (int i = 0; i < 6; ++i) {
+    const int r = 16 * (6 * half + i) + (lane >> 2), lc = (lane & 3) ^ f16_aswz(r);
+    voa[i] = static_cast<unsigned>(((m0 + r) * a.Kpad + 8 * lc) * 2);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int crow = 4 * (2 * wave + i) + (lane >> 4), lc = (lane & 15) ^ f16_bswz(crow);
+    const int col = n0 + 8 * lc;
+    crow_of[i] = crow;
+    if (col < a.ntot) {
+      const int b = col / a.HW, n = col - b * a.HW;
+      vox[i] = static_cast<unsigned>(((b * a.C + crow) * a.HW + n) * 2);
     } else {
-      const int crow = 4 * (q - 24) + (lane >> 4), pc = lane & 15, lc = pc ^ f16_bswz(crow);
-      const int col = n0 + 8 * lc;
-      crow_of[i] = crow;
-      if (col < a.ntot) {
-        const int b = col / a.HW, n = col - b * a.HW;
-        voff[i] = static_cast<unsigned>(((b * a.C + crow) * a.HW + n) * 2);
-      } else {
-        voff[i] = kOOB;
-      }
+      vox[i] = kOOB;
     }
   }
+  const unsigned lda_off = static_cast<unsigned>(pl * kF16ATerm + 6 * half * 1024);
+  const unsigned ldx_off = static_cast<unsigned>(2 * kF16ATerm + 2 * wave * 1024);
   auto issue = [&](int st) __attribute__((always_inline)) {
     const int k0 = st * kF16TK;
     const unsigned base = S0 + static_cast<unsigned>((st % kF16NS) * kF16Stage);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int q = 8 * wave + i;  // wave-uniform
-      if (q < 24) {
-        dma16(q < 12 ? rah : ral, base + static_cast<unsigned>((q / 12) * kF16ATerm + (q % 12) * 1024), voff[i],
-              static_cast<unsigned>(k0 * 2));
-      } else {
-        const bool ok = voff[i] != kOOB && k0 + crow_of[i] < a.C;
-        dma16(rx, base + static_cast<unsigned>(2 * kF16ATerm + (q - 24) * 1024), ok ? voff[i] : kOOB,
-              static_cast<unsigned>(k0 * a.HW * 2));
-      }
-    }
+    for (int i = 0; i < 6; ++i)
+      dma16(ra, base + lda_off + static_cast<unsigned>(i * 1024), voa[i], static_cast<unsigned>(k0 * 2));
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      dma16(rx, base + ldx_off + static_cast<unsigned>(i * 1024), k0 + crow_of[i] < a.C ? vox[i] : kOOB,
+            static_cast<unsigned>(k0 * a.HW * 2));
   };
 
   // wave w: prototype rows 96 (w & 1) + 32 i (i < 3), pixel columns 64 (w >> 1) + 32 jj (jj < 2)
@@ -824,9 +852,9 @@ __global__ __launch_bounds__(256, 1) void wide_dist_f16_kernel(F16DistArgs a) {
   f32x16 acc[3][2];
 #pragma unroll
   for (int i = 0; i < 3; ++i) acc[i][0] = acc[i][1] = zero16();
-  // x2: thread t sums columns 2 (t & 63), 2 (t & 63) + 1 over channel rows 8 (t >> 6) .. + 7 of each stage
-  float xs0 = 0.f, xs1 = 0.f;
-  const int xcp = threadIdx.x & 63, xsl = threadIdx.x >> 6;
+  // x2: thread t sums columns 8 (t & 15) .. + 7 over channel rows 2 (t >> 4), + 1 of each stage
+  float xs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int xcc = threadIdx.x & 15, xrg = threadIdx.x >> 4;
 
   const int nst = a.Kpad / kF16TK;
   issue(0);
@@ -834,20 +862,13 @@ __global__ __launch_bounds__(256, 1) void wide_dist_f16_kernel(F16DistArgs a) {
   for (int st = 0; st < nst; ++st) {
     if (st + 1 < nst) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    if (st + 2 < nst) issue(st + 2);
     const unsigned sb = S0 + static_cast<unsigned>((st % kF16NS) * kF16Stage);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      f16x8 af[3][2], bfr[2];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int r = 96 * rg + 32 * i + j;
-        const unsigned ao = static_cast<unsigned>(r * 64 + 16 * ((2 * ks + h) ^ f16_aswz(r)));
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-          af[i][t] = *reinterpret_cast<const __attribute__((address_space(3))) f16x8*>(
-              static_cast<uintptr_t>(sb + static_cast<unsigned>(t * kF16ATerm) + ao));
-      }
+    // Schedule (one wave per SIMD: nothing else hides an LDS round trip): the first 16-k step's
+    // fragments are read up front, the second step's and the x2 rows go out one per MFMA of the
+    // first step, then the second step's MFMAs and the x2 arithmetic. Left alone the compiler
+    // reloaded one fragment register per MFMA pair and waited on every read.
+    f16x8 af[2][3][2], bfr[2][2];
+    auto read_step = [&](int ks) __attribute__((always_inline)) {
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
         // block (channel rows 16 ks + 8 h (+4), pixel columns 64 cp + 32 jj + 16 (g & 1) ..):
@@ -861,37 +882,71 @@ __global__ __launch_bounds__(256, 1) void wide_dist_f16_kernel(F16DistArgs a) {
           v[hf] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
               reinterpret_cast<__attribute__((address_space(3))) f16s4*>(static_cast<uintptr_t>(sb + bo)));
         }
-        bfr[jj] = __builtin_bit_cast(f16x8, __builtin_shufflevector(v[0], v[1], 0, 1, 2, 3, 4, 5, 6, 7));
+        bfr[ks][jj] = __builtin_bit_cast(f16x8, __builtin_shufflevector(v[0], v[1], 0, 1, 2, 3, 4, 5, 6, 7));
       }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int r = 96 * rg + 32 * i + j;
+        const unsigned ao = static_cast<unsigned>(r * 64 + 16 * ((2 * ks + h) ^ f16_aswz(r)));
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          af[ks][i][t] = *reinterpret_cast<const __attribute__((address_space(3))) f16x8*>(
+              static_cast<uintptr_t>(sb + static_cast<unsigned>(t * kF16ATerm) + ao));
+      }
+    };
+    auto mfma_step = [&](int ks) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < 3; ++i)
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
-          acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i][1], bfr[jj], acc[i][jj], 0, 0, 0);
-          acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i][0], bfr[jj], acc[i][jj], 0, 0, 0);
+          acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[ks][i][1], bfr[ks][jj], acc[i][jj], 0, 0, 0);
+          acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[ks][i][0], bfr[ks][jj], acc[i][jj], 0, 0, 0);
         }
-    }
-    // this thread's x2 rows of the stage (zeros past C / past the pixels: the DMA filled them so)
+    };
+    read_step(0);
+    __builtin_amdgcn_sched_barrier(0);
+    // x2 rows of the stage: this thread's 8 columns 8 xcc .. + 7 of channel rows 2 xrg, 2 xrg + 1
+    // (zeros past C / past the pixels: the DMA filled them so)
+    f16x8 xr[2];
 #pragma unroll
-    for (int rr = 0; rr < 8; ++rr) {
-      const int r = 8 * xsl + rr, col = 2 * xcp;
-      const unsigned o = static_cast<unsigned>(2 * kF16ATerm + 256 * r + 16 * ((col >> 3) ^ f16_bswz(r)) + 2 * (col & 7));
-      const uint32_t w2 = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(static_cast<uintptr_t>(sb + o));
-      const float v0 = static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(w2 & 0xffffu)));
-      const float v1 = static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(w2 >> 16)));
-      xs0 = fmaf(v0, v0, xs0);
-      xs1 = fmaf(v1, v1, xs1);
+    for (int rr = 0; rr < 2; ++rr) {
+      const int r = 2 * xrg + rr;
+      xr[rr] = *reinterpret_cast<const __attribute__((address_space(3))) f16x8*>(
+          static_cast<uintptr_t>(sb + static_cast<unsigned>(2 * kF16ATerm + 256 * r + 16 * (xcc ^ f16_bswz(r)))));
     }
+    read_step(1);
+    mfma_step(0);
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one LDS read
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_step(1);
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = static_cast<float>(xr[rr][e]);
+        xs[e] = fmaf(v, v, xs[e]);
+      }
+    // the stage after next goes out behind the MFMAs (their pipe is busy while the wave issues
+    // it); its buffer was last read in stage st - 1, which every wave finished before this
+    // stage's barrier
+    __builtin_amdgcn_sched_barrier(0);
+    if (st + 2 < nst) issue(st + 2);
   }
-  red[xsl * kF16TN + 2 * xcp] = xs0;
-  red[xsl * kF16TN + 2 * xcp + 1] = xs1;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[xrg * kF16TN + 8 * xcc + e] = xs[e];
   __syncthreads();
 
   const rsrc_t rd = make_rsrc(a.dist, a.d_bytes);
 #pragma unroll
   for (int jj = 0; jj < 2; ++jj) {
     const int cn = 64 * cp + 32 * jj + j, col = n0 + cn;
-    const float x2 = ((red[cn] + red[kF16TN + cn]) + red[2 * kF16TN + cn]) + red[3 * kF16TN + cn];
+    float x2 = red[cn];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) x2 += red[q * kF16TN + cn];
     const int b = col < a.ntot ? col / a.HW : 0, n = col - b * a.HW;
     // the lane's part of the address (pixel, row 4h) in the voffset, the register's row in the
     // (uniform) soffset
@@ -999,7 +1054,7 @@ template <> struct BufIO2<_Float16> {
 };
 
 template <int EPI, bool BT, typename TO>
-__global__ __launch_bounds__(256, 1) void wide_pre_gemm_kernel(PreArgs a) {
+__global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void wide_pre_gemm_kernel(PreArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
   const unsigned S0 = static_cast<unsigned>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)psm));
   const int lane = threadIdx.x & 63, wave = bf16l::wave_id(), j = lane & 31, h = lane >> 5;
@@ -1012,53 +1067,65 @@ __global__ __launch_bounds__(256, 1) void wide_pre_gemm_kernel(PreArgs a) {
   const int st1 = static_cast<int>((static_cast<long long>(nst_all) * (z + 1)) / a.ksplit);
   const int nst = st1 - st0;
 
-  // 40 DMA pieces per stage, 10 per wave: 0..23 A (plane q / 12, rows 16 (q % 12) ..), 24..39 B
-  // (plane (q - 24) / 8; BT = 0: rows = columns 16 ((q - 24) % 8) ..; BT = 1: k rows 4 ((q - 24) % 8) ..)
-  unsigned voff[10];
-  int krow[10];
+  // 40 DMA pieces per stage (1 KiB each): A planes of 12 pieces (16 rows each), B planes of 8
+  // (BT = 0: 16 columns each; BT = 1: 4 k rows each). Wave w issues plane w >> 1 of both
+  // operands: A pieces 6 (w & 1) .. + 5, B pieces 4 (w & 1) .. + 3 — one buffer resource per
+  // operand, no wave-dependent branches in the stage loop.
+  const int pl = wave >> 1, half = wave & 1;
+  const rsrc_t ra = pl ? ral : rah, rb = pl ? rbl : rbh;
+  unsigned voa[6], vob[4];
+  int krow[4];
 #pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    const int q = 10 * wave + i;
-    krow[i] = -1;
-    if (q < 24) {
-      const int r = 16 * (q % 12) + (lane >> 2), lc = (lane & 3) ^ f16_aswz(r);
-      voff[i] = m0 + r < a.arows ? static_cast<unsigned>((static_cast<long long>(m0 + r) * a.lda + 8 * lc) * 2) : kOOB;
-    } else if (!BT) {
-      const int r = 16 * ((q - 24) % 8) + (lane >> 2), lc = (lane & 3) ^ f16_aswz(r);
-      voff[i] = n0 + r < a.bcols ? static_cast<unsigned>((static_cast<long long>(n0 + r) * a.ldb + 8 * lc) * 2) : kOOB;
+  for (int i = 0; i < 6; ++i) {
+    const int r = 16 * (6 * half + i) + (lane >> 2), lc = (lane & 3) ^ f16_aswz(r);
+    voa[i] = m0 + r < a.arows ? static_cast<unsigned>((static_cast<long long>(m0 + r) * a.lda + 8 * lc) * 2) : kOOB;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int qb = 4 * half + i;
+    krow[i] = 0;
+    if constexpr (!BT) {
+      const int r = 16 * qb + (lane >> 2), lc = (lane & 3) ^ f16_aswz(r);
+      vob[i] = n0 + r < a.bcols ? static_cast<unsigned>((static_cast<long long>(n0 + r) * a.ldb + 8 * lc) * 2) : kOOB;
     } else {
-      const int kr = 4 * ((q - 24) % 8) + (lane >> 4), lc = (lane & 15) ^ f16_bswz(kr);
+      const int kr = 4 * qb + (lane >> 4), lc = (lane & 15) ^ f16_bswz(kr);
       const int col = n0 + 8 * lc;
       krow[i] = kr;
       if (col < a.bcols) {
         const int cb = col / a.bnb, n = col - cb * a.bnb;
-        voff[i] = static_cast<unsigned>((cb * a.sbb + static_cast<long long>(kr) * a.ldb + n) * 2);
+        vob[i] = static_cast<unsigned>((cb * a.sbb + static_cast<long long>(kr) * a.ldb + n) * 2);
       } else {
-        voff[i] = kOOB;
+        vob[i] = kOOB;
       }
     }
   }
+  const unsigned lda_off = static_cast<unsigned>(pl * kPreAPlane + 6 * half * 1024);
+  const unsigned ldb_off = static_cast<unsigned>(2 * kPreAPlane + pl * kPreBPlane + 4 * half * 1024);
+  // stage soffsets advance by 32 k per issue (issue() runs for st = 0, 1, 2, ... in order): the
+  // (block, rest) of kg in the A (and BT = 0 B) k-blocking, without a division per stage
+  int kga = st0 * kPreTK, ka_b = kga / a.akb, ka_r = kga - ka_b * a.akb;
+  int kb_b = BT ? 0 : kga / a.bkb, kb_r = BT ? 0 : kga - kb_b * a.bkb;
   auto issue = [&](int st) __attribute__((always_inline)) {  // global stage st0 + st into buffer st % 3
-    const int kg = (st0 + st) * kPreTK;
     const unsigned base = S0 + static_cast<unsigned>((st % kPreNS) * kPreStage);
-    const unsigned sa = static_cast<unsigned>(((kg / a.akb) * a.sab + kg % a.akb) * 2);
+    const unsigned sa = static_cast<unsigned>((ka_b * a.sab + ka_r) * 2);
 #pragma unroll
-    for (int i = 0; i < 10; ++i) {
-      const int q = 10 * wave + i;  // wave-uniform
-      if (q < 24) {
-        dma16(q < 12 ? rah : ral, base + static_cast<unsigned>((q / 12) * kPreAPlane + (q % 12) * 1024), voff[i], sa);
-      } else {
-        const int qb = q - 24;
-        const unsigned dst = base + static_cast<unsigned>(2 * kPreAPlane + (qb / 8) * kPreBPlane + (qb % 8) * 1024);
-        if constexpr (!BT) {
-          const unsigned sb = static_cast<unsigned>(((kg / a.bkb) * a.sbb + kg % a.bkb) * 2);
-          dma16(qb < 8 ? rbh : rbl, dst, voff[i], sb);
-        } else {
-          const bool ok = voff[i] != kOOB && kg + krow[i] < a.bk;
-          dma16(qb < 8 ? rbh : rbl, dst, ok ? voff[i] : kOOB, static_cast<unsigned>(static_cast<long long>(kg) * a.ldb * 2));
-        }
-      }
+    for (int i = 0; i < 6; ++i) dma16(ra, base + lda_off + static_cast<unsigned>(i * 1024), voa[i], sa);
+    if constexpr (!BT) {
+      const unsigned sb = static_cast<unsigned>((kb_b * a.sbb + kb_r) * 2);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dma16(rb, base + ldb_off + static_cast<unsigned>(i * 1024), vob[i], sb);
+      kb_r += kPreTK;
+      if (kb_r == a.bkb) kb_r = 0, ++kb_b;
+    } else {
+      const int kg = kga;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        dma16(rb, base + ldb_off + static_cast<unsigned>(i * 1024), kg + krow[i] < a.bk ? vob[i] : kOOB,
+              static_cast<unsigned>(static_cast<long long>(kg) * a.ldb * 2));
     }
+    kga += kPreTK;
+    ka_r += kPreTK;
+    if (ka_r == a.akb) ka_r = 0, ++ka_b;
   };
 
   const int rg = wave & 1, cp = wave >> 1;
@@ -1066,28 +1133,21 @@ __global__ __launch_bounds__(256, 1) void wide_pre_gemm_kernel(PreArgs a) {
   f32x16 acc[3][2];
 #pragma unroll
   for (int i = 0; i < 3; ++i) acc[i][0] = acc[i][1] = zero16();
-  float cs0 = 0.f, cs1 = 0.f;  // EPI 1: column sums of B (sum_p G_s) over this thread's slice
-  const int xcp = threadIdx.x & 63, xsl = threadIdx.x >> 6;
+  // EPI 1: column sums of B (sum_p G_s): thread t sums columns 8 (t & 15) .. + 7 over k rows
+  // 2 (t >> 4), + 1 of each stage
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int xcc = threadIdx.x & 15, xrg = threadIdx.x >> 4;
 
   if (nst > 0) issue(0);
   if (nst > 1) issue(1);
   for (int st = 0; st < nst; ++st) {
     if (st + 1 < nst) asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    if (st + 2 < nst) issue(st + 2);
     const unsigned sb = S0 + static_cast<unsigned>((st % kPreNS) * kPreStage);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[3][2], bfr[2][2];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int r = 96 * rg + 32 * i + j;
-        const unsigned ao = static_cast<unsigned>(r * 64 + 16 * ((2 * ks + h) ^ f16_aswz(r)));
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-          af[i][t] = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(
-              static_cast<uintptr_t>(sb + static_cast<unsigned>(t * kPreAPlane) + ao));
-      }
+    // schedule as in wide_dist_f16_kernel: step 0's fragments up front, step 1's (and the EPI 1
+    // column-sum rows) one per MFMA of step 0, then step 1's MFMAs
+    bf16x8 af[2][3][2], bfr[2][2][2];
+    auto read_step = [&](int ks) __attribute__((always_inline)) {
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
 #pragma unroll
@@ -1095,7 +1155,7 @@ __global__ __launch_bounds__(256, 1) void wide_pre_gemm_kernel(PreArgs a) {
           const unsigned pb = sb + static_cast<unsigned>(2 * kPreAPlane + t * kPreBPlane);
           if constexpr (!BT) {
             const int c = 64 * cp + 32 * jj + j;
-            bfr[jj][t] = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(
+            bfr[ks][jj][t] = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(
                 static_cast<uintptr_t>(pb + static_cast<unsigned>(c * 64 + 16 * ((2 * ks + h) ^ f16_aswz(c)))));
           } else {
             const int ch = 8 * cp + 4 * jj + 2 * (g & 1) + (p4 >> 1);
@@ -1106,32 +1166,62 @@ __global__ __launch_bounds__(256, 1) void wide_pre_gemm_kernel(PreArgs a) {
               v[hf] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(reinterpret_cast<__attribute__((address_space(3))) f16s4*>(
                   static_cast<uintptr_t>(pb + static_cast<unsigned>(256 * r + 16 * (ch ^ f16_bswz(r)) + 8 * (p4 & 1)))));
             }
-            bfr[jj][t] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v[0], v[1], 0, 1, 2, 3, 4, 5, 6, 7));
+            bfr[ks][jj][t] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v[0], v[1], 0, 1, 2, 3, 4, 5, 6, 7));
           }
         }
       }
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
+      for (int i = 0; i < 3; ++i) {
+        const int r = 96 * rg + 32 * i + j;
+        const unsigned ao = static_cast<unsigned>(r * 64 + 16 * ((2 * ks + h) ^ f16_aswz(r)));
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mma_split<2>(af[i], bfr[jj], acc[i][jj]);
-    }
-    if constexpr (EPI == 1) {  // sum_p G_s: this thread's 8 k rows of the stage, columns 2 xcp, 2 xcp + 1
-#pragma unroll
-      for (int rr = 0; rr < 8; ++rr) {
-        const int r = 8 * xsl + rr, col = 2 * xcp;
-        const unsigned o = static_cast<unsigned>(2 * kPreAPlane + 256 * r + 16 * ((col >> 3) ^ f16_bswz(r)) + 2 * (col & 7));
-        const uint32_t wh = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(static_cast<uintptr_t>(sb + o));
-        const uint32_t wl = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
-            static_cast<uintptr_t>(sb + o + kPreBPlane));
-        cs0 += __uint_as_float(wh << 16) + __uint_as_float(wl << 16);
-        cs1 += __uint_as_float(wh & 0xffff0000u) + __uint_as_float(wl & 0xffff0000u);
+        for (int t = 0; t < 2; ++t)
+          af[ks][i][t] = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(
+              static_cast<uintptr_t>(sb + static_cast<unsigned>(t * kPreAPlane) + ao));
       }
+    };
+    read_step(0);
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8 cr[2][2];  // EPI 1: B rows 2 xrg, 2 xrg + 1, columns 8 xcc .. + 7, hi and lo
+    if constexpr (EPI == 1) {
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int r = 2 * xrg + rr;
+          cr[rr][t] = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(static_cast<uintptr_t>(
+              sb + static_cast<unsigned>(2 * kPreAPlane + t * kPreBPlane + 256 * r + 16 * (xcc ^ f16_bswz(r)))));
+        }
     }
+    read_step(1);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mma_split<2>(af[0][i], bfr[0][jj], acc[i][jj]);
+#pragma unroll
+    for (int k = 0; k < 18; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one LDS read
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mma_split<2>(af[1][i], bfr[1][jj], acc[i][jj]);
+    if constexpr (EPI == 1) {
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cs[e] += static_cast<float>(cr[rr][0][e]) + static_cast<float>(cr[rr][1][e]);
+    }
+    // the stage after next goes out behind the MFMAs (wide_dist_f16_kernel)
+    __builtin_amdgcn_sched_barrier(0);
+    if (st + 2 < nst) issue(st + 2);
   }
   float* red = reinterpret_cast<float*>(psm + kPreNS * kPreStage);
   if constexpr (EPI == 1) {
-    red[xsl * kPreTN + 2 * xcp] = cs0;
-    red[xsl * kPreTN + 2 * xcp + 1] = cs1;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[xrg * kPreTN + 8 * xcc + e] = cs[e];
     __syncthreads();
   }
 
@@ -1151,7 +1241,9 @@ __global__ __launch_bounds__(256, 1) void wide_pre_gemm_kernel(PreArgs a) {
                                                 static_cast<unsigned>(mu * a.N * 4), 0);
         }
     } else {  // g_x (TO) at (b C + c) HW + n: -2 acc + 2 x sum_p G_s
-      const float csum = ((red[cn] + red[kPreTN + cn]) + red[2 * kPreTN + cn]) + red[3 * kPreTN + cn];
+      float csum = red[cn];
+#pragma unroll
+      for (int q = 1; q < 16; ++q) csum += red[q * kPreTN + cn];
       const int b = col < a.N ? col / a.HW : 0, n = col - b * a.HW;
       const unsigned cbase = col < a.N ? static_cast<unsigned>((b * a.C * a.HW + n + 4 * h * a.HW) * sizeof(TO)) : kOOB;
       const rsrc_t ro = make_rsrc(a.gx, a.o_bytes), rxo = make_rsrc(a.x, a.o_bytes);
@@ -1206,11 +1298,20 @@ __global__ __launch_bounds__(256) void wide_rowsum_split_kernel(const uint16_t* 
                                                                 int P, int HW, int B, float* __restrict__ rs) {
   __shared__ float red[256];
   const int p = blockIdx.x;
+  // per pixel n of the thread, the images in order with 8 pairs of loads in flight
   float s = 0.f;
-  for (int b = 0; b < B; ++b) {
-    const size_t o = (static_cast<size_t>(b) * P + p) * HW;
-    for (int n = threadIdx.x; n < HW; n += 256)
-      s += __uint_as_float(static_cast<uint32_t>(gh[o + n]) << 16) + __uint_as_float(static_cast<uint32_t>(gl[o + n]) << 16);
+  for (int n = static_cast<int>(threadIdx.x); n < HW; n += 256) {
+    for (int b0 = 0; b0 < B; b0 += 8) {
+      uint32_t hv[8], lv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const size_t o = (static_cast<size_t>(b0 + u) * P + p) * HW + n;
+        hv[u] = b0 + u < B ? gh[o] : 0u;
+        lv[u] = b0 + u < B ? gl[o] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += __uint_as_float(hv[u] << 16) + __uint_as_float(lv[u] << 16);
+    }
   }
   red[threadIdx.x] = s;
   __syncthreads();

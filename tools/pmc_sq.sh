@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ/LDS counter passes over tools/ablate.py variants, or over CMD (a python3 argument list, e.g.
-# CMD="tools/wide_run.py c4 5"); one counter group per pass, kernel trace only — never combined
+# CMD="tools/wide_run.py c4 5", relative to the repo root); one counter group per pass, kernel trace only — never combined
 # with other tracing domains.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -17,7 +17,7 @@ for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WA
   i=$((i+1))
   echo "== pass $i: $grp"
   timeout -k 10 180 rocprofv3 --kernel-trace --pmc $grp -d "$OUT/p$i" -o p$i --output-format csv -- \
-    python3 ${CMD:-"$R/tools/ablate.py" --reps 3 --only "$ONLY" ${ABLATE_ARGS:-}} > "$OUT/p$i.log" 2>&1
+    python3 $R/${CMD:-tools/ablate.py --reps 3 --only "$ONLY" ${ABLATE_ARGS:-}} > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "rc=$rc"; tail -n 2 "$OUT/p$i.log"
   if [ $rc -ne 0 ]; then exit $rc; fi
