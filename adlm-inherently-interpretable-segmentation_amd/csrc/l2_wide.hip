@@ -1298,20 +1298,11 @@ __global__ __launch_bounds__(256) void wide_rowsum_split_kernel(const uint16_t* 
                                                                 int P, int HW, int B, float* __restrict__ rs) {
   __shared__ float red[256];
   const int p = blockIdx.x;
-  // per pixel n of the thread, the images in order with 8 pairs of loads in flight
   float s = 0.f;
-  for (int n = static_cast<int>(threadIdx.x); n < HW; n += 256) {
-    for (int b0 = 0; b0 < B; b0 += 8) {
-      uint32_t hv[8], lv[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const size_t o = (static_cast<size_t>(b0 + u) * P + p) * HW + n;
-        hv[u] = b0 + u < B ? gh[o] : 0u;
-        lv[u] = b0 + u < B ? gl[o] : 0u;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += __uint_as_float(hv[u] << 16) + __uint_as_float(lv[u] << 16);
-    }
+  for (int b = 0; b < B; ++b) {
+    const size_t o = (static_cast<size_t>(b) * P + p) * HW;
+    for (int n = threadIdx.x; n < HW; n += 256)
+      s += __uint_as_float(static_cast<uint32_t>(gh[o + n]) << 16) + __uint_as_float(static_cast<uint32_t>(gl[o + n]) << 16);
   }
   red[threadIdx.x] = s;
   __syncthreads();
