@@ -38,12 +38,14 @@ constexpr int kWT = 64;        // workgroup output tile (rows and columns)
 constexpr int kWKs = 32;       // contraction per LDS stage
 constexpr int kWThreads = 256;
 
-// the pre-split backward GEMMs' tile (wide_pre_gemm_kernel, below)
-constexpr int kPreTM = 192, kPreTN = 128, kPreTK = 32, kPreNS = 3;
-constexpr int kPreAPlane = kPreTM * kPreTK * 2;      // 12 KiB
-constexpr int kPreBPlane = kPreTN * kPreTK * 2;      // 8 KiB
-constexpr int kPreStage = 2 * kPreAPlane + 2 * kPreBPlane;  // 40 KiB
-constexpr int kPreLds = kPreNS * kPreStage + 16 * kPreTN * 4;
+// the pre-split backward GEMMs' tile (wide_pre_gemm_kernel, below): 64 MI rows (MI = 3 or 4
+// 32-row blocks per wave) x 128 columns x 32 k per stage, three stages
+constexpr int kPreTN = 128, kPreTK = 32, kPreNS = 3;
+constexpr int kPreBPlane = kPreTN * kPreTK * 2;                                  // 8 KiB
+__host__ __device__ constexpr int pre_tm(int MI) { return 64 * MI; }
+__host__ __device__ constexpr int pre_aplane(int MI) { return pre_tm(MI) * kPreTK * 2; }  // 12 / 16 KiB
+__host__ __device__ constexpr int pre_stage(int MI) { return 2 * pre_aplane(MI) + 2 * kPreBPlane; }
+__host__ __device__ constexpr int pre_lds(int MI) { return kPreNS * pre_stage(MI) + 16 * kPreTN * 4; }
 
 enum WideEpi { kEpiStore = 0, kEpiDist = 1, kEpiGs = 2, kEpiGx = 3, kEpiGsSplit = 4 };
 
@@ -641,9 +643,17 @@ bool wide_pre_fits(const Geometry& g) {
   return g.HW % 32 == 0 && static_cast<long long>(g.npix) * g.C * 2 < big &&
          static_cast<long long>(g.npix) * g.P * 2 < big && static_cast<long long>(g.C) * (g.P + 32) * 2 < big;
 }
-int pre_split(const Geometry& g) {  // workgroups along the g_P contraction: about 256 in all, >= 4 stages each
-  const long long tiles = ceil_div(g.P, kPreTM) * ceil_div(g.C, kPreTN);
-  long long s2 = ceil_div(256, tiles);
+// Row blocks per wave of a pre GEMM with M rows and `cols` output tiles along N (times `splits`):
+// the one whose grid takes fewer rounds of 256 workgroups, then the one with fewer padded rows.
+int pre_mi(long long M, long long cols) {
+  const long long t3 = ceil_div(M, pre_tm(3)) * cols, t4 = ceil_div(M, pre_tm(4)) * cols;
+  const long long r3 = ceil_div(t3, 256), r4 = ceil_div(t4, 256);
+  if (r3 != r4) return r4 < r3 ? 4 : 3;
+  return ceil_div(M, pre_tm(4)) * pre_tm(4) < ceil_div(M, pre_tm(3)) * pre_tm(3) ? 4 : 3;
+}
+int pre_split(const Geometry& g) {  // workgroups along the g_P contraction: at most 256 in all (one round), >= 4 stages each
+  const long long tiles = ceil_div(g.P, pre_tm(3)) * ceil_div(g.C, kPreTN);
+  long long s2 = 256 / tiles;
   const long long cap = ceil_div(static_cast<long long>(g.npix), 4 * kPreTK);
   if (s2 > cap) s2 = cap;
   return static_cast<int>(s2 < 1 ? 1 : s2 > 64 ? 64 : s2);
@@ -1053,12 +1063,14 @@ template <> struct BufIO2<_Float16> {
   }
 };
 
-template <int EPI, bool BT, typename TO>
+template <int EPI, bool BT, typename TO, int MI>
 __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void wide_pre_gemm_kernel(PreArgs a) {
+  constexpr int kTM = pre_tm(MI), kAP = pre_aplane(MI), kStage = pre_stage(MI);
+  constexpr int kAW = 2 * MI;  // A pieces per wave and stage (16 rows each)
   extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
   const unsigned S0 = static_cast<unsigned>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)psm));
   const int lane = threadIdx.x & 63, wave = bf16l::wave_id(), j = lane & 31, h = lane >> 5;
-  const int n0 = static_cast<int>(blockIdx.x) * kPreTN, m0 = static_cast<int>(blockIdx.y) * kPreTM;
+  const int n0 = static_cast<int>(blockIdx.x) * kPreTN, m0 = static_cast<int>(blockIdx.y) * kTM;
   const int z = static_cast<int>(blockIdx.z);
   const rsrc_t rah = make_rsrc(a.ahi, a.a_bytes), ral = make_rsrc(a.alo, a.a_bytes);
   const rsrc_t rbh = make_rsrc(a.bhi, a.b_bytes), rbl = make_rsrc(a.blo, a.b_bytes);
@@ -1067,17 +1079,17 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   const int st1 = static_cast<int>((static_cast<long long>(nst_all) * (z + 1)) / a.ksplit);
   const int nst = st1 - st0;
 
-  // 40 DMA pieces per stage (1 KiB each): A planes of 12 pieces (16 rows each), B planes of 8
+  // DMA pieces per stage (1 KiB each): A planes of 4 MI pieces (16 rows each), B planes of 8
   // (BT = 0: 16 columns each; BT = 1: 4 k rows each). Wave w issues plane w >> 1 of both
-  // operands: A pieces 6 (w & 1) .. + 5, B pieces 4 (w & 1) .. + 3 — one buffer resource per
-  // operand, no wave-dependent branches in the stage loop.
+  // operands: A pieces 2 MI (w & 1) .. + 2 MI - 1, B pieces 4 (w & 1) .. + 3 — one buffer
+  // resource per operand, no wave-dependent branches in the stage loop.
   const int pl = wave >> 1, half = wave & 1;
   const rsrc_t ra = pl ? ral : rah, rb = pl ? rbl : rbh;
-  unsigned voa[6], vob[4];
+  unsigned voa[kAW], vob[4];
   int krow[4];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const int r = 16 * (6 * half + i) + (lane >> 2), lc = (lane & 3) ^ f16_aswz(r);
+  for (int i = 0; i < kAW; ++i) {
+    const int r = 16 * (kAW * half + i) + (lane >> 2), lc = (lane & 3) ^ f16_aswz(r);
     voa[i] = m0 + r < a.arows ? static_cast<unsigned>((static_cast<long long>(m0 + r) * a.lda + 8 * lc) * 2) : kOOB;
   }
 #pragma unroll
@@ -1099,17 +1111,17 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       }
     }
   }
-  const unsigned lda_off = static_cast<unsigned>(pl * kPreAPlane + 6 * half * 1024);
-  const unsigned ldb_off = static_cast<unsigned>(2 * kPreAPlane + pl * kPreBPlane + 4 * half * 1024);
+  const unsigned lda_off = static_cast<unsigned>(pl * kAP + kAW * half * 1024);
+  const unsigned ldb_off = static_cast<unsigned>(2 * kAP + pl * kPreBPlane + 4 * half * 1024);
   // stage soffsets advance by 32 k per issue (issue() runs for st = 0, 1, 2, ... in order): the
   // (block, rest) of kg in the A (and BT = 0 B) k-blocking, without a division per stage
   int kga = st0 * kPreTK, ka_b = kga / a.akb, ka_r = kga - ka_b * a.akb;
   int kb_b = BT ? 0 : kga / a.bkb, kb_r = BT ? 0 : kga - kb_b * a.bkb;
   auto issue = [&](int st) __attribute__((always_inline)) {  // global stage st0 + st into buffer st % 3
-    const unsigned base = S0 + static_cast<unsigned>((st % kPreNS) * kPreStage);
+    const unsigned base = S0 + static_cast<unsigned>((st % kPreNS) * kStage);
     const unsigned sa = static_cast<unsigned>((ka_b * a.sab + ka_r) * 2);
 #pragma unroll
-    for (int i = 0; i < 6; ++i) dma16(ra, base + lda_off + static_cast<unsigned>(i * 1024), voa[i], sa);
+    for (int i = 0; i < kAW; ++i) dma16(ra, base + lda_off + static_cast<unsigned>(i * 1024), voa[i], sa);
     if constexpr (!BT) {
       const unsigned sb = static_cast<unsigned>((kb_b * a.sbb + kb_r) * 2);
 #pragma unroll
@@ -1130,9 +1142,9 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 
   const int rg = wave & 1, cp = wave >> 1;
   const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
-  f32x16 acc[3][2];
+  f32x16 acc[MI][2];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) acc[i][0] = acc[i][1] = zero16();
+  for (int i = 0; i < MI; ++i) acc[i][0] = acc[i][1] = zero16();
   // EPI 1: column sums of B (sum_p G_s): thread t sums columns 8 (t & 15) .. + 7 over k rows
   // 2 (t >> 4), + 1 of each stage
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1141,18 +1153,22 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   if (nst > 0) issue(0);
   if (nst > 1) issue(1);
   for (int st = 0; st < nst; ++st) {
-    if (st + 1 < nst) asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    const unsigned sb = S0 + static_cast<unsigned>((st % kPreNS) * kPreStage);
+    if (st + 1 < nst) {  // this stage's pieces landed; the next stage's (kAW + 4 per wave) may be in flight
+      if constexpr (MI == 3) asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    const unsigned sb = S0 + static_cast<unsigned>((st % kPreNS) * kStage);
     // schedule as in wide_dist_f16_kernel: step 0's fragments up front, step 1's (and the EPI 1
     // column-sum rows) one per MFMA of step 0, then step 1's MFMAs
-    bf16x8 af[2][3][2], bfr[2][2][2];
+    bf16x8 af[2][MI][2], bfr[2][2][2];
     auto read_step = [&](int ks) __attribute__((always_inline)) {
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          const unsigned pb = sb + static_cast<unsigned>(2 * kPreAPlane + t * kPreBPlane);
+          const unsigned pb = sb + static_cast<unsigned>(2 * kAP + t * kPreBPlane);
           if constexpr (!BT) {
             const int c = 64 * cp + 32 * jj + j;
             bfr[ks][jj][t] = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(
@@ -1171,13 +1187,13 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         }
       }
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int r = 96 * rg + 32 * i + j;
+      for (int i = 0; i < MI; ++i) {
+        const int r = 32 * MI * rg + 32 * i + j;
         const unsigned ao = static_cast<unsigned>(r * 64 + 16 * ((2 * ks + h) ^ f16_aswz(r)));
 #pragma unroll
         for (int t = 0; t < 2; ++t)
           af[ks][i][t] = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(
-              static_cast<uintptr_t>(sb + static_cast<unsigned>(t * kPreAPlane) + ao));
+              static_cast<uintptr_t>(sb + static_cast<unsigned>(t * kAP) + ao));
       }
     };
     read_step(0);
@@ -1190,22 +1206,22 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         for (int t = 0; t < 2; ++t) {
           const int r = 2 * xrg + rr;
           cr[rr][t] = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(static_cast<uintptr_t>(
-              sb + static_cast<unsigned>(2 * kPreAPlane + t * kPreBPlane + 256 * r + 16 * (xcc ^ f16_bswz(r)))));
+              sb + static_cast<unsigned>(2 * kAP + t * kPreBPlane + 256 * r + 16 * (xcc ^ f16_bswz(r)))));
         }
     }
     read_step(1);
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mma_split<2>(af[0][i], bfr[0][jj], acc[i][jj]);
 #pragma unroll
-    for (int k = 0; k < 18; ++k) {
+    for (int k = 0; k < 6 * MI; ++k) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one LDS read
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mma_split<2>(af[1][i], bfr[1][jj], acc[i][jj]);
     if constexpr (EPI == 1) {
@@ -1218,7 +1234,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     __builtin_amdgcn_sched_barrier(0);
     if (st + 2 < nst) issue(st + 2);
   }
-  float* red = reinterpret_cast<float*>(psm + kPreNS * kPreStage);
+  float* red = reinterpret_cast<float*>(psm + kPreNS * kStage);
   if constexpr (EPI == 1) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) red[xrg * kPreTN + 8 * xcc + e] = cs[e];
@@ -1231,10 +1247,10 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     if constexpr (EPI == 0) {  // slab z: [M][N] f32, lane = column
       const rsrc_t rs = make_rsrc(a.slab + static_cast<size_t>(z) * a.M * a.N, static_cast<unsigned>(static_cast<size_t>(a.M) * a.N * 4));
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int mu = m0 + 96 * rg + 32 * i + row_of(r);  // wave-uniform; the lane's row is mu + 4h
+          const int mu = m0 + 32 * MI * rg + 32 * i + row_of(r);  // wave-uniform; the lane's row is mu + 4h
           const bool ok = mu + 4 * h < a.M && col < a.N;
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][jj][r]), rs,
                                                 ok ? static_cast<unsigned>(((4 * h) * a.N + col) * 4) : kOOB,
@@ -1248,10 +1264,10 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       const unsigned cbase = col < a.N ? static_cast<unsigned>((b * a.C * a.HW + n + 4 * h * a.HW) * sizeof(TO)) : kOOB;
       const rsrc_t ro = make_rsrc(a.gx, a.o_bytes), rxo = make_rsrc(a.x, a.o_bytes);
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int mu = m0 + 96 * rg + 32 * i + row_of(r);
+          const int mu = m0 + 32 * MI * rg + 32 * i + row_of(r);
           const unsigned vo = mu + 4 * h < a.M ? cbase : kOOB, so = static_cast<unsigned>(mu * a.HW * sizeof(TO));
           const float xv = BufIO2<TO>::load(rxo, vo, so);
           BufIO2<TO>::store(ro, -2.f * acc[i][jj][r] + 2.f * xv * csum, vo, so);
@@ -1393,12 +1409,19 @@ namespace {
 #ifndef WIDE_PRE
 #define WIDE_PRE 1  // the pre-split backward GEMMs (0: the 64 x 64 bf16x3 tile, for A/B)
 #endif
-template <int EPI, bool BT, typename TO>
-int pre_gemm(const PreArgs& a, int grid_x, int grid_y, int grid_z, hipStream_t s) {
-  if (int e = ensure_lds<wide_pre_gemm_kernel<EPI, BT, TO>, kPreLds>()) return e;
+// grid: ceil(N / 128) column tiles x ceil(M / (64 MI)) row tiles x ksplit
+template <int EPI, bool BT, typename TO, int MI>
+int pre_gemm_mi(const PreArgs& a, hipStream_t s) {
+  if (int e = ensure_lds<wide_pre_gemm_kernel<EPI, BT, TO, MI>, pre_lds(MI)>()) return e;
   KernelTimer timer(EPI == 0 ? "wide_pre_gp_kernel" : "wide_pre_gx_kernel", s);
-  hipLaunchKernelGGL((wide_pre_gemm_kernel<EPI, BT, TO>), dim3(grid_x, grid_y, grid_z), dim3(256), kPreLds, s, a);
+  const dim3 grid(static_cast<unsigned>(ceil_div(a.N, kPreTN)), static_cast<unsigned>(ceil_div(a.M, pre_tm(MI))),
+                  static_cast<unsigned>(a.ksplit));
+  hipLaunchKernelGGL((wide_pre_gemm_kernel<EPI, BT, TO, MI>), grid, dim3(256), pre_lds(MI), s, a);
   return check_launch("wide_pre_gemm_kernel");
+}
+template <int EPI, bool BT, typename TO>
+int pre_gemm(const PreArgs& a, int MI, hipStream_t s) {
+  return MI == 4 ? pre_gemm_mi<EPI, BT, TO, 4>(a, s) : pre_gemm_mi<EPI, BT, TO, 3>(a, s);
 }
 
 // The wide backward on pre-split operands: G_s as bf16 planes (kEpiGsSplit), then g_x and g_P on
@@ -1435,16 +1458,16 @@ int launch_bwd_wide_pre(const Geometry& g, int x_dtype, const void* x, const flo
     a.sbb = img, a.ldb = g.HW, a.bcols = g.npix, a.bnb = g.HW, a.bk = g.P;
     a.M = g.C, a.N = g.npix, a.K = kp, a.ksplit = 1;
     a.gx = g_x, a.x = x, a.C = g.C, a.HW = g.HW;
-    const int gx_ = static_cast<int>(ceil_div(g.npix, kPreTN)), gy = static_cast<int>(ceil_div(g.C, kPreTM));
+    const int mi = pre_mi(g.C, ceil_div(g.npix, kPreTN));
     if (x_dtype == PROTOSEG_BF16) {
       a.o_bytes = static_cast<unsigned>(static_cast<size_t>(g.npix) * g.C * 2);
-      st = pre_gemm<1, true, uint16_t>(a, gx_, gy, 1, s);
+      st = pre_gemm<1, true, uint16_t>(a, mi, s);
     } else if (x_dtype == PROTOSEG_F16) {
       a.o_bytes = static_cast<unsigned>(static_cast<size_t>(g.npix) * g.C * 2);
-      st = pre_gemm<1, true, _Float16>(a, gx_, gy, 1, s);
+      st = pre_gemm<1, true, _Float16>(a, mi, s);
     } else {
       a.o_bytes = static_cast<unsigned>(static_cast<size_t>(g.npix) * g.C * 4);
-      st = pre_gemm<1, true, float>(a, gx_, gy, 1, s);
+      st = pre_gemm<1, true, float>(a, mi, s);
     }
     if (st) return st;
   }
@@ -1472,9 +1495,7 @@ int launch_bwd_wide_pre(const Geometry& g, int x_dtype, const void* x, const flo
     a.sbb = static_cast<long long>(g.C) * g.HW, a.ldb = g.HW, a.bkb = g.HW, a.bcols = g.C;
     a.M = g.P, a.N = g.C, a.K = g.npix, a.ksplit = S;
     a.slab = part;
-    if ((st = pre_gemm<0, false, float>(a, static_cast<int>(ceil_div(g.C, kPreTN)), static_cast<int>(ceil_div(g.P, kPreTM)),
-                                        S, s)))
-      return st;
+    if ((st = pre_gemm<0, false, float>(a, 3, s))) return st;  // 3: pre_split's tile count
     const long long e = static_cast<long long>(g.P) * g.C;
     hipLaunchKernelGGL(wide_finish_kernel, dim3(static_cast<unsigned>(ceil_div(e, 256))), dim3(256), 0, s, part, S, 1,
                        g.P, g.C, 1, protos, rs, g_protos, static_cast<long long>(g.C), 0LL);
