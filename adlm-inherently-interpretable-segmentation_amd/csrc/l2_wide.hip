@@ -327,6 +327,36 @@ __global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
     if (n >= a.N) continue;
     float colsum = 0.f;
     if constexpr (kSumB) colsum = (redB[0][cn] + redB[1][cn]) + (redB[2][cn] + redB[3][cn]);
+    // The element loads of the 16 rows (D, g_dist, x, the accumulated output) go out as one
+    // batch before any store: through plain pointers the compiler must assume a store may alias
+    // the next row's load, and interleaved they cost one round trip per row. Rows past M load
+    // through row M - 1 (a valid address) and are not stored.
+    constexpr bool kLd = EPI == kEpiGs || EPI == kEpiGsSplit || EPI == kEpiGx;
+    float ld0[16], ld1[16], ldo[16];
+    const bool acc_out = a.accumulate != 0;
+    if constexpr (kLd) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mc = min(m0 + wm * 32 + acc_row(r, h), a.M - 1);
+        const long long oc = bo * a.ob + mc * a.om + static_cast<long long>(n) * a.on;
+        if constexpr (EPI == kEpiGx) {
+          ld0[r] = load_elem<TO>(a.xo, oc);
+        } else {
+          ld0[r] = a.D[oc];
+          ld1[r] = a.gd ? a.gd[oc] : 0.f;
+        }
+      }
+      pin_batch(ld0);
+      if constexpr (EPI != kEpiGx) pin_batch(ld1);
+    }
+    if (acc_out) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mc = min(m0 + wm * 32 + acc_row(r, h), a.M - 1);
+        ldo[r] = XIO<TO>::load(static_cast<TO*>(a.out), static_cast<size_t>(bo * a.ob + mc * a.om + static_cast<long long>(n) * a.on));
+      }
+      pin_batch(ldo);
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int rm = wm * 32 + acc_row(r, h);
@@ -342,9 +372,9 @@ __global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
         v = d;
         if (a.act) a.act[bo * a.ab + m * a.am + static_cast<long long>(n) * a.an] = activation(d, a.eps, a.act_kind);
       } else if constexpr (EPI == kEpiGs || EPI == kEpiGsSplit) {
-        const float d = a.D[o];
+        const float d = ld0[r];
         float g = v * activation_grad(d, a.eps, a.act_kind);
-        if (a.gd) g += a.gd[o];
+        if (a.gd) g += ld1[r];
         v = d > 0.f ? g : 0.f;  // relu backward
         if constexpr (EPI == kEpiGsSplit) {  // the pre-split GEMMs' operand: hi, lo planes
           const bf16 vh = static_cast<bf16>(v);
@@ -354,10 +384,10 @@ __global__ __launch_bounds__(kWThreads) void wide_gemm_kernel(WideArgs a) {
         }
       } else if constexpr (EPI == kEpiGx) {
         // conv(x^2, ones) backward: 2x sum_p g_s; conv(x, P) backward: -2 P^T g_s
-        v = -2.f * v + 2.f * load_elem<TO>(a.xo, o) * colsum;
+        v = -2.f * v + 2.f * ld0[r] * colsum;
       }
       TO* out = static_cast<TO*>(a.out);
-      if (a.accumulate) v += XIO<TO>::load(out, static_cast<size_t>(o));
+      if (acc_out) v += ldo[r];
       XIO<TO>::store(out, static_cast<size_t>(o), v);
     }
   }
@@ -1053,8 +1083,29 @@ struct PreArgs {
 };
 
 // Buffer-resource element IO of g_x / x in the feature map's dtype (out-of-range: load 0, store dropped).
+// load_raw / from_raw: the element's bits (one 32-bit register) and their value, so a batch of
+// loads can be pinned before any conversion (a conversion right behind its load makes the
+// allocator reuse one destination register, i.e. one wait per load).
 template <typename T> struct BufIO2 : BufIO<T> {};
+template <> struct BufIO2<float> : BufIO<float> {
+  static __device__ __forceinline__ uint32_t load_raw(rsrc_t r, unsigned voff, unsigned soff) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
+  }
+  static __device__ __forceinline__ float from_raw(uint32_t v) { return __uint_as_float(v); }
+};
+template <> struct BufIO2<uint16_t> : BufIO<uint16_t> {
+  static __device__ __forceinline__ uint32_t load_raw(rsrc_t r, unsigned voff, unsigned soff) {
+    return static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0));
+  }
+  static __device__ __forceinline__ float from_raw(uint32_t v) { return __uint_as_float(v << 16); }
+};
 template <> struct BufIO2<_Float16> {
+  static __device__ __forceinline__ uint32_t load_raw(rsrc_t r, unsigned voff, unsigned soff) {
+    return static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0));
+  }
+  static __device__ __forceinline__ float from_raw(uint32_t v) {
+    return static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(v)));
+  }
   static __device__ __forceinline__ float load(rsrc_t r, unsigned voff, unsigned soff) {
     return static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(__builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0))));
   }
@@ -1234,6 +1285,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     __builtin_amdgcn_sched_barrier(0);
     if (st + 2 < nst) issue(st + 2);
   }
+
   float* red = reinterpret_cast<float*>(psm + kPreNS * kStage);
   if constexpr (EPI == 1) {
 #pragma unroll
@@ -1263,15 +1315,33 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       const int b = col < a.N ? col / a.HW : 0, n = col - b * a.HW;
       const unsigned cbase = col < a.N ? static_cast<unsigned>((b * a.C * a.HW + n + 4 * h * a.HW) * sizeof(TO)) : kOOB;
       const rsrc_t ro = make_rsrc(a.gx, a.o_bytes), rxo = make_rsrc(a.x, a.o_bytes);
+      // per 32-row block: the 16 x loads first (the stores to g_x may alias them as far as the
+      // compiler knows, so a load after a store would wait a whole round trip each), then the
+      // stores. A tile whose rows are all below M (the common case) keeps one voffset for every
+      // row (the row in the uniform soffset): per-row guarded voffsets ran the 256-VGPR kernel
+      // out of registers and the allocator put a wait behind every load.
+      auto rows = [&](auto full_tag) __attribute__((always_inline)) {
+        constexpr bool kFull = decltype(full_tag)::value;
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
+        for (int i = 0; i < MI; ++i) {
+          uint32_t xr[16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int mu = m0 + 32 * MI * rg + 32 * i + row_of(r);
-          const unsigned vo = mu + 4 * h < a.M ? cbase : kOOB, so = static_cast<unsigned>(mu * a.HW * sizeof(TO));
-          const float xv = BufIO2<TO>::load(rxo, vo, so);
-          BufIO2<TO>::store(ro, -2.f * acc[i][jj][r] + 2.f * xv * csum, vo, so);
+          for (int r = 0; r < 16; ++r) {
+            const int mu = m0 + 32 * MI * rg + 32 * i + row_of(r);
+            xr[r] = BufIO2<TO>::load_raw(rxo, kFull || mu + 4 * h < a.M ? cbase : kOOB,
+                                         static_cast<unsigned>(mu * a.HW * sizeof(TO)));
+          }
+          pin_batch(xr);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int mu = m0 + 32 * MI * rg + 32 * i + row_of(r);
+            BufIO2<TO>::store(ro, -2.f * acc[i][jj][r] + 2.f * BufIO2<TO>::from_raw(xr[r]) * csum,
+                              kFull || mu + 4 * h < a.M ? cbase : kOOB, static_cast<unsigned>(mu * a.HW * sizeof(TO)));
+          }
         }
+      };
+      if (m0 + kTM <= a.M) rows(std::true_type());
+      else rows(std::false_type());
     }
   }
 }
