@@ -573,6 +573,35 @@ __global__ __launch_bounds__(kWThreads) void wide_bf3_kernel(WideArgs a) {
     if constexpr (kSumB) colsum = redB[cn] + redB[kW2 + cn];
 #pragma unroll
     for (int bm = 0; bm < 2; ++bm) {
+      // the rows' element loads as one batch before the stores (wide_bf3 / wide_gemm bf16x3
+      // epilogue: a load behind a possibly aliasing store waits a round trip)
+      constexpr bool kLd = EPI == kEpiGs || EPI == kEpiGsSplit || EPI == kEpiGx;
+      float ld0[16], ld1[16], ldo[16];
+      const bool acc_out = a.accumulate != 0;
+      if constexpr (kLd) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int mc = min(m0 + wm * 64 + bm * 32 + acc_row(r, h), a.M - 1);
+          const long long oc = bo * a.ob + mc * a.om + static_cast<long long>(n) * a.on;
+          if constexpr (EPI == kEpiGx) {
+            ld0[r] = load_elem<TO>(a.xo, oc);
+          } else {
+            ld0[r] = a.D[oc];
+            ld1[r] = a.gd ? a.gd[oc] : 0.f;
+          }
+        }
+        pin_batch(ld0);
+        if constexpr (EPI != kEpiGx) pin_batch(ld1);
+      }
+      if (acc_out) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int mc = min(m0 + wm * 64 + bm * 32 + acc_row(r, h), a.M - 1);
+          ldo[r] = XIO<TO>::load(static_cast<TO*>(a.out),
+                                 static_cast<size_t>(bo * a.ob + mc * a.om + static_cast<long long>(n) * a.on));
+        }
+        pin_batch(ldo);
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int rm = wm * 64 + bm * 32 + acc_row(r, h);
@@ -586,15 +615,15 @@ __global__ __launch_bounds__(kWThreads) void wide_bf3_kernel(WideArgs a) {
           v = d;
           if (a.act) a.act[bo * a.ab + m * a.am + static_cast<long long>(n) * a.an] = activation(d, a.eps, a.act_kind);
         } else if constexpr (EPI == kEpiGs) {
-          const float d = a.D[o];
+          const float d = ld0[r];
           float g = v * activation_grad(d, a.eps, a.act_kind);
-          if (a.gd) g += a.gd[o];
+          if (a.gd) g += ld1[r];
           v = d > 0.f ? g : 0.f;  // relu backward
         } else if constexpr (EPI == kEpiGx) {
-          v = -2.f * v + 2.f * load_elem<TO>(a.xo, o) * colsum;
+          v = -2.f * v + 2.f * ld0[r] * colsum;
         }
         TO* out = static_cast<TO*>(a.out);
-        if (a.accumulate) v += XIO<TO>::load(out, static_cast<size_t>(o));
+        if (acc_out) v += ldo[r];
         XIO<TO>::store(out, static_cast<size_t>(o), v);
       }
     }

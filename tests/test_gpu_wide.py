@@ -4,10 +4,11 @@ The reference's own construct_PPNet default is prototype_shape = (2000, 512, 1, 
 classes (model.py:394); the C in {32, 64, 128}, K <= 32 kernels do not hold it. These tests run
 that shape (and C = 256, odd depths, K > 32 at C = 64) through PPNet's layer op and the push
 argmin, against the oracle (model.py:203-283 restated op for op, autograd for the backward;
-push.py:195-263 restated). Products are exact f32 (v_mfma_f32_32x32x2_f32 fma chains): distances
-within 1e-4 relative (+ a floor of 1e-6 (||x||^2 + ||p||^2) for the expanded form's
-cancellation), logits and gradients within 1e-4 of their own scale (f32 sums over C / P / pixels
-in a different order than torch-CPU's).
+push.py:195-263 restated). Products are bf16x3 splits for the default BF16X3 requests (fp16 maps:
+the fp16 distance GEMM with two-term prototypes) and exact f32 for F32 requests: distances within
+1e-4 relative (+ a floor of 1e-6 (||x||^2 + ||p||^2) for the expanded form's cancellation),
+logits and gradients within 1e-4 of their own scale (f32 sums over C / P / pixels in a different
+order than torch-CPU's).
 """
 import numpy as np
 import pytest
@@ -63,6 +64,33 @@ def test_wide_layer_forward_backward_vs_oracle(device, B, C, h, w, P, K):
     assert bool((derr <= 1e-4 * r_dist.abs() + floor).all()), f"distances: max err {derr.max().item():.3e}"
     _close(logits, r_logits, "logits")
     _close(xd.grad, r_gx, "g_x")
+    _close(pd.grad, r_gp, "g_protos")
+    _close(wd.grad, r_gw, "g_w")
+
+
+@pytest.mark.parametrize("B,C,h,w,P,K,dt", [
+    (2, 192, 8, 8, 100, 7, torch.float32),     # g_x on 192-row tiles (pre_mi 3), every tile full
+    (2, 320, 8, 8, 130, 7, torch.float16),     # 192-row tiles, the last one partial (rows 320..383)
+    (1, 1000, 8, 4, 70, 5, torch.bfloat16),    # 256-row tiles (pre_mi 4), the last one partial
+    (3, 256, 16, 16, 600, 19, torch.float16),  # g_P split over the pixels, several row tiles
+])
+def test_wide_pre_split_backward_vs_oracle(device, B, C, h, w, P, K, dt):
+    """The pre-split backward (launch_bwd_wide_pre: G_s split in its GEMM's epilogue, g_x and g_P
+    on wide_pre_gemm_kernel, HW a multiple of 32) across its tile choices and feature-map dtypes,
+    against the oracle on the same (rounded) feature map: gradients within 1e-4 of their scale
+    (bf16x3 products), g_x within its storage dtype's rounding."""
+    from protoseg_amd import ops
+    x, protos, w_last, g_logits, g_dist = _inputs(B, C, h, w, P, K, seed=C + P)
+    xr = x.to(dt)
+    xd = xr.to(device).requires_grad_(True)
+    pd = protos.to(device).requires_grad_(True)
+    wd = w_last.to(device).requires_grad_(True)
+    dist, logits, _ = ops.prototype_layer(xd, pd, wd)
+    torch.autograd.backward([logits, dist], [g_logits.to(device), g_dist.to(device)])
+    torch.cuda.synchronize()
+    r_logits, r_dist, r_gx, r_gp, r_gw = po.forward_backward(xr.float(), protos, w_last, g_logits, g_dist)
+    _close(logits, r_logits, "logits")
+    _close(xd.grad.float(), r_gx, "g_x", rel=1e-4 if dt == torch.float32 else 1e-2)
     _close(pd.grad, r_gp, "g_protos")
     _close(wd.grad, r_gw, "g_w")
 
