@@ -398,10 +398,22 @@ __global__ __launch_bounds__(256) void wide_rowsum_kernel(const float* __restric
                                                           float* __restrict__ rs) {
   __shared__ float red[256];
   const int p = blockIdx.x;
+  // thread t takes the (image, pixel) pairs t, t + 256, ... of the row's B * HW values, 8 loads
+  // in flight (clamped addresses, pin_batch); small maps (7 x 7) keep every thread busy
   float s = 0.f;
-  for (int b = 0; b < B; ++b) {
-    const float* g = gs + (static_cast<size_t>(b) * P + p) * HW;
-    for (int n = threadIdx.x; n < HW; n += 256) s += g[n];
+  const int tot = B * HW;
+  for (int i0 = static_cast<int>(threadIdx.x); i0 < tot; i0 += 8 * 256) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + 256 * u < tot ? i0 + 256 * u : tot - 1;
+      const int b = i / HW;
+      v[u] = gs[(static_cast<size_t>(b) * P + p) * HW + (i - b * HW)];
+    }
+    pin_batch(v);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (i0 + 256 * u < tot) s += v[u];
   }
   red[threadIdx.x] = s;
   __syncthreads();
@@ -1380,9 +1392,20 @@ __global__ __launch_bounds__(256) void wide_pt_split_kernel(const float* __restr
                                                             uint16_t* __restrict__ hi, uint16_t* __restrict__ lo) {
   __shared__ float t[64][65];
   const int p0 = static_cast<int>(blockIdx.x) * 64, c0 = static_cast<int>(blockIdx.y) * 64;
-  for (int i = static_cast<int>(threadIdx.x); i < 64 * 64; i += 256) {
-    const int pr = i >> 6, cc = i & 63;
-    t[pr][cc] = p0 + pr < P && c0 + cc < C ? protos[static_cast<size_t>(p0 + pr) * C + c0 + cc] : 0.f;
+  {  // the 16 loads of a thread in flight together (clamped addresses, pin_batch)
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int i = static_cast<int>(threadIdx.x) + 256 * k, pr = i >> 6, cc = i & 63;
+      const int pp = p0 + pr < P ? p0 + pr : P - 1, c = c0 + cc < C ? c0 + cc : C - 1;
+      v[k] = protos[static_cast<size_t>(pp) * C + c];
+    }
+    pin_batch(v);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int i = static_cast<int>(threadIdx.x) + 256 * k, pr = i >> 6, cc = i & 63;
+      t[pr][cc] = p0 + pr < P && c0 + cc < C ? v[k] : 0.f;
+    }
   }
   __syncthreads();
   for (int i = static_cast<int>(threadIdx.x); i < 64 * 64; i += 256) {
@@ -1400,11 +1423,25 @@ __global__ __launch_bounds__(256) void wide_pt_split_kernel(const float* __restr
 template <typename TX>
 __global__ __launch_bounds__(256) void wide_x_split_kernel(const TX* __restrict__ x, long long n, uint16_t* __restrict__ hi,
                                                            uint16_t* __restrict__ lo) {
-  for (long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x; i < n; i += static_cast<long long>(gridDim.x) * 256) {
-    const float v = XIO<TX>::load(x, static_cast<size_t>(i));
-    const bf16 vh = static_cast<bf16>(v);
-    hi[i] = __builtin_bit_cast(uint16_t, vh);
-    lo[i] = __builtin_bit_cast(uint16_t, static_cast<bf16>(v - static_cast<float>(vh)));
+  // 8 grid strides per step with their loads in flight (clamped addresses, pin_batch)
+  const long long stride = static_cast<long long>(gridDim.x) * 256;
+  for (long long i0 = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x; i0 < n; i0 += 8 * stride) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long long i = i0 + u * stride;
+      v[u] = XIO<TX>::load(x, static_cast<size_t>(i < n ? i : n - 1));
+    }
+    pin_batch(v);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long long i = i0 + u * stride;
+      if (i < n) {
+        const bf16 vh = static_cast<bf16>(v[u]);
+        hi[i] = __builtin_bit_cast(uint16_t, vh);
+        lo[i] = __builtin_bit_cast(uint16_t, static_cast<bf16>(v[u] - static_cast<float>(vh)));
+      }
+    }
   }
 }
 
@@ -1413,11 +1450,26 @@ __global__ __launch_bounds__(256) void wide_rowsum_split_kernel(const uint16_t* 
                                                                 int P, int HW, int B, float* __restrict__ rs) {
   __shared__ float red[256];
   const int p = blockIdx.x;
+  // per pixel n of the thread, the images in order (the summation order of one image at a time
+  // when HW <= 256); 8 images' loads in flight through clamped addresses (pin_batch), not one
+  // guarded load and its round trip per image
   float s = 0.f;
-  for (int b = 0; b < B; ++b) {
-    const size_t o = (static_cast<size_t>(b) * P + p) * HW;
-    for (int n = threadIdx.x; n < HW; n += 256)
-      s += __uint_as_float(static_cast<uint32_t>(gh[o + n]) << 16) + __uint_as_float(static_cast<uint32_t>(gl[o + n]) << 16);
+  for (int n = threadIdx.x; n < HW; n += 256) {
+    for (int b0 = 0; b0 < B; b0 += 8) {
+      uint32_t hv[8], lv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int bb = b0 + u < B ? b0 + u : B - 1;
+        const size_t o = (static_cast<size_t>(bb) * P + p) * HW + n;
+        hv[u] = gh[o];
+        lv[u] = gl[o];
+      }
+      pin_batch(hv);
+      pin_batch(lv);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (b0 + u < B) s += __uint_as_float(hv[u] << 16) + __uint_as_float(lv[u] << 16);
+    }
   }
   red[threadIdx.x] = s;
   __syncthreads();
