@@ -389,7 +389,10 @@ __host__ __device__ inline size_t pw_lds_bytes(int C, int nptc) {
 #ifndef PUSH_CHUNK_PLAN
 #define PUSH_CHUNK_PLAN 1
 #endif
-constexpr int kPwMaxChunks = 3;
+#ifndef PUSH_MAX_CHUNKS
+#define PUSH_MAX_CHUNKS 3  // (development A/B of the plan: tools/build_var.sh ... -DPUSH_MAX_CHUNKS=n)
+#endif
+constexpr int kPwMaxChunks = PUSH_MAX_CHUNKS;
 struct PushPlan {
   int per;
   long long wgs;
