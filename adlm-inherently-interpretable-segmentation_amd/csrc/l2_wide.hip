@@ -41,6 +41,7 @@ constexpr int kWThreads = 256;
 // the pre-split backward GEMMs' tile (wide_pre_gemm_kernel, below): 64 MI rows (MI = 3 or 4
 // 32-row blocks per wave) x 128 columns x 32 k per stage, three stages
 constexpr int kPreTN = 128, kPreTK = 32, kPreNS = 3;
+constexpr int kColsumQ = 8;  // prototype chunks of the split g_x's column sums (wide_colsum_kernel)
 constexpr int kPreBPlane = kPreTN * kPreTK * 2;                                  // 8 KiB
 __host__ __device__ constexpr int pre_tm(int MI) { return 64 * MI; }
 __host__ __device__ constexpr int pre_aplane(int MI) { return pre_tm(MI) * kPreTK * 2; }  // 12 / 16 KiB
@@ -730,8 +731,15 @@ int pre_split(const Geometry& g) {  // workgroups along the g_P contraction: at 
   return static_cast<int>(s2 < 1 ? 1 : s2 > 64 ? 64 : s2);
 }
 struct WideBwdLayout {
-  size_t D, G, rs, part, xs, pt, total;  // float offsets (G holds f32 G_s, or its two bf16 planes)
+  size_t D, G, rs, part, xs, pt, cs, total;  // float offsets (G holds f32 G_s, or its two bf16 planes)
 };
+// Workgroups along the contraction (P) of the 64 x 64 tile's g_x GEMM: split when its output tiles
+// alone leave the chip mostly idle (the construct_PPNet default: 7 x 7 maps, 256 tiles of 63
+// stages each).
+int gx_split(const Geometry& g) {
+  const long long groups = ceil_div(g.C, tile_rows(g.C)) * ceil_div(g.HW, kWT) * (g.npix / g.HW);
+  return groups >= 512 ? 1 : split_of(groups, g.P);
+}
 WideBwdLayout wide_bwd_layout(const Geometry& g) {
   WideBwdLayout l{};
   const size_t dp = static_cast<size_t>(g.npix) * g.P;
@@ -742,6 +750,9 @@ WideBwdLayout wide_bwd_layout(const Geometry& g) {
     const size_t sq = static_cast<size_t>(pre_split(g)) * g.P * g.C;
     sp = sp > sq ? sp : sq;
   }
+  const int sxs = gx_split(g);
+  const size_t sx = sxs > 1 ? static_cast<size_t>(sxs) * g.npix * g.C : 0;
+  sp = sp > sx ? sp : sx;
   auto al = [](size_t v) { return (v + 63) & ~static_cast<size_t>(63); };
   l.D = 0;
   l.G = al(dp);
@@ -749,7 +760,8 @@ WideBwdLayout wide_bwd_layout(const Geometry& g) {
   l.part = l.rs + al(g.P);
   l.xs = l.part + al(sp > sw ? sp : sw);                                  // x as two bf16 planes
   l.pt = l.xs + (pre ? al(static_cast<size_t>(g.npix) * g.C) : 0);       // P^T as two bf16 planes
-  l.total = l.pt + (pre ? al(static_cast<size_t>(g.C) * (ceil_div(g.P, kPreTK) * kPreTK)) : 0);
+  l.cs = l.pt + (pre ? al(static_cast<size_t>(g.C) * (ceil_div(g.P, kPreTK) * kPreTK)) : 0);
+  l.total = l.cs + (sxs > 1 ? al(static_cast<size_t>(kColsumQ) * g.npix) : 0);  // sum_p G_s partials (split g_x)
   return l;
 }
 
@@ -1480,6 +1492,76 @@ __global__ __launch_bounds__(256) void wide_rowsum_split_kernel(const uint16_t* 
   if (threadIdx.x == 0) rs[p] = red[0];
 }
 
+// Partial column sums of G_s (f32): csq[q][b HW + n] = sum over prototype chunk q (of kColsumQ,
+// blockIdx.y) of G_s[b][p][n]. Workgroup = 32 pixels x 8 prototype groups (group r sums p = r,
+// r + 8, ... of the chunk in order, 4 loads in flight), the groups added in order; the finish adds
+// the chunks in order.
+__global__ __launch_bounds__(256) void wide_colsum_kernel(const float* __restrict__ gs, int P, int HW, int npix,
+                                                          float* __restrict__ csq) {
+  __shared__ float red[8][32];
+  const int j = static_cast<int>(threadIdx.x) & 31, q = static_cast<int>(threadIdx.x) >> 5;
+  const int g = static_cast<int>(blockIdx.x) * 32 + j;
+  const int gc = g < npix ? g : npix - 1;
+  const int b = gc / HW, n = gc - b * HW;
+  const int ch = static_cast<int>(blockIdx.y);
+  const int pb = static_cast<int>(static_cast<long long>(P) * ch / kColsumQ);
+  const int pe = static_cast<int>(static_cast<long long>(P) * (ch + 1) / kColsumQ);
+  const float* col = gs + static_cast<size_t>(b) * P * HW + n;
+  float s = 0.f;
+  for (int p0 = pb + q; p0 < pe; p0 += 32) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = p0 + 8 * u;
+      v[u] = col[static_cast<size_t>(p < pe ? p : p0) * HW];
+    }
+    pin_batch(v);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (p0 + 8 * u < pe) s += v[u];
+  }
+  red[q][j] = s;
+  __syncthreads();
+  if (q == 0 && g < npix) {
+    float t = red[0][j];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) t += red[k][j];
+    csq[static_cast<size_t>(ch) * npix + g] = t;
+  }
+}
+
+// g_x from split-K slabs [B][S][C][HW]: -2 sum_z (slab order) + 2 x cs, stored in x's dtype.
+template <typename TO>
+__global__ __launch_bounds__(256) void wide_finish_gx_kernel(const float* __restrict__ part, int S, int B, int C, int HW,
+                                                             const TO* __restrict__ x, const float* __restrict__ csq,
+                                                             TO* __restrict__ gx) {
+  const long long e = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+  const long long mn = static_cast<long long>(C) * HW;
+  if (e >= mn * B) return;
+  const long long b = e / mn, r = e - b * mn;
+  const int n = static_cast<int>(r % HW);
+  const float* pp = part + static_cast<size_t>(b) * S * mn + r;
+  float s = 0.f;
+  for (int i0 = 0; i0 < S; i0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = pp[static_cast<size_t>(i0 + u < S ? i0 + u : 0) * mn];
+    pin_batch(v);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (i0 + u < S) s += v[u];
+  }
+  const long long npix = static_cast<long long>(B) * HW;
+  float cq[kColsumQ];
+#pragma unroll
+  for (int q = 0; q < kColsumQ; ++q) cq[q] = csq[q * npix + b * HW + n];
+  float cs = cq[0];
+#pragma unroll
+  for (int q = 1; q < kColsumQ; ++q) cs += cq[q];
+  const float xv = XIO<TO>::load(x, static_cast<size_t>(e));
+  XIO<TO>::store(gx, static_cast<size_t>(e), -2.f * s + 2.f * xv * cs);
+}
+
 // D[b][p][n] into `dist` (ld P per image), optional act[g][p].
 template <typename TX>
 int wide_distances(const Geometry& g, const TX* x, const float* protos, float eps, int act_kind, float* dist,
@@ -1702,12 +1784,35 @@ int launch_bwd_wide(const Geometry& g, int x_dtype, const void* x, const float* 
     a.A = op(protos, 1, g.C, 0);          // (c, p) of P[p][c]
     a.B = op(G, 1, g.HW, img);            // (n, p) of G_s[b][p][n]
     a.M = g.C, a.N = g.HW, a.Kd = g.P, a.nb = B;
-    a.out = g_x, a.om = g.HW, a.on = 1, a.ob = static_cast<long long>(g.C) * g.HW;
-    a.xo = x, a.bf3 = bf3;
-    st = x_dtype == PROTOSEG_BF16  ? gemm<kEpiGx, float, float, -1, -1, uint16_t>(a, B, s)
-         : x_dtype == PROTOSEG_F16 ? gemm<kEpiGx, float, float, -1, -1, _Float16>(a, B, s)
-                                   : gemm<kEpiGx, float, float, -1, -1, float>(a, B, s);
-    if (st) return st;
+    a.bf3 = bf3;
+    const int Sx = gx_split(g);
+    if (Sx > 1) {  // split over the prototypes: slabs [B][Sx][C][HW], then the epilogue in the finish
+      float* cs = ws + l.cs;
+      hipLaunchKernelGGL(wide_colsum_kernel, dim3(static_cast<unsigned>(ceil_div(g.npix, 32)), kColsumQ), dim3(256), 0, s, G,
+                         g.P, g.HW, g.npix, cs);
+      if ((st = check_launch("wide_colsum_kernel"))) return st;
+      a.ksplit = Sx;
+      a.out = part, a.om = g.HW, a.on = 1, a.ob = static_cast<long long>(g.C) * g.HW;
+      if ((st = gemm<kEpiStore, float, float, -1, -1, float>(a, B * Sx, s))) return st;
+      const unsigned fg = static_cast<unsigned>(ceil_div(static_cast<long long>(g.npix) * g.C, 256));
+      if (x_dtype == PROTOSEG_BF16)
+        hipLaunchKernelGGL(wide_finish_gx_kernel<uint16_t>, dim3(fg), dim3(256), 0, s, part, Sx, B, g.C, g.HW,
+                           static_cast<const uint16_t*>(x), cs, static_cast<uint16_t*>(g_x));
+      else if (x_dtype == PROTOSEG_F16)
+        hipLaunchKernelGGL(wide_finish_gx_kernel<_Float16>, dim3(fg), dim3(256), 0, s, part, Sx, B, g.C, g.HW,
+                           static_cast<const _Float16*>(x), cs, static_cast<_Float16*>(g_x));
+      else
+        hipLaunchKernelGGL(wide_finish_gx_kernel<float>, dim3(fg), dim3(256), 0, s, part, Sx, B, g.C, g.HW,
+                           static_cast<const float*>(x), cs, static_cast<float*>(g_x));
+      if ((st = check_launch("wide_finish_gx_kernel"))) return st;
+    } else {
+      a.out = g_x, a.om = g.HW, a.on = 1, a.ob = static_cast<long long>(g.C) * g.HW;
+      a.xo = x;
+      st = x_dtype == PROTOSEG_BF16  ? gemm<kEpiGx, float, float, -1, -1, uint16_t>(a, B, s)
+           : x_dtype == PROTOSEG_F16 ? gemm<kEpiGx, float, float, -1, -1, _Float16>(a, B, s)
+                                     : gemm<kEpiGx, float, float, -1, -1, float>(a, B, s);
+      if (st) return st;
+    }
   }
   if (g_protos) {  // g_P[p][c] = -2 sum_{b,n} G_s[b][p][n] x[b][c][n] + 2 p rs[p]
     hipLaunchKernelGGL(wide_rowsum_kernel, dim3(static_cast<unsigned>(g.P)), dim3(256), 0, s, G, g.P, g.HW, B, rs);
