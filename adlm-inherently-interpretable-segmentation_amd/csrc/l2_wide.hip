@@ -627,11 +627,17 @@ __global__ __launch_bounds__(kWThreads) void wide_bf3_kernel(WideArgs a) {
           const float d = l2_distance(colsum, p2, v);
           v = d;
           if (a.act) a.act[bo * a.ab + m * a.am + static_cast<long long>(n) * a.an] = activation(d, a.eps, a.act_kind);
-        } else if constexpr (EPI == kEpiGs) {
+        } else if constexpr (EPI == kEpiGs || EPI == kEpiGsSplit) {
           const float d = ld0[r];
           float g = v * activation_grad(d, a.eps, a.act_kind);
           if (a.gd) g += ld1[r];
           v = d > 0.f ? g : 0.f;  // relu backward
+          if constexpr (EPI == kEpiGsSplit) {  // the pre-split GEMMs' operand: hi, lo planes
+            const bf16 vh = static_cast<bf16>(v);
+            static_cast<uint16_t*>(a.out)[o] = __builtin_bit_cast(uint16_t, vh);
+            static_cast<uint16_t*>(a.out2)[o] = __builtin_bit_cast(uint16_t, static_cast<bf16>(v - static_cast<float>(vh)));
+            continue;
+          }
         } else if constexpr (EPI == kEpiGx) {
           v = -2.f * v + 2.f * ld0[r] * colsum;
         }
