@@ -1,5 +1,5 @@
 """Runs the KLD forward / backward (dense and compact) and the layer backward with each gradient
-at the bench shape (B=32, 65x65, K=19; P from $P, default 190) a few times, for rocprofv3
+at the bench shape (B from $B, default 32, 65x65, K=19; P from $P, default 190) a few times, for rocprofv3
 --kernel-trace --stats."""
 import os
 import sys
@@ -11,10 +11,12 @@ import bench  # noqa: E402
 import torch  # noqa: E402
 
 dev = torch.device("cuda:0")
-st = bench.LayerStep(32, 64, 65, 65, int(os.environ.get("P", 190)), 19, torch.float32, dev, bench.SEED)
+st = bench.LayerStep(int(os.environ.get("B", 32)), 64, 65, 65, int(os.environ.get("P", 190)), 19, torch.float32, dev, bench.SEED)
 st.setup_kld(bench.SEED)
 st.fwd()
 for _ in range(10):
+    st.fwd()
+    st.bwd()
     st.kld_fwd()
     st.kld_bwd()
     st.bwd_gd()
