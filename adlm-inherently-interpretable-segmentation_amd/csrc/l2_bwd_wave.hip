@@ -61,7 +61,7 @@ constexpr int kPartRow = 68 * 4;
 
 // LDS regions (bytes).
 struct WaveLds {
-  int pimg, xa, ga, raw, raw_gl, raw_cls, x2u, ro, cl, tw, tw_bytes, total;
+  int pimg, xa, ga, raw, raw_gl, raw_cls, x2u, ro, cl, tm, tw, tw_bytes, total;
 };
 __host__ __device__ constexpr WaveLds wave_lds(int NB) {
   WaveLds o{};
@@ -75,9 +75,10 @@ __host__ __device__ constexpr WaveLds wave_lds(int NB) {
   o.x2u = o.raw_cls + 64 * 4;          // [4 q][32 n] f32: u_q = s_{q,0} + s_{q,1} (||x||^2 pieces)
   o.ro = o.x2u + 4 * 32 * 4;           // [32] u32: g_dist byte offset per pixel (GD)
   o.cl = o.ro + 32 * 4;                // [32] int: the pixel's KLD class (GD = 2)
+  o.tm = o.cl + 32 * 4;                // u32 (16 B): the tile's KLD classes as a bit mask (GD = 2)
   // per wave: its g_s image for two blocks [T][2][32 p][32 n] bf16 (64-B rows, 8-B slots
   // swizzled), then, in the same bytes, its g_x partial [32 n][64 physical columns | sum_p g_s]
-  o.tw = o.cl + 32 * 4;
+  o.tw = o.tm + 16;
   o.tw_bytes = 32 * kPartRow;         // >= kWT * 2 * 32 * 64 = 8192
   o.total = o.tw + kWW * o.tw_bytes;
   return o;
@@ -192,6 +193,7 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
   bf16x8 wreg[NB][2][kWT];
   uint32_t p2pk[NB][2];
   int pcls[NB], pslot[NB];
+  uint32_t bmask[NB];  // (GD = 2) the classes of block jb's prototypes as a bit mask (K <= 32), uniform
 #pragma unroll
   for (int jb = 0; jb < NB; ++jb) {
     const int p = 32 * (NB * wave + jb) + j;
@@ -216,6 +218,10 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
       const int code = p < P ? cg.slot[gd_p0 + p] : 0;
       pcls[jb] = p < P ? code >> 8 : -2;
       pslot[jb] = (code & 255) * 4;
+      uint32_t m = pcls[jb] >= 0 && pcls[jb] < 32 ? 1u << pcls[jb] : 0u;  // (bucket K never matches a pixel)
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) m |= static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), o));
+      bmask[jb] = __builtin_amdgcn_readfirstlane(m);
     }
   }
   // bf16 (1, 1) in the k-steps' first dword for the lanes of half 0 (k = 0..7), 0 for half 1
@@ -312,6 +318,10 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
           const int cl = ok ? static_cast<int>(lds_ldu(S0 + L.raw_cls + 4 * j)) : -1;
           lds_stu(S0 + L.ro + 4 * j, cl >= 0 ? static_cast<unsigned>(gp * cg.mpc * 4) : kOOB);
           lds_stu(S0 + L.cl + 4 * j, static_cast<uint32_t>(cl));
+          uint32_t m = cl >= 0 ? 1u << cl : 0u;  // (lanes 32..63: the shuffles stay in the half)
+#pragma unroll
+          for (int o = 1; o < 32; o <<= 1) m |= static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), o));
+          if (j == 0) lds_stu(S0 + L.tm, m);
         }
       }
     }
@@ -402,6 +412,8 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
       ax2 = h == 0 ? u32x4{pack_bf16(x2h, x2m), pack_bf16((x2 - x2h) - x2m, 1.f), one2, 0u} : u32x4{0u, 0u, 0u, 0u};
     }
     const bf16x8 ax2f = __builtin_bit_cast(bf16x8, ax2);
+    // (GD = 2) the tile's class mask: blocks with none of its classes skip their g_dist loads
+    const uint32_t tmask = GD == 2 ? __builtin_amdgcn_readfirstlane(lds_ldu(S0 + L.tm)) : 0u;
 
     struct Front {
       f32x16 acc, gacc;
@@ -411,6 +423,11 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
     auto front_gd = [&](int jb, Front& fr, int hf) __attribute__((always_inline)) {
       const int p = 32 * (NB * wave + jb) + j;
       if constexpr (GD == 2) {
+        if ((tmask & bmask[jb]) == 0u) {  // no pixel of the tile has a class of the block: all 0
+#pragma unroll
+          for (int e = 8 * hf; e < 8 * hf + 8; ++e) fr.gdv[e] = 0.f;
+          return;
+        }
 #pragma unroll
         for (int g4 = 2 * hf; g4 < 2 * hf + 2; ++g4) {
           const u32x4 ro = __builtin_bit_cast(u32x4, lds_frag(S0 + L.ro + 16 * h + 32 * g4));
