@@ -1097,10 +1097,11 @@ __global__ __launch_bounds__(64 * kRG) void l2_bwd_reduce_bf16_kernel(const floa
   if (g_w) g_w += p0;
   P = P - p0 < per ? P - p0 : per;
   // slab layout: [R][64] g_P | [KR][R] g_W | [R] sum_n g_s with R = Pp rows and KR = 32 class
-  // rows; gp_t (the wave kernel's): exact rows R = P, KR = K, and g_P transposed ([64][R]);
-  // gp_t 2: the g_P slabs already hold 2 p sum_n g_s (no sum_n g_s loads, no 2 p term here)
+  // rows; gp_t 1: exact rows R = P, KR = K, and g_P transposed ([64][R]); gp_t 2 (the wave
+  // kernel's): as gp_t 1 with rows padded to R = Pp, and the g_P slabs already hold 2 p sum_n g_s
+  // (no sum_n g_s loads, no 2 p term here)
   const int Pp = (P + 31) & ~31;
-  const int R = gp_t ? P : Pp, KR = gp_t ? K : 32;
+  const int R = gp_t == 1 ? P : Pp, KR = gp_t ? K : 32;
   const int E = R * kC + KR * R + R;
   const int e = blockIdx.x * 64 + (threadIdx.x & 63);
   const int grp = threadIdx.x >> 6;
@@ -1354,7 +1355,7 @@ int launch_bwd_reduce_bf16_chunks(const Geometry& g, int per, int nchunk, const 
                                   size_t chunk_elems, const float* protos, int act_kind, float* g_protos, float* g_w,
                                   hipStream_t stream, int gp_t) {
   const int Pp = static_cast<int>(ceil_div(per, 32) * 32);
-  const int elems = gp_t ? per * (kC + g.K) : Pp * kC + 32 * Pp;
+  const int elems = gp_t == 1 ? per * (kC + g.K) : gp_t == 2 ? Pp * (kC + g.K) : Pp * kC + 32 * Pp;
   hipLaunchKernelGGL(l2_bwd_reduce_bf16_kernel, dim3(static_cast<unsigned>(ceil_div(elems, 64)), nchunk), dim3(64 * kRG),
                      0, stream, ws, slabs, g.P, per, g.K, g.ldw, protos, act_unit(act_kind), g_protos, g_w,
                      chunk_elems, gp_t);

@@ -75,10 +75,11 @@ __host__ __device__ constexpr WaveLds wave_lds(int NB) {
   o.x2u = o.raw_cls + 64 * 4;          // [4 q][32 n] f32: u_q = s_{q,0} + s_{q,1} (||x||^2 pieces)
   o.ro = o.x2u + 4 * 32 * 4;           // [32] u32: g_dist byte offset per pixel (GD)
   o.cl = o.ro + 32 * 4;                // [32] int: the pixel's KLD class (GD = 2)
-  o.tm = o.cl + 32 * 4;                // u32 (16 B): the tile's KLD classes as a bit mask (GD = 2)
+  o.tm = o.cl + 32 * 4;                // u32: the tile's KLD classes as a bit mask (GD = 2); 256 B
+                                       // so the regions below keep their bank alignment
   // per wave: its g_s image for two blocks [T][2][32 p][32 n] bf16 (64-B rows, 8-B slots
   // swizzled), then, in the same bytes, its g_x partial [32 n][64 physical columns | sum_p g_s]
-  o.tw = o.tm + 16;
+  o.tw = o.tm + 256;
   o.tw_bytes = 32 * kPartRow;         // >= kWT * 2 * 32 * 64 = 8192
   o.total = o.tw + kWW * o.tw_bytes;
   return o;
@@ -739,10 +740,10 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
 
   // ---- slab: this workgroup's g_P^T = -2 X^T g_s + 2 p sum_n g_s (x -2: the x image holds +x;
   // the conv(x^2, ones) term's 2 p sum g_s is added per workgroup, so the reduce sums g_P slabs
-  // alone) and g_W in the reduce kernel's layout (gp_t 2): [64][P] g_P^T | [K][P] g_W | [P]
-  // unused (every store: 32 consecutive prototypes per half-wave; rows past P and classes past K
-  // are not written)
-  const int E = P * kC + K * P + P;
+  // alone) and g_W in the reduce kernel's layout (gp_t 2): [64][Pi] g_P^T | [K][Pi] g_W | [Pi]
+  // unused, rows padded to Pi = 32 ceil(P / 32) prototypes so that every half-wave store is one
+  // whole aligned 128-B line (rows past P and classes past K are not written)
+  const int E = Pi * kC + K * Pi + Pi;
   float* my_slab = slab + static_cast<size_t>(vb) * E;
 #ifdef WAVE_ABL_NOSLAB
   if (npix != -7) return;
@@ -760,11 +761,11 @@ __global__ __launch_bounds__(kWThreads, 1) void l2_bwd_wave_bf16_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int c = chan_col(32 * ct + acc_row(r, h));
-          my_slab[static_cast<size_t>(c) * P + p] = fmaf(s2, protos[static_cast<size_t>(p) * kC + c], -2.f * gp[jb][ct][r]);
+          my_slab[static_cast<size_t>(c) * Pi + p] = fmaf(s2, protos[static_cast<size_t>(p) * kC + c], -2.f * gp[jb][ct][r]);
         }
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        if (acc_row(r, h) < K) my_slab[static_cast<size_t>(P) * kC + acc_row(r, h) * P + p] = gw[jb][r];
+        if (acc_row(r, h) < K) my_slab[static_cast<size_t>(Pi) * kC + acc_row(r, h) * Pi + p] = gw[jb][r];
     }
   }
 #ifdef WAVE_STAMP
@@ -812,7 +813,7 @@ int bf16_bwd_wave_grid(const Geometry& g) {
 }
 
 size_t bf16_bwd_wave_slab_elems(const Geometry& g) {
-  const size_t P = static_cast<size_t>(g.P);
+  const size_t P = static_cast<size_t>(g.P + 31) & ~static_cast<size_t>(31);  // padded rows (the slab write)
   return static_cast<size_t>(bf16_bwd_wave_grid(g)) * (P * kC + static_cast<size_t>(g.K) * P + P);
 }
 
