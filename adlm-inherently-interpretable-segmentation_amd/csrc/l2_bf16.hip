@@ -1098,7 +1098,8 @@ __global__ __launch_bounds__(64 * kRG) void l2_bwd_reduce_bf16_kernel(const floa
   P = P - p0 < per ? P - p0 : per;
   // slab layout: [R][64] g_P | [KR][R] g_W | [R] sum_n g_s with R = Pp rows and KR = 32 class
   // rows; gp_t 1: exact rows R = P, KR = K, and g_P transposed ([64][R]); gp_t 2 (the wave
-  // kernel's): as gp_t 1 with rows padded to R = Pp, and the g_P slabs already hold 2 p sum_n g_s
+  // kernel's): as gp_t 1 with rows padded to R = Pp (columns P .. Pp are never written: their sums
+  // are formed and dropped, like every p >= P below), and the g_P slabs already hold 2 p sum_n g_s
   // (no sum_n g_s loads, no 2 p term here)
   const int Pp = (P + 31) & ~31;
   const int R = gp_t == 1 ? P : Pp, KR = gp_t ? K : 32;
